@@ -1,0 +1,95 @@
+"""Pins the CPU oracle (oracle/) to the reference before anything is checked
+against it: sklearn's own known-answer tests, global sklearn DBSCAN outputs,
+and the stage outputs of the reference pipeline run under an RDD stand-in
+(tests/golden/make_golden.py)."""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN, golden_names, load_golden
+
+NAMES = golden_names()
+
+
+def _metric(g):
+    m = str(g["metric"])
+    return "euclidean" if m == "callable" else m
+
+
+def _P(g):
+    P = int(g["max_partitions"])
+    return None if P < 0 else P
+
+
+def test_sklearn_kats():
+    z = np.load(f"{GOLDEN}/sklearn_kat.npz")
+    for ms in (1, 2, 3, 4):
+        lab, core, _, _ = oracle.dbscan(z["toy_X"], 1.0, ms)
+        assert np.array_equal(lab, z[f"toy_ms{ms}_labels"])
+        assert np.array_equal(np.nonzero(core)[0], z[f"toy_ms{ms}_core"])
+    # eps inclusive, min_samples counts the point itself (SK test_boundaries)
+    assert np.array_equal(np.nonzero(oracle.dbscan(z["bnd_a_X"], 2, 2)[1])[0], z["bnd_a_core"])
+    assert np.array_equal(np.nonzero(oracle.dbscan(z["bnd_b_X"], 1, 2)[1])[0], z["bnd_b_core_eps1"])
+    assert np.array_equal(np.nonzero(oracle.dbscan(z["bnd_b_X"], 0.99, 2)[1])[0],
+                          z["bnd_b_core_eps099"])
+    lab, core, _, _ = oracle.dbscan(z["clustered_X"], 0.8, 10)
+    assert np.array_equal(lab, z["clustered_labels"])
+    assert np.array_equal(np.nonzero(core)[0], z["clustered_core"])
+    lab, core, _, nc = oracle.dbscan(z["nocore_X"], 0.5, 6)
+    assert nc == 0 and core.sum() == 0 and np.all(lab == -1)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_matches_global_sklearn(name):
+    g = load_golden(name)
+    lab, core, cnt, _ = oracle.dbscan(g["X"], float(g["eps"]), int(g["min_samples"]), _metric(g))
+    assert np.array_equal(cnt, g["sk_counts"])
+    assert np.array_equal(core, g["sk_core"])
+    assert np.array_equal(lab, g["sk_labels"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_kd_partition_matches_reference(name):
+    g = load_golden(name)
+    kd = oracle.kd_partition(g["X"], _P(g))
+    sp = np.array([s[:6] for s in kd["splits"]], np.int64).reshape(-1, 6)
+    sf = np.array([s[6:] for s in kd["splits"]], np.float64).reshape(-1, 3)
+    assert np.array_equal(sp, g["splits"])
+    assert np.array_equal(sf, g["split_f"])          # bit-exact mean/var/boundary
+    assert np.array_equal(kd["box_lo"], g["box_lo"])
+    assert np.array_equal(kd["box_hi"], g["box_hi"])
+    assert np.array_equal(kd["owner"], g["owner"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_halo_matches_reference(name):
+    g = load_golden(name)
+    elo, ehi, members = oracle.halo(g["X"], g["box_lo"], g["box_hi"], float(g["eps"]))
+    assert np.array_equal(elo, g["ebox_lo"]) and np.array_equal(ehi, g["ebox_hi"])
+    pairs = np.array(sorted((L, int(i)) for L, m in enumerate(members) for i in m),
+                     np.int64).reshape(-1, 2)
+    assert np.array_equal(pairs, g["halo"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_partition_dbscan_matches_reference(name):
+    """dbscan_partition (R:dbscan/dbscan.py:12-34) per neighbourhood: local
+    labels and core flags, record for record."""
+    g = load_golden(name)
+    X, eps, ms = g["X"], float(g["eps"]), int(g["min_samples"])
+    po = g["part_out"]
+    for L in range(int(g["P"])):
+        rows = po[po[:, 0] == L]
+        keys = rows[:, 1]
+        lab, core, _, _ = oracle.dbscan(X[keys], eps, ms, _metric(g))
+        assert np.array_equal(lab, rows[:, 2]), L
+        assert np.array_equal(core, rows[:, 3].astype(np.uint8)), L
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_pipeline_equals_global_dbscan(name):
+    """Owner-rule merge of the per-neighbourhood results == global sklearn."""
+    g = load_golden(name)
+    out = oracle.pipeline(g["X"], float(g["eps"]), int(g["min_samples"]), _P(g), _metric(g))
+    assert np.array_equal(out["core"], g["sk_core"])
+    assert np.array_equal(out["labels"], g["sk_labels"])

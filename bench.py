@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Benchmark: BASELINE.json's metric on its headline config.
+
+  metric : points clustered/sec (whole node), 100M 3-D pts; % HBM roofline
+  config : C2 = blobs_noise(1e8, 3, side=100, 256 centres, sigma=1, 10% noise,
+           seed=2), eps=0.1, min_samples=10, max_partitions=8
+  step   : one full DBSCAN.train over the device-resident points — KD
+           partition (3 BFS levels of GPU passes), 2·eps halo, per-neighbourhood
+           DBSCAN, merge, global labels (labels stay in HBM).
+
+  python bench.py [--gpus N --steps K --warmup W] [--n POINTS] [--no-cpu]
+
+For N > 1 (torch.distributed.run, one rank per GPU) every rank runs the step
+on its own replica of the workload (weak scaling; the sharded multi-GPU
+train is not built yet), so value = N * points / max-over-ranks time.
+
+Roofline object: the neighbour-count kernel (count_kernel in engine.hip).
+achieved = B_nc / t, B_nc = records * (3^d*4d + 4d + 4) + (cells + 1) * 4 bytes
+(340 B per record in 3-D), t = the kernel's HIP-event time on
+its own stream, averaged over the timed steps.  traffic = FETCH_SIZE*2 +
+WRITE_SIZE per launch from profiles/*pmc*.json when present (gfx950 FETCH_SIZE
+reads half the bytes of wide streaming loads: MI355X_MICROARCH.md §HBM).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--n", type=int, default=None, help="override point count")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-n", type=int, default=1_000_000, help="CPU baseline sample size")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def b_nc(records, cells, d):
+    per = (3 ** d) * 4 * d + 4 * d + 4
+    return records * per + (cells + 1) * 4, per
+
+
+def load_pmc(kernel="count_kernel"):
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*pmc*.json")))
+    if not files:
+        return None
+    try:
+        z = json.load(open(files[-1]))
+        k = z.get(kernel)
+        if not k:
+            return None
+        return dict(bytes_per_launch=k["hbm_bytes_per_launch"], source=os.path.basename(files[-1]))
+    except Exception:
+        return None
+
+
+def cpu_baseline(cfg_name, n_sample):
+    import oracle
+    from oracle import cpu_ref
+    from pypardis_amd import synth
+    X, cfg = synth.make_config(cfg_name, n=n_sample)
+    oracle.build()
+    labels, secs, workers = cpu_ref.run(X, cfg["eps"], cfg["min_samples"],
+                                        cfg.get("max_partitions") or 1)
+    return {"value": n_sample / secs, "unit": "points/s", "cores": workers, "kind": "port",
+            "seconds": secs,
+            "sample": (f"{cfg_name} density-preserving slice, {n_sample} pts, "
+                       f"max_partitions={cfg.get('max_partitions')}: numpy KD + halo, "
+                       f"sklearn 1.7.2 kd_tree DBSCAN per neighbourhood in a {workers}-process "
+                       "pool (Spark local[*] emulation), owner-rule merge")}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    from pypardis_amd import DBSCAN, _native, synth
+
+    X, cfg = synth.make_config(args.config, n=args.n)
+    n, d = X.shape
+    Xd = torch.from_numpy(X).to(dev)
+    del X
+    eps, ms, P = cfg["eps"], cfg["min_samples"], cfg.get("max_partitions") or 1
+    ctx = _native.context(local_rank)
+
+    def step():
+        return DBSCAN(eps=eps, min_samples=ms, max_partitions=P).train(Xd)
+
+    for _ in range(args.warmup):
+        m = step()
+    torch.cuda.synchronize()
+    ctx.set_option(_native.PD_OPT_TIMING, 1)
+    stage_sum = {}
+    count_ms = []
+    rec = cells = 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m = step()
+        t = ctx.timings()
+        for k, v in t.items():
+            stage_sum[k] = stage_sum.get(k, 0.0) + v
+        count_ms.append(t["count"])
+        rec, cells = int(t["records"]), int(t["cells_n"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ctx.set_option(_native.PD_OPT_TIMING, 0)
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms_step = 1e3 * el / args.steps
+    value = world * n * args.steps / el
+    ncl = m.n_clusters_
+
+    if rank == 0:
+        t_cnt = float(np.mean(count_ms))
+        alg_bytes, per = b_nc(rec, cells, d)
+        achieved = alg_bytes / (t_cnt * 1e-3) / 1e9
+        pmc = load_pmc()
+        traffic = pmc["bytes_per_launch"] if pmc else None
+        stages = {k: round(v / args.steps, 3) for k, v in stage_sum.items()
+                  if k not in ("records", "cells_n", "grid_cells", "key_bits")}
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            try:
+                cpu = cpu_baseline(args.config, min(args.cpu_n, n))
+            except Exception as e:   # report, never fake
+                cpu = {"value": None, "error": repr(e)}
+        out = {
+            "metric": "points clustered/sec (whole node), 100M 3-D pts, 1/2/4/8 GPUs; % HBM roofline",
+            "value": value,
+            "unit": "points/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"{args.config}: blobs_noise n={n} d={d} eps={eps} "
+                                   f"min_samples={ms} max_partitions={P}",
+                       "n_points": n, "d": d, "eps": eps, "min_samples": ms,
+                       "max_partitions": P, "input": "fp32 device-resident",
+                       "parallelism": f"replicas{world}" if world > 1 else "single"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "kernel": "count_kernel",
+                         "kernel_ms": t_cnt, "bytes_per_record": per, "records": rec,
+                         "cells": cells, "algorithmic_bytes": alg_bytes},
+            "cpu_baseline": cpu,
+            "stages_ms": stages,
+            "n_clusters": ncl,
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

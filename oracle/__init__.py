@@ -158,19 +158,30 @@ def mean_var_bounds(mean, variance):
     return np.array([mean + (i - 3) * 0.3 * std for i in range(7)])
 
 
-def min_var_moments(V):
-    """R:dbscan/partition.py:86-89: sequential fp64 sum of [1, v, v**2] with
-    v**2 taken in the input precision (numpy squares fp32 vectors in fp32)."""
+def min_var_moments(V, sums="sequential"):
+    """R:dbscan/partition.py:86-89: fp64 sums of [1, v, v**2] with v**2 taken
+    in the input precision (numpy squares fp32 vectors in fp32).
+
+    sums='sequential': the reference's left-to-right fold (single Spark slice)
+    — bit-exact with the shim-run reference.
+    sums='exact': correctly rounded sums (math.fsum), the order-independent
+    value the GPU's double-double reduction produces."""
+    import math
     if len(V) == 0:
         return np.zeros((3, V.shape[1]))
     sq = (V * V).astype(np.float64)
+    V64 = V.astype(np.float64)
     m0 = float(len(V))
-    m1 = np.cumsum(V.astype(np.float64), axis=0)[-1]
-    m2 = np.cumsum(sq, axis=0)[-1]
+    if sums == "exact":
+        m1 = np.array([math.fsum(V64[:, j]) for j in range(V.shape[1])])
+        m2 = np.array([math.fsum(sq[:, j]) for j in range(V.shape[1])])
+    else:
+        m1 = np.cumsum(V64, axis=0)[-1]
+        m2 = np.cumsum(sq, axis=0)[-1]
     return np.stack([np.full(V.shape[1], m0), m1, m2])
 
 
-def kd_partition(X, max_partitions=None, split_method="min_var"):
+def kd_partition(X, max_partitions=None, split_method="min_var", sums="sequential"):
     """KDPartitioner (R:dbscan/partition.py:111-183).
 
     Returns dict(owner=int64[n] KD label per point, box_lo/box_hi (P,k) fp64,
@@ -190,7 +201,7 @@ def kd_partition(X, max_partitions=None, split_method="min_var"):
             idx = np.nonzero(owner == cur)[0]        # key order, as the RDD keeps it
             V = X[idx]
             if split_method == "min_var":
-                mom = min_var_moments(V)
+                mom = min_var_moments(V, sums)
                 with np.errstate(invalid="ignore", divide="ignore"):
                     means = mom[1] / mom[0]
                     var = mom[2] / mom[0] - means ** 2

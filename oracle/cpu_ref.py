@@ -1,0 +1,90 @@
+"""ORACLE — TEST/BENCH INFRASTRUCTURE ONLY: the timed CPU baseline.
+
+The reference's own pipeline restated for a multi-core host, as SURVEY.md
+§8(d) / BASELINE.md prescribe (the Spark path itself cannot run here or on
+the GPU box: no JVM, and the reference never travels):
+
+  1. KD partition, the reference's min_var/mean_var rule   (oracle.kd_partition,
+     R:dbscan/partition.py:33-183)
+  2. 2·eps halo                                            (oracle.halo,
+     R:dbscan/dbscan.py:136-151)
+  3. per-neighbourhood ``sklearn.cluster.DBSCAN(eps, min_samples, metric,
+     algorithm='kd_tree')`` — the reference's arithmetic engine
+     (R:dbscan/dbscan.py:28-29) — one task per neighbourhood in a process
+     pool, as Spark ``local[*]`` runs ``mapPartitions``
+  4. merge: local clusters linked through points core in two neighbourhoods;
+     a point takes its owner neighbourhood's label (R:dbscan/dbscan.py:153-165
+     intent).
+
+Only bench.py's ``cpu_baseline`` leg calls this.
+"""
+from __future__ import annotations
+
+import multiprocessing as mp
+import os
+import time
+
+import numpy as np
+
+from . import halo, kd_partition
+
+
+def _sk_task(args):
+    X, eps, ms, metric = args
+    from sklearn.cluster import DBSCAN
+    db = DBSCAN(eps=eps, min_samples=ms, metric=metric, algorithm="kd_tree", n_jobs=1).fit(X)
+    core = np.zeros(len(X), bool)
+    core[db.core_sample_indices_] = True
+    return db.labels_.astype(np.int64), core
+
+
+def run(X, eps, min_samples, max_partitions, metric="euclidean", workers=None):
+    """Returns (labels, seconds, workers_used)."""
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
+
+    t0 = time.perf_counter()
+    X = np.asarray(X)
+    n = len(X)
+    kd = kd_partition(X, max_partitions)
+    _, _, members = halo(X, kd["box_lo"], kd["box_hi"], eps)
+    P = len(members)
+    workers = workers or min(P, 16, os.cpu_count() or 1)
+    tasks = [(X[m].astype(np.float64), eps, min_samples, metric) for m in members]
+    if workers > 1:
+        with mp.get_context("fork").Pool(workers) as pool:
+            local = pool.map(_sk_task, tasks, chunksize=1)
+    else:
+        local = [_sk_task(t) for t in tasks]
+    # nodes = (neighbourhood, local cluster)
+    base = np.zeros(P + 1, np.int64)
+    for L, (lab, _) in enumerate(local):
+        base[L + 1] = base[L] + (lab.max() + 1 if len(lab) else 0)
+    pts, nodes = [], []
+    for L, (lab, core) in enumerate(local):
+        pts.append(members[L][core])
+        nodes.append(base[L] + lab[core])
+    pts = np.concatenate(pts) if pts else np.zeros(0, np.int64)
+    nodes = np.concatenate(nodes) if nodes else np.zeros(0, np.int64)
+    order = np.argsort(pts, kind="stable")
+    pts, nodes = pts[order], nodes[order]
+    same = pts[1:] == pts[:-1]
+    nn = int(base[-1])
+    g = coo_matrix((np.ones(int(same.sum())), (nodes[:-1][same], nodes[1:][same])), shape=(nn, nn))
+    _, comp = connected_components(g, directed=False)
+    labels = np.full(n, -1, np.int64)
+    owner = kd["owner"]
+    for L, (lab, _) in enumerate(local):
+        mem = members[L]
+        own = (owner[mem] == L) & (lab >= 0)
+        labels[mem[own]] = comp[base[L] + lab[own]]
+    # number components by their smallest member, as sklearn would
+    ok = labels >= 0
+    if ok.any():
+        first = np.full(nn, n, np.int64)
+        np.minimum.at(first, labels[ok], np.nonzero(ok)[0])
+        used = np.unique(labels[ok])
+        rank = np.empty(nn, np.int64)
+        rank[used[np.argsort(first[used])]] = np.arange(len(used))
+        labels[ok] = rank[labels[ok]]
+    return labels, time.perf_counter() - t0, workers

@@ -1,0 +1,100 @@
+"""Ingestion: every input form the reference's ``train`` / ``KDPartitioner``
+would be fed, turned into one device-resident point set.
+
+The reference takes an RDD of ``(key, k-dim vector)`` (R:dbscan/dbscan.py:104-109,
+R:dbscan/partition.py:111-121).  Accepted here:
+  * an RDD-like object (anything with ``collect()``, e.g. a pyspark RDD),
+  * an iterable of ``(key, vector)`` pairs,
+  * a numpy array or torch tensor of shape (n, d) — keys are 0..n-1,
+  * a ``(keys, X)`` tuple,
+  * a ``PointSet`` (passed through).
+float32 inputs stay float32, float64 stay float64 (the predicate is exact for
+either); anything else becomes float64.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+
+class PointSet:
+    """keys (host numpy, or None meaning 0..n-1) + X (CUDA tensor, (n, d))."""
+
+    def __init__(self, X, keys=None):
+        self.X = X
+        self.keys = keys
+
+    @property
+    def n(self):
+        return int(self.X.shape[0])
+
+    @property
+    def d(self):
+        return int(self.X.shape[1])
+
+    def key_array(self):
+        return np.arange(self.n, dtype=np.int64) if self.keys is None else self.keys
+
+    def vectors(self, idx=None):
+        """Host copies of the vectors (API views only, never the hot path)."""
+        X = self.X if idx is None else self.X[idx]
+        return X.cpu().numpy()
+
+
+def _device(device):
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device(device) if not isinstance(device, torch.device) else device
+
+
+def _to_tensor(X, device):
+    if isinstance(X, torch.Tensor):
+        t = X
+    else:
+        a = np.asarray(X)
+        if a.dtype not in (np.float32, np.float64):
+            a = a.astype(np.float64)
+        t = torch.from_numpy(np.ascontiguousarray(a))
+    if t.dtype not in (torch.float32, torch.float64):
+        t = t.to(torch.float64)
+    if t.dim() == 1:
+        t = t.reshape(-1, 1)
+    if t.dim() != 2:
+        raise ValueError(f"expected (n, d) points, got shape {tuple(t.shape)}")
+    return t.to(device).contiguous()
+
+
+def _keys(keys):
+    try:
+        a = np.asarray(keys)
+        if a.dtype.kind in "iu":
+            return a.astype(np.int64)
+    except Exception:
+        pass
+    a = np.empty(len(keys), dtype=object)
+    a[:] = list(keys)
+    return a
+
+
+def as_points(data, device=None):
+    if isinstance(data, PointSet):
+        return data
+    dev = _device(device)
+    if isinstance(data, (torch.Tensor, np.ndarray)):
+        return PointSet(_to_tensor(data, dev))
+    if isinstance(data, tuple) and len(data) == 2 and not np.isscalar(data[0]) \
+            and hasattr(data[0], "__len__") and hasattr(data[1], "__len__") \
+            and len(data[0]) == len(data[1]) and len(data[0]) != 2:
+        keys, X = data
+        return PointSet(_to_tensor(X, dev), _keys(keys))
+    recs = data.collect() if hasattr(data, "collect") else list(data)
+    if not recs:
+        raise ValueError("no points")
+    keys = [k for k, _ in recs]
+    vecs = [np.asarray(v) for _, v in recs]
+    dt = np.result_type(*[v.dtype for v in vecs[:64]])
+    X = np.stack(vecs).astype(dt if dt in (np.float32, np.float64) else np.float64)
+    k = _keys(keys)
+    if k.dtype == np.int64 and np.array_equal(k, np.arange(len(k))):
+        k = None
+    return PointSet(_to_tensor(X, dev), k)

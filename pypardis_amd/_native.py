@@ -1,0 +1,274 @@
+"""ctypes binding of libpardis.so (the C ABI in include/pardis.h).
+
+This is the only way the package computes anything: there is no CPU or
+PyTorch fallback.  If the library is missing or no ROCm GPU is visible the
+calls raise.  ``torch`` is imported first so the process has exactly one HIP
+runtime (torch's libamdhip64.so.7, which libpardis then binds to).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpardis.so")
+
+PD_F32, PD_F64 = 0, 1
+PD_EUCLIDEAN, PD_CITYBLOCK = 0, 1
+PD_OPT_TIMING, PD_OPT_FULL_COUNTS, PD_OPT_SEQUENTIAL_MOMENTS = 1, 2, 3
+TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "border",
+                "label", "total", "records", "cells_n", "grid_cells", "key_bits"]
+
+# every symbol include/pardis.h declares (tests/test_abi.py checks the .so)
+EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
+           "pd_ctx_set_option", "pd_ctx_timings", "pd_bbox", "pd_kd_moments", "pd_kd_counts",
+           "pd_kd_split", "pd_halo_members", "pd_cluster", "pd_train"]
+
+
+class PardisError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libpardis error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+_lock = threading.Lock()
+_tls = threading.local()
+
+
+def load():
+    """Load the in-tree library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -m pypardis_amd.build` "
+                "(hipcc --offload-arch=gfx950).  There is no CPU fallback.")
+        lib = ctypes.CDLL(LIB_PATH)
+        P, I32, I64, D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+        sig = {
+            "pd_abi_version": ([], I32),
+            "pd_last_error": ([], ctypes.c_char_p),
+            "pd_ctx_create": ([I32, ctypes.POINTER(P)], I32),
+            "pd_ctx_destroy": ([P], I32),
+            "pd_ctx_set_option": ([P, I32, I64], I32),
+            "pd_ctx_timings": ([P, P, I32], I32),
+            "pd_bbox": ([P, P, I32, I64, I32, P, P, P], I32),
+            "pd_kd_moments": ([P, P, I32, I64, I32, P, I32, P, P, P], I32),
+            "pd_kd_counts": ([P, P, I32, I64, I32, P, I32, P, P, P, P, P], I32),
+            "pd_kd_split": ([P, P, I32, I64, I32, P, I32, P, P, P, P, P], I32),
+            "pd_halo_members": ([P, P, I32, I64, I32, I32, P, P, P, I64, P], I32),
+            "pd_cluster": ([P, P, I32, I64, I32, D, I32, I32, P, P, P, P, P], I32),
+            "pd_train": ([P, P, I32, I64, I32, D, I32, I32, I32, P, P, P, P, P, P, P, P], I32),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(lib, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = lib
+        return lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise PardisError(rc, load().pd_last_error().decode(errors="replace"))
+
+
+class Context:
+    """One pd_ctx per (host thread, device)."""
+
+    def __init__(self, device):
+        self.device = int(device)
+        self.ptr = ctypes.c_void_p()
+        _check(load().pd_ctx_create(self.device, ctypes.byref(self.ptr)))
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                load().pd_ctx_destroy(self.ptr)
+        except Exception:
+            pass
+
+    def set_option(self, opt, value):
+        _check(load().pd_ctx_set_option(self.ptr, opt, int(value)))
+
+    def timings(self):
+        out = np.zeros(len(TIMING_SLOTS), np.float64)
+        _check(load().pd_ctx_timings(self.ptr, out.ctypes.data, len(out)))
+        return dict(zip(TIMING_SLOTS, out.tolist()))
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("pypardis_amd needs a ROCm GPU (MI355X / gfx950); none is visible. "
+                           "There is no CPU fallback.")
+
+
+def context(device=None):
+    require_gpu()
+    load()
+    dev = torch.cuda.current_device() if device is None else int(device)
+    cache = getattr(_tls, "ctx", None)
+    if cache is None:
+        cache = _tls.ctx = {}
+    if dev not in cache:
+        cache[dev] = Context(dev)
+    return cache[dev]
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _dtype_code(t):
+    if t.dtype == torch.float32:
+        return PD_F32
+    if t.dtype == torch.float64:
+        return PD_F64
+    raise TypeError(f"coordinates must be float32 or float64, got {t.dtype}")
+
+
+def _check_points(X):
+    if not isinstance(X, torch.Tensor) or not X.is_cuda:
+        raise TypeError("X must be a CUDA (ROCm) torch tensor")
+    if X.dim() != 2 or not X.is_contiguous():
+        raise ValueError("X must be a contiguous (n, d) tensor")
+    return _dtype_code(X)
+
+
+def metric_code(metric):
+    if callable(metric):
+        metric = getattr(metric, "__name__", repr(metric))
+    m = str(metric).lower()
+    if m in ("euclidean", "l2", "minkowski"):
+        return PD_EUCLIDEAN
+    if m in ("cityblock", "manhattan", "l1"):
+        return PD_CITYBLOCK
+    raise ValueError(f"metric {metric!r}: only euclidean and cityblock keep the 2*eps box "
+                     "expansion exact (R:dbscan/dbscan.py:88-91)")
+
+
+# ----------------------------------------------------------------- stages
+def bbox(X, ctx=None):
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    d = X.shape[1]
+    out = np.zeros(2 * d, np.float64)
+    bad = np.zeros(1, np.int64)
+    _check(load().pd_bbox(ctx.ptr, X.data_ptr(), dt, X.shape[0], d, out.ctypes.data,
+                          bad.ctypes.data, _stream(X.device)))
+    return out[:d], out[d:], int(bad[0])
+
+
+def kd_moments(X, labels, sel, sequential=False, ctx=None):
+    """sequential=True: the reference's left-to-right fold (bit-identical
+    boundaries, slow); default: correctly rounded double-double sums."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    d = X.shape[1]
+    sel = np.ascontiguousarray(sel, np.int32)
+    out = np.zeros((len(sel), 3, d), np.float64)
+    if sequential:
+        ctx.set_option(PD_OPT_SEQUENTIAL_MOMENTS, 1)
+    try:
+        _check(load().pd_kd_moments(ctx.ptr, X.data_ptr(), dt, X.shape[0], d, labels.data_ptr(),
+                                    len(sel), sel.ctypes.data, out.ctypes.data,
+                                    _stream(X.device)))
+    finally:
+        if sequential:
+            ctx.set_option(PD_OPT_SEQUENTIAL_MOMENTS, 0)
+    return out
+
+
+def kd_counts(X, labels, sel, axis, bounds, ctx=None):
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    sel = np.ascontiguousarray(sel, np.int32)
+    axis = np.ascontiguousarray(axis, np.int32)
+    bounds = np.ascontiguousarray(bounds, np.float64).reshape(len(sel), 7)
+    out = np.zeros((len(sel), 8), np.int64)
+    _check(load().pd_kd_counts(ctx.ptr, X.data_ptr(), dt, X.shape[0], X.shape[1],
+                               labels.data_ptr(), len(sel), sel.ctypes.data, axis.ctypes.data,
+                               bounds.ctypes.data, out.ctypes.data, _stream(X.device)))
+    return out
+
+
+def kd_split(X, labels, sel, axis, boundary, new, ctx=None):
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    sel = np.ascontiguousarray(sel, np.int32)
+    axis = np.ascontiguousarray(axis, np.int32)
+    boundary = np.ascontiguousarray(boundary, np.float64)
+    new = np.ascontiguousarray(new, np.int32)
+    _check(load().pd_kd_split(ctx.ptr, X.data_ptr(), dt, X.shape[0], X.shape[1],
+                              labels.data_ptr(), len(sel), sel.ctypes.data, axis.ctypes.data,
+                              boundary.ctypes.data, new.ctypes.data, _stream(X.device)))
+
+
+def halo_members(X, ebox, ctx=None):
+    """ebox: (P, 2, d) fp64.  Returns (counts[P], members int64 device tensor)."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    ebox = np.ascontiguousarray(ebox, np.float64)
+    P = ebox.shape[0]
+    counts = np.zeros(P, np.int64)
+    lib = load()
+    _check(lib.pd_halo_members(ctx.ptr, X.data_ptr(), dt, X.shape[0], X.shape[1], P,
+                               ebox.ctypes.data, counts.ctypes.data, None, 0, _stream(X.device)))
+    total = int(counts.sum())
+    members = torch.empty(max(total, 1), dtype=torch.int64, device=X.device)
+    _check(lib.pd_halo_members(ctx.ptr, X.data_ptr(), dt, X.shape[0], X.shape[1], P,
+                               ebox.ctypes.data, counts.ctypes.data, members.data_ptr(), total,
+                               _stream(X.device)))
+    return counts, members[:total]
+
+
+def cluster(X, eps, min_samples, metric=PD_EUCLIDEAN, want_counts=False, ctx=None):
+    """sklearn fit_predict semantics on one point set (device tensors out)."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n = X.shape[0]
+    labels = torch.empty(n, dtype=torch.int32, device=X.device)
+    core = torch.empty(n, dtype=torch.uint8, device=X.device)
+    counts = torch.empty(n, dtype=torch.int32, device=X.device) if want_counts else None
+    ncl = np.zeros(1, np.int64)
+    _check(load().pd_cluster(ctx.ptr, X.data_ptr(), dt, n, X.shape[1], float(eps),
+                             int(min_samples), int(metric), labels.data_ptr(), core.data_ptr(),
+                             counts.data_ptr() if counts is not None else None,
+                             ncl.ctypes.data, _stream(X.device)))
+    return labels, core, counts, int(ncl[0])
+
+
+def train(X, eps, min_samples, metric, ebox, owner=None, data_box=None, want_counts=False,
+          out=None, ctx=None):
+    """The fused per-device pipeline (pd_train).  ebox: (P, 2, d) fp64."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    ebox = np.ascontiguousarray(ebox, np.float64)
+    P = ebox.shape[0]
+    if out is None:
+        labels = torch.empty(n, dtype=torch.int32, device=X.device)
+        core = torch.empty(n, dtype=torch.uint8, device=X.device)
+    else:
+        labels, core = out
+    counts = torch.empty(n, dtype=torch.int32, device=X.device) if want_counts else None
+    dbox = None
+    if data_box is not None:
+        dbox = np.ascontiguousarray(data_box, np.float64).reshape(2 * d)
+    ncl = np.zeros(1, np.int64)
+    _check(load().pd_train(ctx.ptr, X.data_ptr(), dt, n, d, float(eps), int(min_samples),
+                           int(metric), P, ebox.ctypes.data,
+                           dbox.ctypes.data if dbox is not None else None,
+                           owner.data_ptr() if owner is not None else None, labels.data_ptr(),
+                           core.data_ptr(), counts.data_ptr() if counts is not None else None,
+                           ncl.ctypes.data, _stream(X.device)))
+    return labels, core, counts, int(ncl[0])

@@ -1,0 +1,266 @@
+// C ABI (include/pardis.h): argument checks, error translation, contexts.
+#include "../../include/pardis.h"
+
+#include <cstring>
+#include <string>
+
+#include "internal.hpp"
+
+struct pd_ctx {
+    pd::Ctx c;
+};
+
+namespace pd {
+
+static thread_local std::string g_err;
+void* pinned(Ctx& ctx, size_t bytes) {
+    // One grow-only pinned block per context.  Callers never keep two views
+    // alive across a stream synchronisation (see kd.hip / engine.hip); a grow
+    // first drains the device so no async copy still reads the old block.
+    struct Hdr {
+        size_t bytes;
+    };
+    Hdr* h = (Hdr*)ctx.pinned;
+    if (!h || h->bytes < bytes) {
+        if (h) {
+            PD_HIP(hipDeviceSynchronize());
+            PD_HIP(hipHostFree(h));
+            ctx.pinned = nullptr;
+        }
+        size_t want = std::max<size_t>(bytes + 64, 1 << 20);
+        void* p = nullptr;
+        PD_HIP(hipHostMalloc(&p, want + 64, hipHostMallocDefault));
+        ctx.pinned = p;
+        h = (Hdr*)p;
+        h->bytes = want;
+    }
+    return (char*)h + 64;
+}
+
+void sync(hipStream_t s) { PD_HIP(hipStreamSynchronize(s)); }
+
+template <typename F>
+static int32_t guard(pd_ctx* ctx, F&& f) {
+    try {
+        if (ctx) PD_HIP(hipSetDevice(ctx->c.device));
+        f();
+        return PD_OK;
+    } catch (const Error& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return PD_EINVAL;
+    } catch (...) {
+        g_err = "unknown error";
+        return PD_EINVAL;
+    }
+}
+
+static void check_common(pd_ctx* ctx, const void* X, int64_t n, int32_t d) {
+    if (!ctx) throw Error(PD_EINVAL, "null context");
+    if (n < 0) throw Error(PD_EINVAL, "n < 0");
+    if (d < 1) throw Error(PD_EINVAL, "d < 1");
+    if (n > 0 && !X) throw Error(PD_EINVAL, "null X");
+}
+
+}  // namespace pd
+
+using namespace pd;
+
+extern "C" {
+
+int32_t pd_abi_version(void) { return PD_ABI_VERSION; }
+
+const char* pd_last_error(void) { return g_err.c_str(); }
+
+int32_t pd_ctx_create(int32_t device, pd_ctx** out) {
+    return guard(nullptr, [&] {
+        if (!out) throw Error(PD_EINVAL, "null out");
+        int ndev = 0;
+        PD_HIP(hipGetDeviceCount(&ndev));
+        if (device < 0 || device >= ndev)
+            throw Error(PD_EINVAL, "device " + std::to_string(device) + " not present (" +
+                                       std::to_string(ndev) + " visible)");
+        PD_HIP(hipSetDevice(device));
+        pd_ctx* c = new pd_ctx();
+        c->c.device = device;
+        *out = c;
+    });
+}
+
+int32_t pd_ctx_destroy(pd_ctx* ctx) {
+    if (!ctx) return PD_OK;
+    int32_t rc = guard(ctx, [&] {
+        ctx->c.arena.release();
+        if (ctx->c.pinned) (void)hipHostFree(ctx->c.pinned);
+        for (auto& e : ctx->c.ev)
+            if (e) (void)hipEventDestroy(e);
+    });
+    delete ctx;
+    return rc;
+}
+
+int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
+    return guard(ctx, [&] {
+        if (!ctx) throw Error(PD_EINVAL, "null context");
+        if (option == PD_OPT_TIMING)
+            ctx->c.timing = value != 0;
+        else if (option == PD_OPT_FULL_COUNTS)
+            ctx->c.full_counts = value != 0;
+        else if (option == PD_OPT_SEQUENTIAL_MOMENTS)
+            ctx->c.seq_moments = value != 0;
+        else
+            throw Error(PD_EINVAL, "unknown option");
+    });
+}
+
+int32_t pd_ctx_timings(pd_ctx* ctx, double* out, int32_t n) {
+    return guard(ctx, [&] {
+        if (!ctx || !out) throw Error(PD_EINVAL, "null argument");
+        const Timings& t = ctx->c.t;
+        const double v[PD_T_NSLOTS] = {t.halo,    t.sort,   t.gather, t.cells,
+                                       t.count,   t.link,   t.merge,  t.border,
+                                       t.label,   t.total,  (double)t.records,
+                                       (double)t.cells_n, (double)t.grid_cells,
+                                       (double)t.key_bits};
+        for (int i = 0; i < n && i < PD_T_NSLOTS; ++i) out[i] = v[i];
+    });
+}
+
+int32_t pd_bbox(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, double* lohi,
+                int64_t* bad, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (!lohi) throw Error(PD_EINVAL, "null lohi");
+        if (n == 0) throw Error(PD_EINVAL, "bbox of an empty set");
+        bbox(ctx->c, X, dtype, n, d, lohi, bad, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_kd_moments(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                      const int32_t* labels, int32_t n_sel, const int32_t* sel, double* out,
+                      void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (n_sel < 0 || (n_sel && (!sel || !out)) || (n && !labels))
+            throw Error(PD_EINVAL, "bad selection");
+        if (n == 0) {
+            std::memset(out, 0, sizeof(double) * 3 * d * n_sel);
+            return;
+        }
+        kd_moments(ctx->c, X, dtype, n, d, labels, n_sel, sel, out, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_kd_counts(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                     const int32_t* labels, int32_t n_sel, const int32_t* sel,
+                     const int32_t* axis, const double* bounds, int64_t* out, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (n_sel < 0 || (n_sel && (!sel || !axis || !bounds || !out)) || (n && !labels))
+            throw Error(PD_EINVAL, "bad selection");
+        for (int s = 0; s < n_sel; ++s)
+            if (axis[s] < 0 || axis[s] >= d || sel[s] < 0) throw Error(PD_EINVAL, "bad axis/label");
+        if (n == 0) {
+            std::memset(out, 0, sizeof(int64_t) * 8 * n_sel);
+            return;
+        }
+        kd_counts(ctx->c, X, dtype, n, d, labels, n_sel, sel, axis, bounds, out,
+                  (hipStream_t)stream);
+    });
+}
+
+int32_t pd_kd_split(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                    int32_t* labels, int32_t n_sel, const int32_t* sel, const int32_t* axis,
+                    const double* boundary, const int32_t* newlab, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (n_sel < 0 || (n_sel && (!sel || !axis || !boundary || !newlab)) || (n && !labels))
+            throw Error(PD_EINVAL, "bad selection");
+        for (int s = 0; s < n_sel; ++s)
+            if (axis[s] < 0 || axis[s] >= d || sel[s] < 0) throw Error(PD_EINVAL, "bad axis/label");
+        if (n == 0) return;
+        kd_split(ctx->c, X, dtype, n, d, labels, n_sel, sel, axis, boundary, newlab,
+                 (hipStream_t)stream);
+    });
+}
+
+int32_t pd_halo_members(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                        int32_t P, const double* ebox, int64_t* counts, int64_t* members,
+                        int64_t capacity, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (P < 1 || !ebox || !counts) throw Error(PD_EINVAL, "bad boxes");
+        if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "d > 4");
+        if (n == 0) {
+            std::memset(counts, 0, sizeof(int64_t) * P);
+            return;
+        }
+        halo_members(ctx->c, X, dtype, n, d, P, ebox, counts, members, capacity,
+                     (hipStream_t)stream);
+    });
+}
+
+int32_t pd_train(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, double eps,
+                 int32_t min_samples, int32_t metric, int32_t P, const double* ebox,
+                 const double* data_box, const int32_t* owner, int32_t* labels, uint8_t* core,
+                 uint32_t* counts, int64_t* n_clusters, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (!ebox) throw Error(PD_EINVAL, "null ebox");
+        if (P > 1 && n > 0 && !owner) throw Error(PD_EINVAL, "owner labels required for P > 1");
+        TrainArgs a;
+        a.X = X;
+        a.dtype = dtype;
+        a.n = n;
+        a.d = d;
+        a.eps = eps;
+        a.min_samples = min_samples;
+        a.metric = metric;
+        a.P = P;
+        a.ebox = ebox;
+        a.data_box = data_box;
+        a.owner = owner;
+        a.labels = labels;
+        a.core = core;
+        a.counts = counts;
+        a.stream = (hipStream_t)stream;
+        train(ctx->c, a);
+        if (n_clusters) *n_clusters = a.n_clusters;
+    });
+}
+
+int32_t pd_cluster(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, double eps,
+                   int32_t min_samples, int32_t metric, int32_t* labels, uint8_t* core,
+                   uint32_t* counts, int64_t* n_clusters, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        TrainArgs a;
+        a.X = X;
+        a.dtype = dtype;
+        a.n = n;
+        a.d = d;
+        a.eps = eps;
+        a.min_samples = min_samples;
+        a.metric = metric;
+        a.P = 1;
+        a.labels = labels;
+        a.core = core;
+        a.counts = counts;
+        a.stream = (hipStream_t)stream;
+        double box[2 * kMaxDim] = {0};
+        if (n > 0) {
+            if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "d > 4: the dense-tile path is not built yet");
+            int64_t bad = 0;
+            bbox(ctx->c, X, dtype, n, d, box, &bad, a.stream);
+            if (bad) throw Error(PD_EINVAL, "input contains NaN or infinity");
+        }
+        a.ebox = box;
+        a.data_box = box;
+        train(ctx->c, a);
+        if (n_clusters) *n_clusters = a.n_clusters;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,63 @@
+// Shared device/host helpers for libpardis (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace pd {
+
+// Launch geometry: 256-thread blocks (4 waves), grid-stride beyond this.
+constexpr int kBlock = 256;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kOwnerBit = 0x80000000u;   // record value: point id | owner flag
+constexpr int kMaxDim = 4;                    // grid path; d > 4 is the tile path
+constexpr int kMaxParts = 64;                 // one bit per neighbourhood in the halo mask
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define PD_HIP(expr)                                                                 \
+    do {                                                                             \
+        hipError_t _e = (expr);                                                      \
+        if (_e != hipSuccess)                                                        \
+            throw ::pd::Error(-3, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+inline unsigned grid_for(int64_t n, int64_t cap = 256 * 64) {
+    int64_t b = (n + kBlock - 1) / kBlock;
+    if (b < 1) b = 1;
+    if (b > cap) b = cap;
+    return (unsigned)b;
+}
+
+// Per-neighbourhood grid: cell side = eps * (1 + 2^-20) so that any pair the
+// fp64 predicate can accept lies in adjacent cells; origin and extent clipped
+// to the data's tight bbox (the reference's root box can reach to ±0 through
+// the float_info.min sentinel, R:dbscan/geometry.py:28-29).
+struct PartGrid {
+    double lo[kMaxDim];     // origin (fp64)
+    double inv;             // 1 / cell side
+    int64_t nc[kMaxDim];    // cells per axis (0 => empty neighbourhood)
+    uint64_t base;          // first key of this neighbourhood
+    double elo[kMaxDim];    // expanded box (halo membership test), inclusive
+    double ehi[kMaxDim];
+};
+
+// XCD-aware block remap (cdna_hip_programming.md T1, bijective form): blocks
+// b and b+8 share an XCD, so give each XCD a contiguous run of block ids —
+// neighbouring records (which read the same cells) then share one L2.
+__device__ __forceinline__ unsigned xcd_block(unsigned bid, unsigned nblk) {
+    const unsigned q = nblk / 8, r = nblk % 8, x = bid % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+template <typename T> struct Vec;
+template <> struct Vec<float> { using type = float; };
+template <> struct Vec<double> { using type = double; };
+
+}  // namespace pd

@@ -1,0 +1,770 @@
+// The per-neighbourhood DBSCAN engine, batched over every KD neighbourhood
+// held by this device, plus the cross-neighbourhood label merge.
+//
+// Replaces, in one device-resident pipeline:
+//   DBSCAN._create_neighborhoods   (halo records)        R:dbscan/dbscan.py:136-151
+//   partitionBy(P) shuffle         (sort by key)         R:dbscan/dbscan.py:116-118
+//   dbscan_partition -> sklearn    (count/core/union)    R:dbscan/dbscan.py:12-34
+//   _remap_cluster_ids + ClusterAggregator (merge)       R:dbscan/dbscan.py:153-165,
+//                                                        R:dbscan/aggregator.py:9-73
+//
+// Data layout in HBM (R = halo records = sum of neighbourhood sizes):
+//   keys  K[R]   neighbourhood base + row-major eps-cell index (axis 0 fastest)
+//   vals  u32[R] point id | owner bit (record is the point's own KD partition)
+//   Xs    T[R*d] coordinates gathered into key order (AoS, input precision)
+//   dir   u64[W] occupancy bit per cell + u32[W] prefix ranks (W = G/64):
+//         rank_lt(k) = number of occupied cells with key < k, O(1)
+//   cstart u32[ncells+1] first record of each occupied cell
+//   core  u8[R], parent u32[R] (union-find, root = min record in component)
+//
+// Exactness: the neighbour predicate is sklearn's kd_tree leaf test
+// (SK:neighbors/_binary_tree.pxi.tp:1951-1955, SK:metrics/_dist_metrics.pxd.tp:
+// 39-49): fp64, per-axis difference, squared and summed in axis order with
+// every product and sum rounded separately (__dmul_rn/__dadd_rn: no FMA), then
+// `<= eps*eps`.  Inputs (fp32 or fp64) are widened exactly.  No fp32 shortcut
+// band is needed: the fp64 VALU rate is not the bound here.
+//
+// Labels: components of the core graph get the id of their smallest core
+// point (global index); a border point takes the smallest id among its core
+// neighbours; ids are ranked.  That is precisely sklearn's dbscan_inner order
+// (SK:cluster/_dbscan_inner.pyx:19-41), so fit_predict labels come out equal,
+// not merely equal up to permutation.
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace pd {
+namespace {
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint32_t ld_rlx(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rlx(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Union-find with the invariant parent[x] <= x; links always hook the larger
+// root under the smaller, so a component's root is its minimum record and
+// every stale (older) parent value is still an ancestor — plain path halving
+// is safe without locks (ECL-CC style).
+__device__ __forceinline__ uint32_t uf_find(uint32_t* par, uint32_t x) {
+    uint32_t p = ld_rlx(par + x);
+    while (p != x) {
+        uint32_t g = ld_rlx(par + p);
+        if (g == p) return p;
+        st_rlx(par + x, g);
+        x = g;
+        p = ld_rlx(par + x);
+    }
+    return x;
+}
+
+__device__ __forceinline__ void uf_unite(uint32_t* par, uint32_t a, uint32_t b) {
+    a = uf_find(par, a);
+    b = uf_find(par, b);
+    while (a != b) {
+        if (a > b) {
+            uint32_t t = a;
+            a = b;
+            b = t;
+        }
+        uint32_t expected = b;
+        if (__hip_atomic_compare_exchange_strong(par + b, &expected, a, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return;
+        b = uf_find(par, expected);
+        a = uf_find(par, a);
+    }
+}
+
+template <typename T, int D>
+__device__ __forceinline__ void load_d(const T* __restrict__ X, uint64_t i, double (&v)[D]) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) v[j] = (double)X[i * D + j];
+}
+
+// sklearn kd_tree leaf predicate, exact.
+template <typename T, int D, int M>
+__device__ __forceinline__ bool within(const double (&a)[D], const T* __restrict__ b,
+                                       double eps, double eps2) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const double t = __dadd_rn(a[j], -(double)b[j]);
+        if constexpr (M == 0)
+            acc = __dadd_rn(acc, __dmul_rn(t, t));
+        else
+            acc = __dadd_rn(acc, fabs(t));
+    }
+    return M == 0 ? (acc <= eps2) : (acc <= eps);
+}
+
+template <int D>
+__device__ __forceinline__ void cell_of(const double (&v)[D], const PartGrid& g, int64_t (&c)[D]) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        int64_t q = (int64_t)floor((v[j] - g.lo[j]) * g.inv);
+        q = q < 0 ? 0 : q;
+        q = q >= g.nc[j] ? g.nc[j] - 1 : q;
+        c[j] = q;
+    }
+}
+
+template <int D>
+__device__ __forceinline__ uint64_t lin_of(const int64_t (&c)[D], const PartGrid& g) {
+    uint64_t k = 0;
+#pragma unroll
+    for (int j = D - 1; j >= 0; --j) k = k * (uint64_t)g.nc[j] + (uint64_t)c[j];
+    return k;
+}
+
+template <int D>
+__device__ __forceinline__ bool in_box(const double (&v)[D], const PartGrid& g) {
+    bool in = g.nc[0] > 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) in &= (g.elo[j] <= v[j]) & (g.ehi[j] >= v[j]);
+    return in;
+}
+
+__device__ __forceinline__ uint32_t rank_lt(const uint64_t* __restrict__ bits,
+                                            const uint32_t* __restrict__ rank, uint64_t k) {
+    const uint64_t w = k >> 6;
+    const uint32_t b = (uint32_t)(k & 63);
+    const uint64_t m = b ? (bits[w] & ((~0ull) >> (64 - b))) : 0ull;
+    return rank[w] + (uint32_t)__popcll(m);
+}
+
+// Partition of a record: part_start is sorted, P <= kMaxParts*4.
+__device__ __forceinline__ int part_of(const uint32_t* __restrict__ ps, int P, uint32_t r) {
+    int lo = 0, hi = P - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (ps[mid] <= r)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ uint32_t rec_index() {
+    return xcd_block(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+}
+
+// Shared view of the cell structure for the neighbour sweeps.
+struct Cells {
+    const PartGrid* parts;
+    const uint32_t* part_start;
+    int P;
+    const uint64_t* bits;
+    const uint32_t* rank;
+    const uint32_t* cstart;
+};
+
+// Visit every candidate record j of the 3^(D-1) rows around record r's cell;
+// each row is one contiguous record range covering cells c0-1..c0+1.
+template <typename T, int D, typename F>
+__device__ __forceinline__ void for_rows(const Cells& C, const double (&a)[D], int L, F&& row) {
+    const PartGrid& g = C.parts[L];
+    int64_t c[D];
+    cell_of<D>(a, g, c);
+    const int64_t x0 = c[0] > 0 ? c[0] - 1 : 0;
+    const int64_t x1 = c[0] + 1 < g.nc[0] ? c[0] + 1 : g.nc[0] - 1;
+    constexpr int NR = (D == 1) ? 1 : (D == 2 ? 3 : (D == 3 ? 9 : 27));
+    for (int q = 0; q < NR; ++q) {
+        int64_t cc[D];
+        cc[0] = x0;
+        int t = q;
+        bool ok = true;
+#pragma unroll
+        for (int j = 1; j < D; ++j) {
+            const int64_t v = c[j] + (t % 3) - 1;
+            t /= 3;
+            ok &= (v >= 0) & (v < g.nc[j]);
+            cc[j] = v;
+        }
+        if (!ok) continue;
+        const uint64_t k0 = g.base + lin_of<D>(cc, g);
+        const uint64_t k1 = k0 + (uint64_t)(x1 - x0) + 1;
+        const uint32_t s = C.cstart[rank_lt(C.bits, C.rank, k0)];
+        const uint32_t e = C.cstart[rank_lt(C.bits, C.rank, k1)];
+        if (!row(s, e)) return;
+    }
+}
+
+// ------------------------------------------------------------------ kernels
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void halo_count_kernel(const T* __restrict__ X, uint64_t n,
+                                                            const PartGrid* __restrict__ parts,
+                                                            int P, uint32_t* __restrict__ cnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    double v[D];
+    load_d<T, D>(X, i, v);
+    uint32_t c = 0;
+    for (int L = 0; L < P; ++L) c += in_box<D>(v, parts[L]) ? 1u : 0u;
+    cnt[i] = c;
+}
+
+template <typename T, int D, typename K>
+__global__ __launch_bounds__(kBlock) void records_kernel(
+    const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
+    const int32_t* __restrict__ owner, const uint64_t* __restrict__ off, K* __restrict__ keys,
+    uint32_t* __restrict__ vals) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    double v[D];
+    load_d<T, D>(X, i, v);
+    const int own = owner ? owner[i] : 0;
+    uint64_t o = off[i];
+    for (int L = 0; L < P; ++L) {
+        const PartGrid& g = parts[L];
+        if (!in_box<D>(v, g)) continue;
+        int64_t c[D];
+        cell_of<D>(v, g, c);
+        keys[o] = (K)(g.base + lin_of<D>(c, g));
+        vals[o] = (uint32_t)i | (L == own ? kOwnerBit : 0u);
+        ++o;
+    }
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void gather_kernel(const T* __restrict__ X, uint64_t R,
+                                                        const uint32_t* __restrict__ vals,
+                                                        T* __restrict__ Xs) {
+    const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= R) return;
+    const uint64_t i = vals[r] & ~kOwnerBit;
+#pragma unroll
+    for (int j = 0; j < D; ++j) Xs[r * D + j] = X[i * D + j];
+}
+
+template <typename K>
+__global__ void part_start_kernel(const K* __restrict__ keys, uint64_t R,
+                                  const PartGrid* __restrict__ parts, int P,
+                                  uint32_t* __restrict__ ps) {
+    const int L = blockIdx.x * blockDim.x + threadIdx.x;
+    if (L > P) return;
+    if (L == P) {
+        ps[P] = (uint32_t)R;
+        return;
+    }
+    const uint64_t b = parts[L].base;
+    uint64_t lo = 0, hi = R;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        if ((uint64_t)keys[mid] < b)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    ps[L] = (uint32_t)lo;
+}
+
+template <typename K>
+__global__ __launch_bounds__(kBlock) void run_flag_kernel(const K* __restrict__ keys, uint64_t R,
+                                                          uint32_t* __restrict__ flag,
+                                                          unsigned long long* __restrict__ bits) {
+    const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= R) return;
+    const uint64_t k = keys[r];
+    const bool start = (r == 0) || ((uint64_t)keys[r - 1] != k);
+    flag[r] = start ? 1u : 0u;
+    if (start) atomicOr(bits + (k >> 6), 1ull << (k & 63));
+}
+
+__global__ __launch_bounds__(kBlock) void cell_start_kernel(const uint32_t* __restrict__ flag,
+                                                            const uint32_t* __restrict__ cid,
+                                                            uint64_t R,
+                                                            uint32_t* __restrict__ cstart,
+                                                            uint32_t* __restrict__ ncells) {
+    const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (r >= R) return;
+    if (flag[r]) cstart[cid[r]] = (uint32_t)r;
+    if (r == R - 1) {
+        const uint32_t nc = cid[r] + flag[r];
+        cstart[nc] = (uint32_t)R;
+        *ncells = nc;
+    }
+}
+
+struct Popc {
+    __device__ uint32_t operator()(unsigned long long x) const { return (uint32_t)__popcll(x); }
+};
+
+// Neighbour count + core flag: the roofline kernel (SURVEY.md §8(d) B_nc).
+template <typename T, int D, int M>
+__global__ __launch_bounds__(kBlock) void count_kernel(const T* __restrict__ Xs, uint32_t R,
+                                                       Cells C, double eps, double eps2,
+                                                       uint32_t ms, int full,
+                                                       uint8_t* __restrict__ core,
+                                                       uint32_t* __restrict__ cnt_out) {
+    const uint32_t r = rec_index();
+    if (r >= R) return;
+    double a[D];
+    load_d<T, D>(Xs, r, a);
+    const int L = part_of(C.part_start, C.P, r);
+    uint32_t cnt = 0;
+    const uint32_t stop = full ? 0xFFFFFFFFu : ms;
+    for_rows<T, D>(C, a, L, [&](uint32_t s, uint32_t e) {
+        for (uint32_t j = s; j < e; ++j) {
+            cnt += within<T, D, M>(a, Xs + (uint64_t)j * D, eps, eps2) ? 1u : 0u;
+            if (cnt >= stop) return false;
+        }
+        return true;
+    });
+    core[r] = cnt >= ms ? 1 : 0;
+    if (cnt_out) cnt_out[r] = cnt;
+}
+
+// Core-core edges (j > r only; the predicate is symmetric) → union-find.
+template <typename T, int D, int M>
+__global__ __launch_bounds__(kBlock) void link_kernel(const T* __restrict__ Xs, uint32_t R, Cells C,
+                                                      double eps, double eps2,
+                                                      const uint8_t* __restrict__ core,
+                                                      uint32_t* __restrict__ par) {
+    const uint32_t r = rec_index();
+    if (r >= R || !core[r]) return;
+    double a[D];
+    load_d<T, D>(Xs, r, a);
+    const int L = part_of(C.part_start, C.P, r);
+    for_rows<T, D>(C, a, L, [&](uint32_t s, uint32_t e) {
+        for (uint32_t j = (s > r + 1 ? s : r + 1); j < e; ++j) {
+            if (!core[j]) continue;
+            if (!within<T, D, M>(a, Xs + (uint64_t)j * D, eps, eps2)) continue;
+            uf_unite(par, r, j);
+        }
+        return true;
+    });
+}
+
+__global__ __launch_bounds__(kBlock) void iota_kernel(uint32_t* __restrict__ p, uint32_t R) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r < R) p[r] = r;
+}
+
+// A point's copies in several neighbourhoods: link every core copy to one
+// representative (the smallest record), gluing the neighbourhoods' clusters.
+__global__ __launch_bounds__(kBlock) void rep_kernel(const uint32_t* __restrict__ vals, uint32_t R,
+                                                     const uint8_t* __restrict__ core,
+                                                     uint32_t* __restrict__ rep) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= R || !core[r]) return;
+    atomicMin(rep + (vals[r] & ~kOwnerBit), r);
+}
+
+__global__ __launch_bounds__(kBlock) void merge_kernel(const uint32_t* __restrict__ vals,
+                                                       uint32_t R,
+                                                       const uint8_t* __restrict__ core,
+                                                       const uint32_t* __restrict__ rep,
+                                                       uint32_t* __restrict__ par) {
+    const uint32_t r = rec_index();
+    if (r >= R || !core[r]) return;
+    const uint32_t q = rep[vals[r] & ~kOwnerBit];
+    if (q != r) uf_unite(par, r, q);
+}
+
+__global__ __launch_bounds__(kBlock) void flatten_kernel(uint32_t R,
+                                                         const uint8_t* __restrict__ core,
+                                                         uint32_t* __restrict__ par) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= R || !core[r]) return;
+    uint32_t x = par[r];
+    while (true) {
+        const uint32_t p = par[x];
+        if (p == x) break;
+        x = p;
+    }
+    par[r] = x;
+}
+
+__global__ __launch_bounds__(kBlock) void gmin_kernel(const uint32_t* __restrict__ vals,
+                                                      uint32_t R,
+                                                      const uint8_t* __restrict__ core,
+                                                      const uint32_t* __restrict__ par,
+                                                      uint32_t* __restrict__ gmin) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= R || !core[r]) return;
+    atomicMin(gmin + par[r], vals[r] & ~kOwnerBit);
+}
+
+// Owner records only: cluster key of the point (core: its component's
+// smallest core point; border: smallest such key among core neighbours).
+template <typename T, int D, int M>
+__global__ __launch_bounds__(kBlock) void border_kernel(
+    const T* __restrict__ Xs, uint32_t R, Cells C, double eps, double eps2,
+    const uint32_t* __restrict__ vals, const uint8_t* __restrict__ core,
+    const uint32_t* __restrict__ par, const uint32_t* __restrict__ gmin,
+    const uint32_t* __restrict__ cnt_rec, uint32_t* __restrict__ key_out,
+    uint8_t* __restrict__ core_out, uint32_t* __restrict__ cnt_out) {
+    const uint32_t r = rec_index();
+    if (r >= R) return;
+    const uint32_t v = vals[r];
+    if (!(v & kOwnerBit)) return;
+    const uint32_t pt = v & ~kOwnerBit;
+    if (core_out) core_out[pt] = core[r];
+    if (cnt_out) cnt_out[pt] = cnt_rec[r];
+    if (core[r]) {
+        key_out[pt] = gmin[par[r]];
+        return;
+    }
+    double a[D];
+    load_d<T, D>(Xs, r, a);
+    const int L = part_of(C.part_start, C.P, r);
+    uint32_t best = kNone;
+    for_rows<T, D>(C, a, L, [&](uint32_t s, uint32_t e) {
+        for (uint32_t j = s; j < e; ++j) {
+            if (!core[j]) continue;
+            if (!within<T, D, M>(a, Xs + (uint64_t)j * D, eps, eps2)) continue;
+            const uint32_t k = gmin[par[j]];
+            best = k < best ? k : best;
+        }
+        return true;
+    });
+    key_out[pt] = best;
+}
+
+__global__ __launch_bounds__(kBlock) void root_flag_kernel(const uint32_t* __restrict__ key,
+                                                           uint64_t n,
+                                                           uint32_t* __restrict__ flag) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) flag[i] = key[i] == (uint32_t)i ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void label_kernel(const uint32_t* __restrict__ key,
+                                                       const uint32_t* __restrict__ rnk,
+                                                       const uint32_t* __restrict__ flag,
+                                                       uint64_t n, int32_t* __restrict__ labels,
+                                                       int64_t* __restrict__ ncl) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = key[i];
+    labels[i] = k == kNone ? -1 : (int32_t)rnk[k];
+    if (i == n - 1) *ncl = (int64_t)rnk[i] + flag[i];
+}
+
+__global__ void total_kernel(const uint64_t* __restrict__ off, const uint32_t* __restrict__ cnt,
+                             uint64_t n, uint64_t* __restrict__ tot) {
+    *tot = n ? off[n - 1] + cnt[n - 1] : 0;
+}
+
+// ------------------------------------------------------------------ driver
+struct EvTimer {
+    Ctx& ctx;
+    hipStream_t s;
+    int k = 0;
+    explicit EvTimer(Ctx& c, hipStream_t st) : ctx(c), s(st) {}
+    void mark() {
+        if (!ctx.timing) return;
+        if (!ctx.ev[k]) PD_HIP(hipEventCreate(&ctx.ev[k]));
+        PD_HIP(hipEventRecord(ctx.ev[k], s));
+        ++k;
+    }
+    float span(int a, int b) {
+        if (!ctx.timing || b >= k) return 0;
+        float ms = 0;
+        PD_HIP(hipEventElapsedTime(&ms, ctx.ev[a], ctx.ev[b]));
+        return ms;
+    }
+};
+
+inline unsigned blocks(uint64_t n) { return n ? (unsigned)((n + kBlock - 1) / kBlock) : 1u; }
+
+template <typename T, int D, typename K, int M>
+void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t Gtot,
+         int key_bits) {
+    hipStream_t s = a.stream;
+    const uint64_t n = (uint64_t)a.n;
+    const int P = a.P;
+    EvTimer tm(ctx, s);
+    tm.mark();   // 0
+
+    PartGrid* parts = ctx.arena.get<PartGrid>("parts", P);
+    {
+        PartGrid* h = (PartGrid*)pinned(ctx, sizeof(PartGrid) * P);
+        std::memcpy(h, hparts.data(), sizeof(PartGrid) * P);
+        PD_HIP(hipMemcpyAsync(parts, h, sizeof(PartGrid) * P, hipMemcpyHostToDevice, s));
+    }
+    const T* X = (const T*)a.X;
+
+    // ---- halo records (R:dbscan/dbscan.py:136-151)
+    uint32_t* hcnt = ctx.arena.get<uint32_t>("hcnt", n);
+    uint64_t* hoff = ctx.arena.get<uint64_t>("hoff", n);
+    uint64_t* dtot = ctx.arena.get<uint64_t>("tot", 4);
+    hipLaunchKernelGGL((halo_count_kernel<T, D>), dim3(blocks(n)), dim3(kBlock), 0, s, X, n, parts,
+                       P, hcnt);
+    {
+        size_t tb = 0;
+        PD_HIP(rocprim::exclusive_scan(nullptr, tb, hcnt, hoff, (uint64_t)0, (size_t)n,
+                                       rocprim::plus<uint64_t>(), s));
+        void* tmp = ctx.arena.get<char>("scan_tmp", tb);
+        PD_HIP(rocprim::exclusive_scan(tmp, tb, hcnt, hoff, (uint64_t)0, (size_t)n,
+                                       rocprim::plus<uint64_t>(), s));
+    }
+    hipLaunchKernelGGL(total_kernel, dim3(1), dim3(1), 0, s, hoff, hcnt, n, dtot);
+    uint64_t* htot = (uint64_t*)pinned(ctx, sizeof(uint64_t));
+    PD_HIP(hipMemcpyAsync(htot, dtot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    sync(s);
+    const uint64_t R64 = *htot;
+    if (R64 >= 0xFFFFFFFEull) throw Error(-5, "more than 2^32-2 halo records on one device");
+    const uint32_t R = (uint32_t)R64;
+    ctx.t.records = R;
+
+    K* keys = ctx.arena.get<K>("keys", R);
+    K* keys2 = ctx.arena.get<K>("keys2", R);
+    uint32_t* vals = ctx.arena.get<uint32_t>("vals", R);
+    uint32_t* vals2 = ctx.arena.get<uint32_t>("vals2", R);
+    hipLaunchKernelGGL((records_kernel<T, D, K>), dim3(blocks(n)), dim3(kBlock), 0, s, X, n, parts,
+                       P, a.owner, hoff, keys, vals);
+    PD_HIP(hipGetLastError());
+    tm.mark();   // 1
+
+    // ---- shuffle by neighbourhood == sort by (neighbourhood, cell) key
+    {
+        rocprim::double_buffer<K> kb(keys, keys2);
+        rocprim::double_buffer<uint32_t> vb(vals, vals2);
+        size_t tb = 0;
+        PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
+        void* tmp = ctx.arena.get<char>("sort_tmp", tb);
+        PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
+        keys = kb.current();
+        vals = vb.current();
+    }
+    tm.mark();   // 2
+    T* Xs = ctx.arena.get<T>("Xs", (size_t)R * D);
+    hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X, (uint64_t)R,
+                       vals, Xs);
+    tm.mark();   // 3
+
+    // ---- cell directory
+    uint32_t* part_start = ctx.arena.get<uint32_t>("part_start", P + 1);
+    hipLaunchKernelGGL((part_start_kernel<K>), dim3((P + 1 + 63) / 64), dim3(64), 0, s, keys,
+                       (uint64_t)R, parts, P, part_start);
+    const uint64_t W = (Gtot >> 6) + 2;
+    uint64_t* bits = ctx.arena.get<uint64_t>("dir_bits", W);
+    uint32_t* rank = ctx.arena.get<uint32_t>("dir_rank", W);
+    PD_HIP(hipMemsetAsync(bits, 0, sizeof(uint64_t) * W, s));
+    uint32_t* flag = ctx.arena.get<uint32_t>("flag", R);
+    uint32_t* cid = ctx.arena.get<uint32_t>("cid", R);
+    uint32_t* cstart = ctx.arena.get<uint32_t>("cstart", (size_t)R + 1);
+    uint32_t* dncells = ctx.arena.get<uint32_t>("ncells", 4);
+    if (R) {
+        hipLaunchKernelGGL((run_flag_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s, keys,
+                           (uint64_t)R, flag, (unsigned long long*)bits);
+        size_t tb = 0;
+        PD_HIP(rocprim::exclusive_scan(nullptr, tb, flag, cid, 0u, (size_t)R,
+                                       rocprim::plus<uint32_t>(), s));
+        void* tmp = ctx.arena.get<char>("scan_tmp", tb);
+        PD_HIP(rocprim::exclusive_scan(tmp, tb, flag, cid, 0u, (size_t)R,
+                                       rocprim::plus<uint32_t>(), s));
+        hipLaunchKernelGGL(cell_start_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, flag, cid,
+                           (uint64_t)R, cstart, dncells);
+    } else {
+        PD_HIP(hipMemsetAsync(cstart, 0, sizeof(uint32_t), s));
+    }
+    {
+        rocprim::transform_iterator<unsigned long long*, Popc, uint32_t> pit(
+            (unsigned long long*)bits, Popc());
+        size_t tb = 0;
+        PD_HIP(rocprim::exclusive_scan(nullptr, tb, pit, rank, 0u, (size_t)W,
+                                       rocprim::plus<uint32_t>(), s));
+        void* tmp = ctx.arena.get<char>("scan_tmp", tb);
+        PD_HIP(rocprim::exclusive_scan(tmp, tb, pit, rank, 0u, (size_t)W,
+                                       rocprim::plus<uint32_t>(), s));
+    }
+    PD_HIP(hipGetLastError());
+    tm.mark();   // 4
+
+    Cells C{parts, part_start, P, bits, rank, cstart};
+    const double eps = a.eps, eps2 = a.eps * a.eps;
+    uint8_t* core = ctx.arena.get<uint8_t>("core", R);
+    uint32_t* cnt_rec = a.counts ? ctx.arena.get<uint32_t>("cnt_rec", R) : nullptr;
+    if (R)
+        hipLaunchKernelGGL((count_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R, C,
+                           eps, eps2, (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0, core,
+                           cnt_rec);
+    PD_HIP(hipGetLastError());
+    tm.mark();   // 5
+
+    uint32_t* par = ctx.arena.get<uint32_t>("parent", R);
+    if (R) {
+        hipLaunchKernelGGL(iota_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, par, R);
+        hipLaunchKernelGGL((link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R, C,
+                           eps, eps2, core, par);
+    }
+    PD_HIP(hipGetLastError());
+    tm.mark();   // 6
+    if (P > 1 && R) {
+        uint32_t* rep = ctx.arena.get<uint32_t>("rep", n);
+        PD_HIP(hipMemsetAsync(rep, 0xFF, sizeof(uint32_t) * n, s));
+        hipLaunchKernelGGL(rep_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, vals, R, core, rep);
+        hipLaunchKernelGGL(merge_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, vals, R, core, rep,
+                           par);
+    }
+    uint32_t* gmin = ctx.arena.get<uint32_t>("gmin", R);
+    if (R) {
+        hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
+        PD_HIP(hipMemsetAsync(gmin, 0xFF, sizeof(uint32_t) * R, s));
+        hipLaunchKernelGGL(gmin_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, vals, R, core, par,
+                           gmin);
+    }
+    PD_HIP(hipGetLastError());
+    tm.mark();   // 7
+
+    uint32_t* key_out = ctx.arena.get<uint32_t>("key_out", n);
+    PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
+    if (a.core) PD_HIP(hipMemsetAsync(a.core, 0, n, s));
+    if (R)
+        hipLaunchKernelGGL((border_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R, C,
+                           eps, eps2, vals, core, par, gmin, cnt_rec, key_out, a.core, a.counts);
+    PD_HIP(hipGetLastError());
+    tm.mark();   // 8
+
+    uint32_t* rflag = ctx.arena.get<uint32_t>("rflag", n);
+    uint32_t* rnk = ctx.arena.get<uint32_t>("rnk", n);
+    int64_t* dncl = ctx.arena.get<int64_t>("ncl", 2);
+    PD_HIP(hipMemsetAsync(dncl, 0, sizeof(int64_t), s));
+    if (n) {
+        hipLaunchKernelGGL(root_flag_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key_out, n, rflag);
+        size_t tb = 0;
+        PD_HIP(rocprim::exclusive_scan(nullptr, tb, rflag, rnk, 0u, (size_t)n,
+                                       rocprim::plus<uint32_t>(), s));
+        void* tmp = ctx.arena.get<char>("scan_tmp", tb);
+        PD_HIP(rocprim::exclusive_scan(tmp, tb, rflag, rnk, 0u, (size_t)n,
+                                       rocprim::plus<uint32_t>(), s));
+        hipLaunchKernelGGL(label_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key_out, rnk, rflag,
+                           n, a.labels, dncl);
+    }
+    PD_HIP(hipGetLastError());
+    tm.mark();   // 9
+    int64_t* hres = (int64_t*)pinned(ctx, 2 * sizeof(int64_t));
+    PD_HIP(hipMemcpyAsync(hres, dncl, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    uint32_t* hnc = (uint32_t*)(hres + 1);
+    if (R)
+        PD_HIP(hipMemcpyAsync(hnc, dncells, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    else
+        *hnc = 0;
+    sync(s);
+    a.n_clusters = hres[0];
+    ctx.t.cells_n = *hnc;
+    ctx.t.grid_cells = (int64_t)Gtot;
+    ctx.t.key_bits = key_bits;
+    if (ctx.timing) {
+        ctx.t.halo = tm.span(0, 1);
+        ctx.t.sort = tm.span(1, 2);
+        ctx.t.gather = tm.span(2, 3);
+        ctx.t.cells = tm.span(3, 4);
+        ctx.t.count = tm.span(4, 5);
+        ctx.t.link = tm.span(5, 6);
+        ctx.t.merge = tm.span(6, 7);
+        ctx.t.border = tm.span(7, 8);
+        ctx.t.label = tm.span(8, 9);
+        ctx.t.total = tm.span(0, 9);
+    }
+}
+
+template <typename T, int D, typename K>
+void run_m(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& p, uint64_t G, int kb) {
+    if (a.metric == 0)
+        run<T, D, K, 0>(ctx, a, p, G, kb);
+    else
+        run<T, D, K, 1>(ctx, a, p, G, kb);
+}
+
+template <typename T, typename K>
+void run_d(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& p, uint64_t G, int kb) {
+    switch (a.d) {
+        case 1: run_m<T, 1, K>(ctx, a, p, G, kb); break;
+        case 2: run_m<T, 2, K>(ctx, a, p, G, kb); break;
+        case 3: run_m<T, 3, K>(ctx, a, p, G, kb); break;
+        case 4: run_m<T, 4, K>(ctx, a, p, G, kb); break;
+        default: throw Error(-5, "grid path supports d <= 4");
+    }
+}
+
+}  // namespace
+
+void train(Ctx& ctx, TrainArgs& a) {
+    if (a.n < 0 || a.d < 1) throw Error(-1, "invalid shape");
+    if (a.d > kMaxDim) throw Error(-5, "d > 4: the dense-tile path is not built yet");
+    if (!(a.eps > 0) || !std::isfinite(a.eps)) throw Error(-1, "eps must be a finite value > 0");
+    if (a.min_samples < 1) throw Error(-1, "min_samples must be >= 1");
+    if (a.metric != 0 && a.metric != 1) throw Error(-1, "metric must be 0 (euclidean) or 1 (cityblock)");
+    if (a.P < 1) throw Error(-1, "need at least one neighbourhood");
+    if (a.n >= (int64_t)kOwnerBit) throw Error(-5, "n must be < 2^31 per device");
+    if (!a.labels && a.n) throw Error(-1, "labels output is required");
+    ctx.t = Timings{};
+    const int d = a.d;
+    double box[2 * kMaxDim];
+    if (a.data_box) {
+        std::memcpy(box, a.data_box, sizeof(double) * 2 * d);
+    } else if (a.n) {
+        int64_t bad = 0;
+        bbox(ctx, a.X, a.dtype, a.n, d, box, &bad, a.stream);
+        if (bad) throw Error(-1, "input contains NaN or infinity");
+    }
+    if (a.n == 0) {
+        a.n_clusters = 0;
+        return;
+    }
+    // per-neighbourhood grids
+    const double cw = a.eps * (1.0 + 1.0 / 1048576.0);
+    std::vector<PartGrid> parts(a.P);
+    uint64_t G = 0;
+    for (int L = 0; L < a.P; ++L) {
+        PartGrid& g = parts[L];
+        std::memset(&g, 0, sizeof(g));
+        g.inv = 1.0 / cw;
+        g.base = G;
+        bool empty = false;
+        long double cells = 1;
+        for (int j = 0; j < d; ++j) {
+            g.elo[j] = a.ebox[(size_t)L * 2 * d + j];
+            g.ehi[j] = a.ebox[(size_t)L * 2 * d + d + j];
+            const double lo = std::max(g.elo[j], box[j]);
+            const double hi = std::min(g.ehi[j], box[d + j]);
+            if (!(lo <= hi)) empty = true;
+            g.lo[j] = lo;
+            if (!empty) {
+                const double nc = std::floor((hi - lo) * g.inv) + 1.0;
+                if (!(nc < 4.0e18)) throw Error(-5, "grid too large along one axis");
+                g.nc[j] = (int64_t)nc;
+                cells *= (long double)g.nc[j];
+            }
+        }
+        if (empty) {
+            for (int j = 0; j < d; ++j) g.nc[j] = 0;
+            continue;
+        }
+        if (cells > 4.0e18L) throw Error(-5, "grid too large (sum of cells > 4e18)");
+        G += (uint64_t)cells;
+        if ((long double)G > 4.0e18L) throw Error(-5, "grid too large");
+    }
+    // directory: G/64 words of 12 B; refuse beyond 64 GiB (future: hashed rows)
+    if ((long double)G / 64.0L * 12.0L > 64.0L * (1ull << 30))
+        throw Error(-5, "eps-grid directory would exceed 64 GiB; eps too small for the extent");
+    int key_bits = 1;
+    while (key_bits < 64 && ((G - (G ? 1 : 0)) >> key_bits)) ++key_bits;
+    if (a.dtype == 0) {
+        if (G < 0xFFFFFFFFull)
+            run_d<float, uint32_t>(ctx, a, parts, G, key_bits);
+        else
+            run_d<float, uint64_t>(ctx, a, parts, G, key_bits);
+    } else if (a.dtype == 1) {
+        if (G < 0xFFFFFFFFull)
+            run_d<double, uint32_t>(ctx, a, parts, G, key_bits);
+        else
+            run_d<double, uint64_t>(ctx, a, parts, G, key_bits);
+    } else {
+        throw Error(-1, "dtype must be 0 (float32) or 1 (float64)");
+    }
+}
+
+}  // namespace pd

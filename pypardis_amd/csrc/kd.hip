@@ -1,0 +1,513 @@
+// KD partition stages: R:dbscan/partition.py:33-183 on the device.
+//
+//  bbox       — data.aggregate(BoundingBox(k), union)          partition.py:135-137
+//  kd_moments — aggregate of [1, v, v**2] per label            partition.py:86-89
+//  kd_counts  — aggregate of 2*(v[axis] < bounds) - 1          partition.py:60-63
+//  kd_split   — filter(v[axis] >= boundary) -> next_label      partition.py:66-68
+//  halo_members — DBSCAN._create_neighborhoods membership      dbscan.py:136-151
+//
+// The host keeps the reference's scalar arithmetic (mean, variance, the 7
+// candidate bounds, argmin) in numpy; only the per-point passes live here.
+// Every reduction is deterministic: per-block partials in a fixed order, then
+// a fixed-order host sum.  HBM-bound streaming passes (one read of X each).
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace pd {
+namespace {
+
+constexpr int kRedBlocks = 1024;
+constexpr int kGroup = 4;   // labels per moments pass (register budget)
+
+template <typename T, int D>
+__device__ __forceinline__ void load_pt(const T* __restrict__ X, uint64_t i, double (&v)[D]) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) v[j] = (double)X[i * D + j];
+}
+
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+__device__ __forceinline__ double wave_min(double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o, 64));
+    return x;
+}
+__device__ __forceinline__ double wave_max(double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o, 64));
+    return x;
+}
+
+// ---------------------------------------------------------------- bbox
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void bbox_kernel(const T* __restrict__ X, uint64_t n,
+                                                      double* __restrict__ part) {
+    double lo[D], hi[D];
+    double bad = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        lo[j] = INFINITY;
+        hi[j] = -INFINITY;
+    }
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kBlock) {
+        double v[D];
+        load_pt<T, D>(X, i, v);
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            if (!isfinite(v[j])) bad += 1;
+            lo[j] = fmin(lo[j], v[j]);
+            hi[j] = fmax(hi[j], v[j]);
+        }
+    }
+    __shared__ double sm[kBlock / 64][2 * D + 1];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        double a = wave_min(lo[j]), b = wave_max(hi[j]);
+        if (l == 0) {
+            sm[w][j] = a;
+            sm[w][D + j] = b;
+        }
+    }
+    double bb = wave_sum(bad);
+    if (l == 0) sm[w][2 * D] = bb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int j = 0; j < D; ++j) {
+            double a = sm[0][j], b = sm[0][D + j];
+            for (int q = 1; q < kBlock / 64; ++q) {
+                a = fmin(a, sm[q][j]);
+                b = fmax(b, sm[q][D + j]);
+            }
+            part[blockIdx.x * (2 * D + 1) + j] = a;
+            part[blockIdx.x * (2 * D + 1) + D + j] = b;
+        }
+        double s = 0;
+        for (int q = 0; q < kBlock / 64; ++q) s += sm[q][2 * D];
+        part[blockIdx.x * (2 * D + 1) + 2 * D] = s;
+    }
+}
+
+// ---------------------------------------------------------------- moments
+// Squares are taken in the input precision then widened, as numpy does for
+// ``vector[1] ** 2`` of an fp32 vector (R:dbscan/partition.py:88).
+// Sums are double-double (error-free TwoSum per term, dd merges in the
+// reductions), so the result is the correctly rounded sum — independent of
+// thread/block/device order.  The reference's sequential fold can differ in
+// the last bits; with exact ties (e.g. StandardScaler output, where every
+// axis has variance 1) only the exact value makes the argmax well defined.
+struct DD {
+    double hi, lo;
+};
+
+__device__ __host__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
+    s = a + b;
+    const double bb = s - a;
+    e = (a - (s - bb)) + (b - bb);
+}
+
+__device__ __host__ __forceinline__ DD dd_add(DD a, DD b) {
+    double s, e;
+    two_sum(a.hi, b.hi, s, e);
+    e += a.lo + b.lo;
+    DD r;
+    r.hi = s + e;
+    r.lo = e - (r.hi - s);
+    return r;
+}
+
+__device__ __forceinline__ void dd_acc(DD& a, double x) {
+    double s, e;
+    two_sum(a.hi, x, s, e);
+    a.hi = s;
+    a.lo += e;
+}
+
+__device__ __forceinline__ DD wave_dd(DD a) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        DD b;
+        b.hi = __shfl_xor(a.hi, o, 64);
+        b.lo = __shfl_xor(a.lo, o, 64);
+        a = dd_add(a, b);
+    }
+    return a;
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void moments_kernel(const T* __restrict__ X, uint64_t n,
+                                                         const int32_t* __restrict__ labels,
+                                                         int4 sel, double* __restrict__ part) {
+    double c[kGroup];
+    DD s[kGroup][D], q[kGroup][D];
+#pragma unroll
+    for (int g = 0; g < kGroup; ++g) {
+        c[g] = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) s[g][j] = q[g][j] = DD{0.0, 0.0};
+    }
+    const int sl[kGroup] = {sel.x, sel.y, sel.z, sel.w};
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kBlock) {
+        const int lab = labels[i];
+#pragma unroll
+        for (int g = 0; g < kGroup; ++g) {
+            if (lab == sl[g]) {
+                c[g] += 1.0;
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    const T v = X[i * D + j];
+                    const T vv = v * v;
+                    dd_acc(s[g][j], (double)v);
+                    dd_acc(q[g][j], (double)vv);
+                }
+            }
+        }
+    }
+    // per block: kGroup x [count, (s.hi, s.lo) x D, (q.hi, q.lo) x D]
+    constexpr int G = 1 + 4 * D;
+    constexpr int W = kGroup * G;
+    __shared__ double sm[kBlock / 64][W];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+    for (int g = 0; g < kGroup; ++g) {
+        double x = wave_sum(c[g]);
+        if (l == 0) sm[w][g * G] = x;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const DD a = wave_dd(s[g][j]);
+            const DD b = wave_dd(q[g][j]);
+            if (l == 0) {
+                sm[w][g * G + 1 + 2 * j] = a.hi;
+                sm[w][g * G + 2 + 2 * j] = a.lo;
+                sm[w][g * G + 1 + 2 * D + 2 * j] = b.hi;
+                sm[w][g * G + 2 + 2 * D + 2 * j] = b.lo;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kGroup * (1 + 2 * D)) {
+        // one thread per (group, quantity): fixed-order dd merge over waves
+        const int g = threadIdx.x / (1 + 2 * D), qd = threadIdx.x % (1 + 2 * D);
+        if (qd == 0) {
+            double acc = 0;
+            for (int k = 0; k < kBlock / 64; ++k) acc += sm[k][g * G];
+            part[(uint64_t)blockIdx.x * W + g * G] = acc;
+        } else {
+            const int off = g * G + 1 + 2 * (qd - 1);
+            DD acc{0.0, 0.0};
+            for (int k = 0; k < kBlock / 64; ++k) acc = dd_add(acc, DD{sm[k][off], sm[k][off + 1]});
+            part[(uint64_t)blockIdx.x * W + off] = acc.hi;
+            part[(uint64_t)blockIdx.x * W + off + 1] = acc.lo;
+        }
+    }
+}
+
+// Reference-order variant (PD_OPT_SEQUENTIAL_MOMENTS): one lane per
+// (label, axis, moment) stream folds the points left to right in index order,
+// i.e. exactly ``partition.aggregate(zeros, x + [1, v, v**2], add)`` over a
+// single slice (R:dbscan/partition.py:86-89).  O(n) serial per lane: a
+// compatibility mode for bit-identical split boundaries, not the fast path.
+template <typename T, int D>
+__global__ void moments_seq_kernel(const T* __restrict__ X, uint64_t n,
+                                   const int32_t* __restrict__ labels, int4 sel,
+                                   double* __restrict__ out) {
+    const int lane = threadIdx.x;
+    if (lane >= kGroup * 2 * D) return;
+    const int g = lane / (2 * D), rem = lane % (2 * D), j = rem % D, sq = rem / D;
+    const int want = (&sel.x)[g];
+    double acc = 0.0, cnt = 0.0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (labels[i] != want) continue;
+        const T v = X[i * D + j];
+        const T vv = v * v;
+        acc = acc + (sq ? (double)vv : (double)v);
+        cnt += 1.0;
+    }
+    constexpr int G = 1 + 4 * D;
+    // same layout as moments_kernel's block partial (lo words = 0), block 0
+    out[g * G + 1 + 2 * D * sq + 2 * j] = acc;
+    out[g * G + 2 + 2 * D * sq + 2 * j] = 0.0;
+    if (rem == 0) out[g * G] = cnt;
+}
+
+// ---------------------------------------------------------------- counts
+// counts[slot][i] = #points of the slot's label with v[axis] < bounds[slot][i]
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void counts_kernel(
+    const T* __restrict__ X, uint64_t n, const int32_t* __restrict__ labels,
+    const int32_t* __restrict__ slot_of, int n_label_tab, const int32_t* __restrict__ axis,
+    const double* __restrict__ bounds, int n_sel, unsigned long long* __restrict__ out) {
+    extern __shared__ unsigned int lcnt[];   // n_sel * 8
+    for (int k = threadIdx.x; k < n_sel * 8; k += kBlock) lcnt[k] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kBlock) {
+        const int lab = labels[i];
+        if (lab < 0 || lab >= n_label_tab) continue;
+        const int sl = slot_of[lab];
+        if (sl < 0) continue;
+        const double v = (double)X[i * D + axis[sl]];
+        for (int b = 0; b < 7; ++b)
+            if (v < bounds[sl * 7 + b]) atomicAdd(&lcnt[sl * 8 + b], 1u);
+        atomicAdd(&lcnt[sl * 8 + 7], 1u);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < n_sel * 8; k += kBlock)
+        if (lcnt[k]) atomicAdd(&out[k], (unsigned long long)lcnt[k]);
+}
+
+// ---------------------------------------------------------------- split
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void split_kernel(
+    const T* __restrict__ X, uint64_t n, int32_t* __restrict__ labels,
+    const int32_t* __restrict__ slot_of, int n_label_tab, const int32_t* __restrict__ axis,
+    const double* __restrict__ boundary, const int32_t* __restrict__ newlab) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kBlock) {
+        const int lab = labels[i];
+        if (lab < 0 || lab >= n_label_tab) continue;
+        const int sl = slot_of[lab];
+        if (sl < 0) continue;
+        const double v = (double)X[i * D + axis[sl]];
+        if (v >= boundary[sl]) labels[i] = newlab[sl];
+    }
+}
+
+// ---------------------------------------------------------------- halo membership
+template <typename T, int D>
+struct InBox {
+    const T* X;
+    const double* box;   // lo[D], hi[D]
+    __device__ bool operator()(int64_t i) const {
+        bool in = true;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const double v = (double)X[i * D + j];
+            in &= (box[j] <= v) & (box[D + j] >= v);
+        }
+        return in;
+    }
+};
+
+template <int D, typename F>
+void dispatch_d(int d, F&& f) {
+    switch (d) {
+        case 1: f(std::integral_constant<int, 1>{}); break;
+        case 2: f(std::integral_constant<int, 2>{}); break;
+        case 3: f(std::integral_constant<int, 3>{}); break;
+        case 4: f(std::integral_constant<int, 4>{}); break;
+        default: throw Error(-5, "dimension " + std::to_string(d) + " > 4 not supported yet");
+    }
+}
+
+template <typename F>
+void dispatch(int dtype, int d, F&& f) {
+    if (dtype == 0)
+        dispatch_d<0>(d, [&](auto D) { f((float*)nullptr, D); });
+    else if (dtype == 1)
+        dispatch_d<0>(d, [&](auto D) { f((double*)nullptr, D); });
+    else
+        throw Error(-1, "dtype must be 0 (float32) or 1 (float64)");
+}
+
+struct LabelTables {
+    int32_t* slot_of;
+    int32_t* axis;
+    double* dbl;
+    int32_t* newlab;
+    int ntab;
+};
+
+// Upload the (label -> slot) map and the per-slot tables.  Pinned staging is
+// safe to reuse because every KD entry point synchronises before returning.
+LabelTables upload_tables(Ctx& ctx, int n_sel, const int32_t* sel, const int32_t* axis,
+                          const double* dbl, int dbl_per, const int32_t* newlab,
+                          hipStream_t s) {
+    int ntab = 1;
+    for (int k = 0; k < n_sel; ++k) ntab = std::max(ntab, sel[k] + 1);
+    const size_t bytes = sizeof(int32_t) * (ntab + 2 * n_sel) + sizeof(double) * n_sel * dbl_per;
+    char* h = (char*)pinned(ctx, bytes + 64);
+    int32_t* h_slot = (int32_t*)h;
+    for (int k = 0; k < ntab; ++k) h_slot[k] = -1;
+    for (int k = 0; k < n_sel; ++k) h_slot[sel[k]] = k;
+    int32_t* h_axis = h_slot + ntab;
+    int32_t* h_new = h_axis + n_sel;
+    for (int k = 0; k < n_sel; ++k) {
+        h_axis[k] = axis ? axis[k] : 0;
+        h_new[k] = newlab ? newlab[k] : 0;
+    }
+    size_t off_d = ((sizeof(int32_t) * (ntab + 2 * n_sel)) + 7) & ~size_t(7);
+    double* h_d = (double*)(h + off_d);
+    if (dbl) std::memcpy(h_d, dbl, sizeof(double) * n_sel * dbl_per);
+    char* dmem = ctx.arena.get<char>("kd_tables", off_d + sizeof(double) * n_sel * dbl_per + 64);
+    PD_HIP(hipMemcpyAsync(dmem, h, off_d + sizeof(double) * n_sel * dbl_per,
+                          hipMemcpyHostToDevice, s));
+    LabelTables t;
+    t.slot_of = (int32_t*)dmem;
+    t.axis = t.slot_of + ntab;
+    t.newlab = t.axis + n_sel;
+    t.dbl = (double*)(dmem + off_d);
+    t.ntab = ntab;
+    return t;
+}
+
+}  // namespace
+
+void bbox(Ctx& ctx, const void* X, int dtype, int64_t n, int d, double* lohi, int64_t* bad,
+          hipStream_t s) {
+    const int nb = (int)std::min<int64_t>(kRedBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
+    const int W = 2 * d + 1;
+    double* part = ctx.arena.get<double>("bbox_part", (size_t)nb * W);
+    dispatch(dtype, d, [&](auto tp, auto Dc) {
+        using T = std::remove_pointer_t<decltype(tp)>;
+        constexpr int D = decltype(Dc)::value;
+        hipLaunchKernelGGL((bbox_kernel<T, D>), dim3(nb), dim3(kBlock), 0, s, (const T*)X,
+                           (uint64_t)n, part);
+    });
+    PD_HIP(hipGetLastError());
+    double* h = (double*)pinned(ctx, sizeof(double) * nb * W);
+    PD_HIP(hipMemcpyAsync(h, part, sizeof(double) * nb * W, hipMemcpyDeviceToHost, s));
+    sync(s);
+    double nbad = 0;
+    for (int j = 0; j < d; ++j) {
+        double a = INFINITY, b = -INFINITY;
+        for (int k = 0; k < nb; ++k) {
+            a = std::fmin(a, h[k * W + j]);
+            b = std::fmax(b, h[k * W + d + j]);
+        }
+        lohi[j] = a;
+        lohi[d + j] = b;
+    }
+    for (int k = 0; k < nb; ++k) nbad += h[k * W + 2 * d];
+    if (bad) *bad = (int64_t)nbad;
+}
+
+void kd_moments(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
+                int n_sel, const int32_t* sel, double* out, hipStream_t s) {
+    const int nb = (int)std::min<int64_t>(kRedBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
+    const int G = 1 + 4 * d;
+    const int W = kGroup * G;
+    for (int g0 = 0; g0 < n_sel; g0 += kGroup) {
+        int4 sl = make_int4(-2, -2, -2, -2);
+        int* sp = &sl.x;
+        for (int g = 0; g < kGroup && g0 + g < n_sel; ++g) sp[g] = sel[g0 + g];
+        double* part = ctx.arena.get<double>("mom_part", (size_t)nb * W);
+        const int nbk = ctx.seq_moments ? 1 : nb;
+        dispatch(dtype, d, [&](auto tp, auto Dc) {
+            using T = std::remove_pointer_t<decltype(tp)>;
+            constexpr int D = decltype(Dc)::value;
+            if (ctx.seq_moments)
+                hipLaunchKernelGGL((moments_seq_kernel<T, D>), dim3(1), dim3(64), 0, s,
+                                   (const T*)X, (uint64_t)n, labels, sl, part);
+            else
+                hipLaunchKernelGGL((moments_kernel<T, D>), dim3(nb), dim3(kBlock), 0, s,
+                                   (const T*)X, (uint64_t)n, labels, sl, part);
+        });
+        PD_HIP(hipGetLastError());
+        double* h = (double*)pinned(ctx, sizeof(double) * nbk * W);
+        PD_HIP(hipMemcpyAsync(h, part, sizeof(double) * nbk * W, hipMemcpyDeviceToHost, s));
+        sync(s);
+        for (int g = 0; g < kGroup && g0 + g < n_sel; ++g) {
+            // out layout per selected label: [3][d] = count row, sum row, sumsq row
+            double* o = out + (size_t)(g0 + g) * 3 * d;
+            double cnt = 0;
+            std::vector<DD> sum(d, DD{0.0, 0.0}), sq(d, DD{0.0, 0.0});
+            for (int k = 0; k < nbk; ++k) {
+                const double* p = h + (size_t)k * W + g * G;
+                cnt += p[0];
+                for (int j = 0; j < d; ++j) {
+                    sum[j] = dd_add(sum[j], DD{p[1 + 2 * j], p[2 + 2 * j]});
+                    sq[j] = dd_add(sq[j], DD{p[1 + 2 * d + 2 * j], p[2 + 2 * d + 2 * j]});
+                }
+            }
+            for (int j = 0; j < d; ++j) {
+                o[j] = cnt;
+                o[d + j] = sum[j].hi + sum[j].lo;
+                o[2 * d + j] = sq[j].hi + sq[j].lo;
+            }
+        }
+    }
+}
+
+void kd_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
+               int n_sel, const int32_t* sel, const int32_t* axis, const double* bounds,
+               int64_t* out, hipStream_t s) {
+    if (n_sel <= 0) return;
+    LabelTables t = upload_tables(ctx, n_sel, sel, axis, bounds, 7, nullptr, s);
+    unsigned long long* dcnt = ctx.arena.get<unsigned long long>("kd_cnt", (size_t)n_sel * 8);
+    PD_HIP(hipMemsetAsync(dcnt, 0, sizeof(unsigned long long) * n_sel * 8, s));
+    const unsigned nb = grid_for(n, 2048);
+    dispatch(dtype, d, [&](auto tp, auto Dc) {
+        using T = std::remove_pointer_t<decltype(tp)>;
+        constexpr int D = decltype(Dc)::value;
+        hipLaunchKernelGGL((counts_kernel<T, D>), dim3(nb), dim3(kBlock),
+                           sizeof(unsigned int) * n_sel * 8, s, (const T*)X, (uint64_t)n, labels,
+                           t.slot_of, t.ntab, t.axis, t.dbl, n_sel, dcnt);
+    });
+    PD_HIP(hipGetLastError());
+    unsigned long long* h = (unsigned long long*)pinned(ctx, sizeof(unsigned long long) * n_sel * 8);
+    PD_HIP(hipMemcpyAsync(h, dcnt, sizeof(unsigned long long) * n_sel * 8, hipMemcpyDeviceToHost, s));
+    sync(s);
+    // out[slot][0..6] = n_less per bound, out[slot][7] = n_total
+    for (int k = 0; k < n_sel * 8; ++k) out[k] = (int64_t)h[k];
+}
+
+void kd_split(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels, int n_sel,
+              const int32_t* sel, const int32_t* axis, const double* boundary,
+              const int32_t* newlab, hipStream_t s) {
+    if (n_sel <= 0) return;
+    LabelTables t = upload_tables(ctx, n_sel, sel, axis, boundary, 1, newlab, s);
+    const unsigned nb = grid_for(n, 4096);
+    dispatch(dtype, d, [&](auto tp, auto Dc) {
+        using T = std::remove_pointer_t<decltype(tp)>;
+        constexpr int D = decltype(Dc)::value;
+        hipLaunchKernelGGL((split_kernel<T, D>), dim3(nb), dim3(kBlock), 0, s, (const T*)X,
+                           (uint64_t)n, labels, t.slot_of, t.ntab, t.axis, t.dbl, t.newlab);
+    });
+    PD_HIP(hipGetLastError());
+    sync(s);
+}
+
+void halo_members(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P,
+                  const double* ebox, int64_t* counts, int64_t* members, int64_t cap,
+                  hipStream_t s) {
+    double* dbox = ctx.arena.get<double>("halo_box", (size_t)P * 2 * d);
+    double* hbox = (double*)pinned(ctx, sizeof(double) * P * 2 * d + sizeof(int64_t));
+    std::memcpy(hbox, ebox, sizeof(double) * P * 2 * d);
+    PD_HIP(hipMemcpyAsync(dbox, hbox, sizeof(double) * P * 2 * d, hipMemcpyHostToDevice, s));
+    int64_t* dsel = ctx.arena.get<int64_t>("halo_nsel", 1);
+    int64_t* scratch = members ? nullptr : ctx.arena.get<int64_t>("halo_scratch", (size_t)n);
+    int64_t used = 0;
+    for (int L = 0; L < P; ++L) {
+        int64_t* outp = members ? members + used : scratch;
+        dispatch(dtype, d, [&](auto tp, auto Dc) {
+            using T = std::remove_pointer_t<decltype(tp)>;
+            constexpr int D = decltype(Dc)::value;
+            InBox<T, D> pred{(const T*)X, dbox + (size_t)L * 2 * D};
+            rocprim::counting_iterator<int64_t> it(0);
+            size_t tb = 0;
+            PD_HIP(rocprim::select(nullptr, tb, it, outp, dsel, (size_t)n, pred, s));
+            void* tmp = ctx.arena.get<char>("halo_tmp", tb);
+            PD_HIP(rocprim::select(tmp, tb, it, outp, dsel, (size_t)n, pred, s));
+        });
+        int64_t* h = (int64_t*)pinned(ctx, sizeof(int64_t));
+        PD_HIP(hipMemcpyAsync(h, dsel, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        sync(s);
+        counts[L] = *h;
+        used += *h;
+        if (members && used > cap) throw Error(-1, "halo_members: members buffer too small");
+    }
+}
+
+}  // namespace pd

@@ -1,0 +1,208 @@
+"""``DBSCAN`` driver — the surface of R:dbscan/dbscan.py:56-165 on MI355X.
+
+What ``train`` does, stage by stage, against the reference:
+
+    KDPartitioner(data, max_partitions)      R:dbscan/dbscan.py:110   GPU passes (partition.py)
+    _create_neighborhoods: box.expand(2·eps)  R:dbscan/dbscan.py:136-151
+    partitionBy + mapPartitions(dbscan_partition)
+                                              R:dbscan/dbscan.py:116-124
+    _remap_cluster_ids (+ ClusterAggregator)  R:dbscan/dbscan.py:153-165
+        └── the last three fused into ONE device call, pd_train (engine.hip):
+            halo records → (neighbourhood, eps-cell) sort → neighbour count /
+            core flags → union-find on core–core edges → merge of the copies
+            of each halo point → border attach → global labels.
+
+The labels are the ones sklearn's ``DBSCAN(eps, min_samples).fit_predict``
+gives on the whole data set (what the reference's merge intends; its literal
+merge is hash-order dependent), and are independent of
+``max_partitions``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+from scipy.spatial.distance import euclidean
+
+from . import _native
+from ._data import PointSet, as_points
+from .partition import KDPartitioner
+
+
+def dbscan_partition(iterable, params):
+    """R:dbscan/dbscan.py:12-34: cluster one neighbourhood.
+
+    :param iterable: ((key, partition), vector) records of one neighbourhood
+    :param params: {'eps', 'min_samples', 'metric'}
+    :return: yields (key, '%i:%i%s' % (partition, cluster_id, '' or '*'))
+    Runs ``pd_cluster`` (sklearn fit_predict semantics) on the GPU.  An empty
+    neighbourhood yields nothing (the reference raises IndexError, :24).
+    """
+    data = list(iterable)
+    if not data:
+        return
+    (key, part), vector = data[0]
+    X = np.array([v for (_, __), v in data])
+    y = [k for (k, _), __ in data]
+    pts = as_points(X)
+    labels, core, _, _ = _native.cluster(pts.X, params['eps'], params['min_samples'],
+                                         _native.metric_code(params.get('metric', 'euclidean')))
+    c = labels.cpu().numpy()
+    cores = core.cpu().numpy()
+    for i in range(len(c)):
+        flag = '' if cores[i] else '*'
+        yield (y[i], '%i:%i%s' % (part, c[i], flag))
+
+
+def map_cluster_id(x, broadcast_dict):
+    """R:dbscan/dbscan.py:37-53 (string-label compatibility): first label of
+    the group, '*' stripped; -1 if it is noise or unmapped."""
+    key, cluster_id = x
+    cluster_id = next(iter(cluster_id)).strip('*')
+    cluster_dict = getattr(broadcast_dict, 'value', broadcast_dict)
+    if '-1' not in cluster_id and cluster_id in cluster_dict:
+        return key, cluster_dict[cluster_id]
+    return key, -1
+
+
+class _Neighborhood(object):
+    """``neighbors[label]``: points inside the 2·eps-expanded box of one KD
+    partition (membership computed on the GPU by pd_halo_members)."""
+
+    def __init__(self, owner, label):
+        self._owner = owner
+        self.label = label
+
+    def indices(self):
+        return self._owner._members(self.label)
+
+    def keys(self):
+        return self._owner.points.key_array()[self.indices()]
+
+    def collect(self):
+        idx = self.indices()
+        vecs = self._owner.points.vectors(torch.from_numpy(idx).to(self._owner.points.X.device))
+        return [((k, self.label), v) for k, v in zip(self.keys().tolist(), vecs)]
+
+    def count(self):
+        return len(self.indices())
+
+    __len__ = count
+
+
+class _Neighborhoods(dict):
+    def __init__(self, points, expanded):
+        super().__init__()
+        self.points = points
+        self._ebox = np.stack([expanded[L].as_array() for L in sorted(expanded)])
+        self._cache = None
+        for L in sorted(expanded):
+            self[L] = _Neighborhood(self, L)
+
+    def _members(self, L):
+        if self._cache is None:
+            counts, members = _native.halo_members(self.points.X, self._ebox)
+            m = members.cpu().numpy()
+            off = np.concatenate([[0], np.cumsum(counts)])
+            self._cache = [m[off[i]:off[i + 1]] for i in range(len(counts))]
+        return self._cache[L]
+
+    def iteritems(self):
+        return iter(self.items())
+
+
+class _Assignments(object):
+    """``DBSCAN.result``: (key, cluster id) pairs sorted by key
+    (``.sortByKey()``, R:dbscan/dbscan.py:162-164)."""
+
+    def __init__(self, points, labels):
+        self.points = points
+        self.labels = labels
+
+    def labels_by_key(self):
+        lab = self.labels.cpu().numpy().astype(np.int64)
+        keys = self.points.key_array()
+        if self.points.keys is None:
+            return keys, lab
+        order = np.argsort(keys, kind="stable")
+        return keys[order], lab[order]
+
+    def collect(self):
+        keys, lab = self.labels_by_key()
+        return list(zip(keys.tolist(), lab.tolist()))
+
+    def count(self):
+        return self.points.n
+
+
+class DBSCAN(object):
+    """
+    :eps: nearest neighbor radius
+    :min_samples: minimum number of samples within radius eps
+    :metric: distance metric (euclidean or cityblock, string or scipy callable)
+    :max_partitions: maximum number of partitions used by KDPartitioner
+    :data: the training points (PointSet: keys + device coordinates)
+    :result: (key, cluster label) pairs, sorted by key, via ``collect()``
+    :bounding_boxes: label -> BoundingBox of each KD partition
+    :expanded_boxes: label -> BoundingBox grown by 2·eps
+    :neighbors: label -> points inside the expanded box
+    :cluster_dict: kept for API parity; the reference never assigns it
+
+    MI355X additions: ``labels_`` (device int32, input order),
+    ``core_sample_mask_`` (device uint8), ``n_clusters_``; ``kd_sums`` selects
+    the KD moment summation (see KDPartitioner) — it changes the boxes only,
+    never the labels.
+    """
+
+    def __init__(self, eps=0.5, min_samples=5, metric=euclidean, max_partitions=None,
+                 kd_sums='exact'):
+        self.eps = eps
+        self.kd_sums = kd_sums
+        self.min_samples = int(min_samples)
+        self.metric = metric
+        self.max_partitions = max_partitions
+        self.data = None
+        self.result = None
+        self.bounding_boxes = None
+        self.expanded_boxes = None
+        self.neighbors = None
+        self.cluster_dict = None
+        self.labels_ = None
+        self.core_sample_mask_ = None
+        self.n_clusters_ = None
+        self.partitioner = None
+
+    def train(self, data):
+        """
+        :param data: RDD-like / iterable of (key, vector), or (n, d) array/tensor
+        Train the model (R:dbscan/dbscan.py:104-126).
+        """
+        if not (self.eps > 0):
+            raise ValueError("eps must be > 0")
+        if self.min_samples < 1:
+            raise ValueError("min_samples must be >= 1")
+        metric = _native.metric_code(self.metric)
+        points = as_points(data)
+        parts = KDPartitioner(points, self.max_partitions, sums=self.kd_sums)
+        self.partitioner = parts
+        self.data = points
+        self.bounding_boxes = parts.bounding_boxes
+        self.expanded_boxes = {L: box.expand(2 * self.eps)
+                               for L, box in sorted(parts.bounding_boxes.items())}
+        self.neighbors = _Neighborhoods(points, self.expanded_boxes)
+        ebox = np.stack([self.expanded_boxes[L].as_array() for L in sorted(self.expanded_boxes)])
+        owner = parts.labels if len(ebox) > 1 else None
+        lo, hi = parts.data_box
+        labels, core, _, ncl = _native.train(points.X, self.eps, self.min_samples, metric, ebox,
+                                             owner=owner, data_box=np.stack([lo, hi]))
+        self.labels_ = labels
+        self.core_sample_mask_ = core
+        self.n_clusters_ = ncl
+        self.result = _Assignments(points, labels)
+        return self
+
+    def assignments(self):
+        """
+        :rtype: list
+        :return: list of (key, cluster_id), sorted by key
+        """
+        return self.result.collect()

@@ -1,0 +1,223 @@
+"""KD partitioner — R:dbscan/partition.py:8-183, with the per-point passes
+on the GPU.
+
+Host side keeps exactly the reference's scalar arithmetic (mean, variance,
+the seven candidate bounds ``mean + (i - 3) * 0.3 * std``, first argmin,
+left-keeps-label / right-gets-next_label, BFS label order).  The passes over
+the points run as HIP kernels through the C ABI:
+
+    moments  Σ[1, v, v²] per label    pd_kd_moments   (R:dbscan/partition.py:86-89)
+    counts   Σ 2·[v < b_i] − 1        pd_kd_counts    (R:dbscan/partition.py:60-63)
+    split    v >= boundary → relabel  pd_kd_split     (R:dbscan/partition.py:66-68)
+    bbox     union of all points      pd_bbox         (R:dbscan/partition.py:135-137)
+
+All splits of one BFS level run in the same passes (each split only reads its
+own label's points, so batching cannot change a result).  The fp64 sums are
+deterministic but not in the reference's sequential order, so a boundary can
+differ from the reference's in the last bits (tests allow 1e-12 relative and
+require the candidate index and child sizes to match).
+
+Deliberate deviation: a variance that round-off makes negative is clamped to
+0 before the sqrt; the reference takes sqrt(<0) = NaN there and silently
+drops every point of that partition.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _native
+from ._data import PointSet, as_points
+from .geometry import BoundingBox
+
+
+def _split_schedule(max_partitions):
+    """The todo/done queue walk of R:dbscan/partition.py:159-183 as BFS levels
+    of (current_label, next_label) pairs."""
+    levels, todo, done, nxt, cur_level = [], [0], [], 1, []
+    while nxt < max_partitions:
+        if todo:
+            cur = todo.pop(0)
+            cur_level.append((cur, nxt))
+            done += [cur, nxt]
+            nxt += 1
+        else:
+            levels.append(cur_level)
+            cur_level, todo, done = [], done, []
+    if cur_level:
+        levels.append(cur_level)
+    return levels
+
+
+def _bounds(mean, variance):
+    """R:dbscan/partition.py:58-59, same expression order in fp64."""
+    std_dev = np.sqrt(np.float64(variance) if variance >= 0 else np.float64(0.0)) \
+        if not np.isnan(variance) else np.float64(np.nan)
+    return np.array([mean + (i - 3) * 0.3 * std_dev for i in range(7)])
+
+
+class PartitionView(object):
+    """The points currently carrying one KD label — what the reference keeps
+    as the RDD ``((key, label), vector)`` of that partition."""
+
+    def __init__(self, points, labels, label):
+        self.points = points
+        self.labels = labels
+        self.label = int(label)
+
+    def indices(self):
+        return torch.nonzero(self.labels == self.label).flatten()
+
+    def count(self):
+        return int((self.labels == self.label).sum().item())
+
+    def keys(self):
+        return self.points.key_array()[self.indices().cpu().numpy()]
+
+    def collect(self):
+        idx = self.indices()
+        keys = self.points.key_array()[idx.cpu().numpy()]
+        vecs = self.points.vectors(idx)
+        return [((k, self.label), v) for k, v in zip(keys.tolist(), vecs)]
+
+    def __len__(self):
+        return self.count()
+
+    def __repr__(self):
+        return f"PartitionView(label={self.label})"
+
+
+class _Union(object):
+    """``KDPartitioner.result``: the union of every partition."""
+
+    def __init__(self, parts):
+        self.parts = parts
+
+    def collect(self):
+        out = []
+        for L in sorted(self.parts):
+            out += self.parts[L].collect()
+        return out
+
+    def count(self):
+        return sum(p.count() for p in self.parts.values())
+
+
+def _labels_of(partition):
+    if not isinstance(partition, PartitionView):
+        raise TypeError("expected a PartitionView (from KDPartitioner.partitions)")
+    return partition.points.X, partition.labels
+
+
+def mean_var_split(partition, k, axis, next_label, mean, variance):
+    """R:dbscan/partition.py:33-69.  Returns (part1, part2, boundary); part1
+    keeps the label (v < boundary), part2 becomes ``next_label``.  The split
+    is applied to the partition's shared label array in place."""
+    X, labels = _labels_of(partition)
+    bounds = _bounds(mean, variance)
+    cnt = _native.kd_counts(X, labels, [partition.label], [axis], bounds[None])[0]
+    counts = np.abs(2.0 * cnt[:7].astype(np.float64) - float(cnt[7]))
+    boundary = bounds[int(np.argmin(counts))]
+    _native.kd_split(X, labels, [partition.label], [axis], [boundary], [next_label])
+    return (partition, PartitionView(partition.points, labels, next_label), boundary)
+
+
+def min_var_split(partition, k, next_label, sums='exact'):
+    """R:dbscan/partition.py:72-95: split on the axis of largest variance."""
+    X, labels = _labels_of(partition)
+    mom = _native.kd_moments(X, labels, [partition.label], sequential=(sums == 'sequential'))[0]
+    with np.errstate(invalid="ignore", divide="ignore"):
+        means = mom[1] / mom[0]
+        variances = mom[2] / mom[0] - means ** 2
+    axis = int(np.argmax(variances))
+    return mean_var_split(partition, k, axis, next_label, means[axis], variances[axis]), axis
+
+
+def median_search_split(partition, axis, next_part):
+    """R:dbscan/partition.py:8-30 (split_method='rotation').  Not built yet:
+    the reference itself cannot run it on Python 3 (float list index, :26);
+    SURVEY.md §8(f) item 2 ranks the GPU radix-select version after (a)-(e)."""
+    raise NotImplementedError("split_method='rotation' (median_search_split) is not built yet")
+
+
+class KDPartitioner(object):
+    """R:dbscan/partition.py:98-183.
+
+    :partitions: label -> PartitionView
+    :bounding_boxes: label -> BoundingBox
+    :result: union of the partitions
+    :labels: device int32 tensor, the KD label of every point
+    :splits: per split (cur, new, axis, cand, n_left, n_right, mean, var, boundary)
+
+    ``sums`` (extension): 'exact' (default) takes each label's moments as
+    correctly rounded, order-independent sums; 'sequential' folds them in
+    point order exactly as the reference's single-slice aggregate does, so
+    boundaries are bit-identical to it (one GPU lane per moment: slow, a
+    compatibility mode).  The two differ only where the reference's choice is
+    decided by round-off (e.g. StandardScaler data: all variances are 1).
+    """
+
+    def __init__(self, data, max_partitions=None, k=None, split_method='min_var', sums='exact'):
+        self.split_method = split_method if split_method in ['min_var', 'rotation'] else 'min_var'
+        if self.split_method == 'rotation':
+            raise NotImplementedError("split_method='rotation' is not built yet")
+        if sums not in ('exact', 'sequential'):
+            raise ValueError("sums must be 'exact' or 'sequential'")
+        self.sums = sums
+        self.points = as_points(data)
+        X = self.points.X
+        self.k = int(k) if k is not None else self.points.d
+        self.max_partitions = int(max_partitions) if max_partitions is not None else 4 ** self.k
+        if self.max_partitions < 1:
+            raise ValueError("max_partitions must be >= 1")
+        lo, hi, bad = _native.bbox(X)
+        if bad:
+            raise ValueError("Input contains NaN or infinity.")
+        self.data_box = (lo, hi)     # tight box: the engine clips its grids to it
+        box = BoundingBox(k=self.k).union(BoundingBox(lo, hi))
+        self.labels = torch.zeros(self.points.n, dtype=torch.int32, device=X.device)
+        self.splits = []
+        self._create_partitions(box)
+        self.partitions = {L: PartitionView(self.points, self.labels, L)
+                           for L in sorted(self.bounding_boxes)}
+        self.result = _Union(self.partitions)
+
+    def _create_partitions(self, box):
+        X, labels = self.points.X, self.labels
+        self.bounding_boxes = {0: box}
+        for level in _split_schedule(self.max_partitions):
+            sel = [c for c, _ in level]
+            new = [nl for _, nl in level]
+            mom = _native.kd_moments(X, labels, sel, sequential=(self.sums == 'sequential'))
+            axes, means, vars_, bounds = [], [], [], []
+            for s in range(len(sel)):
+                with np.errstate(invalid="ignore", divide="ignore"):
+                    m = mom[s, 1] / mom[s, 0]
+                    v = mom[s, 2] / mom[s, 0] - m ** 2
+                a = int(np.argmax(v))
+                axes.append(a)
+                means.append(m[a])
+                vars_.append(v[a])
+                bounds.append(_bounds(m[a], v[a]))
+            bounds = np.array(bounds).reshape(len(sel), 7)
+            cnt = _native.kd_counts(X, labels, sel, axes, bounds)
+            boundary, cand = [], []
+            for s in range(len(sel)):
+                c = np.abs(2.0 * cnt[s, :7].astype(np.float64) - float(cnt[s, 7]))
+                i = int(np.argmin(c))
+                cand.append(i)
+                boundary.append(bounds[s, i])
+            _native.kd_split(X, labels, sel, axes, boundary, new)
+            for s, (cur, nl) in enumerate(level):
+                left, right = self.bounding_boxes[cur].split(axes[s], boundary[s])
+                self.bounding_boxes[cur] = left
+                self.bounding_boxes[nl] = right
+                n_tot = int(cnt[s, 7])
+                # left child = points with v < boundary: counts of the chosen bound
+                n_left = int(cnt[s, cand[s]])
+                self.splits.append((cur, nl, axes[s], cand[s], n_left, n_tot - n_left,
+                                    float(means[s]), float(vars_[s]), float(boundary[s])))
+
+    def box_array(self):
+        """(P, 2, k) fp64 boxes in label order."""
+        return np.stack([self.bounding_boxes[L].as_array() for L in sorted(self.bounding_boxes)])

@@ -1,0 +1,278 @@
+"""GPU parity: the HIP path (through the C ABI) against the pinned oracle and
+the reference goldens.  Bit-exact for everything integer-valued (labels, core
+flags, neighbour counts, halo membership, split sizes); split boundaries
+within 1e-12 relative (their fp64 sums run in a different order than the
+reference's sequential fold)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import GOLDEN, golden_names, load_golden
+
+pytestmark = pytest.mark.gpu
+
+NAMES = golden_names()
+
+
+def _metric(g):
+    m = str(g["metric"])
+    return "euclidean" if m == "callable" else m
+
+
+def _P(g):
+    P = int(g["max_partitions"])
+    return None if P < 0 else P
+
+
+def _dev(X):
+    return torch.from_numpy(np.ascontiguousarray(X)).cuda()
+
+
+@pytest.fixture(scope="module")
+def native():
+    from pypardis_amd import _native
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    _native.load()
+    return _native
+
+
+def _cluster(native, X, eps, ms, metric="euclidean", full=False):
+    ctx = native.context()
+    ctx.set_option(native.PD_OPT_FULL_COUNTS, 1 if full else 0)
+    try:
+        lab, core, cnt, ncl = native.cluster(_dev(X), eps, ms, native.metric_code(metric),
+                                             want_counts=full)
+    finally:
+        ctx.set_option(native.PD_OPT_FULL_COUNTS, 0)
+    out = (lab.cpu().numpy().astype(np.int64), core.cpu().numpy(), ncl)
+    if full:
+        out = out + (cnt.cpu().numpy().astype(np.int64),)
+    return out
+
+
+# ------------------------------------------------------------ pd_cluster
+def test_sklearn_kats(native):
+    z = np.load(f"{GOLDEN}/sklearn_kat.npz")
+    for ms in (1, 2, 3, 4):
+        lab, core, _ = _cluster(native, z["toy_X"], 1.0, ms)
+        assert np.array_equal(lab, z[f"toy_ms{ms}_labels"])
+        assert np.array_equal(np.nonzero(core)[0], z[f"toy_ms{ms}_core"])
+    assert np.array_equal(np.nonzero(_cluster(native, z["bnd_a_X"], 2, 2)[1])[0], z["bnd_a_core"])
+    assert np.array_equal(np.nonzero(_cluster(native, z["bnd_b_X"], 1, 2)[1])[0],
+                          z["bnd_b_core_eps1"])
+    assert np.array_equal(np.nonzero(_cluster(native, z["bnd_b_X"], 0.99, 2)[1])[0],
+                          z["bnd_b_core_eps099"])
+    lab, core, _ = _cluster(native, z["clustered_X"], 0.8, 10)
+    assert np.array_equal(lab, z["clustered_labels"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_cluster_equals_sklearn(native, name):
+    g = load_golden(name)
+    lab, core, ncl, cnt = _cluster(native, g["X"], float(g["eps"]), int(g["min_samples"]),
+                                   _metric(g), full=True)
+    assert np.array_equal(cnt, g["sk_counts"])
+    assert np.array_equal(core, g["sk_core"])
+    assert np.array_equal(lab, g["sk_labels"])
+    assert ncl == int(g["sk_labels"].max()) + 1
+
+
+# ------------------------------------------------------------ KD + halo
+def _kd_arrays(splits):
+    sp = np.array([s[:6] for s in splits], np.int64).reshape(-1, 6)
+    sf = np.array([s[6:] for s in splits], np.float64).reshape(-1, 3)
+    return sp, sf
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_kd_partitioner_sequential_is_bit_exact_with_reference(native, name):
+    """sums='sequential': every split, boundary, box and owner label is
+    bit-identical to the reference run (same fold order)."""
+    from pypardis_amd import KDPartitioner
+    g = load_golden(name)
+    kd = KDPartitioner(_dev(g["X"]), _P(g), sums="sequential")
+    sp, sf = _kd_arrays(kd.splits)
+    assert np.array_equal(sp, g["splits"])
+    assert np.array_equal(sf, g["split_f"])
+    assert np.array_equal(kd.box_array()[:, 0], g["box_lo"])
+    assert np.array_equal(kd.box_array()[:, 1], g["box_hi"])
+    assert np.array_equal(kd.labels.cpu().numpy(), g["owner"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_kd_partitioner_exact_sums_match_oracle(native, name):
+    """Default sums='exact': bit-identical to the oracle's correctly rounded
+    restatement (and to the reference wherever its decision is not a tie —
+    tests/test_oracle.py::test_exact_sums_agree_with_reference_except_ties)."""
+    from pypardis_amd import KDPartitioner
+    g = load_golden(name)
+    kd = KDPartitioner(_dev(g["X"]), _P(g))
+    ref = oracle.kd_partition(g["X"], _P(g), sums="exact")
+    sp, sf = _kd_arrays(kd.splits)
+    rp, rf = _kd_arrays(ref["splits"])
+    assert np.array_equal(sp, rp)
+    assert np.array_equal(sf, rf)
+    assert np.array_equal(kd.box_array()[:, 0], ref["box_lo"])
+    assert np.array_equal(kd.box_array()[:, 1], ref["box_hi"])
+    assert np.array_equal(kd.labels.cpu().numpy(), ref["owner"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_halo_members_match_reference(native, name):
+    g = load_golden(name)
+    ebox = np.stack([g["ebox_lo"], g["ebox_hi"]], axis=1)
+    counts, members = native.halo_members(_dev(g["X"]), ebox)
+    m = members.cpu().numpy()
+    off = np.concatenate([[0], np.cumsum(counts)])
+    pairs = np.array(sorted((L, int(i)) for L in range(len(counts)) for i in m[off[L]:off[L + 1]]),
+                     np.int64).reshape(-1, 2)
+    assert np.array_equal(pairs, g["halo"])
+
+
+# ------------------------------------------------------------ end to end
+@pytest.mark.parametrize("name", NAMES)
+def test_train_equals_global_dbscan(native, name):
+    import dbscan   # the drop-in import name
+    g = load_golden(name)
+    X = g["X"]
+    model = dbscan.DBSCAN(eps=float(g["eps"]), min_samples=int(g["min_samples"]),
+                          metric=_metric(g), max_partitions=_P(g), kd_sums="sequential")
+    model.train([(i, X[i]) for i in range(len(X))])
+    a = model.assignments()
+    assert [k for k, _ in a] == list(range(len(X)))
+    assert np.array_equal(np.array([v for _, v in a]), g["sk_labels"])
+    assert np.array_equal(model.core_sample_mask_.cpu().numpy(), g["sk_core"])
+    P = int(g["P"])
+    assert sorted(model.bounding_boxes) == list(range(P))
+    for L in range(P):
+        assert np.array_equal(model.expanded_boxes[L].lower, g["ebox_lo"][L])
+        assert np.array_equal(model.expanded_boxes[L].upper, g["ebox_hi"][L])
+        ref = g["halo"][g["halo"][:, 0] == L, 1]
+        assert np.array_equal(np.sort(model.neighbors[L].keys()), ref)
+
+
+def test_dbscan_partition_string_records(native):
+    from pypardis_amd import dbscan_partition
+    g = load_golden("c0_p3")
+    po = g["part_out"]
+    X = g["X"]
+    params = {"eps": float(g["eps"]), "min_samples": int(g["min_samples"]), "metric": "euclidean"}
+    for L in range(int(g["P"])):
+        rows = po[po[:, 0] == L]
+        recs = [((int(k), L), X[k]) for k in rows[:, 1]]
+        out = list(dbscan_partition(iter(recs), params))
+        want = [(int(k), "%i:%i%s" % (L, c, "" if core else "*")) for _, k, c, core in rows]
+        assert [(int(k), s) for k, s in out] == want
+
+
+# ------------------------------------------------------------ larger vs oracle
+CASES = [
+    ("2d_c1slice", dict(n=150_000, d=2, side=100 * (0.015 ** 0.5), n_centers=1, sigma=1.0,
+                        noise_frac=0.1, seed=21), 0.05, 10, "euclidean", 4),
+    ("3d_c2slice", dict(n=200_000, d=3, side=100 * (0.002 ** (1 / 3)), n_centers=1, sigma=1.0,
+                        noise_frac=0.1, seed=22), 0.1, 10, "euclidean", 8),
+    ("3d_dense", dict(n=120_000, d=3, side=8.0, n_centers=6, sigma=0.5, noise_frac=0.05,
+                      seed=23), 0.08, 20, "euclidean", 8),
+    ("2d_cityblock", dict(n=100_000, d=2, side=30.0, n_centers=10, sigma=0.7, noise_frac=0.2,
+                          seed=24), 0.06, 8, "cityblock", 5),
+    ("4d", dict(n=60_000, d=4, side=6.0, n_centers=8, sigma=0.4, noise_frac=0.1, seed=25),
+     0.25, 10, "euclidean", 4),
+    ("1d", dict(n=50_000, d=1, side=50.0, n_centers=20, sigma=0.3, noise_frac=0.3, seed=26),
+     0.002, 5, "euclidean", 4),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_train_matches_oracle(native, case):
+    from pypardis_amd import DBSCAN, synth
+    _, kw, eps, ms, metric, P = case
+    X = synth.blobs_noise(**kw)
+    lab_o, core_o, cnt_o, _ = oracle.dbscan(X, eps, ms, metric)
+    lab, core, ncl, cnt = _cluster(native, X, eps, ms, metric, full=True)
+    assert np.array_equal(cnt, cnt_o)
+    assert np.array_equal(core, core_o)
+    assert np.array_equal(lab, lab_o)
+    m = DBSCAN(eps=eps, min_samples=ms, metric=metric, max_partitions=P).train(_dev(X))
+    assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)
+    assert m.n_clusters_ == ncl
+
+
+def test_fp64_input_exact(native):
+    from pypardis_amd import synth
+    X = synth.blobs_noise(40_000, 2, side=10.0, n_centers=5, sigma=0.3, seed=31).astype(np.float64)
+    X += np.random.default_rng(0).uniform(-1e-9, 1e-9, X.shape)   # not fp32-representable
+    lab_o, core_o, _, _ = oracle.dbscan(X, 0.05, 7)
+    lab, core, _ = _cluster(native, X, 0.05, 7)
+    assert np.array_equal(lab, lab_o) and np.array_equal(core, core_o)
+
+
+def test_exact_ties_lattice(native):
+    g = np.arange(60, dtype=np.float32) * np.float32(0.05)
+    X = np.stack(np.meshgrid(g, g, indexing="ij"), -1).reshape(-1, 2)
+    for eps in (float(np.float32(0.05)), 0.05, float(np.float32(0.05) * np.sqrt(2))):
+        lab_o, core_o, cnt_o, _ = oracle.dbscan(X, eps, 5)
+        lab, core, _, cnt = _cluster(native, X, eps, 5, full=True)
+        assert np.array_equal(cnt, cnt_o), eps
+        assert np.array_equal(lab, lab_o), eps
+
+
+def test_edge_cases(native):
+    from pypardis_amd import DBSCAN
+    # all identical points, several partitions (A5)
+    X = np.full((500, 3), 0.7, np.float32)
+    m = DBSCAN(eps=0.1, min_samples=5, max_partitions=4).train(_dev(X))
+    assert np.all(m.labels_.cpu().numpy() == 0)
+    # min_samples = 1: every point is core
+    X = np.random.default_rng(1).uniform(0, 100, (2000, 2)).astype(np.float32)
+    lab_o, _, _, _ = oracle.dbscan(X, 0.5, 1)
+    lab, core, _ = _cluster(native, X, 0.5, 1)
+    assert np.array_equal(lab, lab_o) and core.all()
+    # eps larger than the whole extent: one cell
+    lab, core, ncl = _cluster(native, X, 1000.0, 3)
+    assert ncl == 1 and np.all(lab == 0)
+    # single point; all noise
+    lab, core, ncl = _cluster(native, X[:1], 0.1, 2)
+    assert ncl == 0 and lab[0] == -1
+    # empty input
+    lab, core, ncl = _cluster(native, np.zeros((0, 2), np.float32), 0.1, 2)
+    assert ncl == 0 and len(lab) == 0
+    # negative / huge offsets (grid clipped to the data, not the sentinel box)
+    Y = (X - np.float32(1e6)).astype(np.float32)
+    lab_o, _, _, _ = oracle.dbscan(Y, 0.5, 3)
+    m = DBSCAN(eps=0.5, min_samples=3, max_partitions=4).train(_dev(Y))
+    assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)
+
+
+def test_nan_rejected(native):
+    from pypardis_amd import _native
+    X = np.zeros((10, 2), np.float32)
+    X[3, 1] = np.nan
+    with pytest.raises(_native.PardisError):
+        _native.cluster(_dev(X), 0.1, 2)
+    from pypardis_amd import DBSCAN
+    with pytest.raises(ValueError):
+        DBSCAN(eps=0.1, min_samples=2).train(_dev(X))
+
+
+def test_partition_count_invariance_large(native):
+    """Size-independent property at 4M 3-D points: labels do not depend on
+    max_partitions (the halo + merge reproduce the one-partition answer)."""
+    from pypardis_amd import DBSCAN, synth
+    X, cfg = synth.make_config("C2", n=4_000_000)
+    Xd = _dev(X)
+    ref, core1, _, nc1 = native.cluster(Xd, cfg["eps"], cfg["min_samples"])
+    for P in (2, 8, 13):
+        m = DBSCAN(eps=cfg["eps"], min_samples=cfg["min_samples"], max_partitions=P).train(Xd)
+        assert m.n_clusters_ == nc1
+        assert torch.equal(m.labels_, ref), P
+        assert torch.equal(m.core_sample_mask_, core1), P
+    # sklearn numbering: cluster ids appear in order of their smallest core index
+    lab = ref.cpu().numpy()
+    c = core1.cpu().numpy().astype(bool)
+    idx = np.nonzero(c)[0]
+    first = np.full(nc1, -1)
+    seen = np.zeros(nc1, bool)
+    u, fi = np.unique(lab[idx], return_index=True)
+    first[u] = idx[fi]
+    assert np.all(np.diff(first) > 0)

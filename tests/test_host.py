@@ -1,0 +1,89 @@
+"""CPU tests of the host-side logic that mirrors the reference (no GPU)."""
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import golden_names, load_golden
+from pypardis_amd import BoundingBox, ClusterAggregator, default_value
+from pypardis_amd import partition as part
+from pypardis_amd._data import as_points
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 5, 8, 16, 17, 64, 100])
+def test_split_schedule_matches_reference_bfs(P):
+    assert part._split_schedule(P) == oracle.split_schedule(P)
+
+
+def test_split_schedule_label_order_p8():
+    # 0→1 · 0→2, 1→3 · 0→4, 2→5, 1→6, 3→7
+    assert part._split_schedule(8) == [[(0, 1)], [(0, 2), (1, 3)], [(0, 4), (2, 5), (1, 6), (3, 7)]]
+
+
+@pytest.mark.parametrize("name", golden_names())
+def test_bounds_expression_bit_exact(name):
+    g = load_golden(name)
+    for (mean, var, boundary), (_, _, _, cand, _, _) in zip(g["split_f"], g["splits"]):
+        assert part._bounds(mean, var)[cand] == boundary
+
+
+def test_bounding_box_sentinels_and_ops():
+    b = BoundingBox(k=2)
+    assert b.lower[0] == sys.float_info.max and b.upper[0] == sys.float_info.min
+    u = b.union(BoundingBox(np.array([-5.0, 1.0])))
+    assert u.upper[0] == sys.float_info.min and u.lower[0] == -5.0 and u.upper[1] == 1.0
+    left, right = BoundingBox([0.0, 0.0], [2.0, 2.0]).split(1, 0.5)
+    assert left.upper[1] == 0.5 and right.lower[1] == 0.5 and left.lower[1] == 0.0
+    e = BoundingBox([0.0], [1.0]).expand(0.25)
+    assert e.lower[0] == -0.25 and e.upper[0] == 1.25
+    m = BoundingBox([0.0], [2.0]).expand(0.5, how="multiply")
+    assert m.lower[0] == -1.0 and m.upper[0] == 3.0
+    assert BoundingBox([0.0, 0.0], [1.0, 1.0]).contains(np.array([1.0, 0.0]))
+    assert not BoundingBox([0.0, 0.0], [1.0, 1.0]).contains(np.array([1.0, 1.0 + 1e-12]))
+    i = BoundingBox([0.0], [2.0]).intersection(BoundingBox([1.0], [3.0]))
+    assert i.lower[0] == 1.0 and i.upper[0] == 2.0
+
+
+@pytest.mark.parametrize("name", ["c0", "neg_3k", "b3d_20k"])
+def test_expanded_boxes_from_golden_boxes(name):
+    g = load_golden(name)
+    eps = float(g["eps"])
+    for L in range(int(g["P"])):
+        e = BoundingBox(g["box_lo"][L], g["box_hi"][L]).expand(2 * eps)
+        assert np.array_equal(e.lower, g["ebox_lo"][L]) and np.array_equal(e.upper, g["ebox_hi"][L])
+
+
+def test_cluster_aggregator_links_core_labels_only():
+    agg = ClusterAggregator()
+    agg + (0, ["0:0", "1:3"])          # core in two neighbourhoods: link
+    agg + (1, ["1:3", "2:1"])
+    agg + (2, ["0:5*", "1:3"])         # border label must not link 0:5
+    agg + (3, ["0:5", "1:-1*"])
+    assert agg.fwd["0:0"] == agg.fwd["1:3"] == agg.fwd["2:1"]
+    assert agg.fwd["0:5"] != agg.fwd["0:0"]
+    assert "1:-1*" not in agg.fwd and "0:5*" not in agg.fwd
+    other = ClusterAggregator()
+    other + (9, ["0:5", "2:1"])
+    agg + other
+    assert agg.fwd["0:5"] == agg.fwd["0:0"]
+    assert default_value() == sys.maxsize
+
+
+def test_as_points_forms_cpu():
+    X = np.random.default_rng(0).normal(size=(10, 3)).astype(np.float32)
+    p = as_points(X, device="cpu")
+    assert p.X.dtype == torch.float32 and p.keys is None and p.n == 10
+    p = as_points([(i, X[i]) for i in range(10)], device="cpu")
+    assert p.keys is None and torch.equal(p.X, torch.from_numpy(X))
+    p = as_points([(f"k{i}", X[i].astype(np.float64)) for i in range(10)], device="cpu")
+    assert p.X.dtype == torch.float64 and p.keys[3] == "k3"
+
+    class RDD:
+        def collect(self):
+            return [(10 - i, X[i]) for i in range(10)]
+    p = as_points(RDD(), device="cpu")
+    assert list(p.keys) == list(range(10, 0, -1))
+    p = as_points((np.arange(10) * 2, X), device="cpu")
+    assert p.keys[1] == 2

@@ -50,16 +50,21 @@ enum pd_metric { PD_EUCLIDEAN = 0, PD_CITYBLOCK = 1 };
 enum pd_option {
     PD_OPT_TIMING = 1,      /* record per-stage HIP events inside pd_train */
     PD_OPT_FULL_COUNTS = 2,  /* neighbour counts without the >= min_samples early exit */
-    PD_OPT_SEQUENTIAL_MOMENTS = 3  /* pd_kd_moments folds points in index order, exactly as
+    PD_OPT_SEQUENTIAL_MOMENTS = 3, /* pd_kd_moments folds points in index order, exactly as
                                       the reference's single-slice aggregate (slow; for
                                       bit-identical split boundaries).  Default: correctly
                                       rounded, order-independent double-double sums. */
+    PD_OPT_LINK_MODE = 4,  /* union strategy (tuning): 0 (default) initial forest from the count
+                              pass's smallest neighbour + pointer jumping, then lock-free union
+                              over core-core edges; 2 the union pass alone; 1 diagnostic sweep
+                              only (labels invalid) */
+    PD_OPT_JUMP_ROUNDS = 5 /* pointer-jumping rounds for link mode 0 (default 2) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */
 enum pd_timing_slot {
     PD_T_HALO = 0, PD_T_SORT, PD_T_GATHER, PD_T_CELLS, PD_T_COUNT, PD_T_LINK, PD_T_MERGE,
-    PD_T_BORDER, PD_T_LABEL, PD_T_TOTAL, PD_T_RECORDS, PD_T_CELLS_N, PD_T_GRID_CELLS,
+    PD_T_ROOTS, PD_T_BORDER, PD_T_LABEL, PD_T_TOTAL, PD_T_RECORDS, PD_T_CELLS_N, PD_T_GRID_CELLS,
     PD_T_KEY_BITS, PD_T_NSLOTS
 };
 

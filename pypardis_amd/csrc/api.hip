@@ -110,6 +110,10 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.full_counts = value != 0;
         else if (option == PD_OPT_SEQUENTIAL_MOMENTS)
             ctx->c.seq_moments = value != 0;
+        else if (option == PD_OPT_LINK_MODE)
+            ctx->c.link_mode = (int)value;
+        else if (option == PD_OPT_JUMP_ROUNDS)
+            ctx->c.jump_rounds = (int)value;
         else
             throw Error(PD_EINVAL, "unknown option");
     });
@@ -120,7 +124,7 @@ int32_t pd_ctx_timings(pd_ctx* ctx, double* out, int32_t n) {
         if (!ctx || !out) throw Error(PD_EINVAL, "null argument");
         const Timings& t = ctx->c.t;
         const double v[PD_T_NSLOTS] = {t.halo,    t.sort,   t.gather, t.cells,
-                                       t.count,   t.link,   t.merge,  t.border,
+                                       t.count,   t.link,   t.merge,  t.roots,  t.border,
                                        t.label,   t.total,  (double)t.records,
                                        (double)t.cells_n, (double)t.grid_cells,
                                        (double)t.key_bits};

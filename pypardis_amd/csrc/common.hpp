@@ -12,7 +12,9 @@ namespace pd {
 // Launch geometry: 256-thread blocks (4 waves), grid-stride beyond this.
 constexpr int kBlock = 256;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr uint32_t kOwnerBit = 0x80000000u;   // record value: point id | owner flag
+constexpr uint32_t kOwnerBit = 0x80000000u;   // record value: point id | flags
+constexpr uint32_t kDupBit = 0x40000000u;     // point lies in >= 2 neighbourhoods
+constexpr uint32_t kIdMask = 0x3FFFFFFFu;     // => n < 2^30 points per device
 constexpr int kMaxDim = 4;                    // grid path; d > 4 is the tile path
 constexpr int kMaxParts = 64;                 // one bit per neighbourhood in the halo mask
 

@@ -33,6 +33,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -84,20 +85,122 @@ __device__ __forceinline__ void uf_unite(uint32_t* par, uint32_t a, uint32_t b) 
     }
 }
 
+// L1-cacheable variant for the hot link loop: workgroup-scope relaxed loads
+// compile to plain global_loads; stale values are older ancestors, which the
+// algorithm tolerates (every retry starts from the CAS's returned value, and
+// indices only decrease, so it terminates).  Halving stores stay write-through.
+__device__ __forceinline__ uint32_t ld_l1(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ uint32_t uf_find_l1(uint32_t* par, uint32_t x) {
+    uint32_t p = ld_l1(par + x);
+    while (p != x) {
+        uint32_t g = ld_l1(par + p);
+        if (g == p) return p;
+        st_rlx(par + x, g);
+        x = g;
+        p = ld_l1(par + x);
+    }
+    return x;
+}
+
+// Link two roots (a = caller's current root); returns the caller's new root.
+__device__ __forceinline__ uint32_t uf_link_roots(uint32_t* par, uint32_t a, uint32_t b) {
+    while (a != b) {
+        if (a > b) {
+            uint32_t t = a;
+            a = b;
+            b = t;
+        }
+        uint32_t expected = b;
+        if (__hip_atomic_compare_exchange_strong(par + b, &expected, a, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return a;
+        b = uf_find_l1(par, expected);
+        a = uf_find_l1(par, a);
+    }
+    return a;
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+
+// atomicMin(base[key], val) for the lanes with `valid`, one atomic per
+// distinct key per wave: consecutive records mostly share a component, and a
+// big cluster's root otherwise takes ~1e5 serialised atomics.  Every lane of
+// the wave must call this (no early return before it).
+__device__ __forceinline__ void wave_atomic_min(uint32_t* base, bool valid, uint32_t key,
+                                                uint32_t val) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long active = __ballot(valid);
+    while (active) {
+        const int leader = __ffsll(active) - 1;
+        const uint32_t lk = (uint32_t)__shfl((int)key, leader, 64);
+        const bool mine = valid && ((active >> lane) & 1ull) && key == lk;
+        const uint32_t m = wave_min_u32(mine ? val : kNone);
+        if (lane == leader) atomicMin(base + lk, m);
+        active &= ~__ballot(mine);
+    }
+}
+
 template <typename T, int D>
 __device__ __forceinline__ void load_d(const T* __restrict__ X, uint64_t i, double (&v)[D]) {
 #pragma unroll
     for (int j = 0; j < D; ++j) v[j] = (double)X[i * D + j];
 }
 
-// sklearn kd_tree leaf predicate, exact.
-template <typename T, int D, int M>
-__device__ __forceinline__ bool within(const double (&a)[D], const T* __restrict__ b,
-                                       double eps, double eps2) {
+// Sorted-record layout: 3-D records are padded to 4 components so one
+// 16-byte (fp32) load fetches a candidate; other D are packed.
+template <int D>
+struct Stride {
+    static constexpr int v = (D == 3) ? 4 : D;
+};
+
+template <typename T, int D>
+__device__ __forceinline__ void load_rec(const T* __restrict__ Xs, uint32_t j, double (&v)[D]) {
+    constexpr int S = Stride<D>::v;
+    if constexpr (std::is_same<T, float>::value && S == 4) {
+        const float4 f = *reinterpret_cast<const float4*>(Xs + (uint64_t)j * 4);
+        v[0] = f.x;
+        v[1] = f.y;
+        v[2] = f.z;
+        if constexpr (D == 4) v[3] = f.w;
+    } else if constexpr (std::is_same<T, float>::value && S == 2) {
+        const float2 f = *reinterpret_cast<const float2*>(Xs + (uint64_t)j * 2);
+        v[0] = f.x;
+        v[1] = f.y;
+    } else if constexpr (std::is_same<T, double>::value && S >= 2) {
+        const double2* p = reinterpret_cast<const double2*>(Xs + (uint64_t)j * S);
+        const double2 u = p[0];
+        v[0] = u.x;
+        v[1] = u.y;
+        if constexpr (S == 4) {
+            const double2 w = p[1];
+            v[2] = w.x;
+            if constexpr (D == 4) v[3] = w.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) v[k] = (double)Xs[(uint64_t)j * S + k];
+    }
+}
+
+// sklearn kd_tree leaf predicate, exact: fp64, axis order, every product and
+// sum rounded separately (no FMA), `<= eps*eps` (cityblock: `<= eps`).
+template <int D, int M>
+__device__ __forceinline__ bool within(const double (&a)[D], const double (&b)[D], double eps,
+                                       double eps2) {
     double acc = 0.0;
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-        const double t = __dadd_rn(a[j], -(double)b[j]);
+        const double t = __dadd_rn(a[j], -b[j]);
         if constexpr (M == 0)
             acc = __dadd_rn(acc, __dmul_rn(t, t));
         else
@@ -133,15 +236,17 @@ __device__ __forceinline__ bool in_box(const double (&v)[D], const PartGrid& g) 
     return in;
 }
 
-__device__ __forceinline__ uint32_t rank_lt(const uint64_t* __restrict__ bits,
-                                            const uint32_t* __restrict__ rank, uint64_t k) {
-    const uint64_t w = k >> 6;
+// Directory word (16 B, one load): occupancy bits of 64 consecutive cell
+// keys + the number of occupied cells before them.
+__device__ __forceinline__ uint32_t rank_lt(const uint4* __restrict__ dir, uint64_t k) {
+    const uint4 w = dir[k >> 6];
+    const uint64_t bits = ((uint64_t)w.y << 32) | (uint64_t)w.x;
     const uint32_t b = (uint32_t)(k & 63);
-    const uint64_t m = b ? (bits[w] & ((~0ull) >> (64 - b))) : 0ull;
-    return rank[w] + (uint32_t)__popcll(m);
+    const uint64_t m = b ? (bits & ((~0ull) >> (64 - b))) : 0ull;
+    return w.z + (uint32_t)__popcll(m);
 }
 
-// Partition of a record: part_start is sorted, P <= kMaxParts*4.
+// Partition of a record: part_start is sorted.
 __device__ __forceinline__ int part_of(const uint32_t* __restrict__ ps, int P, uint32_t r) {
     int lo = 0, hi = P - 1;
     while (lo < hi) {
@@ -163,22 +268,30 @@ struct Cells {
     const PartGrid* parts;
     const uint32_t* part_start;
     int P;
-    const uint64_t* bits;
-    const uint32_t* rank;
+    const uint4* dir;
     const uint32_t* cstart;
 };
 
-// Visit every candidate record j of the 3^(D-1) rows around record r's cell;
-// each row is one contiguous record range covering cells c0-1..c0+1.
-template <typename T, int D, typename F>
-__device__ __forceinline__ void for_rows(const Cells& C, const double (&a)[D], int L, F&& row) {
+template <int D>
+struct NRows {
+    static constexpr int v = (D == 1) ? 1 : (D == 2 ? 3 : (D == 3 ? 9 : 27));
+};
+
+// The 3^(D-1) candidate rows around a record's cell, each one contiguous
+// record range [s, e) covering cells c0-1..c0+1 of that row.  All lookups
+// are issued before any candidate is read (unrolled: independent loads).
+// Row q enumerates offsets in ascending key order.
+template <int D>
+__device__ __forceinline__ void row_ranges(const Cells& C, const double (&a)[D], int L,
+                                           uint32_t (&s)[NRows<D>::v],
+                                           uint32_t (&e)[NRows<D>::v]) {
     const PartGrid& g = C.parts[L];
     int64_t c[D];
     cell_of<D>(a, g, c);
     const int64_t x0 = c[0] > 0 ? c[0] - 1 : 0;
     const int64_t x1 = c[0] + 1 < g.nc[0] ? c[0] + 1 : g.nc[0] - 1;
-    constexpr int NR = (D == 1) ? 1 : (D == 2 ? 3 : (D == 3 ? 9 : 27));
-    for (int q = 0; q < NR; ++q) {
+#pragma unroll
+    for (int q = 0; q < NRows<D>::v; ++q) {
         int64_t cc[D];
         cc[0] = x0;
         int t = q;
@@ -190,12 +303,15 @@ __device__ __forceinline__ void for_rows(const Cells& C, const double (&a)[D], i
             ok &= (v >= 0) & (v < g.nc[j]);
             cc[j] = v;
         }
-        if (!ok) continue;
-        const uint64_t k0 = g.base + lin_of<D>(cc, g);
-        const uint64_t k1 = k0 + (uint64_t)(x1 - x0) + 1;
-        const uint32_t s = C.cstart[rank_lt(C.bits, C.rank, k0)];
-        const uint32_t e = C.cstart[rank_lt(C.bits, C.rank, k1)];
-        if (!row(s, e)) return;
+        if (ok) {
+            const uint64_t k0 = g.base + lin_of<D>(cc, g);
+            const uint64_t k1 = k0 + (uint64_t)(x1 - x0) + 1;
+            s[q] = C.cstart[rank_lt(C.dir, k0)];
+            e[q] = C.cstart[rank_lt(C.dir, k1)];
+        } else {
+            s[q] = 0;
+            e[q] = 0;
+        }
     }
 }
 
@@ -216,13 +332,14 @@ __global__ __launch_bounds__(kBlock) void halo_count_kernel(const T* __restrict_
 template <typename T, int D, typename K>
 __global__ __launch_bounds__(kBlock) void records_kernel(
     const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
-    const int32_t* __restrict__ owner, const uint64_t* __restrict__ off, K* __restrict__ keys,
-    uint32_t* __restrict__ vals) {
+    const int32_t* __restrict__ owner, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ hcnt, K* __restrict__ keys, uint32_t* __restrict__ vals) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     double v[D];
     load_d<T, D>(X, i, v);
     const int own = owner ? owner[i] : 0;
+    const uint32_t dup = hcnt[i] >= 2 ? kDupBit : 0u;
     uint64_t o = off[i];
     for (int L = 0; L < P; ++L) {
         const PartGrid& g = parts[L];
@@ -230,7 +347,7 @@ __global__ __launch_bounds__(kBlock) void records_kernel(
         int64_t c[D];
         cell_of<D>(v, g, c);
         keys[o] = (K)(g.base + lin_of<D>(c, g));
-        vals[o] = (uint32_t)i | (L == own ? kOwnerBit : 0u);
+        vals[o] = (uint32_t)i | dup | (L == own ? kOwnerBit : 0u);
         ++o;
     }
 }
@@ -241,9 +358,10 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const T* __restrict__ X,
                                                         T* __restrict__ Xs) {
     const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (r >= R) return;
-    const uint64_t i = vals[r] & ~kOwnerBit;
+    const uint64_t i = vals[r] & kIdMask;
+    constexpr int S = Stride<D>::v;
 #pragma unroll
-    for (int j = 0; j < D; ++j) Xs[r * D + j] = X[i * D + j];
+    for (int j = 0; j < S; ++j) Xs[r * S + j] = j < D ? X[i * D + j] : T(0);
 }
 
 template <typename K>
@@ -271,13 +389,26 @@ __global__ void part_start_kernel(const K* __restrict__ keys, uint64_t R,
 template <typename K>
 __global__ __launch_bounds__(kBlock) void run_flag_kernel(const K* __restrict__ keys, uint64_t R,
                                                           uint32_t* __restrict__ flag,
-                                                          unsigned long long* __restrict__ bits) {
+                                                          uint4* __restrict__ dir) {
     const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (r >= R) return;
     const uint64_t k = keys[r];
     const bool start = (r == 0) || ((uint64_t)keys[r - 1] != k);
     flag[r] = start ? 1u : 0u;
-    if (start) atomicOr(bits + (k >> 6), 1ull << (k & 63));
+    if (start) atomicOr(reinterpret_cast<unsigned long long*>(dir + (k >> 6)), 1ull << (k & 63));
+}
+
+struct DirPopc {
+    __device__ uint32_t operator()(const uint4& w) const {
+        return (uint32_t)__popc(w.x) + (uint32_t)__popc(w.y);
+    }
+};
+
+__global__ __launch_bounds__(kBlock) void dir_pack_kernel(uint4* __restrict__ dir,
+                                                          const uint32_t* __restrict__ rank,
+                                                          uint64_t W) {
+    const uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (w < W) dir[w].z = rank[w];
 }
 
 __global__ __launch_bounds__(kBlock) void cell_start_kernel(const uint32_t* __restrict__ flag,
@@ -295,60 +426,172 @@ __global__ __launch_bounds__(kBlock) void cell_start_kernel(const uint32_t* __re
     }
 }
 
-struct Popc {
-    __device__ uint32_t operator()(unsigned long long x) const { return (uint32_t)__popcll(x); }
-};
-
 // Neighbour count + core flag: the roofline kernel (SURVEY.md §8(d) B_nc).
+// Centre row first (the early exit usually fires inside it), candidates four
+// at a time so each lane keeps four 16-byte gathers in flight.  It also keeps
+// the smallest neighbour index it saw: for a core record whose smallest seen
+// neighbour is core and below it, that is a free initial parent for the
+// union-find (ECL-CC's init step without a sweep of its own).
 template <typename T, int D, int M>
 __global__ __launch_bounds__(kBlock) void count_kernel(const T* __restrict__ Xs, uint32_t R,
                                                        Cells C, double eps, double eps2,
                                                        uint32_t ms, int full,
                                                        uint8_t* __restrict__ core,
+                                                       uint32_t* __restrict__ mn_out,
                                                        uint32_t* __restrict__ cnt_out) {
+    constexpr int NR = NRows<D>::v;
     const uint32_t r = rec_index();
     if (r >= R) return;
     double a[D];
-    load_d<T, D>(Xs, r, a);
+    load_rec<T, D>(Xs, r, a);
     const int L = part_of(C.part_start, C.P, r);
-    uint32_t cnt = 0;
+    uint32_t s[NR], e[NR];
+    row_ranges<D>(C, a, L, s, e);
+    uint32_t cnt = 0, mn = r;
     const uint32_t stop = full ? 0xFFFFFFFFu : ms;
-    for_rows<T, D>(C, a, L, [&](uint32_t s, uint32_t e) {
-        for (uint32_t j = s; j < e; ++j) {
-            cnt += within<T, D, M>(a, Xs + (uint64_t)j * D, eps, eps2) ? 1u : 0u;
-            if (cnt >= stop) return false;
+#pragma unroll
+    for (int qq = 0; qq < NR; ++qq) {
+        const int q = (qq + NR / 2) % NR;
+        uint32_t j = s[q];
+        const uint32_t end = e[q];
+        for (; j + 4 <= end; j += 4) {
+            double b0[D], b1[D], b2[D], b3[D];
+            load_rec<T, D>(Xs, j, b0);
+            load_rec<T, D>(Xs, j + 1, b1);
+            load_rec<T, D>(Xs, j + 2, b2);
+            load_rec<T, D>(Xs, j + 3, b3);
+            const bool w0 = within<D, M>(a, b0, eps, eps2), w1 = within<D, M>(a, b1, eps, eps2),
+                       w2 = within<D, M>(a, b2, eps, eps2), w3 = within<D, M>(a, b3, eps, eps2);
+            cnt += (uint32_t)w0 + (uint32_t)w1 + (uint32_t)w2 + (uint32_t)w3;
+            const uint32_t h = w0 ? j : (w1 ? j + 1 : (w2 ? j + 2 : (w3 ? j + 3 : mn)));
+            mn = h < mn ? h : mn;
+            if (cnt >= stop) goto done;
         }
-        return true;
-    });
-    core[r] = cnt >= ms ? 1 : 0;
+        for (; j < end; ++j) {
+            double b0[D];
+            load_rec<T, D>(Xs, j, b0);
+            if (within<D, M>(a, b0, eps, eps2)) {
+                ++cnt;
+                mn = j < mn ? j : mn;
+            }
+            if (cnt >= stop) goto done;
+        }
+    }
+done:
+    // bit0: core; bit1: has a neighbour besides itself (else it is noise and
+    // the border pass skips it)
+    core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
+    mn_out[r] = mn;
     if (cnt_out) cnt_out[r] = cnt;
 }
 
+// Initial forest.  parent doubles as the core flag: kNone marks a non-core
+// record, so an edge test costs one load.
+__global__ __launch_bounds__(kBlock) void init_kernel(uint32_t R, const uint8_t* __restrict__ core,
+                                                      const uint32_t* __restrict__ mn,
+                                                      int use_mn, uint32_t* __restrict__ par) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= R) return;
+    uint32_t p = kNone;
+    if (core[r] & 1) {
+        p = r;
+        if (use_mn) {
+            const uint32_t m = mn[r];
+            if (m < r && (core[m] & 1)) p = m;
+        }
+    }
+    par[r] = p;
+}
+
 // Core-core edges (j > r only; the predicate is symmetric) → union-find.
+// The caller's root is cached: an edge to a record already under it costs
+// one L1 load, no find and no CAS.  The distance test comes first (its
+// operands are already loaded); the core flag is read only for neighbours.
+struct Linker {
+    uint32_t* par;
+    uint32_t rr;
+    __device__ __forceinline__ void edge(uint32_t j) {
+        const uint32_t pj = ld_l1(par + j);
+        if (pj == kNone || pj == rr) return;   // non-core, or already under our root
+        const uint32_t rj = uf_find_l1(par, pj);
+        if (rj == rr) return;
+        rr = uf_link_roots(par, rr, rj);
+    }
+};
+
 template <typename T, int D, int M>
 __global__ __launch_bounds__(kBlock) void link_kernel(const T* __restrict__ Xs, uint32_t R, Cells C,
                                                       double eps, double eps2,
                                                       const uint8_t* __restrict__ core,
                                                       uint32_t* __restrict__ par) {
+    constexpr int NR = NRows<D>::v;
     const uint32_t r = rec_index();
-    if (r >= R || !core[r]) return;
+    if (r >= R || !(core[r] & 1)) return;
     double a[D];
-    load_d<T, D>(Xs, r, a);
+    load_rec<T, D>(Xs, r, a);
     const int L = part_of(C.part_start, C.P, r);
-    for_rows<T, D>(C, a, L, [&](uint32_t s, uint32_t e) {
-        for (uint32_t j = (s > r + 1 ? s : r + 1); j < e; ++j) {
-            if (!core[j]) continue;
-            if (!within<T, D, M>(a, Xs + (uint64_t)j * D, eps, eps2)) continue;
-            uf_unite(par, r, j);
+    uint32_t s[NR], e[NR];
+    row_ranges<D>(C, a, L, s, e);
+    Linker lk{par, uf_find_l1(par, r)};
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        uint32_t j = s[q] > r + 1 ? s[q] : r + 1;
+        const uint32_t end = e[q];
+        for (; j + 4 <= end; j += 4) {
+            double b0[D], b1[D], b2[D], b3[D];
+            load_rec<T, D>(Xs, j, b0);
+            load_rec<T, D>(Xs, j + 1, b1);
+            load_rec<T, D>(Xs, j + 2, b2);
+            load_rec<T, D>(Xs, j + 3, b3);
+            const bool w0 = within<D, M>(a, b0, eps, eps2), w1 = within<D, M>(a, b1, eps, eps2),
+                       w2 = within<D, M>(a, b2, eps, eps2), w3 = within<D, M>(a, b3, eps, eps2);
+            if (w0) lk.edge(j);
+            if (w1) lk.edge(j + 1);
+            if (w2) lk.edge(j + 2);
+            if (w3) lk.edge(j + 3);
         }
-        return true;
-    });
+        for (; j < end; ++j) {
+            double b0[D];
+            load_rec<T, D>(Xs, j, b0);
+            if (within<D, M>(a, b0, eps, eps2)) lk.edge(j);
+        }
+    }
 }
 
-__global__ __launch_bounds__(kBlock) void iota_kernel(uint32_t* __restrict__ p, uint32_t R) {
+// One pointer-jumping round over the core records: par[r] = par[par[r]].
+__global__ __launch_bounds__(kBlock) void jump_kernel(uint32_t R, const uint8_t* __restrict__ core,
+                                                      uint32_t* __restrict__ par) {
     const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r < R) p[r] = r;
+    if (r >= R || !(core[r] & 1)) return;
+    par[r] = par[par[r]];   // chains hold core records only
 }
+
+// Diagnostic: the link sweep without unions (counts edges so nothing is dead).
+template <typename T, int D, int M>
+__global__ __launch_bounds__(kBlock) void link_sweep_kernel(const T* __restrict__ Xs, uint32_t R,
+                                                            Cells C, double eps, double eps2,
+                                                            const uint8_t* __restrict__ core,
+                                                            unsigned long long* __restrict__ edges) {
+    constexpr int NR = NRows<D>::v;
+    const uint32_t r = rec_index();
+    if (r >= R || !(core[r] & 1)) return;
+    double a[D];
+    load_rec<T, D>(Xs, r, a);
+    const int L = part_of(C.part_start, C.P, r);
+    uint32_t s[NR], e[NR];
+    row_ranges<D>(C, a, L, s, e);
+    uint32_t ne = 0;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        for (uint32_t j = s[q] > r + 1 ? s[q] : r + 1; j < e[q]; ++j) {
+            double b0[D];
+            load_rec<T, D>(Xs, j, b0);
+            if (within<D, M>(a, b0, eps, eps2) && (core[j] & 1)) ++ne;
+        }
+    }
+    atomicAdd(edges, (unsigned long long)ne);
+}
+
 
 // A point's copies in several neighbourhoods: link every core copy to one
 // representative (the smallest record), gluing the neighbourhoods' clusters.
@@ -356,8 +599,9 @@ __global__ __launch_bounds__(kBlock) void rep_kernel(const uint32_t* __restrict_
                                                      const uint8_t* __restrict__ core,
                                                      uint32_t* __restrict__ rep) {
     const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R || !core[r]) return;
-    atomicMin(rep + (vals[r] & ~kOwnerBit), r);
+    if (r >= R || !(core[r] & 1)) return;
+    const uint32_t v = vals[r];
+    if (v & kDupBit) atomicMin(rep + (v & kIdMask), r);
 }
 
 __global__ __launch_bounds__(kBlock) void merge_kernel(const uint32_t* __restrict__ vals,
@@ -366,8 +610,10 @@ __global__ __launch_bounds__(kBlock) void merge_kernel(const uint32_t* __restric
                                                        const uint32_t* __restrict__ rep,
                                                        uint32_t* __restrict__ par) {
     const uint32_t r = rec_index();
-    if (r >= R || !core[r]) return;
-    const uint32_t q = rep[vals[r] & ~kOwnerBit];
+    if (r >= R || !(core[r] & 1)) return;
+    const uint32_t v = vals[r];
+    if (!(v & kDupBit)) return;
+    const uint32_t q = rep[v & kIdMask];
     if (q != r) uf_unite(par, r, q);
 }
 
@@ -375,7 +621,7 @@ __global__ __launch_bounds__(kBlock) void flatten_kernel(uint32_t R,
                                                          const uint8_t* __restrict__ core,
                                                          uint32_t* __restrict__ par) {
     const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R || !core[r]) return;
+    if (r >= R || !(core[r] & 1)) return;
     uint32_t x = par[r];
     while (true) {
         const uint32_t p = par[x];
@@ -391,8 +637,10 @@ __global__ __launch_bounds__(kBlock) void gmin_kernel(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ par,
                                                       uint32_t* __restrict__ gmin) {
     const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R || !core[r]) return;
-    atomicMin(gmin + par[r], vals[r] & ~kOwnerBit);
+    const bool ok = r < R && (core[r] & 1);
+    const uint32_t root = ok ? par[r] : 0u;
+    const uint32_t pt = ok ? (vals[r] & kIdMask) : kNone;
+    wave_atomic_min(gmin, ok, root, pt);
 }
 
 // Owner records only: cluster key of the point (core: its component's
@@ -408,26 +656,49 @@ __global__ __launch_bounds__(kBlock) void border_kernel(
     if (r >= R) return;
     const uint32_t v = vals[r];
     if (!(v & kOwnerBit)) return;
-    const uint32_t pt = v & ~kOwnerBit;
-    if (core_out) core_out[pt] = core[r];
+    const uint32_t pt = v & kIdMask;
+    const uint8_t fl = core[r];
+    if (core_out) core_out[pt] = fl & 1;
     if (cnt_out) cnt_out[pt] = cnt_rec[r];
-    if (core[r]) {
+    if (fl & 1) {
         key_out[pt] = gmin[par[r]];
         return;
     }
+    if (!(fl & 2)) return;   // no neighbour at all: noise (key_out stays kNone)
+    constexpr int NR = NRows<D>::v;
     double a[D];
-    load_d<T, D>(Xs, r, a);
+    load_rec<T, D>(Xs, r, a);
     const int L = part_of(C.part_start, C.P, r);
+    uint32_t s[NR], e[NR];
+    row_ranges<D>(C, a, L, s, e);
     uint32_t best = kNone;
-    for_rows<T, D>(C, a, L, [&](uint32_t s, uint32_t e) {
-        for (uint32_t j = s; j < e; ++j) {
-            if (!core[j]) continue;
-            if (!within<T, D, M>(a, Xs + (uint64_t)j * D, eps, eps2)) continue;
-            const uint32_t k = gmin[par[j]];
-            best = k < best ? k : best;
+    auto take = [&](uint32_t j) {
+        const uint32_t pj = par[j];
+        if (pj == kNone) return;   // not core
+        const uint32_t k = gmin[pj];
+        best = k < best ? k : best;
+    };
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        uint32_t j = s[q];
+        const uint32_t end = e[q];
+        for (; j + 4 <= end; j += 4) {
+            double b0[D], b1[D], b2[D], b3[D];
+            load_rec<T, D>(Xs, j, b0);
+            load_rec<T, D>(Xs, j + 1, b1);
+            load_rec<T, D>(Xs, j + 2, b2);
+            load_rec<T, D>(Xs, j + 3, b3);
+            if (within<D, M>(a, b0, eps, eps2)) take(j);
+            if (within<D, M>(a, b1, eps, eps2)) take(j + 1);
+            if (within<D, M>(a, b2, eps, eps2)) take(j + 2);
+            if (within<D, M>(a, b3, eps, eps2)) take(j + 3);
         }
-        return true;
-    });
+        for (; j < end; ++j) {
+            double b0[D];
+            load_rec<T, D>(Xs, j, b0);
+            if (within<D, M>(a, b0, eps, eps2)) take(j);
+        }
+    }
     key_out[pt] = best;
 }
 
@@ -522,7 +793,7 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
     uint32_t* vals = ctx.arena.get<uint32_t>("vals", R);
     uint32_t* vals2 = ctx.arena.get<uint32_t>("vals2", R);
     hipLaunchKernelGGL((records_kernel<T, D, K>), dim3(blocks(n)), dim3(kBlock), 0, s, X, n, parts,
-                       P, a.owner, hoff, keys, vals);
+                       P, a.owner, hoff, hcnt, keys, vals);
     PD_HIP(hipGetLastError());
     tm.mark();   // 1
 
@@ -538,7 +809,7 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
         vals = vb.current();
     }
     tm.mark();   // 2
-    T* Xs = ctx.arena.get<T>("Xs", (size_t)R * D);
+    T* Xs = ctx.arena.get<T>("Xs", (size_t)R * Stride<D>::v);
     hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X, (uint64_t)R,
                        vals, Xs);
     tm.mark();   // 3
@@ -548,16 +819,16 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
     hipLaunchKernelGGL((part_start_kernel<K>), dim3((P + 1 + 63) / 64), dim3(64), 0, s, keys,
                        (uint64_t)R, parts, P, part_start);
     const uint64_t W = (Gtot >> 6) + 2;
-    uint64_t* bits = ctx.arena.get<uint64_t>("dir_bits", W);
+    uint4* dir = ctx.arena.get<uint4>("dir", W);
     uint32_t* rank = ctx.arena.get<uint32_t>("dir_rank", W);
-    PD_HIP(hipMemsetAsync(bits, 0, sizeof(uint64_t) * W, s));
+    PD_HIP(hipMemsetAsync(dir, 0, sizeof(uint4) * W, s));
     uint32_t* flag = ctx.arena.get<uint32_t>("flag", R);
     uint32_t* cid = ctx.arena.get<uint32_t>("cid", R);
     uint32_t* cstart = ctx.arena.get<uint32_t>("cstart", (size_t)R + 1);
     uint32_t* dncells = ctx.arena.get<uint32_t>("ncells", 4);
     if (R) {
         hipLaunchKernelGGL((run_flag_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s, keys,
-                           (uint64_t)R, flag, (unsigned long long*)bits);
+                           (uint64_t)R, flag, dir);
         size_t tb = 0;
         PD_HIP(rocprim::exclusive_scan(nullptr, tb, flag, cid, 0u, (size_t)R,
                                        rocprim::plus<uint32_t>(), s));
@@ -570,34 +841,48 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
         PD_HIP(hipMemsetAsync(cstart, 0, sizeof(uint32_t), s));
     }
     {
-        rocprim::transform_iterator<unsigned long long*, Popc, uint32_t> pit(
-            (unsigned long long*)bits, Popc());
+        rocprim::transform_iterator<const uint4*, DirPopc, uint32_t> pit(dir, DirPopc());
         size_t tb = 0;
         PD_HIP(rocprim::exclusive_scan(nullptr, tb, pit, rank, 0u, (size_t)W,
                                        rocprim::plus<uint32_t>(), s));
         void* tmp = ctx.arena.get<char>("scan_tmp", tb);
         PD_HIP(rocprim::exclusive_scan(tmp, tb, pit, rank, 0u, (size_t)W,
                                        rocprim::plus<uint32_t>(), s));
+        hipLaunchKernelGGL(dir_pack_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, rank, W);
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 4
 
-    Cells C{parts, part_start, P, bits, rank, cstart};
+    Cells C{parts, part_start, P, dir, cstart};
     const double eps = a.eps, eps2 = a.eps * a.eps;
     uint8_t* core = ctx.arena.get<uint8_t>("core", R);
+    uint32_t* mn = ctx.arena.get<uint32_t>("minnbr", R);
     uint32_t* cnt_rec = a.counts ? ctx.arena.get<uint32_t>("cnt_rec", R) : nullptr;
     if (R)
         hipLaunchKernelGGL((count_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R, C,
-                           eps, eps2, (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0, core,
+                           eps, eps2, (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0, core, mn,
                            cnt_rec);
     PD_HIP(hipGetLastError());
     tm.mark();   // 5
 
     uint32_t* par = ctx.arena.get<uint32_t>("parent", R);
     if (R) {
-        hipLaunchKernelGGL(iota_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, par, R);
-        hipLaunchKernelGGL((link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R, C,
-                           eps, eps2, core, par);
+        const int mode = ctx.link_mode;
+        hipLaunchKernelGGL(init_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, mn,
+                           mode == 0 ? 1 : 0, par);
+        if (mode == 1) {   // diagnostic: sweep cost alone (labels are NOT valid)
+            unsigned long long* dedge = ctx.arena.get<unsigned long long>("edges", 1);
+            PD_HIP(hipMemsetAsync(dedge, 0, 8, s));
+            hipLaunchKernelGGL((link_sweep_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                               Xs, R, C, eps, eps2, core, dedge);
+        } else {
+            if (mode == 0)
+                for (int it = 0; it < ctx.jump_rounds; ++it)
+                    hipLaunchKernelGGL(jump_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core,
+                                       par);
+            hipLaunchKernelGGL((link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
+                               C, eps, eps2, core, par);
+        }
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 6
@@ -608,6 +893,7 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
         hipLaunchKernelGGL(merge_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, vals, R, core, rep,
                            par);
     }
+    tm.mark();   // 7
     uint32_t* gmin = ctx.arena.get<uint32_t>("gmin", R);
     if (R) {
         hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
@@ -616,7 +902,7 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
                            gmin);
     }
     PD_HIP(hipGetLastError());
-    tm.mark();   // 7
+    tm.mark();   // 8
 
     uint32_t* key_out = ctx.arena.get<uint32_t>("key_out", n);
     PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
@@ -625,7 +911,7 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
         hipLaunchKernelGGL((border_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R, C,
                            eps, eps2, vals, core, par, gmin, cnt_rec, key_out, a.core, a.counts);
     PD_HIP(hipGetLastError());
-    tm.mark();   // 8
+    tm.mark();   // 9
 
     uint32_t* rflag = ctx.arena.get<uint32_t>("rflag", n);
     uint32_t* rnk = ctx.arena.get<uint32_t>("rnk", n);
@@ -643,7 +929,7 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
                            n, a.labels, dncl);
     }
     PD_HIP(hipGetLastError());
-    tm.mark();   // 9
+    tm.mark();   // 10
     int64_t* hres = (int64_t*)pinned(ctx, 2 * sizeof(int64_t));
     PD_HIP(hipMemcpyAsync(hres, dncl, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     uint32_t* hnc = (uint32_t*)(hres + 1);
@@ -664,9 +950,10 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
         ctx.t.count = tm.span(4, 5);
         ctx.t.link = tm.span(5, 6);
         ctx.t.merge = tm.span(6, 7);
-        ctx.t.border = tm.span(7, 8);
-        ctx.t.label = tm.span(8, 9);
-        ctx.t.total = tm.span(0, 9);
+        ctx.t.roots = tm.span(7, 8);
+        ctx.t.border = tm.span(8, 9);
+        ctx.t.label = tm.span(9, 10);
+        ctx.t.total = tm.span(0, 10);
     }
 }
 
@@ -698,7 +985,7 @@ void train(Ctx& ctx, TrainArgs& a) {
     if (a.min_samples < 1) throw Error(-1, "min_samples must be >= 1");
     if (a.metric != 0 && a.metric != 1) throw Error(-1, "metric must be 0 (euclidean) or 1 (cityblock)");
     if (a.P < 1) throw Error(-1, "need at least one neighbourhood");
-    if (a.n >= (int64_t)kOwnerBit) throw Error(-5, "n must be < 2^31 per device");
+    if (a.n > (int64_t)kIdMask) throw Error(-5, "n must be < 2^30 points per device");
     if (!a.labels && a.n) throw Error(-1, "labels output is required");
     ctx.t = Timings{};
     const int d = a.d;

@@ -44,7 +44,7 @@ struct Arena {
 struct Timings {
     // milliseconds of the last pd_train call, HIP events on the call's stream
     float halo = 0, sort = 0, gather = 0, cells = 0, count = 0, link = 0, merge = 0,
-          border = 0, label = 0, total = 0;
+          roots = 0, border = 0, label = 0, total = 0;
     int64_t records = 0, cells_n = 0, grid_cells = 0, core_records = 0, key_bits = 0;
 };
 
@@ -55,6 +55,8 @@ struct Ctx {
     bool timing = false;
     bool full_counts = false;    // debug: count every neighbour (no early exit)
     bool seq_moments = false;    // reference-order (sequential) KD moment sums
+    int link_mode = 0;           // 0 init forest + jumps + union; 2 union only; 1 diagnostic
+    int jump_rounds = 2;
     Timings t;
     hipEvent_t ev[16] = {};
 };

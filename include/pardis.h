@@ -58,7 +58,10 @@ enum pd_option {
                               pass's smallest neighbour + pointer jumping, then lock-free union
                               over core-core edges; 2 the union pass alone; 1 diagnostic sweep
                               only (labels invalid) */
-    PD_OPT_JUMP_ROUNDS = 5 /* pointer-jumping rounds for link mode 0 (default 2) */
+    PD_OPT_JUMP_ROUNDS = 5, /* pointer-jumping rounds for link mode 0 (default 4) */
+    PD_OPT_XSUB = 6         /* sub-cells per eps along axis 0 (default 2): finer rows follow
+                               the eps-ball's chord more tightly, at 1/xsub the directory
+                               density */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -38,12 +38,15 @@ inline unsigned grid_for(int64_t n, int64_t cap = 256 * 64) {
 }
 
 // Per-neighbourhood grid: cell side = eps * (1 + 2^-20) so that any pair the
-// fp64 predicate can accept lies in adjacent cells; origin and extent clipped
+// fp64 predicate can accept lies in adjacent rows; axis 0 (the row axis) is
+// cut finer (eps/xsub) so a row's candidate range can follow the eps-ball's
+// chord at the query point.  Origin and extent clipped
 // to the data's tight bbox (the reference's root box can reach to ±0 through
 // the float_info.min sentinel, R:dbscan/geometry.py:28-29).
 struct PartGrid {
     double lo[kMaxDim];     // origin (fp64)
-    double inv;             // 1 / cell side
+    double inv[kMaxDim];    // 1 / cell side per axis (axis 0 is split into xsub sub-cells)
+    double cs[kMaxDim];     // cell side per axis
     int64_t nc[kMaxDim];    // cells per axis (0 => empty neighbourhood)
     uint64_t base;          // first key of this neighbourhood
     double elo[kMaxDim];    // expanded box (halo membership test), inclusive

@@ -213,7 +213,7 @@ template <int D>
 __device__ __forceinline__ void cell_of(const double (&v)[D], const PartGrid& g, int64_t (&c)[D]) {
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-        int64_t q = (int64_t)floor((v[j] - g.lo[j]) * g.inv);
+        int64_t q = (int64_t)floor((v[j] - g.lo[j]) * g.inv[j]);
         q = q < 0 ? 0 : q;
         q = q >= g.nc[j] ? g.nc[j] - 1 : q;
         c[j] = q;
@@ -277,33 +277,66 @@ struct NRows {
     static constexpr int v = (D == 1) ? 1 : (D == 2 ? 3 : (D == 3 ? 9 : 27));
 };
 
-// The 3^(D-1) candidate rows around a record's cell, each one contiguous
-// record range [s, e) covering cells c0-1..c0+1 of that row.  All lookups
-// are issued before any candidate is read (unrolled: independent loads).
-// Row q enumerates offsets in ascending key order.
-template <int D>
-__device__ __forceinline__ void row_ranges(const Cells& C, const double (&a)[D], int L,
+// The 3^(D-1) candidate rows around a record's cell.  For each row the
+// candidate x-range is the chord of the eps-ball at the query point: the
+// distance from the point to the row's slab in the other axes leaves a
+// half-width w = sqrt(eps^2 - d^2) (cityblock: eps - d) along axis 0, and
+// rows the ball cannot reach are skipped.  d is shrunk and w grown by a
+// 2^-20 relative slack, far above any rounding, so no pair the exact
+// predicate accepts is ever cut.  Each range is one contiguous record range;
+// all lookups are issued before any candidate is read (unrolled).  Row q
+// enumerates offsets in ascending key order.
+template <int D, int M>
+__device__ __forceinline__ void row_ranges(const Cells& C, const double (&a)[D], int L, double eps,
                                            uint32_t (&s)[NRows<D>::v],
                                            uint32_t (&e)[NRows<D>::v]) {
     const PartGrid& g = C.parts[L];
     int64_t c[D];
-    cell_of<D>(a, g, c);
-    const int64_t x0 = c[0] > 0 ? c[0] - 1 : 0;
-    const int64_t x1 = c[0] + 1 < g.nc[0] ? c[0] + 1 : g.nc[0] - 1;
+    double f[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const double u = (a[j] - g.lo[j]) * g.inv[j];
+        int64_t q = (int64_t)floor(u);
+        q = q < 0 ? 0 : q;
+        q = q >= g.nc[j] ? g.nc[j] - 1 : q;
+        c[j] = q;
+        double fr = u - (double)q;
+        f[j] = fr < 0.0 ? 0.0 : (fr > 1.0 ? 1.0 : fr);
+    }
+    const double slack = eps * (1.0 / 1048576.0);
 #pragma unroll
     for (int q = 0; q < NRows<D>::v; ++q) {
         int64_t cc[D];
-        cc[0] = x0;
         int t = q;
         bool ok = true;
+        double d2 = 0.0, d1 = 0.0;
 #pragma unroll
         for (int j = 1; j < D; ++j) {
-            const int64_t v = c[j] + (t % 3) - 1;
+            const int o = (t % 3) - 1;
             t /= 3;
+            const int64_t v = c[j] + o;
             ok &= (v >= 0) & (v < g.nc[j]);
             cc[j] = v;
+            double dist = o == 0 ? 0.0 : (o < 0 ? f[j] : 1.0 - f[j]) * g.cs[j] - slack;
+            dist = dist > 0.0 ? dist : 0.0;
+            d2 += dist * dist;
+            d1 += dist;
         }
+        double w;
+        if constexpr (M == 0) {
+            ok &= d2 <= eps * eps;
+            w = sqrt(fmax(eps * eps - d2, 0.0));
+        } else {
+            ok &= d1 <= eps;
+            w = eps - d1;
+        }
+        w = w * (1.0 + 1.0 / 1048576.0) + slack;
         if (ok) {
+            int64_t x0 = (int64_t)floor((a[0] - w - g.lo[0]) * g.inv[0]);
+            int64_t x1 = (int64_t)floor((a[0] + w - g.lo[0]) * g.inv[0]);
+            x0 = x0 < 0 ? 0 : x0;
+            x1 = x1 >= g.nc[0] ? g.nc[0] - 1 : x1;
+            cc[0] = x0;
             const uint64_t k0 = g.base + lin_of<D>(cc, g);
             const uint64_t k1 = k0 + (uint64_t)(x1 - x0) + 1;
             s[q] = C.cstart[rank_lt(C.dir, k0)];
@@ -446,7 +479,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const T* __restrict__ Xs,
     load_rec<T, D>(Xs, r, a);
     const int L = part_of(C.part_start, C.P, r);
     uint32_t s[NR], e[NR];
-    row_ranges<D>(C, a, L, s, e);
+    row_ranges<D, M>(C, a, L, eps, s, e);
     uint32_t cnt = 0, mn = r;
     const uint32_t stop = full ? 0xFFFFFFFFu : ms;
 #pragma unroll
@@ -520,18 +553,19 @@ struct Linker {
 };
 
 template <typename T, int D, int M>
-__global__ __launch_bounds__(kBlock) void link_kernel(const T* __restrict__ Xs, uint32_t R, Cells C,
+__global__ __launch_bounds__(kBlock) void link_kernel(const T* __restrict__ Xs, uint32_t NL,
+                                                      const uint32_t* __restrict__ list, Cells C,
                                                       double eps, double eps2,
-                                                      const uint8_t* __restrict__ core,
                                                       uint32_t* __restrict__ par) {
     constexpr int NR = NRows<D>::v;
-    const uint32_t r = rec_index();
-    if (r >= R || !(core[r] & 1)) return;
+    const uint32_t i = rec_index();
+    if (i >= NL) return;
+    const uint32_t r = list[i];   // core records, ascending
     double a[D];
     load_rec<T, D>(Xs, r, a);
     const int L = part_of(C.part_start, C.P, r);
     uint32_t s[NR], e[NR];
-    row_ranges<D>(C, a, L, s, e);
+    row_ranges<D, M>(C, a, L, eps, s, e);
     Linker lk{par, uf_find_l1(par, r)};
 #pragma unroll
     for (int q = 0; q < NR; ++q) {
@@ -579,7 +613,7 @@ __global__ __launch_bounds__(kBlock) void link_sweep_kernel(const T* __restrict_
     load_rec<T, D>(Xs, r, a);
     const int L = part_of(C.part_start, C.P, r);
     uint32_t s[NR], e[NR];
-    row_ranges<D>(C, a, L, s, e);
+    row_ranges<D, M>(C, a, L, eps, s, e);
     uint32_t ne = 0;
 #pragma unroll
     for (int q = 0; q < NR; ++q) {
@@ -643,16 +677,17 @@ __global__ __launch_bounds__(kBlock) void gmin_kernel(const uint32_t* __restrict
     wave_atomic_min(gmin, ok, root, pt);
 }
 
-// Owner records only: cluster key of the point (core: its component's
-// smallest core point; border: smallest such key among core neighbours).
-template <typename T, int D, int M>
-__global__ __launch_bounds__(kBlock) void border_kernel(
-    const T* __restrict__ Xs, uint32_t R, Cells C, double eps, double eps2,
-    const uint32_t* __restrict__ vals, const uint8_t* __restrict__ core,
-    const uint32_t* __restrict__ par, const uint32_t* __restrict__ gmin,
-    const uint32_t* __restrict__ cnt_rec, uint32_t* __restrict__ key_out,
-    uint8_t* __restrict__ core_out, uint32_t* __restrict__ cnt_out) {
-    const uint32_t r = rec_index();
+// Owner records: publish core flag / count, and the cluster key of core
+// points (their component's smallest core point).
+__global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_t* __restrict__ vals,
+                                                       const uint8_t* __restrict__ core,
+                                                       const uint32_t* __restrict__ par,
+                                                       const uint32_t* __restrict__ gmin,
+                                                       const uint32_t* __restrict__ cnt_rec,
+                                                       uint32_t* __restrict__ key_out,
+                                                       uint8_t* __restrict__ core_out,
+                                                       uint32_t* __restrict__ cnt_out) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
     if (r >= R) return;
     const uint32_t v = vals[r];
     if (!(v & kOwnerBit)) return;
@@ -660,17 +695,39 @@ __global__ __launch_bounds__(kBlock) void border_kernel(
     const uint8_t fl = core[r];
     if (core_out) core_out[pt] = fl & 1;
     if (cnt_out) cnt_out[pt] = cnt_rec[r];
-    if (fl & 1) {
-        key_out[pt] = gmin[par[r]];
-        return;
+    if (fl & 1) key_out[pt] = gmin[par[r]];
+}
+
+struct IsCore {
+    const uint8_t* core;
+    __device__ bool operator()(uint32_t r) const { return core[r] & 1; }
+};
+
+struct IsBorderCandidate {   // owner record, not core, has a neighbour
+    const uint8_t* core;
+    const uint32_t* vals;
+    __device__ bool operator()(uint32_t r) const {
+        return (core[r] & 3) == 2 && (vals[r] & kOwnerBit);
     }
-    if (!(fl & 2)) return;   // no neighbour at all: noise (key_out stays kNone)
+};
+
+// Border records (compacted list): smallest cluster key among the core
+// neighbours — sklearn's first-discovered-cluster rule.
+template <typename T, int D, int M>
+__global__ __launch_bounds__(kBlock) void border_kernel(
+    const T* __restrict__ Xs, uint32_t NL, const uint32_t* __restrict__ list, Cells C, double eps,
+    double eps2, const uint32_t* __restrict__ vals, const uint32_t* __restrict__ par,
+    const uint32_t* __restrict__ gmin, uint32_t* __restrict__ key_out) {
+    const uint32_t i = rec_index();
+    if (i >= NL) return;
+    const uint32_t r = list[i];   // owner, non-core records with a neighbour, ascending
+    const uint32_t pt = vals[r] & kIdMask;
     constexpr int NR = NRows<D>::v;
     double a[D];
     load_rec<T, D>(Xs, r, a);
     const int L = part_of(C.part_start, C.P, r);
     uint32_t s[NR], e[NR];
-    row_ranges<D>(C, a, L, s, e);
+    row_ranges<D, M>(C, a, L, eps, s, e);
     uint32_t best = kNone;
     auto take = [&](uint32_t j) {
         const uint32_t pj = par[j];
@@ -747,6 +804,25 @@ struct EvTimer {
 };
 
 inline unsigned blocks(uint64_t n) { return n ? (unsigned)((n + kBlock - 1) / kBlock) : 1u; }
+
+// Ordered compaction of record ids satisfying `pred` (keeps the spatial
+// order, so a wave's records stay neighbours).  Returns the count (syncs).
+template <typename Pred>
+uint32_t select_records(Ctx& ctx, const char* name, uint32_t R, Pred pred, uint32_t** out,
+                        hipStream_t s) {
+    uint32_t* list = ctx.arena.get<uint32_t>(name, R);
+    uint32_t* dcount = ctx.arena.get<uint32_t>("sel_count", 4);
+    rocprim::counting_iterator<uint32_t> it(0u);
+    size_t tb = 0;
+    PD_HIP(rocprim::select(nullptr, tb, it, list, dcount, (size_t)R, pred, s));
+    void* tmp = ctx.arena.get<char>("sel_tmp", tb);
+    PD_HIP(rocprim::select(tmp, tb, it, list, dcount, (size_t)R, pred, s));
+    uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+    PD_HIP(hipMemcpyAsync(h, dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    sync(s);
+    *out = list;
+    return *h;
+}
 
 template <typename T, int D, typename K, int M>
 void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t Gtot,
@@ -880,8 +956,12 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
                 for (int it = 0; it < ctx.jump_rounds; ++it)
                     hipLaunchKernelGGL(jump_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core,
                                        par);
-            hipLaunchKernelGGL((link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
-                               C, eps, eps2, core, par);
+            uint32_t* clist = nullptr;
+            const uint32_t NC = select_records(ctx, "core_list", R, IsCore{core}, &clist, s);
+            ctx.t.core_records = NC;
+            if (NC)
+                hipLaunchKernelGGL((link_kernel<T, D, M>), dim3(blocks(NC)), dim3(kBlock), 0, s,
+                                   Xs, NC, clist, C, eps, eps2, par);
         }
     }
     PD_HIP(hipGetLastError());
@@ -908,8 +988,16 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
     PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
     if (a.core) PD_HIP(hipMemsetAsync(a.core, 0, n, s));
     if (R)
-        hipLaunchKernelGGL((border_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R, C,
-                           eps, eps2, vals, core, par, gmin, cnt_rec, key_out, a.core, a.counts);
+    {
+        hipLaunchKernelGGL(owner_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, vals, core, par,
+                           gmin, cnt_rec, key_out, a.core, a.counts);
+        uint32_t* blist = nullptr;
+        const uint32_t NB =
+            select_records(ctx, "border_list", R, IsBorderCandidate{core, vals}, &blist, s);
+        if (NB)
+            hipLaunchKernelGGL((border_kernel<T, D, M>), dim3(blocks(NB)), dim3(kBlock), 0, s, Xs,
+                               NB, blist, C, eps, eps2, vals, par, gmin, key_out);
+    }
     PD_HIP(hipGetLastError());
     tm.mark();   // 9
 
@@ -1003,12 +1091,16 @@ void train(Ctx& ctx, TrainArgs& a) {
     }
     // per-neighbourhood grids
     const double cw = a.eps * (1.0 + 1.0 / 1048576.0);
+    const int xsub = ctx.xsub < 1 ? 1 : ctx.xsub;
     std::vector<PartGrid> parts(a.P);
     uint64_t G = 0;
     for (int L = 0; L < a.P; ++L) {
         PartGrid& g = parts[L];
         std::memset(&g, 0, sizeof(g));
-        g.inv = 1.0 / cw;
+        for (int j = 0; j < d; ++j) {
+            g.cs[j] = j == 0 ? cw / (double)xsub : cw;
+            g.inv[j] = j == 0 ? (double)xsub / cw : 1.0 / cw;
+        }
         g.base = G;
         bool empty = false;
         long double cells = 1;
@@ -1020,7 +1112,7 @@ void train(Ctx& ctx, TrainArgs& a) {
             if (!(lo <= hi)) empty = true;
             g.lo[j] = lo;
             if (!empty) {
-                const double nc = std::floor((hi - lo) * g.inv) + 1.0;
+                const double nc = std::floor((hi - lo) * g.inv[j]) + 1.0;
                 if (!(nc < 4.0e18)) throw Error(-5, "grid too large along one axis");
                 g.nc[j] = (int64_t)nc;
                 cells *= (long double)g.nc[j];

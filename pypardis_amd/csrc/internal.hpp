@@ -56,7 +56,8 @@ struct Ctx {
     bool full_counts = false;    // debug: count every neighbour (no early exit)
     bool seq_moments = false;    // reference-order (sequential) KD moment sums
     int link_mode = 0;           // 0 init forest + jumps + union; 2 union only; 1 diagnostic
-    int jump_rounds = 2;
+    int jump_rounds = 4;
+    int xsub = 2;                // axis-0 sub-cells per eps
     Timings t;
     hipEvent_t ev[16] = {};
 };

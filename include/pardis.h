@@ -56,12 +56,14 @@ enum pd_option {
                                       rounded, order-independent double-double sums. */
     PD_OPT_LINK_MODE = 4,  /* union strategy (tuning): 0 (default) initial forest from the count
                               pass's smallest neighbour + pointer jumping, then lock-free union
-                              over core-core edges; 2 the union pass alone; 1 diagnostic sweep
-                              only (labels invalid) */
+                              over core-core edges; 2 the union pass alone */
     PD_OPT_JUMP_ROUNDS = 5, /* pointer-jumping rounds for link mode 0 (default 4) */
-    PD_OPT_XSUB = 6         /* sub-cells per eps along axis 0 (default 2): finer rows follow
+    PD_OPT_XSUB = 6,        /* sub-cells per eps along axis 0 (default 2): finer rows follow
                                the eps-ball's chord more tightly, at 1/xsub the directory
                                density */
+    PD_OPT_FP32_SCREEN = 7  /* fp32 inputs: decide pairs outside a 2^-18 band around eps with
+                               fp32 arithmetic, the rest with the exact fp64 predicate
+                               (default 1; results are identical with 0) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -20,7 +20,7 @@ LIB_PATH = os.path.join(HERE, "libpardis.so")
 PD_F32, PD_F64 = 0, 1
 PD_EUCLIDEAN, PD_CITYBLOCK = 0, 1
 PD_OPT_TIMING, PD_OPT_FULL_COUNTS, PD_OPT_SEQUENTIAL_MOMENTS = 1, 2, 3
-PD_OPT_LINK_MODE, PD_OPT_JUMP_ROUNDS, PD_OPT_XSUB = 4, 5, 6
+PD_OPT_LINK_MODE, PD_OPT_JUMP_ROUNDS, PD_OPT_XSUB, PD_OPT_FP32_SCREEN = 4, 5, 6, 7
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits"]
 

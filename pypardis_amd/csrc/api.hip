@@ -114,6 +114,8 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.link_mode = (int)value;
         else if (option == PD_OPT_JUMP_ROUNDS)
             ctx->c.jump_rounds = (int)value;
+        else if (option == PD_OPT_FP32_SCREEN)
+            ctx->c.screen = value != 0;
         else if (option == PD_OPT_XSUB) {
             if (value < 1 || value > 16) throw Error(PD_EINVAL, "xsub must be in [1, 16]");
             ctx->c.xsub = (int)value;

@@ -209,6 +209,84 @@ __device__ __forceinline__ bool within(const double (&a)[D], const double (&b)[D
     return M == 0 ? (acc <= eps2) : (acc <= eps);
 }
 
+// Raw candidate load (input precision).
+template <typename T, int D>
+__device__ __forceinline__ void load_raw(const T* __restrict__ Xs, uint32_t j, T (&v)[D]) {
+    constexpr int S = Stride<D>::v;
+    if constexpr (std::is_same<T, float>::value && S == 4) {
+        const float4 f = *reinterpret_cast<const float4*>(Xs + (uint64_t)j * 4);
+        v[0] = f.x;
+        v[1] = f.y;
+        v[2] = f.z;
+        if constexpr (D == 4) v[3] = f.w;
+    } else if constexpr (std::is_same<T, float>::value && S == 2) {
+        const float2 f = *reinterpret_cast<const float2*>(Xs + (uint64_t)j * 2);
+        v[0] = f.x;
+        v[1] = f.y;
+    } else if constexpr (std::is_same<T, double>::value && S >= 2) {
+        const double2* p = reinterpret_cast<const double2*>(Xs + (uint64_t)j * S);
+        const double2 u = p[0];
+        v[0] = u.x;
+        v[1] = u.y;
+        if constexpr (S == 4) {
+            const double2 w = p[1];
+            v[2] = w.x;
+            if constexpr (D == 4) v[3] = w.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) v[k] = Xs[(uint64_t)j * S + k];
+    }
+}
+
+// The neighbour predicate as the sweeps use it.  fp32 inputs are screened
+// in fp32 first: with every coordinate an fp32 value, the fp32 distance has
+// relative error <= (D+2)*2^-24 < 2^-18, so a result below eps^2*(1-2^-18)
+// (rounded down to fp32) or above eps^2*(1+2^-18) (rounded up) already
+// decides the exact fp64 test; only pairs inside that band (ties) run it.
+// fp64 inputs always take the exact path.
+template <typename T, int D, int M>
+struct Pred {
+    double a[D];
+    T ar[D];
+    double eps, eps2;
+    float lo, hi;
+    __device__ __forceinline__ bool operator()(const T (&b)[D]) const {
+        if constexpr (std::is_same<T, float>::value) {
+            float d = 0.0f;
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const float t = ar[j] - b[j];
+                if constexpr (M == 0)
+                    d = __builtin_fmaf(t, t, d);
+                else
+                    d += fabsf(t);
+            }
+            if (d <= lo) return true;
+            if (!(d <= hi)) return false;
+        }
+        double bb[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) bb[j] = (double)b[j];
+        return within<D, M>(a, bb, eps, eps2);
+    }
+};
+
+template <typename T, int D, int M>
+__device__ __forceinline__ Pred<T, D, M> make_pred(const T* __restrict__ Xs, uint32_t r,
+                                                   const double (&a)[D], double eps, double eps2,
+                                                   float lo, float hi) {
+    Pred<T, D, M> p;
+#pragma unroll
+    for (int j = 0; j < D; ++j) p.a[j] = a[j];
+    load_raw<T, D>(Xs, r, p.ar);
+    p.eps = eps;
+    p.eps2 = eps2;
+    p.lo = lo;
+    p.hi = hi;
+    return p;
+}
+
 template <int D>
 __device__ __forceinline__ void cell_of(const double (&v)[D], const PartGrid& g, int64_t (&c)[D]) {
 #pragma unroll
@@ -283,69 +361,124 @@ struct NRows {
 // half-width w = sqrt(eps^2 - d^2) (cityblock: eps - d) along axis 0, and
 // rows the ball cannot reach are skipped.  d is shrunk and w grown by a
 // 2^-20 relative slack, far above any rounding, so no pair the exact
-// predicate accepts is ever cut.  Each range is one contiguous record range;
-// all lookups are issued before any candidate is read (unrolled).  Row q
-// enumerates offsets in ascending key order.
+// predicate accepts is ever cut.  Each range is one contiguous record range.
+// Row q enumerates offsets in ascending key order.
+//
+// Latency: the grid fields are copied to registers once, keys for a batch
+// of rows are computed first, then the batch's directory words are loaded
+// together, then its cstart words — two round trips per batch instead of
+// two per row (the compiler otherwise serialises them behind the per-row
+// branches: ~36 dependent loads per record).
 template <int D, int M>
 __device__ __forceinline__ void row_ranges(const Cells& C, const double (&a)[D], int L, double eps,
                                            uint32_t (&s)[NRows<D>::v],
                                            uint32_t (&e)[NRows<D>::v]) {
-    const PartGrid& g = C.parts[L];
+    constexpr int NR = NRows<D>::v;
+    constexpr int B = NR < 3 ? NR : 3;   // rows per batch
+    const PartGrid* gp = C.parts + L;
+    double lo[D], inv[D], cs[D];
+    int64_t nc[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        lo[j] = gp->lo[j];
+        inv[j] = gp->inv[j];
+        cs[j] = gp->cs[j];
+        nc[j] = gp->nc[j];
+    }
+    const uint64_t base = gp->base;
     int64_t c[D];
     double f[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-        const double u = (a[j] - g.lo[j]) * g.inv[j];
+        const double u = (a[j] - lo[j]) * inv[j];
         int64_t q = (int64_t)floor(u);
         q = q < 0 ? 0 : q;
-        q = q >= g.nc[j] ? g.nc[j] - 1 : q;
+        q = q >= nc[j] ? nc[j] - 1 : q;
         c[j] = q;
-        double fr = u - (double)q;
+        const double fr = u - (double)q;
         f[j] = fr < 0.0 ? 0.0 : (fr > 1.0 ? 1.0 : fr);
     }
     const double slack = eps * (1.0 / 1048576.0);
 #pragma unroll
-    for (int q = 0; q < NRows<D>::v; ++q) {
-        int64_t cc[D];
-        int t = q;
-        bool ok = true;
-        double d2 = 0.0, d1 = 0.0;
+    for (int q0 = 0; q0 < NR; q0 += B) {
+        uint64_t k0[B], k1[B];
+        bool ok[B];
 #pragma unroll
-        for (int j = 1; j < D; ++j) {
-            const int o = (t % 3) - 1;
-            t /= 3;
-            const int64_t v = c[j] + o;
-            ok &= (v >= 0) & (v < g.nc[j]);
-            cc[j] = v;
-            double dist = o == 0 ? 0.0 : (o < 0 ? f[j] : 1.0 - f[j]) * g.cs[j] - slack;
-            dist = dist > 0.0 ? dist : 0.0;
-            d2 += dist * dist;
-            d1 += dist;
-        }
-        double w;
-        if constexpr (M == 0) {
-            ok &= d2 <= eps * eps;
-            w = sqrt(fmax(eps * eps - d2, 0.0));
-        } else {
-            ok &= d1 <= eps;
-            w = eps - d1;
-        }
-        w = w * (1.0 + 1.0 / 1048576.0) + slack;
-        if (ok) {
-            int64_t x0 = (int64_t)floor((a[0] - w - g.lo[0]) * g.inv[0]);
-            int64_t x1 = (int64_t)floor((a[0] + w - g.lo[0]) * g.inv[0]);
+        for (int b = 0; b < B; ++b) {
+            const int q = q0 + b;
+            int t = q;
+            bool okq = true;
+            double d2 = 0.0, d1 = 0.0;
+            int64_t cc[D];
+#pragma unroll
+            for (int j = 1; j < D; ++j) {
+                const int o = (t % 3) - 1;
+                t /= 3;
+                const int64_t v = c[j] + o;
+                okq &= (v >= 0) & (v < nc[j]);
+                cc[j] = v;
+                double dist = o == 0 ? 0.0 : (o < 0 ? f[j] : 1.0 - f[j]) * cs[j] - slack;
+                dist = dist > 0.0 ? dist : 0.0;
+                d2 += dist * dist;
+                d1 += dist;
+            }
+            double w;
+            if constexpr (M == 0) {
+                okq &= d2 <= eps * eps;
+                w = sqrt(fmax(eps * eps - d2, 0.0));
+            } else {
+                okq &= d1 <= eps;
+                w = eps - d1;
+            }
+            w = w * (1.0 + 1.0 / 1048576.0) + slack;
+            int64_t x0 = (int64_t)floor((a[0] - w - lo[0]) * inv[0]);
+            int64_t x1 = (int64_t)floor((a[0] + w - lo[0]) * inv[0]);
             x0 = x0 < 0 ? 0 : x0;
-            x1 = x1 >= g.nc[0] ? g.nc[0] - 1 : x1;
+            x1 = x1 >= nc[0] ? nc[0] - 1 : x1;
             cc[0] = x0;
-            const uint64_t k0 = g.base + lin_of<D>(cc, g);
-            const uint64_t k1 = k0 + (uint64_t)(x1 - x0) + 1;
-            s[q] = C.cstart[rank_lt(C.dir, k0)];
-            e[q] = C.cstart[rank_lt(C.dir, k1)];
-        } else {
-            s[q] = 0;
-            e[q] = 0;
+            uint64_t lin = 0;
+#pragma unroll
+            for (int j = D - 1; j >= 0; --j) lin = lin * (uint64_t)nc[j] + (uint64_t)(j == 0 ? x0 : cc[j]);
+            const uint64_t kk0 = base + lin;
+            k0[b] = okq ? kk0 : 0;
+            k1[b] = okq ? kk0 + (uint64_t)(x1 - x0) + 1 : 0;
+            ok[b] = okq;
+        }
+        uint4 w0[B], w1[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            w0[b] = C.dir[k0[b] >> 6];
+            w1[b] = C.dir[k1[b] >> 6];
+        }
+        uint32_t i0[B], i1[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            auto rk = [](const uint4& w, uint64_t k) {
+                const uint64_t bits = ((uint64_t)w.y << 32) | (uint64_t)w.x;
+                const uint32_t sh = (uint32_t)(k & 63);
+                const uint64_t m = sh ? (bits & ((~0ull) >> (64 - sh))) : 0ull;
+                return w.z + (uint32_t)__popcll(m);
+            };
+            i0[b] = rk(w0[b], k0[b]);
+            i1[b] = rk(w1[b], k1[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            const uint32_t sv = C.cstart[i0[b]], ev = C.cstart[i1[b]];
+            s[q0 + b] = ok[b] ? sv : 0u;
+            e[q0 + b] = ok[b] ? ev : 0u;
         }
     }
+}
+
+// Partition of a record.  Waves almost always sit inside one partition: try
+// the first lane's partition on the scalar path, fall back per lane.
+__device__ __forceinline__ int part_of_wave(const uint32_t* __restrict__ ps, int P, uint32_t r) {
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane(r);
+    const int L0 = part_of(ps, P, r0);
+    const uint32_t lo = ps[L0], hi = ps[L0 + 1];
+    if (__all(r >= lo && r < hi)) return L0;
+    return part_of(ps, P, r);
 }
 
 // ------------------------------------------------------------------ kernels
@@ -468,7 +601,7 @@ __global__ __launch_bounds__(kBlock) void cell_start_kernel(const uint32_t* __re
 template <typename T, int D, int M>
 __global__ __launch_bounds__(kBlock) void count_kernel(const T* __restrict__ Xs, uint32_t R,
                                                        Cells C, double eps, double eps2,
-                                                       uint32_t ms, int full,
+                                                       float lo, float hi, uint32_t ms, int full,
                                                        uint8_t* __restrict__ core,
                                                        uint32_t* __restrict__ mn_out,
                                                        uint32_t* __restrict__ cnt_out) {
@@ -477,9 +610,10 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const T* __restrict__ Xs,
     if (r >= R) return;
     double a[D];
     load_rec<T, D>(Xs, r, a);
-    const int L = part_of(C.part_start, C.P, r);
+    const int L = part_of_wave(C.part_start, C.P, r);
     uint32_t s[NR], e[NR];
     row_ranges<D, M>(C, a, L, eps, s, e);
+    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
     uint32_t cnt = 0, mn = r;
     const uint32_t stop = full ? 0xFFFFFFFFu : ms;
 #pragma unroll
@@ -488,22 +622,22 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const T* __restrict__ Xs,
         uint32_t j = s[q];
         const uint32_t end = e[q];
         for (; j + 4 <= end; j += 4) {
-            double b0[D], b1[D], b2[D], b3[D];
-            load_rec<T, D>(Xs, j, b0);
-            load_rec<T, D>(Xs, j + 1, b1);
-            load_rec<T, D>(Xs, j + 2, b2);
-            load_rec<T, D>(Xs, j + 3, b3);
-            const bool w0 = within<D, M>(a, b0, eps, eps2), w1 = within<D, M>(a, b1, eps, eps2),
-                       w2 = within<D, M>(a, b2, eps, eps2), w3 = within<D, M>(a, b3, eps, eps2);
+            T b0[D], b1[D], b2[D], b3[D];
+            load_raw<T, D>(Xs, j, b0);
+            load_raw<T, D>(Xs, j + 1, b1);
+            load_raw<T, D>(Xs, j + 2, b2);
+            load_raw<T, D>(Xs, j + 3, b3);
+            const bool w0 = pr(b0), w1 = pr(b1),
+                       w2 = pr(b2), w3 = pr(b3);
             cnt += (uint32_t)w0 + (uint32_t)w1 + (uint32_t)w2 + (uint32_t)w3;
             const uint32_t h = w0 ? j : (w1 ? j + 1 : (w2 ? j + 2 : (w3 ? j + 3 : mn)));
             mn = h < mn ? h : mn;
             if (cnt >= stop) goto done;
         }
         for (; j < end; ++j) {
-            double b0[D];
-            load_rec<T, D>(Xs, j, b0);
-            if (within<D, M>(a, b0, eps, eps2)) {
+            T b0[D];
+            load_raw<T, D>(Xs, j, b0);
+            if (pr(b0)) {
                 ++cnt;
                 mn = j < mn ? j : mn;
             }
@@ -543,8 +677,10 @@ __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t R, const uint8_t*
 struct Linker {
     uint32_t* par;
     uint32_t rr;
-    __device__ __forceinline__ void edge(uint32_t j) {
-        const uint32_t pj = ld_l1(par + j);
+    __device__ __forceinline__ void edge(uint32_t j) { edge(j, ld_l1(par + j)); }
+    // pj: parent[j] read ahead of the distance test (stale is fine: an older
+    // ancestor still proves membership, and a mismatch falls through to find)
+    __device__ __forceinline__ void edge(uint32_t j, uint32_t pj) {
         if (pj == kNone || pj == rr) return;   // non-core, or already under our root
         const uint32_t rj = uf_find_l1(par, pj);
         if (rj == rr) return;
@@ -555,7 +691,7 @@ struct Linker {
 template <typename T, int D, int M>
 __global__ __launch_bounds__(kBlock) void link_kernel(const T* __restrict__ Xs, uint32_t NL,
                                                       const uint32_t* __restrict__ list, Cells C,
-                                                      double eps, double eps2,
+                                                      double eps, double eps2, float lo, float hi,
                                                       uint32_t* __restrict__ par) {
     constexpr int NR = NRows<D>::v;
     const uint32_t i = rec_index();
@@ -563,31 +699,34 @@ __global__ __launch_bounds__(kBlock) void link_kernel(const T* __restrict__ Xs, 
     const uint32_t r = list[i];   // core records, ascending
     double a[D];
     load_rec<T, D>(Xs, r, a);
-    const int L = part_of(C.part_start, C.P, r);
+    const int L = part_of_wave(C.part_start, C.P, r);
     uint32_t s[NR], e[NR];
     row_ranges<D, M>(C, a, L, eps, s, e);
+    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
     Linker lk{par, uf_find_l1(par, r)};
 #pragma unroll
     for (int q = 0; q < NR; ++q) {
         uint32_t j = s[q] > r + 1 ? s[q] : r + 1;
         const uint32_t end = e[q];
         for (; j + 4 <= end; j += 4) {
-            double b0[D], b1[D], b2[D], b3[D];
-            load_rec<T, D>(Xs, j, b0);
-            load_rec<T, D>(Xs, j + 1, b1);
-            load_rec<T, D>(Xs, j + 2, b2);
-            load_rec<T, D>(Xs, j + 3, b3);
-            const bool w0 = within<D, M>(a, b0, eps, eps2), w1 = within<D, M>(a, b1, eps, eps2),
-                       w2 = within<D, M>(a, b2, eps, eps2), w3 = within<D, M>(a, b3, eps, eps2);
-            if (w0) lk.edge(j);
-            if (w1) lk.edge(j + 1);
-            if (w2) lk.edge(j + 2);
-            if (w3) lk.edge(j + 3);
+            // coordinates and parents of four candidates in flight together
+            T b0[D], b1[D], b2[D], b3[D];
+            load_raw<T, D>(Xs, j, b0);
+            load_raw<T, D>(Xs, j + 1, b1);
+            load_raw<T, D>(Xs, j + 2, b2);
+            load_raw<T, D>(Xs, j + 3, b3);
+            const uint32_t p0 = ld_l1(par + j), p1 = ld_l1(par + j + 1), p2 = ld_l1(par + j + 2),
+                           p3 = ld_l1(par + j + 3);
+            if (pr(b0)) lk.edge(j, p0);
+            if (pr(b1)) lk.edge(j + 1, p1);
+            if (pr(b2)) lk.edge(j + 2, p2);
+            if (pr(b3)) lk.edge(j + 3, p3);
         }
         for (; j < end; ++j) {
-            double b0[D];
-            load_rec<T, D>(Xs, j, b0);
-            if (within<D, M>(a, b0, eps, eps2)) lk.edge(j);
+            T b0[D];
+            load_raw<T, D>(Xs, j, b0);
+            const uint32_t p0 = ld_l1(par + j);
+            if (pr(b0)) lk.edge(j, p0);
         }
     }
 }
@@ -599,33 +738,6 @@ __global__ __launch_bounds__(kBlock) void jump_kernel(uint32_t R, const uint8_t*
     if (r >= R || !(core[r] & 1)) return;
     par[r] = par[par[r]];   // chains hold core records only
 }
-
-// Diagnostic: the link sweep without unions (counts edges so nothing is dead).
-template <typename T, int D, int M>
-__global__ __launch_bounds__(kBlock) void link_sweep_kernel(const T* __restrict__ Xs, uint32_t R,
-                                                            Cells C, double eps, double eps2,
-                                                            const uint8_t* __restrict__ core,
-                                                            unsigned long long* __restrict__ edges) {
-    constexpr int NR = NRows<D>::v;
-    const uint32_t r = rec_index();
-    if (r >= R || !(core[r] & 1)) return;
-    double a[D];
-    load_rec<T, D>(Xs, r, a);
-    const int L = part_of(C.part_start, C.P, r);
-    uint32_t s[NR], e[NR];
-    row_ranges<D, M>(C, a, L, eps, s, e);
-    uint32_t ne = 0;
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-        for (uint32_t j = s[q] > r + 1 ? s[q] : r + 1; j < e[q]; ++j) {
-            double b0[D];
-            load_rec<T, D>(Xs, j, b0);
-            if (within<D, M>(a, b0, eps, eps2) && (core[j] & 1)) ++ne;
-        }
-    }
-    atomicAdd(edges, (unsigned long long)ne);
-}
-
 
 // A point's copies in several neighbourhoods: link every core copy to one
 // representative (the smallest record), gluing the neighbourhoods' clusters.
@@ -716,7 +828,8 @@ struct IsBorderCandidate {   // owner record, not core, has a neighbour
 template <typename T, int D, int M>
 __global__ __launch_bounds__(kBlock) void border_kernel(
     const T* __restrict__ Xs, uint32_t NL, const uint32_t* __restrict__ list, Cells C, double eps,
-    double eps2, const uint32_t* __restrict__ vals, const uint32_t* __restrict__ par,
+    double eps2, float lo, float hi, const uint32_t* __restrict__ vals,
+    const uint32_t* __restrict__ par,
     const uint32_t* __restrict__ gmin, uint32_t* __restrict__ key_out) {
     const uint32_t i = rec_index();
     if (i >= NL) return;
@@ -725,12 +838,12 @@ __global__ __launch_bounds__(kBlock) void border_kernel(
     constexpr int NR = NRows<D>::v;
     double a[D];
     load_rec<T, D>(Xs, r, a);
-    const int L = part_of(C.part_start, C.P, r);
+    const int L = part_of_wave(C.part_start, C.P, r);
     uint32_t s[NR], e[NR];
     row_ranges<D, M>(C, a, L, eps, s, e);
+    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
     uint32_t best = kNone;
-    auto take = [&](uint32_t j) {
-        const uint32_t pj = par[j];
+    auto take = [&](uint32_t pj) {
         if (pj == kNone) return;   // not core
         const uint32_t k = gmin[pj];
         best = k < best ? k : best;
@@ -740,20 +853,22 @@ __global__ __launch_bounds__(kBlock) void border_kernel(
         uint32_t j = s[q];
         const uint32_t end = e[q];
         for (; j + 4 <= end; j += 4) {
-            double b0[D], b1[D], b2[D], b3[D];
-            load_rec<T, D>(Xs, j, b0);
-            load_rec<T, D>(Xs, j + 1, b1);
-            load_rec<T, D>(Xs, j + 2, b2);
-            load_rec<T, D>(Xs, j + 3, b3);
-            if (within<D, M>(a, b0, eps, eps2)) take(j);
-            if (within<D, M>(a, b1, eps, eps2)) take(j + 1);
-            if (within<D, M>(a, b2, eps, eps2)) take(j + 2);
-            if (within<D, M>(a, b3, eps, eps2)) take(j + 3);
+            T b0[D], b1[D], b2[D], b3[D];
+            load_raw<T, D>(Xs, j, b0);
+            load_raw<T, D>(Xs, j + 1, b1);
+            load_raw<T, D>(Xs, j + 2, b2);
+            load_raw<T, D>(Xs, j + 3, b3);
+            const uint32_t p0 = par[j], p1 = par[j + 1], p2 = par[j + 2], p3 = par[j + 3];
+            if (pr(b0)) take(p0);
+            if (pr(b1)) take(p1);
+            if (pr(b2)) take(p2);
+            if (pr(b3)) take(p3);
         }
         for (; j < end; ++j) {
-            double b0[D];
-            load_rec<T, D>(Xs, j, b0);
-            if (within<D, M>(a, b0, eps, eps2)) take(j);
+            T b0[D];
+            load_raw<T, D>(Xs, j, b0);
+            const uint32_t p0 = par[j];
+            if (pr(b0)) take(p0);
         }
     }
     key_out[pt] = best;
@@ -931,12 +1046,22 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
 
     Cells C{parts, part_start, P, dir, cstart};
     const double eps = a.eps, eps2 = a.eps * a.eps;
+    // fp32 screening band (see Pred): thresholds rounded outward
+    float slo = -1.0f, shi = INFINITY;
+    {
+        const double thr = a.metric == 0 ? eps2 : eps;
+        if (std::is_same<T, float>::value && thr > 1e-30 && thr < 1e30 && ctx.screen) {
+            slo = std::nextafter((float)(thr * (1.0 - 1.0 / 262144.0)), 0.0f);
+            shi = std::nextafter((float)(thr * (1.0 + 1.0 / 262144.0)), INFINITY);
+        }
+    }
     uint8_t* core = ctx.arena.get<uint8_t>("core", R);
     uint32_t* mn = ctx.arena.get<uint32_t>("minnbr", R);
     uint32_t* cnt_rec = a.counts ? ctx.arena.get<uint32_t>("cnt_rec", R) : nullptr;
     if (R)
         hipLaunchKernelGGL((count_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R, C,
-                           eps, eps2, (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0, core, mn,
+                           eps, eps2, slo, shi, (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
+                           core, mn,
                            cnt_rec);
     PD_HIP(hipGetLastError());
     tm.mark();   // 5
@@ -946,12 +1071,7 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
         const int mode = ctx.link_mode;
         hipLaunchKernelGGL(init_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, mn,
                            mode == 0 ? 1 : 0, par);
-        if (mode == 1) {   // diagnostic: sweep cost alone (labels are NOT valid)
-            unsigned long long* dedge = ctx.arena.get<unsigned long long>("edges", 1);
-            PD_HIP(hipMemsetAsync(dedge, 0, 8, s));
-            hipLaunchKernelGGL((link_sweep_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                               Xs, R, C, eps, eps2, core, dedge);
-        } else {
+        {
             if (mode == 0)
                 for (int it = 0; it < ctx.jump_rounds; ++it)
                     hipLaunchKernelGGL(jump_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core,
@@ -961,7 +1081,7 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
             ctx.t.core_records = NC;
             if (NC)
                 hipLaunchKernelGGL((link_kernel<T, D, M>), dim3(blocks(NC)), dim3(kBlock), 0, s,
-                                   Xs, NC, clist, C, eps, eps2, par);
+                                   Xs, NC, clist, C, eps, eps2, slo, shi, par);
         }
     }
     PD_HIP(hipGetLastError());
@@ -996,7 +1116,7 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
             select_records(ctx, "border_list", R, IsBorderCandidate{core, vals}, &blist, s);
         if (NB)
             hipLaunchKernelGGL((border_kernel<T, D, M>), dim3(blocks(NB)), dim3(kBlock), 0, s, Xs,
-                               NB, blist, C, eps, eps2, vals, par, gmin, key_out);
+                               NB, blist, C, eps, eps2, slo, shi, vals, par, gmin, key_out);
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 9

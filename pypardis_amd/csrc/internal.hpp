@@ -58,6 +58,7 @@ struct Ctx {
     int link_mode = 0;           // 0 init forest + jumps + union; 2 union only; 1 diagnostic
     int jump_rounds = 4;
     int xsub = 2;                // axis-0 sub-cells per eps
+    bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     Timings t;
     hipEvent_t ev[16] = {};
 };

@@ -276,3 +276,25 @@ def test_partition_count_invariance_large(native):
     u, fi = np.unique(lab[idx], return_index=True)
     first[u] = idx[fi]
     assert np.all(np.diff(first) > 0)
+
+
+def test_fp32_screen_is_exact(native):
+    """The fp32 screen only decides pairs outside a 2^-18 band around eps; the
+    result must be identical with the screen disabled (exact fp64 for every
+    pair), including on exact ties."""
+    from pypardis_amd import synth
+    g = np.arange(80, dtype=np.float32) * np.float32(0.05)
+    lattice = np.stack(np.meshgrid(g, g, indexing="ij"), -1).reshape(-1, 2)
+    blobs = synth.blobs_noise(60_000, 3, side=6.0, n_centers=5, sigma=0.4, seed=41)
+    ctx = native.context()
+    for X, eps, ms in ((lattice, float(np.float32(0.05)), 5), (lattice, 0.05, 5),
+                       (blobs, 0.07, 8)):
+        out = []
+        for screen in (1, 0):
+            ctx.set_option(native.PD_OPT_FP32_SCREEN, screen)
+            try:
+                out.append(_cluster(native, X, eps, ms, full=True))
+            finally:
+                ctx.set_option(native.PD_OPT_FP32_SCREEN, 1)
+        (l1, c1, n1, k1), (l0, c0, n0, k0) = out
+        assert np.array_equal(k1, k0) and np.array_equal(l1, l0) and n1 == n0

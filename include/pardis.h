@@ -133,6 +133,75 @@ int32_t pd_train(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d
                  const double* data_box_host, const int32_t* owner, int32_t* labels,
                  uint8_t* core, uint32_t* counts, int64_t* n_clusters_host, void* stream);
 
+/* ---- sharded train (one process per device; the caller moves the buffers
+ * between devices, e.g. torch.distributed over RCCL).  Replaces Spark's
+ * partitionBy shuffle of the halo records (R:dbscan/dbscan.py:114-118) and the
+ * driver-side ClusterAggregator merge (R:dbscan/dbscan.py:153-165,
+ * R:dbscan/aggregator.py:9-73).  Global ids must stay below 2^32 - 1. */
+
+/* pd_kd_moments with the double-double partial sums left unrounded, so that
+ * devices can add them exactly: out_host[s][1 + 4d] = {count, (sum hi, sum
+ * lo) per axis, (sumsq hi, sumsq lo) per axis}.  R:dbscan/partition.py:86-89 */
+int32_t pd_kd_moments_dd(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                         const int32_t* labels, int32_t n_sel, const int32_t* sel_host,
+                         double* out_host, void* stream);
+
+/* mask[n] (device, u64): bit r set when some neighbourhood L with
+ * part_rank_host[L] == r has an expanded box containing point i;
+ * counts_host[r] = points routed to device r.  n_ranks <= 64. */
+int32_t pd_route(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, int32_t P,
+                 const double* ebox_host, const int32_t* part_rank_host, int32_t n_ranks,
+                 uint64_t* mask, int64_t* counts_host, void* stream);
+
+/* Pack the points routed to device `dest` (ascending local index): coords
+ * (d values each, input dtype), gid = gid_base + local index, owner = index of
+ * the point's KD partition kdlab[i] among dest's neighbourhoods
+ * (local_index_host) when part_rank_host[kdlab[i]] == dest, else -1, xr = the
+ * point was routed to more than one device.  *m_host = points packed. */
+int32_t pd_pack(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                const uint64_t* mask, int32_t dest, const int32_t* kdlab, int32_t P,
+                const int32_t* part_rank_host, const int32_t* local_index_host,
+                uint32_t gid_base, void* coords, uint32_t* gid, int32_t* owner, uint8_t* xr,
+                int64_t capacity, int64_t* m_host, void* stream);
+
+/* Phase A on this device's neighbourhoods (arguments as pd_train; gid[n] =
+ * global id of each local point, xr[n] = point also lives on another device).
+ * *n_exports_host = number of (global id, component key) exports. */
+int32_t pd_train_begin(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                       double eps, int32_t min_samples, int32_t metric, int32_t P,
+                       const double* ebox_host, const double* data_box_host,
+                       const int32_t* owner, const uint32_t* gid, const uint8_t* xr,
+                       int64_t* n_exports_host, void* stream);
+
+/* Copy the exports of the last pd_train_begin into device buffers. */
+int32_t pd_train_exports(pd_ctx* ctx, uint32_t* gid, uint32_t* key, int64_t capacity,
+                         void* stream);
+
+/* Union of all devices' exports over the id space [0, n_space):
+ * parent[n_space] (device) receives each id's global key (its component's
+ * smallest id; identity for ids in no export). */
+int32_t pd_merge_exports(pd_ctx* ctx, uint32_t n_space, const uint32_t* gid,
+                         const uint32_t* key, int64_t m, uint32_t* parent, void* stream);
+
+/* Phase B: keymap (device, nullable) from pd_merge_exports; keys[n] = global
+ * cluster key of each owned point (0xFFFFFFFF = noise or not owned here),
+ * core[n] (nullable) = owned core point. */
+int32_t pd_train_end(pd_ctx* ctx, int64_t n, const uint32_t* keymap, uint32_t* keys,
+                     uint8_t* core, void* stream);
+
+/* roots (device, capacity n) = global ids of owned points that are their
+ * cluster's key, i.e. one id per cluster over all devices; *m_host = count. */
+int32_t pd_select_roots(pd_ctx* ctx, const uint32_t* keys, const uint32_t* gid, int64_t n,
+                        uint32_t* roots, int64_t* m_host, void* stream);
+
+/* In-place ascending sort of n u32 (device). */
+int32_t pd_sort_u32(pd_ctx* ctx, uint32_t* data, int64_t n, void* stream);
+
+/* labels[i] = rank of keys[i] among the sorted roots (all devices' roots),
+ * -1 for 0xFFFFFFFF — sklearn's numbering, as pd_train's labels. */
+int32_t pd_rank_labels(pd_ctx* ctx, const uint32_t* keys, int64_t n, const uint32_t* roots,
+                       int64_t n_roots, int32_t* labels, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

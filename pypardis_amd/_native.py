@@ -27,7 +27,9 @@ TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "ro
 # every symbol include/pardis.h declares (tests/test_abi.py checks the .so)
 EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
            "pd_ctx_set_option", "pd_ctx_timings", "pd_bbox", "pd_kd_moments", "pd_kd_counts",
-           "pd_kd_split", "pd_halo_members", "pd_cluster", "pd_train"]
+           "pd_kd_split", "pd_halo_members", "pd_cluster", "pd_train", "pd_kd_moments_dd",
+           "pd_route", "pd_pack", "pd_train_begin", "pd_train_exports", "pd_merge_exports",
+           "pd_train_end", "pd_select_roots", "pd_sort_u32", "pd_rank_labels"]
 
 
 class PardisError(RuntimeError):
@@ -55,6 +57,7 @@ def load():
                 "(hipcc --offload-arch=gfx950).  There is no CPU fallback.")
         lib = ctypes.CDLL(LIB_PATH)
         P, I32, I64, D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+        U32 = ctypes.c_uint32
         sig = {
             "pd_abi_version": ([], I32),
             "pd_last_error": ([], ctypes.c_char_p),
@@ -69,6 +72,17 @@ def load():
             "pd_halo_members": ([P, P, I32, I64, I32, I32, P, P, P, I64, P], I32),
             "pd_cluster": ([P, P, I32, I64, I32, D, I32, I32, P, P, P, P, P], I32),
             "pd_train": ([P, P, I32, I64, I32, D, I32, I32, I32, P, P, P, P, P, P, P, P], I32),
+            "pd_kd_moments_dd": ([P, P, I32, I64, I32, P, I32, P, P, P], I32),
+            "pd_route": ([P, P, I32, I64, I32, I32, P, P, I32, P, P, P], I32),
+            "pd_pack": ([P, P, I32, I64, I32, P, I32, P, I32, P, P, U32, P, P, P, P, I64, P, P],
+                        I32),
+            "pd_train_begin": ([P, P, I32, I64, I32, D, I32, I32, I32, P, P, P, P, P, P, P], I32),
+            "pd_train_exports": ([P, P, P, I64, P], I32),
+            "pd_merge_exports": ([P, U32, P, P, I64, P, P], I32),
+            "pd_train_end": ([P, I64, P, P, P, P], I32),
+            "pd_select_roots": ([P, P, P, I64, P, P, P], I32),
+            "pd_sort_u32": ([P, P, I64, P], I32),
+            "pd_rank_labels": ([P, P, I64, P, I64, P, P], I32),
         }
         for name, (args, res) in sig.items():
             f = getattr(lib, name)
@@ -273,3 +287,135 @@ def train(X, eps, min_samples, metric, ebox, owner=None, data_box=None, want_cou
                            core.data_ptr(), counts.data_ptr() if counts is not None else None,
                            ncl.ctypes.data, _stream(X.device)))
     return labels, core, counts, int(ncl[0])
+
+
+# ------------------------------------------------------- sharded train stages
+# u32 ids/keys live in int32 tensors (same bits; 0xFFFFFFFF reads as -1), the
+# u64 route mask in an int64 tensor: both move through torch.distributed as is.
+KEY_NONE = -1
+
+
+def kd_moments_dd(X, labels, sel, ctx=None):
+    """(n_sel, 1 + 4d) unrounded double-double partials (pd_kd_moments_dd)."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    d = X.shape[1]
+    sel = np.ascontiguousarray(sel, np.int32)
+    out = np.zeros((len(sel), 1 + 4 * d), np.float64)
+    _check(load().pd_kd_moments_dd(ctx.ptr, X.data_ptr(), dt, X.shape[0], d, labels.data_ptr(),
+                                   len(sel), sel.ctypes.data, out.ctypes.data, _stream(X.device)))
+    return out
+
+
+def route(X, ebox, part_rank, n_ranks, ctx=None):
+    """Returns (mask int64[n] device, counts int64[n_ranks] host)."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    ebox = np.ascontiguousarray(ebox, np.float64)
+    part_rank = np.ascontiguousarray(part_rank, np.int32)
+    mask = torch.empty(max(n, 1), dtype=torch.int64, device=X.device)
+    counts = np.zeros(n_ranks, np.int64)
+    _check(load().pd_route(ctx.ptr, X.data_ptr(), dt, n, d, ebox.shape[0], ebox.ctypes.data,
+                           part_rank.ctypes.data, int(n_ranks), mask.data_ptr(),
+                           counts.ctypes.data, _stream(X.device)))
+    return mask[:n], counts
+
+
+def pack(X, mask, dest, kdlab, part_rank, local_index, gid_base, out, ctx=None):
+    """Fill out = (coords (m, d), gid int32[m], owner int32[m], xr uint8[m]) views
+    with the points routed to `dest`; returns m."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    coords, gid, owner, xr = out
+    cap = gid.shape[0]
+    part_rank = np.ascontiguousarray(part_rank, np.int32)
+    local_index = np.ascontiguousarray(local_index, np.int32)
+    m = np.zeros(1, np.int64)
+    ptr = (lambda t: t.data_ptr() if t.numel() else None)
+    _check(load().pd_pack(ctx.ptr, X.data_ptr() if n else None, dt, n, d,
+                          mask.data_ptr() if n else None, int(dest),
+                          kdlab.data_ptr() if n else None, len(part_rank),
+                          part_rank.ctypes.data, local_index.ctypes.data, int(gid_base),
+                          ptr(coords), ptr(gid), ptr(owner), ptr(xr), cap, m.ctypes.data,
+                          _stream(X.device)))
+    return int(m[0])
+
+
+def train_begin(X, eps, min_samples, metric, ebox, owner, gid, xr, data_box, ctx=None):
+    """Phase A of a sharded train; returns the number of exports."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    ebox = np.ascontiguousarray(ebox, np.float64).reshape(-1, 2, d)
+    dbox = np.ascontiguousarray(data_box, np.float64).reshape(2 * d)
+    ne = np.zeros(1, np.int64)
+    _check(load().pd_train_begin(ctx.ptr, X.data_ptr() if n else None, dt, n, d, float(eps),
+                                 int(min_samples), int(metric), ebox.shape[0], ebox.ctypes.data,
+                                 dbox.ctypes.data, owner.data_ptr() if n else None,
+                                 gid.data_ptr() if n else None, xr.data_ptr() if n else None,
+                                 ne.ctypes.data, _stream(X.device)))
+    return int(ne[0])
+
+
+def train_exports(m, device, ctx=None):
+    """(gid int32[m], key int32[m]) device tensors of the last train_begin."""
+    ctx = ctx or context(device)
+    gid = torch.empty(max(m, 1), dtype=torch.int32, device=device)
+    key = torch.empty(max(m, 1), dtype=torch.int32, device=device)
+    _check(load().pd_train_exports(ctx.ptr, gid.data_ptr(), key.data_ptr(), m, _stream(device)))
+    return gid[:m], key[:m]
+
+
+def merge_exports(n_space, gid, key, ctx=None):
+    """Global key of every id in [0, n_space) (int32 device tensor)."""
+    device = gid.device
+    ctx = ctx or context(device.index)
+    parent = torch.empty(max(n_space, 1), dtype=torch.int32, device=device)
+    m = gid.shape[0]
+    _check(load().pd_merge_exports(ctx.ptr, int(n_space), gid.data_ptr() if m else None,
+                                   key.data_ptr() if m else None, m, parent.data_ptr(),
+                                   _stream(device)))
+    return parent[:n_space]
+
+
+def train_end(n, keymap, device, ctx=None):
+    """Phase B: (keys int32[n], core uint8[n]) device tensors (owned points)."""
+    ctx = ctx or context(device)
+    keys = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    core = torch.empty(max(n, 1), dtype=torch.uint8, device=device)
+    _check(load().pd_train_end(ctx.ptr, n, keymap.data_ptr() if keymap is not None else None,
+                               keys.data_ptr(), core.data_ptr(), _stream(device)))
+    return keys[:n], core[:n]
+
+
+def select_roots(keys, gid, ctx=None):
+    device = keys.device
+    ctx = ctx or context(device.index)
+    n = keys.shape[0]
+    roots = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    m = np.zeros(1, np.int64)
+    _check(load().pd_select_roots(ctx.ptr, keys.data_ptr() if n else None,
+                                  gid.data_ptr() if n else None, n, roots.data_ptr(),
+                                  m.ctypes.data, _stream(device)))
+    return roots[:int(m[0])]
+
+
+def sort_u32(data, ctx=None):
+    """In-place ascending sort (u32 order) of an int32 device tensor."""
+    ctx = ctx or context(data.device.index)
+    n = data.shape[0]
+    _check(load().pd_sort_u32(ctx.ptr, data.data_ptr() if n else None, n, _stream(data.device)))
+    return data
+
+
+def rank_labels(keys, roots, ctx=None):
+    device = keys.device
+    ctx = ctx or context(device.index)
+    n, nr = keys.shape[0], roots.shape[0]
+    labels = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    _check(load().pd_rank_labels(ctx.ptr, keys.data_ptr() if n else None, n,
+                                 roots.data_ptr() if nr else None, nr, labels.data_ptr(),
+                                 _stream(device)))
+    return labels[:n]

@@ -273,4 +273,137 @@ int32_t pd_cluster(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t
     });
 }
 
+// ---------------------------------------------------------------- sharded train
+
+int32_t pd_kd_moments_dd(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                         const int32_t* labels, int32_t n_sel, const int32_t* sel, double* out,
+                         void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (n_sel < 0 || (n_sel && (!sel || !out)) || (n && !labels))
+            throw Error(PD_EINVAL, "bad selection");
+        if (n == 0) {
+            std::memset(out, 0, sizeof(double) * (1 + 4 * d) * n_sel);
+            return;
+        }
+        kd_moments_dd(ctx->c, X, dtype, n, d, labels, n_sel, sel, out, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_route(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, int32_t P,
+                 const double* ebox, const int32_t* part_rank, int32_t n_ranks, uint64_t* mask,
+                 int64_t* counts, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "d > 4");
+        if (!ebox || !part_rank || !counts || (n && !mask)) throw Error(PD_EINVAL, "null argument");
+        route(ctx->c, X, dtype, n, d, P, ebox, part_rank, n_ranks, mask, counts,
+              (hipStream_t)stream);
+    });
+}
+
+int32_t pd_pack(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                const uint64_t* mask, int32_t dest, const int32_t* kdlab, int32_t P,
+                const int32_t* part_rank, const int32_t* local_index, uint32_t gid_base,
+                void* coords, uint32_t* gid, int32_t* owner, uint8_t* xr, int64_t capacity,
+                int64_t* m, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "d > 4");
+        if (P < 1 || !part_rank || !local_index || !m) throw Error(PD_EINVAL, "null argument");
+        if (n && (!mask || !kdlab)) throw Error(PD_EINVAL, "null argument");
+        if (capacity > 0 && (!coords || !gid || !owner || !xr))
+            throw Error(PD_EINVAL, "null output buffer");
+        *m = pack(ctx->c, X, dtype, n, d, mask, dest, kdlab, P, part_rank, local_index, gid_base,
+                  coords, gid, owner, xr, capacity, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_train_begin(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                       double eps, int32_t min_samples, int32_t metric, int32_t P,
+                       const double* ebox, const double* data_box, const int32_t* owner,
+                       const uint32_t* gid, const uint8_t* xr, int64_t* n_exports, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (!ebox) throw Error(PD_EINVAL, "null ebox");
+        if (n > 0 && (!owner || !gid || !xr)) throw Error(PD_EINVAL, "owner, gid and xr required");
+        TrainArgs a;
+        a.X = X;
+        a.dtype = dtype;
+        a.n = n;
+        a.d = d;
+        a.eps = eps;
+        a.min_samples = min_samples;
+        a.metric = metric;
+        a.P = P;
+        a.ebox = ebox;
+        a.data_box = data_box;
+        a.owner = owner;
+        a.gid = gid;
+        a.xr = xr;
+        a.phase = 1;
+        a.stream = (hipStream_t)stream;
+        train(ctx->c, a);
+        if (n_exports) *n_exports = a.n_exports;
+    });
+}
+
+int32_t pd_train_exports(pd_ctx* ctx, uint32_t* gid, uint32_t* key, int64_t capacity,
+                         void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx) throw Error(PD_EINVAL, "null context");
+        if (capacity > 0 && (!gid || !key)) throw Error(PD_EINVAL, "null output buffer");
+        train_exports(ctx->c, gid, key, capacity, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_merge_exports(pd_ctx* ctx, uint32_t n_space, const uint32_t* gid, const uint32_t* key,
+                         int64_t m, uint32_t* parent, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx) throw Error(PD_EINVAL, "null context");
+        if (m < 0 || (m && (!gid || !key)) || (n_space && !parent))
+            throw Error(PD_EINVAL, "null argument");
+        merge_exports(ctx->c, n_space, gid, key, m, parent, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_train_end(pd_ctx* ctx, int64_t n, const uint32_t* keymap, uint32_t* keys, uint8_t* core,
+                     void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx) throw Error(PD_EINVAL, "null context");
+        TrainArgs a;
+        a.n = n;
+        a.keymap = keymap;
+        a.keys_out = keys;
+        a.core = core;
+        a.phase = 2;
+        a.stream = (hipStream_t)stream;
+        train(ctx->c, a);
+    });
+}
+
+int32_t pd_select_roots(pd_ctx* ctx, const uint32_t* keys, const uint32_t* gid, int64_t n,
+                        uint32_t* roots, int64_t* m, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || !m || n < 0 || (n && (!keys || !roots))) throw Error(PD_EINVAL, "bad argument");
+        *m = select_roots(ctx->c, keys, gid, n, roots, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_sort_u32(pd_ctx* ctx, uint32_t* data, int64_t n, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || n < 0 || (n && !data)) throw Error(PD_EINVAL, "bad argument");
+        sort_u32(ctx->c, data, n, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_rank_labels(pd_ctx* ctx, const uint32_t* keys, int64_t n, const uint32_t* roots,
+                       int64_t n_roots, int32_t* labels, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || n < 0 || n_roots < 0 || (n && (!keys || !labels)) || (n_roots && !roots))
+            throw Error(PD_EINVAL, "bad argument");
+        rank_labels(ctx->c, keys, n, roots, n_roots, labels, (hipStream_t)stream);
+    });
+}
+
 }  // extern "C"

@@ -777,16 +777,57 @@ __global__ __launch_bounds__(kBlock) void flatten_kernel(uint32_t R,
     par[r] = x;
 }
 
+// Component key = smallest (global) id of its core points.  gid maps local
+// point ids to global ids on a sharded train (null: identity).
 __global__ __launch_bounds__(kBlock) void gmin_kernel(const uint32_t* __restrict__ vals,
                                                       uint32_t R,
                                                       const uint8_t* __restrict__ core,
                                                       const uint32_t* __restrict__ par,
+                                                      const uint32_t* __restrict__ gid,
                                                       uint32_t* __restrict__ gmin) {
     const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
     const bool ok = r < R && (core[r] & 1);
     const uint32_t root = ok ? par[r] : 0u;
-    const uint32_t pt = ok ? (vals[r] & kIdMask) : kNone;
+    uint32_t pt = ok ? (vals[r] & kIdMask) : kNone;
+    if (ok && gid) pt = gid[pt];
     wave_atomic_min(gmin, ok, root, pt);
+}
+
+// Sharded train, phase A exports: (global id, local component key) of every
+// core record whose point was also routed to another device.
+struct IsExport {
+    const uint8_t* core;
+    const uint32_t* vals;
+    const uint8_t* xr;
+    __device__ bool operator()(uint32_t r) const {
+        return (core[r] & 1) && xr[vals[r] & kIdMask];
+    }
+};
+
+__global__ __launch_bounds__(kBlock) void export_kernel(uint32_t NL,
+                                                        const uint32_t* __restrict__ list,
+                                                        const uint32_t* __restrict__ vals,
+                                                        const uint32_t* __restrict__ par,
+                                                        const uint32_t* __restrict__ gmin,
+                                                        const uint32_t* __restrict__ gid,
+                                                        uint32_t* __restrict__ out_gid,
+                                                        uint32_t* __restrict__ out_key) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= NL) return;
+    const uint32_t r = list[i];
+    const uint32_t pt = vals[r] & kIdMask;
+    out_gid[i] = gid ? gid[pt] : pt;
+    out_key[i] = gmin[par[r]];
+}
+
+// Phase B: replace each local component's key by its global key.
+__global__ __launch_bounds__(kBlock) void remap_kernel(uint32_t R, const uint8_t* __restrict__ core,
+                                                       const uint32_t* __restrict__ par,
+                                                       const uint32_t* __restrict__ keymap,
+                                                       uint32_t* __restrict__ gmin) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= R || !(core[r] & 1) || par[r] != r) return;
+    gmin[r] = keymap[gmin[r]];
 }
 
 // Owner records: publish core flag / count, and the cluster key of core
@@ -939,13 +980,14 @@ uint32_t select_records(Ctx& ctx, const char* name, uint32_t R, Pred pred, uint3
     return *h;
 }
 
+// Phase A: halo records, sort, cell directory, core counts, union-find,
+// component keys (marks 0..8).  Leaves its device state in ctx.st.
 template <typename T, int D, typename K, int M>
-void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t Gtot,
-         int key_bits) {
+void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t Gtot,
+           int key_bits, EvTimer& tm) {
     hipStream_t s = a.stream;
     const uint64_t n = (uint64_t)a.n;
     const int P = a.P;
-    EvTimer tm(ctx, s);
     tm.mark();   // 0
 
     PartGrid* parts = ctx.arena.get<PartGrid>("parts", P);
@@ -1099,18 +1141,81 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
         hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
         PD_HIP(hipMemsetAsync(gmin, 0xFF, sizeof(uint32_t) * R, s));
         hipLaunchKernelGGL(gmin_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, vals, R, core, par,
-                           gmin);
+                           a.gid, gmin);
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 8
 
-    uint32_t* key_out = ctx.arena.get<uint32_t>("key_out", n);
+    PhaseState& st = ctx.st;
+    st.R = R;
+    st.n = n;
+    st.G = Gtot;
+    st.P = P;
+    st.d = D;
+    st.dtype = std::is_same<T, float>::value ? 0 : 1;
+    st.metric = M;
+    st.min_samples = a.min_samples;
+    st.key_bits = key_bits;
+    st.eps = a.eps;
+    st.slo = slo;
+    st.shi = shi;
+    st.Xs = Xs;
+    st.parts = parts;
+    st.part_start = part_start;
+    st.dir = dir;
+    st.cstart = cstart;
+    st.vals = vals;
+    st.core = core;
+    st.par = par;
+    st.gmin = gmin;
+    st.cnt_rec = cnt_rec;
+    st.n_exports = 0;
+    if (a.phase == 1 && R && a.xr) {
+        uint32_t* elist = nullptr;
+        const uint32_t NE = select_records(ctx, "export_list", R, IsExport{core, vals, a.xr},
+                                           &elist, s);
+        st.exp_gid = ctx.arena.get<uint32_t>("exp_gid", NE + 1);
+        st.exp_key = ctx.arena.get<uint32_t>("exp_key", NE + 1);
+        if (NE)
+            hipLaunchKernelGGL(export_kernel, dim3(blocks(NE)), dim3(kBlock), 0, s, NE, elist, vals,
+                               par, gmin, a.gid, st.exp_gid, st.exp_key);
+        PD_HIP(hipGetLastError());
+        st.n_exports = NE;
+    }
+    a.n_exports = st.n_exports;
+    st.valid = true;
+}
+
+
+// Phase B: (sharded: global key remap,) owner records, border attach,
+// then labels (single device) or keys (sharded).
+template <typename T, int D, int M>
+void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
+    hipStream_t s = a.stream;
+    PhaseState& st = ctx.st;
+    const uint64_t n = st.n;
+    const uint32_t R = st.R;
+    const T* Xs = (const T*)st.Xs;
+    const uint32_t* vals = st.vals;
+    const uint8_t* core = st.core;
+    const uint32_t* par = st.par;
+    uint32_t* gmin = st.gmin;
+    const Cells C{(const PartGrid*)st.parts, st.part_start, st.P, (const uint4*)st.dir, st.cstart};
+    const double eps = st.eps, eps2 = st.eps * st.eps;
+    const float slo = st.slo, shi = st.shi;
+    if (a.phase == 2) {
+        tm.mark();   // 0
+        if (a.keymap && R)
+            hipLaunchKernelGGL(remap_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par,
+                               a.keymap, gmin);
+    }
+    uint32_t* key_out = a.phase == 2 ? a.keys_out : ctx.arena.get<uint32_t>("key_out", n);
     PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
     if (a.core) PD_HIP(hipMemsetAsync(a.core, 0, n, s));
     if (R)
     {
         hipLaunchKernelGGL(owner_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, vals, core, par,
-                           gmin, cnt_rec, key_out, a.core, a.counts);
+                           gmin, st.cnt_rec, key_out, a.core, a.counts);
         uint32_t* blist = nullptr;
         const uint32_t NB =
             select_records(ctx, "border_list", R, IsBorderCandidate{core, vals}, &blist, s);
@@ -1119,7 +1224,11 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
                                NB, blist, C, eps, eps2, slo, shi, vals, par, gmin, key_out);
     }
     PD_HIP(hipGetLastError());
-    tm.mark();   // 9
+    tm.mark();   // 9 (phase 2: 1)
+    if (a.phase == 2) {
+        tm.mark();
+        return;
+    }
 
     uint32_t* rflag = ctx.arena.get<uint32_t>("rflag", n);
     uint32_t* rnk = ctx.arena.get<uint32_t>("rnk", n);
@@ -1138,30 +1247,79 @@ void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t G
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 10
-    int64_t* hres = (int64_t*)pinned(ctx, 2 * sizeof(int64_t));
+    int64_t* hres = (int64_t*)pinned(ctx, sizeof(int64_t));
     PD_HIP(hipMemcpyAsync(hres, dncl, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    uint32_t* hnc = (uint32_t*)(hres + 1);
-    if (R)
-        PD_HIP(hipMemcpyAsync(hnc, dncells, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    else
-        *hnc = 0;
     sync(s);
     a.n_clusters = hres[0];
-    ctx.t.cells_n = *hnc;
-    ctx.t.grid_cells = (int64_t)Gtot;
-    ctx.t.key_bits = key_bits;
-    if (ctx.timing) {
-        ctx.t.halo = tm.span(0, 1);
-        ctx.t.sort = tm.span(1, 2);
-        ctx.t.gather = tm.span(2, 3);
-        ctx.t.cells = tm.span(3, 4);
-        ctx.t.count = tm.span(4, 5);
-        ctx.t.link = tm.span(5, 6);
-        ctx.t.merge = tm.span(6, 7);
-        ctx.t.roots = tm.span(7, 8);
-        ctx.t.border = tm.span(8, 9);
-        ctx.t.label = tm.span(9, 10);
-        ctx.t.total = tm.span(0, 10);
+}
+
+// Host-side bookkeeping after phase A (and B): cell count, stage times.
+void finish(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
+    hipStream_t s = a.stream;
+    if (a.phase != 2) {
+        uint32_t* hnc = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+        *hnc = 0;
+        if (ctx.st.R)
+            PD_HIP(hipMemcpyAsync(hnc, ctx.arena.get<uint32_t>("ncells", 4), sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, s));
+        sync(s);
+        ctx.t.cells_n = *hnc;
+        ctx.t.grid_cells = (int64_t)ctx.st.G;
+        ctx.t.key_bits = ctx.st.key_bits;
+    } else {
+        sync(s);
+    }
+    if (!ctx.timing) return;
+    if (a.phase == 2) {
+        ctx.t.border = tm.span(0, 1);
+        ctx.t.label = tm.span(1, 2);
+        ctx.t.total += tm.span(0, 2);
+        return;
+    }
+    ctx.t.halo = tm.span(0, 1);
+    ctx.t.sort = tm.span(1, 2);
+    ctx.t.gather = tm.span(2, 3);
+    ctx.t.cells = tm.span(3, 4);
+    ctx.t.count = tm.span(4, 5);
+    ctx.t.link = tm.span(5, 6);
+    ctx.t.merge = tm.span(6, 7);
+    ctx.t.roots = tm.span(7, 8);
+    if (a.phase == 1) {
+        ctx.t.total = tm.span(0, 8);
+        return;
+    }
+    ctx.t.border = tm.span(8, 9);
+    ctx.t.label = tm.span(9, 10);
+    ctx.t.total = tm.span(0, 10);
+}
+
+template <typename T, int D, typename K, int M>
+void run(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t Gtot,
+         int key_bits) {
+    EvTimer tm(ctx, a.stream);
+    run_a<T, D, K, M>(ctx, a, hparts, Gtot, key_bits, tm);
+    if (a.phase == 0) run_b<T, D, M>(ctx, a, tm);
+    finish(ctx, a, tm);
+}
+
+template <typename T, int D>
+void run_b_m(Ctx& ctx, TrainArgs& a) {
+    EvTimer tm(ctx, a.stream);
+    if (ctx.st.metric == 0)
+        run_b<T, D, 0>(ctx, a, tm);
+    else
+        run_b<T, D, 1>(ctx, a, tm);
+    finish(ctx, a, tm);
+}
+
+template <typename T>
+void run_b_d(Ctx& ctx, TrainArgs& a) {
+    switch (ctx.st.d) {
+        case 1: run_b_m<T, 1>(ctx, a); break;
+        case 2: run_b_m<T, 2>(ctx, a); break;
+        case 3: run_b_m<T, 3>(ctx, a); break;
+        case 4: run_b_m<T, 4>(ctx, a); break;
+        default: throw Error(-5, "grid path supports d <= 4");
     }
 }
 
@@ -1187,6 +1345,21 @@ void run_d(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& p, uint64_t G, i
 }  // namespace
 
 void train(Ctx& ctx, TrainArgs& a) {
+    if (a.phase == 2) {   // resume a sharded train after the global key merge
+        PhaseState& st = ctx.st;
+        if (!st.valid) throw Error(-1, "pd_train_end without a matching pd_train_begin");
+        if (a.n != (int64_t)st.n) throw Error(-1, "pd_train_end: n differs from pd_train_begin");
+        if (!a.keys_out && a.n) throw Error(-1, "keys output is required");
+        if (a.n) {
+            if (st.dtype == 0)
+                run_b_d<float>(ctx, a);
+            else
+                run_b_d<double>(ctx, a);
+        }
+        st.valid = false;
+        return;
+    }
+    ctx.st.valid = false;
     if (a.n < 0 || a.d < 1) throw Error(-1, "invalid shape");
     if (a.d > kMaxDim) throw Error(-5, "d > 4: the dense-tile path is not built yet");
     if (!(a.eps > 0) || !std::isfinite(a.eps)) throw Error(-1, "eps must be a finite value > 0");
@@ -1194,7 +1367,7 @@ void train(Ctx& ctx, TrainArgs& a) {
     if (a.metric != 0 && a.metric != 1) throw Error(-1, "metric must be 0 (euclidean) or 1 (cityblock)");
     if (a.P < 1) throw Error(-1, "need at least one neighbourhood");
     if (a.n > (int64_t)kIdMask) throw Error(-5, "n must be < 2^30 points per device");
-    if (!a.labels && a.n) throw Error(-1, "labels output is required");
+    if (a.phase == 0 && !a.labels && a.n) throw Error(-1, "labels output is required");
     ctx.t = Timings{};
     const int d = a.d;
     double box[2 * kMaxDim];
@@ -1207,6 +1380,11 @@ void train(Ctx& ctx, TrainArgs& a) {
     }
     if (a.n == 0) {
         a.n_clusters = 0;
+        a.n_exports = 0;
+        if (a.phase == 1) {
+            ctx.st = PhaseState{};
+            ctx.st.valid = true;
+        }
         return;
     }
     // per-neighbourhood grids

@@ -48,6 +48,32 @@ struct Timings {
     int64_t records = 0, cells_n = 0, grid_cells = 0, core_records = 0, key_bits = 0;
 };
 
+// Device state carried from phase A (local clustering) to phase B (border
+// attach, keys).  The pointers are arena buffers; any other train call on the
+// context invalidates it.
+struct PhaseState {
+    bool valid = false;
+    uint32_t R = 0;
+    uint64_t n = 0, G = 0;
+    int P = 0, d = 0, dtype = 0, metric = 0, min_samples = 0, key_bits = 0;
+    double eps = 0;
+    float slo = -1.0f, shi = 0.0f;
+    uint32_t ncells = 0;
+    uint32_t n_exports = 0;
+    void* Xs = nullptr;
+    void* parts = nullptr;
+    uint32_t* part_start = nullptr;
+    void* dir = nullptr;
+    uint32_t* cstart = nullptr;
+    uint32_t* vals = nullptr;
+    uint8_t* core = nullptr;
+    uint32_t* par = nullptr;
+    uint32_t* gmin = nullptr;
+    uint32_t* cnt_rec = nullptr;
+    uint32_t* exp_gid = nullptr;
+    uint32_t* exp_key = nullptr;
+};
+
 struct Ctx {
     int device = 0;
     Arena arena;
@@ -60,6 +86,7 @@ struct Ctx {
     int xsub = 2;                // axis-0 sub-cells per eps
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     Timings t;
+    PhaseState st;
     hipEvent_t ev[16] = {};
 };
 
@@ -80,6 +107,14 @@ struct TrainArgs {
     uint32_t* counts = nullptr;       // device out, n (nullable; owner-record counts)
     int64_t n_clusters = 0;           // out
     hipStream_t stream = nullptr;
+    // sharded (multi-device) train: phase 1 = local clustering + exports,
+    // phase 2 = key remap + border attach; phase 0 = both, single device
+    int phase = 0;
+    const uint32_t* gid = nullptr;    // device, global id per local point (null: identity)
+    const uint8_t* xr = nullptr;      // device, point also lives on another device
+    const uint32_t* keymap = nullptr; // device, global parent over the id space (phase 2)
+    uint32_t* keys_out = nullptr;     // device out, n: cluster key per owned point (phase 2)
+    int64_t n_exports = 0;            // out (phase 1)
 };
 
 void train(Ctx& ctx, TrainArgs& a);
@@ -95,6 +130,23 @@ void kd_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32
 void kd_split(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels,
               int n_sel, const int32_t* sel_host, const int32_t* axis_host,
               const double* boundary_host, const int32_t* new_host, hipStream_t s);
+void kd_moments_dd(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
+                   int n_sel, const int32_t* sel_host, double* out_host, hipStream_t s);
+void route(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P, const double* ebox_host,
+           const int32_t* part_rank_host, int n_ranks, uint64_t* mask, int64_t* counts_host,
+           hipStream_t s);
+int64_t pack(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const uint64_t* mask, int dest,
+             const int32_t* kdlab, int P, const int32_t* part_rank_host,
+             const int32_t* local_index_host, uint32_t gid_base, void* coords_out,
+             uint32_t* gid_out, int32_t* owner_out, uint8_t* xr_out, int64_t cap, hipStream_t s);
+void train_exports(Ctx& ctx, uint32_t* gid_out, uint32_t* key_out, int64_t cap, hipStream_t s);
+void merge_exports(Ctx& ctx, uint32_t n_space, const uint32_t* gid, const uint32_t* key, int64_t m,
+                   uint32_t* parent, hipStream_t s);
+int64_t select_roots(Ctx& ctx, const uint32_t* keys, const uint32_t* gid, int64_t n, uint32_t* out,
+                     hipStream_t s);
+void sort_u32(Ctx& ctx, uint32_t* data, int64_t n, hipStream_t s);
+void rank_labels(Ctx& ctx, const uint32_t* keys, int64_t n, const uint32_t* roots, int64_t nr,
+                 int32_t* labels, hipStream_t s);
 void halo_members(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P,
                   const double* ebox_host, int64_t* counts_host, int64_t* members_dev,
                   int64_t members_cap, hipStream_t s);

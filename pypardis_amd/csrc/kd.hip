@@ -393,8 +393,9 @@ void bbox(Ctx& ctx, const void* X, int dtype, int64_t n, int d, double* lohi, in
     if (bad) *bad = (int64_t)nbad;
 }
 
-void kd_moments(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
-                int n_sel, const int32_t* sel, double* out, hipStream_t s) {
+namespace {
+void moments_impl(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
+                  int n_sel, const int32_t* sel, double* out, bool dd_out, hipStream_t s) {
     const int nb = (int)std::min<int64_t>(kRedBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
     const int G = 1 + 4 * d;
     const int W = kGroup * G;
@@ -419,8 +420,9 @@ void kd_moments(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int3
         PD_HIP(hipMemcpyAsync(h, part, sizeof(double) * nbk * W, hipMemcpyDeviceToHost, s));
         sync(s);
         for (int g = 0; g < kGroup && g0 + g < n_sel; ++g) {
-            // out layout per selected label: [3][d] = count row, sum row, sumsq row
-            double* o = out + (size_t)(g0 + g) * 3 * d;
+            // out layout per selected label: [3][d] = count row, sum row, sumsq row;
+            // dd_out: [1 + 4d] = count, (hi, lo) per axis of the sums, then of the squares
+            double* o = out + (size_t)(g0 + g) * (dd_out ? G : 3 * d);
             double cnt = 0;
             std::vector<DD> sum(d, DD{0.0, 0.0}), sq(d, DD{0.0, 0.0});
             for (int k = 0; k < nbk; ++k) {
@@ -431,6 +433,16 @@ void kd_moments(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int3
                     sq[j] = dd_add(sq[j], DD{p[1 + 2 * d + 2 * j], p[2 + 2 * d + 2 * j]});
                 }
             }
+            if (dd_out) {
+                o[0] = cnt;
+                for (int j = 0; j < d; ++j) {
+                    o[1 + 2 * j] = sum[j].hi;
+                    o[2 + 2 * j] = sum[j].lo;
+                    o[1 + 2 * d + 2 * j] = sq[j].hi;
+                    o[2 + 2 * d + 2 * j] = sq[j].lo;
+                }
+                continue;
+            }
             for (int j = 0; j < d; ++j) {
                 o[j] = cnt;
                 o[d + j] = sum[j].hi + sum[j].lo;
@@ -438,6 +450,18 @@ void kd_moments(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int3
             }
         }
     }
+}
+}  // namespace
+
+void kd_moments(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
+                int n_sel, const int32_t* sel, double* out, hipStream_t s) {
+    moments_impl(ctx, X, dtype, n, d, labels, n_sel, sel, out, false, s);
+}
+
+void kd_moments_dd(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
+                   int n_sel, const int32_t* sel, double* out, hipStream_t s) {
+    if (ctx.seq_moments) throw Error(-5, "double-double partials need exact (non-sequential) sums");
+    moments_impl(ctx, X, dtype, n, d, labels, n_sel, sel, out, true, s);
 }
 
 void kd_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,

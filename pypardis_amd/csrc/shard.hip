@@ -1,0 +1,360 @@
+// Sharded (multi-device) train: routing of points to the devices that own
+// their neighbourhoods, the global key merge, and global label ranks.
+//
+// The reference has no device split: its equivalent is Spark's
+// partitionBy(max_partitions) shuffle of the halo records
+// (R:dbscan/dbscan.py:114-118) and the driver-side ClusterAggregator merge
+// (R:dbscan/dbscan.py:153-165, R:dbscan/aggregator.py:9-73).  Here each
+// device holds a slice of the input; a point travels once to every device
+// whose neighbourhoods' expanded boxes contain it (pd_route / pd_pack), each
+// device clusters its neighbourhoods (pd_train_begin), exports the component
+// keys of its cross-device core points, and the union of all exports
+// (pd_merge_exports, identical on every device) maps local keys to global
+// ones (pd_train_end).  Labels are ranks of the global keys
+// (pd_select_roots, pd_sort_u32, pd_rank_labels) - the same numbering
+// single-device pd_train gives.
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include "internal.hpp"
+
+namespace pd {
+namespace {
+
+constexpr int kMaxRanks = 64;   // one bit per device in the route mask
+
+inline unsigned blocks(uint64_t n) { return n ? (unsigned)((n + kBlock - 1) / kBlock) : 1u; }
+
+template <typename F>
+void dispatch(int dtype, int d, F&& f) {
+    auto by_d = [&](auto tp) {
+        switch (d) {
+            case 1: f(tp, std::integral_constant<int, 1>{}); break;
+            case 2: f(tp, std::integral_constant<int, 2>{}); break;
+            case 3: f(tp, std::integral_constant<int, 3>{}); break;
+            case 4: f(tp, std::integral_constant<int, 4>{}); break;
+            default: throw Error(-5, "dimension " + std::to_string(d) + " > 4 not supported yet");
+        }
+    };
+    if (dtype == 0)
+        by_d((float*)nullptr);
+    else if (dtype == 1)
+        by_d((double*)nullptr);
+    else
+        throw Error(-1, "dtype must be 0 (float32) or 1 (float64)");
+}
+
+// Route mask: bit r set when some neighbourhood assigned to device r has an
+// expanded box containing the point (inclusive bounds, the test pd_train's
+// halo uses).  One LDS counter per device, one global atomic per block.
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void route_kernel(const T* __restrict__ X, uint64_t n,
+                                                       const double* __restrict__ ebox, int P,
+                                                       const int32_t* __restrict__ part_rank,
+                                                       int n_ranks,
+                                                       uint64_t* __restrict__ mask,
+                                                       unsigned long long* __restrict__ counts) {
+    __shared__ unsigned int sc[kMaxRanks];
+    for (int k = threadIdx.x; k < n_ranks; k += kBlock) sc[k] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kBlock) {
+        double v[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) v[j] = (double)X[i * D + j];
+        uint64_t m = 0;
+        for (int L = 0; L < P; ++L) {
+            const double* b = ebox + (size_t)L * 2 * D;
+            bool in = true;
+#pragma unroll
+            for (int j = 0; j < D; ++j) in &= (b[j] <= v[j]) & (b[D + j] >= v[j]);
+            if (in) m |= 1ull << part_rank[L];
+        }
+        mask[i] = m;
+        while (m) {
+            const int r = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            atomicAdd(&sc[r], 1u);
+        }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < n_ranks; k += kBlock)
+        if (sc[k]) atomicAdd(counts + k, (unsigned long long)sc[k]);
+}
+
+struct HasBit {
+    const uint64_t* mask;
+    int bit;
+    __device__ bool operator()(uint32_t i) const { return (mask[i] >> bit) & 1ull; }
+};
+
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void pack_kernel(
+    const T* __restrict__ X, const uint32_t* __restrict__ list, uint32_t m,
+    const uint64_t* __restrict__ mask, const int32_t* __restrict__ kdlab,
+    const int32_t* __restrict__ part_rank, const int32_t* __restrict__ local_index, int P,
+    int dest, uint32_t gid_base, T* __restrict__ coords, uint32_t* __restrict__ gid,
+    int32_t* __restrict__ owner, uint8_t* __restrict__ xr) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= m) return;
+    const uint32_t i = list[k];
+#pragma unroll
+    for (int j = 0; j < D; ++j) coords[(size_t)k * D + j] = X[(size_t)i * D + j];
+    gid[k] = gid_base + i;
+    const int32_t L = kdlab[i];
+    owner[k] = (L >= 0 && L < P && part_rank[L] == dest) ? local_index[L] : -1;
+    xr[k] = __popcll(mask[i]) > 1 ? 1 : 0;
+}
+
+__global__ __launch_bounds__(kBlock) void iota_kernel(uint32_t* __restrict__ p, uint32_t n) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) p[i] = i;
+}
+
+// Union-find over the global id space, smaller root wins (the component's
+// root is then its smallest id = its smallest core point).
+__device__ __forceinline__ uint32_t find_root(uint32_t* par, uint32_t x) {
+    uint32_t p = __hip_atomic_load(par + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (p != x) {
+        x = p;
+        p = __hip_atomic_load(par + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return x;
+}
+
+__global__ __launch_bounds__(kBlock) void unite_kernel(const uint32_t* __restrict__ ga,
+                                                       const uint32_t* __restrict__ gb, int64_t m,
+                                                       uint32_t n_space,
+                                                       uint32_t* __restrict__ par,
+                                                       uint32_t* __restrict__ bad) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= m) return;
+    uint32_t a = ga[i], b = gb[i];
+    if (a >= n_space || b >= n_space) {
+        atomicOr(bad, 1u);
+        return;
+    }
+    a = find_root(par, a);
+    b = find_root(par, b);
+    while (a != b) {
+        if (a > b) {
+            const uint32_t t = a;
+            a = b;
+            b = t;
+        }
+        uint32_t expected = b;
+        if (__hip_atomic_compare_exchange_strong(par + b, &expected, a, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return;
+        b = find_root(par, expected);
+        a = find_root(par, a);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void flatten_all_kernel(uint32_t* __restrict__ par,
+                                                             uint32_t n) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint32_t x = par[i];
+    if (x == i) return;
+    while (true) {
+        const uint32_t p = par[x];
+        if (p == x) break;
+        x = p;
+    }
+    par[i] = x;
+}
+
+struct IsRoot {   // owned core point whose key is its own global id
+    const uint32_t* keys;
+    const uint32_t* gid;
+    __device__ bool operator()(uint32_t i) const {
+        const uint32_t k = keys[i];
+        return k != kNone && k == (gid ? gid[i] : i);
+    }
+};
+
+__global__ __launch_bounds__(kBlock) void map_gid_kernel(uint32_t* __restrict__ p, uint32_t m,
+                                                         const uint32_t* __restrict__ gid) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < m) p[i] = gid[p[i]];
+}
+
+__global__ __launch_bounds__(kBlock) void rank_kernel(const uint32_t* __restrict__ keys, uint64_t n,
+                                                      const uint32_t* __restrict__ roots,
+                                                      uint32_t nr, int32_t* __restrict__ labels) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = keys[i];
+    if (k == kNone) {
+        labels[i] = -1;
+        return;
+    }
+    uint32_t lo = 0, hi = nr;   // first root >= k
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (roots[mid] < k)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    labels[i] = (lo < nr && roots[lo] == k) ? (int32_t)lo : -2;   // -2: key without a root
+}
+
+}  // namespace
+
+void route(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P, const double* ebox_host,
+           const int32_t* part_rank_host, int n_ranks, uint64_t* mask, int64_t* counts_host,
+           hipStream_t s) {
+    if (n_ranks < 1 || n_ranks > kMaxRanks) throw Error(-1, "n_ranks must be in [1, 64]");
+    if (P < 1) throw Error(-1, "need at least one neighbourhood");
+    for (int L = 0; L < P; ++L)
+        if (part_rank_host[L] < 0 || part_rank_host[L] >= n_ranks)
+            throw Error(-1, "part_rank out of range");
+    const size_t tb = sizeof(double) * P * 2 * d + sizeof(int32_t) * P;
+    char* h = (char*)pinned(ctx, tb + 64);
+    std::memcpy(h, ebox_host, sizeof(double) * P * 2 * d);
+    std::memcpy(h + sizeof(double) * P * 2 * d, part_rank_host, sizeof(int32_t) * P);
+    char* dt = ctx.arena.get<char>("route_tab", tb + 64);
+    PD_HIP(hipMemcpyAsync(dt, h, tb, hipMemcpyHostToDevice, s));
+    unsigned long long* dc = ctx.arena.get<unsigned long long>("route_cnt", kMaxRanks);
+    PD_HIP(hipMemsetAsync(dc, 0, sizeof(unsigned long long) * kMaxRanks, s));
+    if (n) {
+        dispatch(dtype, d, [&](auto tp, auto Dc) {
+            using T = std::remove_pointer_t<decltype(tp)>;
+            constexpr int D = decltype(Dc)::value;
+            hipLaunchKernelGGL((route_kernel<T, D>), dim3(grid_for(n, 8192)), dim3(kBlock), 0, s,
+                               (const T*)X, (uint64_t)n, (const double*)dt, P,
+                               (const int32_t*)(dt + sizeof(double) * P * 2 * d), n_ranks, mask,
+                               dc);
+        });
+        PD_HIP(hipGetLastError());
+    }
+    unsigned long long* hc = (unsigned long long*)pinned(ctx, sizeof(unsigned long long) * kMaxRanks);
+    PD_HIP(hipMemcpyAsync(hc, dc, sizeof(unsigned long long) * n_ranks, hipMemcpyDeviceToHost, s));
+    sync(s);
+    for (int r = 0; r < n_ranks; ++r) counts_host[r] = (int64_t)hc[r];
+}
+
+int64_t pack(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const uint64_t* mask, int dest,
+             const int32_t* kdlab, int P, const int32_t* part_rank_host,
+             const int32_t* local_index_host, uint32_t gid_base, void* coords_out,
+             uint32_t* gid_out, int32_t* owner_out, uint8_t* xr_out, int64_t cap, hipStream_t s) {
+    if (dest < 0 || dest >= kMaxRanks) throw Error(-1, "dest out of range");
+    if (n > (int64_t)kIdMask) throw Error(-5, "n must be < 2^30 points per device");
+    if ((uint64_t)gid_base + (uint64_t)n > 0xFFFFFFFEull)
+        throw Error(-5, "global ids must stay below 2^32 - 1");
+    const size_t tb = sizeof(int32_t) * 2 * P;
+    int32_t* h = (int32_t*)pinned(ctx, tb + 64);
+    std::memcpy(h, part_rank_host, sizeof(int32_t) * P);
+    std::memcpy(h + P, local_index_host, sizeof(int32_t) * P);
+    int32_t* dt = ctx.arena.get<int32_t>("pack_tab", 2 * P + 16);
+    PD_HIP(hipMemcpyAsync(dt, h, tb, hipMemcpyHostToDevice, s));
+    uint32_t* list = ctx.arena.get<uint32_t>("pack_list", n + 1);
+    uint32_t* dcount = ctx.arena.get<uint32_t>("pack_count", 4);
+    {
+        rocprim::counting_iterator<uint32_t> it(0u);
+        size_t tmp_b = 0;
+        HasBit pred{mask, dest};
+        PD_HIP(rocprim::select(nullptr, tmp_b, it, list, dcount, (size_t)n, pred, s));
+        void* tmp = ctx.arena.get<char>("pack_tmp", tmp_b);
+        PD_HIP(rocprim::select(tmp, tmp_b, it, list, dcount, (size_t)n, pred, s));
+    }
+    uint32_t* hm = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+    PD_HIP(hipMemcpyAsync(hm, dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    sync(s);
+    const uint32_t m = *hm;
+    if ((int64_t)m > cap) throw Error(-1, "pack: output buffers too small");
+    if (m) {
+        dispatch(dtype, d, [&](auto tp, auto Dc) {
+            using T = std::remove_pointer_t<decltype(tp)>;
+            constexpr int D = decltype(Dc)::value;
+            hipLaunchKernelGGL((pack_kernel<T, D>), dim3(blocks(m)), dim3(kBlock), 0, s,
+                               (const T*)X, list, m, mask, kdlab, dt, dt + P, P, dest, gid_base,
+                               (T*)coords_out, gid_out, owner_out, xr_out);
+        });
+        PD_HIP(hipGetLastError());
+    }
+    return (int64_t)m;
+}
+
+void train_exports(Ctx& ctx, uint32_t* gid_out, uint32_t* key_out, int64_t cap, hipStream_t s) {
+    const PhaseState& st = ctx.st;
+    if (!st.valid) throw Error(-1, "pd_train_exports without a matching pd_train_begin");
+    if ((int64_t)st.n_exports > cap) throw Error(-1, "exports buffers too small");
+    if (!st.n_exports) return;
+    PD_HIP(hipMemcpyAsync(gid_out, st.exp_gid, sizeof(uint32_t) * st.n_exports,
+                          hipMemcpyDeviceToDevice, s));
+    PD_HIP(hipMemcpyAsync(key_out, st.exp_key, sizeof(uint32_t) * st.n_exports,
+                          hipMemcpyDeviceToDevice, s));
+}
+
+void merge_exports(Ctx& ctx, uint32_t n_space, const uint32_t* gid, const uint32_t* key, int64_t m,
+                   uint32_t* parent, hipStream_t s) {
+    if (n_space == 0xFFFFFFFFu) throw Error(-5, "id space must be < 2^32 - 1");
+    if (n_space)
+        hipLaunchKernelGGL(iota_kernel, dim3(blocks(n_space)), dim3(kBlock), 0, s, parent, n_space);
+    uint32_t* dbad = ctx.arena.get<uint32_t>("merge_bad", 4);
+    PD_HIP(hipMemsetAsync(dbad, 0, sizeof(uint32_t), s));
+    if (m > 0) {
+        hipLaunchKernelGGL(unite_kernel, dim3(blocks((uint64_t)m)), dim3(kBlock), 0, s, gid, key, m,
+                           n_space, parent, dbad);
+    }
+    if (n_space)
+        hipLaunchKernelGGL(flatten_all_kernel, dim3(blocks(n_space)), dim3(kBlock), 0, s, parent,
+                           n_space);
+    PD_HIP(hipGetLastError());
+    uint32_t* hb = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+    PD_HIP(hipMemcpyAsync(hb, dbad, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    sync(s);
+    if (*hb) throw Error(-1, "merge_exports: id outside the id space");
+}
+
+int64_t select_roots(Ctx& ctx, const uint32_t* keys, const uint32_t* gid, int64_t n, uint32_t* out,
+                     hipStream_t s) {
+    if (n > (int64_t)kIdMask) throw Error(-5, "n must be < 2^30 points per device");
+    uint32_t* dcount = ctx.arena.get<uint32_t>("roots_count", 4);
+    PD_HIP(hipMemsetAsync(dcount, 0, sizeof(uint32_t), s));
+    if (n) {
+        rocprim::counting_iterator<uint32_t> it(0u);
+        size_t tb = 0;
+        IsRoot pred{keys, gid};
+        PD_HIP(rocprim::select(nullptr, tb, it, out, dcount, (size_t)n, pred, s));
+        void* tmp = ctx.arena.get<char>("roots_tmp", tb);
+        PD_HIP(rocprim::select(tmp, tb, it, out, dcount, (size_t)n, pred, s));
+    }
+    uint32_t* hm = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+    PD_HIP(hipMemcpyAsync(hm, dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    sync(s);
+    const uint32_t m = *hm;
+    if (m && gid) {
+        hipLaunchKernelGGL(map_gid_kernel, dim3(blocks(m)), dim3(kBlock), 0, s, out, m, gid);
+        PD_HIP(hipGetLastError());
+    }
+    return (int64_t)m;
+}
+
+void sort_u32(Ctx& ctx, uint32_t* data, int64_t n, hipStream_t s) {
+    if (n <= 1) return;
+    uint32_t* alt = ctx.arena.get<uint32_t>("sortu_alt", (size_t)n);
+    rocprim::double_buffer<uint32_t> kb(data, alt);
+    size_t tb = 0;
+    PD_HIP(rocprim::radix_sort_keys(nullptr, tb, kb, (size_t)n, 0u, 32u, s));
+    void* tmp = ctx.arena.get<char>("sortu_tmp", tb);
+    PD_HIP(rocprim::radix_sort_keys(tmp, tb, kb, (size_t)n, 0u, 32u, s));
+    if (kb.current() != data)
+        PD_HIP(hipMemcpyAsync(data, kb.current(), sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, s));
+    PD_HIP(hipGetLastError());
+}
+
+void rank_labels(Ctx& ctx, const uint32_t* keys, int64_t n, const uint32_t* roots, int64_t nr,
+                 int32_t* labels, hipStream_t s) {
+    (void)ctx;
+    if (nr > (int64_t)0x7FFFFFFF) throw Error(-5, "too many clusters");
+    if (n)
+        hipLaunchKernelGGL(rank_kernel, dim3(blocks((uint64_t)n)), dim3(kBlock), 0, s, keys,
+                           (uint64_t)n, roots, (uint32_t)nr, labels);
+    PD_HIP(hipGetLastError());
+}
+
+}  // namespace pd

@@ -1,0 +1,349 @@
+"""Sharded train: one process per GPU, torch.distributed for the exchanges.
+
+The reference spreads its work over Spark executors: the KD partitioner's
+aggregates run over every RDD slice (R:dbscan/partition.py:60-63,86-89), the
+halo records are shuffled with ``partitionBy(max_partitions)``
+(R:dbscan/dbscan.py:114-118), every partition is clustered where it lands
+(R:dbscan/dbscan.py:12-34) and the driver merges the cluster ids
+(R:dbscan/dbscan.py:153-165, R:dbscan/aggregator.py:9-73).  Here each rank
+holds a slice of the points in its GPU's HBM and the same steps are:
+
+  1. bbox: one all-reduce (min / max / non-finite count);
+  2. KD levels: per level one all-gather of the double-double moment partials
+     (added exactly, so the split axes and bounds equal the single-device
+     ones bit for bit) and one all-reduce of the seven-bound counts;
+  3. routing: neighbourhood L goes to rank ``L * world // P``; every point
+     travels once to each rank whose neighbourhoods' 2·eps boxes hold it
+     (pd_route / pd_pack), one all-to-all-v per field;
+  4. phase A on each rank (pd_train_begin): grid, counts, union-find, local
+     component keys; export (global id, key) of core points that also live on
+     another rank;
+  5. one all-gather of the exports; every rank builds the same global key map
+     (pd_merge_exports) — the RCCL label merge;
+  6. phase B (pd_train_end): border attach with global keys;
+  7. labels: all-gather of the cluster roots (one id per cluster), sorted, and
+     each key's rank is its label (pd_select_roots / pd_sort_u32 /
+     pd_rank_labels) — sklearn's numbering, as the single-device pd_train.
+
+Result: each rank returns the global ids and labels of the points it owns
+(every point is owned by exactly one rank: the one holding its KD partition).
+
+The device work goes through an ``ops`` object (``NativeOps``: libpardis on
+this rank's GPU).  Collectives run on ``comm_device``: the GPU under RCCL
+("nccl"), the host under gloo.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _native
+from .geometry import BoundingBox
+from .partition import _split_schedule, apply_level, level_axes, level_boundaries
+
+
+class NativeOps(object):
+    """The per-rank device stages (libpardis through the C ABI)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.ctx = _native.context(self.device.index)
+
+    # -- buffers
+    def empty(self, n, dtype, d=None):
+        shape = (n, d) if d is not None else (n,)
+        return torch.empty(shape, dtype=dtype, device=self.device)
+
+    def zeros(self, n, dtype):
+        return torch.zeros(n, dtype=dtype, device=self.device)
+
+    # -- KD passes
+    def bbox(self, X):
+        return _native.bbox(X, ctx=self.ctx)
+
+    def moments_dd(self, X, labels, sel):
+        return _native.kd_moments_dd(X, labels, sel, ctx=self.ctx)
+
+    def counts(self, X, labels, sel, axes, bounds):
+        return _native.kd_counts(X, labels, sel, axes, bounds, ctx=self.ctx)
+
+    def split(self, X, labels, sel, axes, boundary, new):
+        _native.kd_split(X, labels, sel, axes, boundary, new, ctx=self.ctx)
+
+    # -- routing
+    def route(self, X, ebox, part_rank, world):
+        return _native.route(X, ebox, part_rank, world, ctx=self.ctx)
+
+    def pack(self, X, mask, dest, kdlab, part_rank, local_index, gid_base, out):
+        return _native.pack(X, mask, dest, kdlab, part_rank, local_index, gid_base, out,
+                            ctx=self.ctx)
+
+    # -- clustering phases
+    def train_begin(self, X, eps, min_samples, metric, ebox, owner, gid, xr, data_box):
+        return _native.train_begin(X, eps, min_samples, metric, ebox, owner, gid, xr, data_box,
+                                   ctx=self.ctx)
+
+    def exports(self, m):
+        return _native.train_exports(m, self.device, ctx=self.ctx)
+
+    def merge(self, n_space, gid, key):
+        return _native.merge_exports(n_space, gid, key, ctx=self.ctx)
+
+    def train_end(self, n, keymap):
+        return _native.train_end(n, keymap, self.device, ctx=self.ctx)
+
+    def select_roots(self, keys, gid):
+        return _native.select_roots(keys, gid, ctx=self.ctx)
+
+    def sort(self, data):
+        return _native.sort_u32(data, ctx=self.ctx)
+
+    def rank_labels(self, keys, roots):
+        return _native.rank_labels(keys, roots, ctx=self.ctx)
+
+    def timings(self):
+        return self.ctx.timings()
+
+
+# ------------------------------------------------------------------ helpers
+def _two_sum(a, b):
+    s = a + b
+    bb = s - a
+    return s, (a - (s - bb)) + (b - bb)
+
+
+def dd_combine(parts):
+    """Add per-rank double-double partials (W, S, 1 + 4d) in rank order and
+    round once: (S, 3, d) moments = {count, Σv, Σv²} (kd.hip dd_add)."""
+    parts = np.asarray(parts, np.float64)
+    W, S, G = parts.shape
+    d = (G - 1) // 4
+    cnt = np.zeros(S)
+    hs = np.zeros((S, 2 * d))
+    ls = np.zeros((S, 2 * d))
+    for w in range(W):
+        p = parts[w]
+        cnt = cnt + p[:, 0]
+        bh = p[:, 1::2]
+        bl = p[:, 2::2]
+        s, e = _two_sum(hs, bh)
+        e = e + (ls + bl)
+        hi = s + e
+        ls = e - (hi - s)
+        hs = hi
+    tot = hs + ls
+    mom = np.empty((S, 3, d))
+    mom[:, 0, :] = cnt[:, None]
+    mom[:, 1, :] = tot[:, :d]
+    mom[:, 2, :] = tot[:, d:]
+    return mom
+
+
+def partition_ranks(P, world):
+    """Neighbourhood -> rank (contiguous blocks of KD labels) and each
+    neighbourhood's index among its rank's neighbourhoods."""
+    part_rank = np.array([L * world // P for L in range(P)], np.int32)
+    local_index = np.zeros(P, np.int32)
+    for r in range(world):
+        idx = np.nonzero(part_rank == r)[0]
+        local_index[idx] = np.arange(len(idx), dtype=np.int32)
+    return part_rank, local_index
+
+
+class _Comm(object):
+    """torch.distributed on the right device for the backend."""
+
+    def __init__(self, group, device):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        backend = dist.get_backend(group)
+        self.device = torch.device(device) if backend == "nccl" else torch.device("cpu")
+
+    def to(self, t):
+        return t.to(self.device)
+
+    def all_reduce(self, arr, op):
+        t = torch.as_tensor(np.ascontiguousarray(arr)).to(self.device)
+        dist.all_reduce(t, op=op, group=self.group)
+        return t.cpu().numpy()
+
+    def all_gather_np(self, arr):
+        t = torch.as_tensor(np.ascontiguousarray(arr)).to(self.device)
+        outs = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(outs, t, group=self.group)
+        return np.stack([o.cpu().numpy() for o in outs])
+
+    def all_gather_var(self, t):
+        """Concatenate 1-D tensors of different lengths from every rank."""
+        sizes = self.all_gather_np(np.array([t.shape[0]], np.int64))[:, 0]
+        mx = max(int(sizes.max()), 1)
+        buf = torch.zeros(mx, dtype=t.dtype, device=self.device)
+        buf[:t.shape[0]] = self.to(t)
+        outs = [torch.empty_like(buf) for _ in range(self.world)]
+        dist.all_gather(outs, buf, group=self.group)
+        return torch.cat([o[:int(s)] for o, s in zip(outs, sizes)])
+
+    def all_to_all_v(self, send, send_counts, recv_counts, width=1):
+        """send (sum(send_counts) * width) elements grouped by destination."""
+        recv = torch.empty(int(sum(recv_counts)) * width, dtype=send.dtype, device=self.device)
+        dist.all_to_all_single(recv, self.to(send.reshape(-1)),
+                               output_split_sizes=[int(c) * width for c in recv_counts],
+                               input_split_sizes=[int(c) * width for c in send_counts],
+                               group=self.group)
+        return recv
+
+
+class ShardedResult(object):
+    """Per-rank output of ``train_sharded``.
+
+    :gid: global ids of the points this rank owns (ascending)
+    :labels: their DBSCAN labels (sklearn numbering over all points, -1 noise)
+    :core: their core flags
+    :n_clusters: number of clusters over all points
+    :splits, boxes: the KD trace and boxes (identical on every rank)
+    """
+
+    def __init__(self, gid, labels, core, n_clusters, splits, boxes, stats):
+        self.gid = gid
+        self.labels = labels
+        self.core = core
+        self.n_clusters = n_clusters
+        self.splits = splits
+        self.boxes = boxes
+        self.stats = stats
+
+
+def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitions=None,
+                  group=None, ops=None):
+    """Sharded DBSCAN train over the ranks of ``group`` (default: world).
+
+    X: this rank's (n_i, d) slice (float32/float64, on this rank's GPU for
+    NativeOps); the global id of row j is sum(n_0 .. n_{i-1}) + j.
+    ``max_partitions`` defaults to the world size (one KD partition per GPU).
+    """
+    ops = ops or NativeOps(X.device)
+    comm = _Comm(group, getattr(ops, "device", X.device))
+    W, rank = comm.world, comm.rank
+    n, d = X.shape
+    P = int(max_partitions) if max_partitions is not None else W
+    if P < 1:
+        raise ValueError("max_partitions must be >= 1")
+    if P > 64 * 1024:
+        raise ValueError("max_partitions too large")
+    metric = _native.metric_code(metric) if not isinstance(metric, int) else metric
+    stats = {}
+    clock = [time.perf_counter()]
+
+    def lap(name):   # host wall time per phase (each phase ends in a host sync)
+        now = time.perf_counter()
+        stats[name + "_ms"] = round(1e3 * (now - clock[0]), 3)
+        clock[0] = now
+
+    # ---- global ids
+    sizes = comm.all_gather_np(np.array([n], np.int64))[:, 0]
+    gid_base = int(sizes[:rank].sum())
+    n_total = int(sizes.sum())
+    if n_total >= 0xFFFFFFFF:
+        raise ValueError("the sharded train addresses points with 32-bit global ids")
+
+    # ---- bbox (R:dbscan/partition.py:135-137)
+    if n:
+        lo, hi, bad = ops.bbox(X)
+    else:
+        lo, hi, bad = np.full(d, np.inf), np.full(d, -np.inf), 0
+    ext = comm.all_reduce(np.concatenate([-np.asarray(lo), np.asarray(hi)]), dist.ReduceOp.MAX)
+    nbad = comm.all_reduce(np.array([bad], np.int64), dist.ReduceOp.SUM)[0]
+    if nbad:
+        raise ValueError("Input contains NaN or infinity.")
+    if n_total == 0:
+        raise ValueError("no points on any rank")
+    data_box = np.concatenate([-ext[:d], ext[d:]])
+    box = BoundingBox(k=d).union(BoundingBox(data_box[:d], data_box[d:]))
+
+    # ---- KD partition (R:dbscan/partition.py:139-183)
+    kdlab = ops.zeros(n, torch.int32)
+    boxes = {0: box}
+    splits = []
+    for level in _split_schedule(P):
+        sel = [c for c, _ in level]
+        new = [nl for _, nl in level]
+        part = ops.moments_dd(X, kdlab, sel) if n else np.zeros((len(sel), 1 + 4 * d))
+        mom = dd_combine(comm.all_gather_np(part))
+        axes, means, vars_, bounds = level_axes(mom)
+        cnt = ops.counts(X, kdlab, sel, axes, bounds) if n else np.zeros((len(sel), 8), np.int64)
+        cnt = comm.all_reduce(cnt.astype(np.int64), dist.ReduceOp.SUM)
+        boundary, cand = level_boundaries(cnt, bounds)
+        if n:
+            ops.split(X, kdlab, sel, axes, boundary, new)
+        apply_level(boxes, splits, level, axes, means, vars_, cnt, cand, boundary)
+    ebox = np.stack([boxes[L].expand(2 * eps).as_array() for L in sorted(boxes)])
+    lap("kd")
+
+    # ---- route + exchange (R:dbscan/dbscan.py:114-118,136-151)
+    part_rank, local_index = partition_ranks(P, W)
+    if n:
+        mask, send_counts = ops.route(X, ebox, part_rank, W)
+    else:
+        mask, send_counts = None, np.zeros(W, np.int64)
+    tot = int(send_counts.sum())
+    s_coords = ops.empty(tot, X.dtype, d)
+    s_gid = ops.empty(tot, torch.int32)
+    s_owner = ops.empty(tot, torch.int32)
+    s_xr = ops.empty(tot, torch.uint8)
+    off = 0
+    for dest in range(W):
+        c = int(send_counts[dest])
+        if c and n:
+            m = ops.pack(X, mask, dest, kdlab, part_rank, local_index, gid_base,
+                         (s_coords[off:off + c], s_gid[off:off + c], s_owner[off:off + c],
+                          s_xr[off:off + c]))
+            if m != c:
+                raise RuntimeError(f"pack: {m} points for rank {dest}, route said {c}")
+        off += c
+    recv_counts = comm.all_to_all_v(torch.as_tensor(send_counts, dtype=torch.int64),
+                                    np.ones(W, np.int64), np.ones(W, np.int64)).cpu().numpy()
+    dev = getattr(ops, "device", X.device)
+    Xr = comm.all_to_all_v(s_coords, send_counts, recv_counts, d).to(dev).reshape(-1, d)
+    gid = comm.all_to_all_v(s_gid, send_counts, recv_counts).to(dev)
+    owner = comm.all_to_all_v(s_owner, send_counts, recv_counts).to(dev)
+    xr = comm.all_to_all_v(s_xr, send_counts, recv_counts).to(dev)
+    del s_coords, s_gid, s_owner, s_xr, mask
+    nr = int(recv_counts.sum())
+    stats["sent"], stats["received"] = tot, nr
+    lap("exchange")
+
+    # ---- phase A on this rank's neighbourhoods
+    mine = [L for L in range(P) if part_rank[L] == rank]
+    if mine:
+        n_exp = ops.train_begin(Xr.contiguous(), eps, min_samples, metric, ebox[mine], owner,
+                                gid, xr, data_box)
+        e_gid, e_key = ops.exports(n_exp)
+    else:
+        e_gid = ops.empty(0, torch.int32)
+        e_key = ops.empty(0, torch.int32)
+    stats["exports"] = int(e_gid.shape[0])
+    lap("phase_a")
+
+    # ---- global key merge (R:dbscan/dbscan.py:153-165)
+    all_gid = comm.all_gather_var(e_gid).to(dev)
+    all_key = comm.all_gather_var(e_key).to(dev)
+    keymap = ops.merge(n_total, all_gid, all_key) if all_gid.shape[0] else None
+    lap("merge")
+
+    # ---- phase B, labels
+    if mine:
+        keys, core = ops.train_end(nr, keymap)
+    else:
+        keys, core = ops.empty(0, torch.int32), ops.empty(0, torch.uint8)
+    roots = ops.select_roots(keys, gid) if nr else ops.empty(0, torch.int32)
+    all_roots = comm.all_gather_var(roots).to(dev)
+    ops.sort(all_roots)
+    labels = ops.rank_labels(keys, all_roots) if nr else ops.empty(0, torch.int32)
+    own = owner >= 0
+    lap("phase_b")
+    return ShardedResult(gid[own], labels[own], core[own], int(all_roots.shape[0]), splits,
+                         ebox, stats)

@@ -12,10 +12,10 @@ the points run as HIP kernels through the C ABI:
     bbox     union of all points      pd_bbox         (R:dbscan/partition.py:135-137)
 
 All splits of one BFS level run in the same passes (each split only reads its
-own label's points, so batching cannot change a result).  The fp64 sums are
-deterministic but not in the reference's sequential order, so a boundary can
-differ from the reference's in the last bits (tests allow 1e-12 relative and
-require the candidate index and child sizes to match).
+own label's points, so batching cannot change a result).  The sums are
+correctly rounded (double-double, order independent — the same on one device
+or summed over many, pypardis_amd/distributed.py); ``sums='sequential'``
+reproduces the reference's left-to-right fold bit for bit instead.
 
 Deliberate deviation: a variance that round-off makes negative is clamped to
 0 before the sqrt; the reference takes sqrt(<0) = NaN there and silently
@@ -140,6 +140,49 @@ def median_search_split(partition, axis, next_part):
     raise NotImplementedError("split_method='rotation' (median_search_split) is not built yet")
 
 
+def level_axes(mom):
+    """Per split of one BFS level, from its moments (S, 3, d) = {count, Σv,
+    Σv²}: the largest-variance axis (first argmax), its mean and variance and
+    the seven candidate bounds (R:dbscan/partition.py:86-95, 58-59)."""
+    axes, means, vars_, bounds = [], [], [], []
+    for s in range(mom.shape[0]):
+        with np.errstate(invalid="ignore", divide="ignore"):
+            m = mom[s, 1] / mom[s, 0]
+            v = mom[s, 2] / mom[s, 0] - m ** 2
+        a = int(np.argmax(v))
+        axes.append(a)
+        means.append(m[a])
+        vars_.append(v[a])
+        bounds.append(_bounds(m[a], v[a]))
+    return axes, means, vars_, np.array(bounds).reshape(len(axes), 7)
+
+
+def level_boundaries(cnt, bounds):
+    """First bound minimising |#left − #right| (R:dbscan/partition.py:60-65);
+    cnt (S, 8) = #points below each bound, #points."""
+    boundary, cand = [], []
+    for s in range(cnt.shape[0]):
+        c = np.abs(2.0 * cnt[s, :7].astype(np.float64) - float(cnt[s, 7]))
+        i = int(np.argmin(c))
+        cand.append(i)
+        boundary.append(bounds[s, i])
+    return boundary, cand
+
+
+def apply_level(boxes, splits, level, axes, means, vars_, cnt, cand, boundary):
+    """Split the boxes of one level (R:dbscan/partition.py:151-152,
+    R:dbscan/geometry.py:51-71) and record the split trace."""
+    for s, (cur, nl) in enumerate(level):
+        left, right = boxes[cur].split(axes[s], boundary[s])
+        boxes[cur] = left
+        boxes[nl] = right
+        n_tot = int(cnt[s, 7])
+        # left child = points with v < boundary: counts of the chosen bound
+        n_left = int(cnt[s, cand[s]])
+        splits.append((cur, nl, axes[s], cand[s], n_left, n_tot - n_left,
+                       float(means[s]), float(vars_[s]), float(boundary[s])))
+
+
 class KDPartitioner(object):
     """R:dbscan/partition.py:98-183.
 
@@ -189,34 +232,12 @@ class KDPartitioner(object):
             sel = [c for c, _ in level]
             new = [nl for _, nl in level]
             mom = _native.kd_moments(X, labels, sel, sequential=(self.sums == 'sequential'))
-            axes, means, vars_, bounds = [], [], [], []
-            for s in range(len(sel)):
-                with np.errstate(invalid="ignore", divide="ignore"):
-                    m = mom[s, 1] / mom[s, 0]
-                    v = mom[s, 2] / mom[s, 0] - m ** 2
-                a = int(np.argmax(v))
-                axes.append(a)
-                means.append(m[a])
-                vars_.append(v[a])
-                bounds.append(_bounds(m[a], v[a]))
-            bounds = np.array(bounds).reshape(len(sel), 7)
+            axes, means, vars_, bounds = level_axes(mom)
             cnt = _native.kd_counts(X, labels, sel, axes, bounds)
-            boundary, cand = [], []
-            for s in range(len(sel)):
-                c = np.abs(2.0 * cnt[s, :7].astype(np.float64) - float(cnt[s, 7]))
-                i = int(np.argmin(c))
-                cand.append(i)
-                boundary.append(bounds[s, i])
+            boundary, cand = level_boundaries(cnt, bounds)
             _native.kd_split(X, labels, sel, axes, boundary, new)
-            for s, (cur, nl) in enumerate(level):
-                left, right = self.bounding_boxes[cur].split(axes[s], boundary[s])
-                self.bounding_boxes[cur] = left
-                self.bounding_boxes[nl] = right
-                n_tot = int(cnt[s, 7])
-                # left child = points with v < boundary: counts of the chosen bound
-                n_left = int(cnt[s, cand[s]])
-                self.splits.append((cur, nl, axes[s], cand[s], n_left, n_tot - n_left,
-                                    float(means[s]), float(vars_[s]), float(boundary[s])))
+            apply_level(self.bounding_boxes, self.splits, level, axes, means, vars_, cnt, cand,
+                        boundary)
 
     def box_array(self):
         """(P, 2, k) fp64 boxes in label order."""

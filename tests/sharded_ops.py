@@ -1,0 +1,123 @@
+"""CPU stand-in for ``pypardis_amd.distributed.NativeOps``: the same stage
+interface computed by the oracle (numpy / oracle.sharded), so the sharded
+orchestration and its collectives run under gloo on a machine without a GPU.
+Test infrastructure only."""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+import oracle
+from oracle import sharded as osh
+
+
+class OracleOps(object):
+    device = torch.device("cpu")
+
+    def __init__(self, metric="euclidean"):
+        self.metric = metric
+        self.state = None
+        self.exp = None
+
+    def empty(self, n, dtype, d=None):
+        return torch.empty((n, d) if d is not None else (n,), dtype=dtype)
+
+    def zeros(self, n, dtype):
+        return torch.zeros(n, dtype=dtype)
+
+    def bbox(self, X):
+        a = X.numpy().astype(np.float64)
+        bad = int((~np.isfinite(a)).sum())
+        return a.min(0), a.max(0), bad
+
+    def moments_dd(self, X, labels, sel):
+        """Exact per-label sums split into (hi, lo); squares rounded in the
+        input precision first (as numpy's ``v ** 2`` of the reference)."""
+        x = X.numpy()
+        lab = labels.numpy()
+        d = x.shape[1]
+        out = np.zeros((len(sel), 1 + 4 * d))
+        for s, L in enumerate(sel):
+            v = x[lab == L]
+            out[s, 0] = len(v)
+            sq = (v * v).astype(np.float64)
+            v = v.astype(np.float64)
+            for j in range(d):
+                for base, col in ((1, v[:, j]), (1 + 2 * d, sq[:, j])):
+                    hi = math.fsum(col)
+                    lo = math.fsum(list(col) + [-hi])
+                    out[s, base + 2 * j] = hi
+                    out[s, base + 2 * j + 1] = lo
+        return out
+
+    def counts(self, X, labels, sel, axes, bounds):
+        x = X.numpy().astype(np.float64)
+        lab = labels.numpy()
+        out = np.zeros((len(sel), 8), np.int64)
+        for s, L in enumerate(sel):
+            v = x[lab == L, axes[s]]
+            out[s, :7] = [(v < b).sum() for b in bounds[s]]
+            out[s, 7] = len(v)
+        return out
+
+    def split(self, X, labels, sel, axes, boundary, new):
+        x = X.numpy().astype(np.float64)
+        lab = labels.numpy()
+        for s, L in enumerate(sel):
+            m = (lab == L) & (x[:, axes[s]] >= boundary[s])
+            lab[m] = new[s]
+
+    def route(self, X, ebox, part_rank, world):
+        x = X.numpy().astype(np.float64)
+        mask = np.zeros(len(x), np.int64)
+        for L in range(len(ebox)):
+            m = np.all(ebox[L, 0] <= x, axis=1) & np.all(ebox[L, 1] >= x, axis=1)
+            mask[m] |= np.int64(1) << int(part_rank[L])
+        counts = np.array([((mask >> r) & 1).sum() for r in range(world)], np.int64)
+        return torch.from_numpy(mask), counts
+
+    def pack(self, X, mask, dest, kdlab, part_rank, local_index, gid_base, out):
+        coords, gid, owner, xr = out
+        mk = mask.numpy()
+        idx = np.nonzero((mk >> dest) & 1)[0]
+        lab = kdlab.numpy()[idx]
+        coords.copy_(X[torch.from_numpy(idx)])
+        gid.copy_(torch.from_numpy((gid_base + idx).astype(np.int32)))
+        own = np.where(part_rank[lab] == dest, local_index[lab], -1).astype(np.int32)
+        owner.copy_(torch.from_numpy(own))
+        many = np.array([bin(int(v) & ((1 << 64) - 1)).count("1") > 1 for v in mk[idx]], bool)
+        xr.copy_(torch.from_numpy(many.astype(np.uint8)))
+        return len(idx)
+
+    def train_begin(self, X, eps, min_samples, metric, ebox, owner, gid, xr, data_box):
+        m = "euclidean" if metric == 0 else "cityblock"
+        self.state, self.exp = osh.phase_a(X.numpy(), eps, min_samples, ebox, owner.numpy(),
+                                           gid.numpy(), xr.numpy(), m)
+        return len(self.exp[0])
+
+    def exports(self, m):
+        g, k = self.exp
+        return (torch.from_numpy(g.astype(np.int32)), torch.from_numpy(k.astype(np.int32)))
+
+    def merge(self, n_space, gid, key):
+        return torch.from_numpy(osh.merge(n_space, gid.numpy(), key.numpy()).astype(np.int32))
+
+    def train_end(self, n, keymap):
+        keys, core = osh.phase_b(self.state, None if keymap is None else keymap.numpy())
+        return torch.from_numpy(keys.astype(np.int32)), torch.from_numpy(core)
+
+    def select_roots(self, keys, gid):
+        k = keys.numpy()
+        return torch.from_numpy(gid.numpy()[(k >= 0) & (k == gid.numpy())].copy())
+
+    def sort(self, data):
+        data.copy_(torch.sort(data).values)
+        return data
+
+    def rank_labels(self, keys, roots):
+        k = keys.numpy().astype(np.int64)
+        r = roots.numpy().astype(np.int64)
+        lab = np.where(k >= 0, np.searchsorted(r, k), -1)
+        return torch.from_numpy(lab.astype(np.int32))

@@ -1,0 +1,66 @@
+"""Sharded train (pypardis_amd/distributed.py) over gloo, world size 2 and 3,
+on CPU: the orchestration and every collective are the product code; the
+per-rank device stages are the oracle stand-in (tests/sharded_ops.py).  The
+assembled labels must equal sklearn's on the golden data sets, and the KD
+trace must equal the single-process exact-sum partition."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import load_golden
+from dist_worker import run_world
+from pypardis_amd.distributed import dd_combine, partition_ranks
+
+CASES = [("c0", 2, 2), ("c0", 3, 4), ("b2d_20k", 2, 8), ("b3d_20k", 2, 4), ("ident_40", 2, 4),
+         ("c0_p5_cityblock", 2, 5), ("dup_1d", 3, 3), ("lattice_900", 2, 8)]
+
+
+@pytest.mark.parametrize("name,world,P", CASES)
+def test_sharded_labels_equal_sklearn(tmp_path, name, world, P):
+    g = load_golden(name)
+    metric = str(g["metric"]) if "metric" in g else "euclidean"
+    X = g["X"]
+    if X.ndim == 1:
+        X = X[:, None]
+    mcode = 1 if metric in ("cityblock", "manhattan") else 0
+    out = run_world(world, X, float(g["eps"]), int(g["min_samples"]), mcode, P, str(tmp_path))
+    assert (out["seen"] == 1).all(), "every point owned by exactly one rank"
+    np.testing.assert_array_equal(out["labels"], g["sk_labels"])
+    np.testing.assert_array_equal(out["core"], g["sk_core"].astype(np.uint8))
+    assert out["ncl"] == {int(g["sk_labels"].max()) + 1}
+    assert out["received"] >= len(X)   # halo copies travel to both sides
+    if name in ("b2d_20k", "b3d_20k", "lattice_900"):
+        assert out["exports"] > 0      # the cross-rank merge is exercised
+    kd = oracle.kd_partition(X, P, sums="exact")
+    for sp in out["splits"]:
+        np.testing.assert_array_equal(sp, np.array(kd["splits"], np.float64))
+
+
+def test_dd_combine_matches_exact_sum():
+    rng = np.random.default_rng(3)
+    v = rng.normal(size=(3, 1000)) * 10.0 ** rng.integers(-8, 8, size=(3, 1000))
+    import math
+    parts = []
+    for chunk in np.array_split(np.arange(1000), 4):
+        p = np.zeros((1, 5))
+        p[0, 0] = len(chunk)
+        hi = math.fsum(v[0, chunk])
+        p[0, 1], p[0, 2] = hi, math.fsum(list(v[0, chunk]) + [-hi])
+        hi = math.fsum(v[1, chunk])
+        p[0, 3], p[0, 4] = hi, math.fsum(list(v[1, chunk]) + [-hi])
+        parts.append(p)
+    mom = dd_combine(np.stack(parts))
+    assert mom[0, 0, 0] == 1000
+    assert mom[0, 1, 0] == math.fsum(v[0])
+    assert mom[0, 2, 0] == math.fsum(v[1])
+
+
+def test_partition_ranks():
+    pr, li = partition_ranks(8, 8)
+    assert pr.tolist() == list(range(8)) and li.tolist() == [0] * 8
+    pr, li = partition_ranks(5, 2)
+    assert pr.tolist() == [0, 0, 0, 1, 1] and li.tolist() == [0, 1, 2, 0, 1]
+    pr, li = partition_ranks(2, 4)
+    assert pr.tolist() == [0, 2] and li.tolist() == [0, 0]

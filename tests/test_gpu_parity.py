@@ -1,8 +1,8 @@
 """GPU parity: the HIP path (through the C ABI) against the pinned oracle and
 the reference goldens.  Bit-exact for everything integer-valued (labels, core
-flags, neighbour counts, halo membership, split sizes); split boundaries
-within 1e-12 relative (their fp64 sums run in a different order than the
-reference's sequential fold)."""
+flags, neighbour counts, halo membership, split sizes, split boundaries —
+the latter in 'sequential' sums mode against the reference, in the default
+correctly-rounded mode against the oracle's exact sums)."""
 import numpy as np
 import pytest
 import torch
@@ -298,3 +298,104 @@ def test_fp32_screen_is_exact(native):
                 ctx.set_option(native.PD_OPT_FP32_SCREEN, 1)
         (l1, c1, n1, k1), (l0, c0, n0, k0) = out
         assert np.array_equal(k1, k0) and np.array_equal(l1, l0) and n1 == n0
+
+
+# ------------------------------------------------------------ sharded train
+def test_sharded_stage_primitives(native):
+    """pd_kd_moments_dd / pd_route / pd_pack / pd_merge_exports /
+    pd_select_roots / pd_sort_u32 / pd_rank_labels against numpy and the
+    oracle restatement (oracle/sharded.py)."""
+    from oracle import sharded as osh
+    from pypardis_amd import synth
+    from pypardis_amd.distributed import dd_combine, partition_ranks
+    rng = np.random.default_rng(5)
+    X = synth.blobs_noise(50_000, 3, side=5.0, n_centers=4, sigma=0.5, seed=51)
+    Xd = _dev(X)
+    lab = torch.from_numpy(rng.integers(0, 5, len(X)).astype(np.int32)).cuda()
+    dd = native.kd_moments_dd(Xd, lab, [0, 2, 4])
+    mom = native.kd_moments(Xd, lab, [0, 2, 4])
+    np.testing.assert_array_equal(dd_combine(dd[None]), mom)
+    # route: 5 boxes over 3 ranks
+    lo, hi = X.min(0).astype(np.float64), X.max(0).astype(np.float64)
+    cuts = np.linspace(lo[0], hi[0], 6)
+    ebox = np.stack([np.stack([np.r_[cuts[i] - 0.1, lo[1:]], np.r_[cuts[i + 1] + 0.1, hi[1:]]])
+                     for i in range(5)])
+    pr, li = partition_ranks(5, 3)
+    mask, counts = native.route(Xd, ebox, pr, 3)
+    x64 = X.astype(np.float64)
+    want = np.zeros(len(X), np.int64)
+    for L in range(5):
+        m = np.all(ebox[L, 0] <= x64, 1) & np.all(ebox[L, 1] >= x64, 1)
+        want[m] |= 1 << int(pr[L])
+    np.testing.assert_array_equal(mask.cpu().numpy(), want)
+    assert counts.tolist() == [int(((want >> r) & 1).sum()) for r in range(3)]
+    kdlab = torch.from_numpy(rng.integers(0, 5, len(X)).astype(np.int32)).cuda()
+    for dest in range(3):
+        c = int(counts[dest])
+        out = (torch.empty((c, 3), dtype=Xd.dtype, device="cuda"),
+               torch.empty(c, dtype=torch.int32, device="cuda"),
+               torch.empty(c, dtype=torch.int32, device="cuda"),
+               torch.empty(c, dtype=torch.uint8, device="cuda"))
+        m = native.pack(Xd, mask, dest, kdlab, pr, li, 1000, out)
+        assert m == c
+        idx = np.nonzero((want >> dest) & 1)[0]
+        kl = kdlab.cpu().numpy()[idx]
+        np.testing.assert_array_equal(out[0].cpu().numpy(), X[idx])
+        np.testing.assert_array_equal(out[1].cpu().numpy(), idx + 1000)
+        np.testing.assert_array_equal(out[2].cpu().numpy(), np.where(pr[kl] == dest, li[kl], -1))
+        many = np.array([bin(v).count("1") > 1 for v in want[idx]])
+        np.testing.assert_array_equal(out[3].cpu().numpy().astype(bool), many)
+    # merge: random pairs over an id space
+    n_space = 20_000
+    ga = rng.integers(0, n_space, 5000)
+    gb = rng.integers(0, n_space, 5000)
+    km = native.merge_exports(n_space, torch.from_numpy(ga.astype(np.int32)).cuda(),
+                              torch.from_numpy(gb.astype(np.int32)).cuda())
+    np.testing.assert_array_equal(km.cpu().numpy(), osh.merge(n_space, ga, gb))
+    # roots / sort / ranks
+    gid = np.sort(rng.choice(1 << 30, 30_000, replace=False)).astype(np.int64)
+    keys = np.where(rng.random(len(gid)) < 0.3, -1, gid[rng.integers(0, len(gid), len(gid))])
+    keys[::7] = gid[::7]
+    kd_, gd_ = (torch.from_numpy(keys.astype(np.int32)).cuda(),
+                torch.from_numpy(gid.astype(np.int32)).cuda())
+    roots = native.select_roots(kd_, gd_).cpu().numpy().astype(np.int64)
+    np.testing.assert_array_equal(roots, gid[(keys >= 0) & (keys == gid)])
+    shuf = torch.from_numpy(rng.permutation(roots).astype(np.int32)).cuda()
+    native.sort_u32(shuf)
+    np.testing.assert_array_equal(shuf.cpu().numpy(), np.sort(roots))
+    labs = native.rank_labels(kd_, shuf).cpu().numpy()
+    ok = (keys >= 0) & np.isin(keys, roots)
+    np.testing.assert_array_equal(labs[ok], np.searchsorted(roots, keys[ok]))
+    assert (labs[keys < 0] == -1).all() and (labs[(keys >= 0) & ~ok] == -2).all()
+
+
+SHARDED = [("b3d_20k", 2, 8), ("c0", 3, 4), ("c0_p5_cityblock", 2, 5), ("dup_1d", 2, 3)]
+
+
+@pytest.mark.parametrize("name,world,P", SHARDED)
+def test_sharded_native_equals_sklearn(native, tmp_path, name, world, P):
+    """Two/three gloo ranks sharing cuda:0, every device stage native."""
+    from dist_worker import run_world
+    g = load_golden(name)
+    X = g["X"] if g["X"].ndim == 2 else g["X"][:, None]
+    mcode = native.metric_code(_metric(g))
+    out = run_world(world, X, float(g["eps"]), int(g["min_samples"]), mcode, P, str(tmp_path),
+                    native=True)
+    assert (out["seen"] == 1).all()
+    np.testing.assert_array_equal(out["labels"], g["sk_labels"])
+    np.testing.assert_array_equal(out["core"], g["sk_core"].astype(np.uint8))
+
+
+def test_sharded_native_large(native, tmp_path):
+    """400k 3-D C2-density points, 2 ranks x 4 neighbourhoods each: labels
+    equal the single-device pd_cluster answer."""
+    from dist_worker import run_world
+    from pypardis_amd import synth
+    X, cfg = synth.make_config("C2", n=400_000)
+    lab1, core1, _, nc1 = native.cluster(_dev(X), cfg["eps"], cfg["min_samples"])
+    out = run_world(2, X, cfg["eps"], cfg["min_samples"], 0, 8, str(tmp_path), native=True)
+    assert (out["seen"] == 1).all()
+    assert out["ncl"] == {nc1}
+    assert out["exports"] > 0
+    np.testing.assert_array_equal(out["labels"], lab1.cpu().numpy().astype(np.int64))
+    np.testing.assert_array_equal(out["core"], core1.cpu().numpy())

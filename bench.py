@@ -8,7 +8,7 @@
            partition (3 BFS levels of GPU passes), 2·eps halo, per-neighbourhood
            DBSCAN, merge, global labels (labels stay in HBM).
 
-  python bench.py [--gpus N --steps K --warmup W] [--n POINTS] [--no-cpu]
+  python bench.py [--gpus N --steps K --warmup W] [--points N] [--no-cpu]
 
 For N > 1 (torch.distributed.run, one rank per GPU, RCCL) the same 100M
 points are split by index over the ranks and the step is the sharded train
@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C2")
-    ap.add_argument("--n", type=int, default=None, help="override point count")
+    ap.add_argument("--points", type=int, default=None, help="override point count")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-n", type=int, default=1_000_000, help="CPU baseline sample size")
     ap.add_argument("--json-out", default=None)
@@ -114,7 +114,7 @@ def main():
 
     from pypardis_amd import DBSCAN, _native, synth
 
-    X, cfg = synth.make_config(args.config, n=args.n)
+    X, cfg = synth.make_config(args.config, n=args.points)
     n, d = X.shape
     eps, ms, P = cfg["eps"], cfg["min_samples"], cfg.get("max_partitions") or 1
     ctx = _native.context(local_rank)
@@ -160,6 +160,14 @@ def main():
         tt = torch.tensor([el], dtype=torch.float64, device="cpu" if args.rehearse else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
+    sweep = None
+    if world == 1:   # one extra, untimed step with the instrumented sweeps
+        ctx.set_option(_native.PD_OPT_SWEEP_STATS, 1)
+        step()
+        torch.cuda.synchronize()
+        ctx.set_option(_native.PD_OPT_SWEEP_STATS, 0)
+        sweep = {k: int(v) for k, v in ctx.timings().items()
+                 if k.startswith("s_") or k in ("records", "core_records")}
     ms_step = 1e3 * el / args.steps
     value = n * args.steps / el
     ncl = m.n_clusters if world > 1 else m.n_clusters_
@@ -171,7 +179,8 @@ def main():
         pmc = load_pmc()
         traffic = pmc["bytes_per_launch"] if pmc else None
         stages = {k: round(v / args.steps, 3) for k, v in stage_sum.items()
-                  if k not in ("records", "cells_n", "grid_cells", "key_bits")}
+                  if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records")
+                  and not k.startswith("s_")}
         cpu = None
         if world == 1 and not args.no_cpu:
             try:
@@ -205,6 +214,7 @@ def main():
             "stages_ms": stages,
             "n_clusters": ncl,
             "shard_stats": m.stats if world > 1 else None,
+            "sweep_stats": sweep,
         }
         line = json.dumps(out)
         print(line, flush=True)

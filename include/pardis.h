@@ -61,16 +61,21 @@ enum pd_option {
     PD_OPT_XSUB = 6,        /* sub-cells per eps along axis 0 (default 2): finer rows follow
                                the eps-ball's chord more tightly, at 1/xsub the directory
                                density */
-    PD_OPT_FP32_SCREEN = 7  /* fp32 inputs: decide pairs outside a 2^-18 band around eps with
+    PD_OPT_FP32_SCREEN = 7, /* fp32 inputs: decide pairs outside a 2^-18 band around eps with
                                fp32 arithmetic, the rest with the exact fp64 predicate
                                (default 1; results are identical with 0) */
+    PD_OPT_SWEEP_STATS = 8  /* tally the neighbour sweeps' candidates and union-find outcomes
+                               into the PD_T_S_* slots (instrumented kernels; default 0) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */
 enum pd_timing_slot {
     PD_T_HALO = 0, PD_T_SORT, PD_T_GATHER, PD_T_CELLS, PD_T_COUNT, PD_T_LINK, PD_T_MERGE,
     PD_T_ROOTS, PD_T_BORDER, PD_T_LABEL, PD_T_TOTAL, PD_T_RECORDS, PD_T_CELLS_N, PD_T_GRID_CELLS,
-    PD_T_KEY_BITS, PD_T_NSLOTS
+    PD_T_KEY_BITS, PD_T_CORE_RECORDS,
+    /* PD_OPT_SWEEP_STATS counters */
+    PD_T_S_COUNT_CAND, PD_T_S_LINK_CAND, PD_T_S_LINK_HIT, PD_T_S_LINK_CORE, PD_T_S_LINK_SAME,
+    PD_T_S_LINK_FIND_SAME, PD_T_S_LINK_UNIONS, PD_T_NSLOTS
 };
 
 typedef struct pd_ctx pd_ctx;

@@ -21,8 +21,11 @@ PD_F32, PD_F64 = 0, 1
 PD_EUCLIDEAN, PD_CITYBLOCK = 0, 1
 PD_OPT_TIMING, PD_OPT_FULL_COUNTS, PD_OPT_SEQUENTIAL_MOMENTS = 1, 2, 3
 PD_OPT_LINK_MODE, PD_OPT_JUMP_ROUNDS, PD_OPT_XSUB, PD_OPT_FP32_SCREEN = 4, 5, 6, 7
+PD_OPT_SWEEP_STATS = 8
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
-                "label", "total", "records", "cells_n", "grid_cells", "key_bits"]
+                "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
+                "s_count_cand", "s_link_cand", "s_link_hit", "s_link_core", "s_link_same",
+                "s_link_find_same", "s_link_unions"]
 
 # every symbol include/pardis.h declares (tests/test_abi.py checks the .so)
 EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",

@@ -116,6 +116,8 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.jump_rounds = (int)value;
         else if (option == PD_OPT_FP32_SCREEN)
             ctx->c.screen = value != 0;
+        else if (option == PD_OPT_SWEEP_STATS)
+            ctx->c.sweep_stats = value != 0;
         else if (option == PD_OPT_XSUB) {
             if (value < 1 || value > 16) throw Error(PD_EINVAL, "xsub must be in [1, 16]");
             ctx->c.xsub = (int)value;
@@ -133,7 +135,11 @@ int32_t pd_ctx_timings(pd_ctx* ctx, double* out, int32_t n) {
                                        t.count,   t.link,   t.merge,  t.roots,  t.border,
                                        t.label,   t.total,  (double)t.records,
                                        (double)t.cells_n, (double)t.grid_cells,
-                                       (double)t.key_bits};
+                                       (double)t.key_bits, (double)t.core_records,
+                                       (double)t.sweep[0], (double)t.sweep[1],
+                                       (double)t.sweep[2], (double)t.sweep[3],
+                                       (double)t.sweep[4], (double)t.sweep[5],
+                                       (double)t.sweep[6]};
         for (int i = 0; i < n && i < PD_T_NSLOTS; ++i) out[i] = v[i];
     });
 }

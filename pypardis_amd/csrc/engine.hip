@@ -598,13 +598,14 @@ __global__ __launch_bounds__(kBlock) void cell_start_kernel(const uint32_t* __re
 // the smallest neighbour index it saw: for a core record whose smallest seen
 // neighbour is core and below it, that is a free initial parent for the
 // union-find (ECL-CC's init step without a sweep of its own).
-template <typename T, int D, int M>
+template <typename T, int D, int M, bool ST>
 __global__ __launch_bounds__(kBlock) void count_kernel(const T* __restrict__ Xs, uint32_t R,
                                                        Cells C, double eps, double eps2,
                                                        float lo, float hi, uint32_t ms, int full,
                                                        uint8_t* __restrict__ core,
                                                        uint32_t* __restrict__ mn_out,
-                                                       uint32_t* __restrict__ cnt_out) {
+                                                       uint32_t* __restrict__ cnt_out,
+                                                       unsigned long long* __restrict__ stats) {
     constexpr int NR = NRows<D>::v;
     const uint32_t r = rec_index();
     if (r >= R) return;
@@ -615,6 +616,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const T* __restrict__ Xs,
     row_ranges<D, M>(C, a, L, eps, s, e);
     const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
     uint32_t cnt = 0, mn = r;
+    uint32_t n_cand = 0;
     const uint32_t stop = full ? 0xFFFFFFFFu : ms;
 #pragma unroll
     for (int qq = 0; qq < NR; ++qq) {
@@ -629,6 +631,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const T* __restrict__ Xs,
             load_raw<T, D>(Xs, j + 3, b3);
             const bool w0 = pr(b0), w1 = pr(b1),
                        w2 = pr(b2), w3 = pr(b3);
+            if constexpr (ST) n_cand += 4;
             cnt += (uint32_t)w0 + (uint32_t)w1 + (uint32_t)w2 + (uint32_t)w3;
             const uint32_t h = w0 ? j : (w1 ? j + 1 : (w2 ? j + 2 : (w3 ? j + 3 : mn)));
             mn = h < mn ? h : mn;
@@ -637,6 +640,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(const T* __restrict__ Xs,
         for (; j < end; ++j) {
             T b0[D];
             load_raw<T, D>(Xs, j, b0);
+            if constexpr (ST) ++n_cand;
             if (pr(b0)) {
                 ++cnt;
                 mn = j < mn ? j : mn;
@@ -650,6 +654,7 @@ done:
     core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
     mn_out[r] = mn;
     if (cnt_out) cnt_out[r] = cnt;
+    if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
 }
 
 // Initial forest.  parent doubles as the core flag: kNone marks a non-core
@@ -674,25 +679,41 @@ __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t R, const uint8_t*
 // The caller's root is cached: an edge to a record already under it costs
 // one L1 load, no find and no CAS.  The distance test comes first (its
 // operands are already loaded); the core flag is read only for neighbours.
+// Sweep statistics (PD_OPT_SWEEP_STATS): per-lane tallies, one atomic each
+// at the end.  ST = false compiles them away.
+struct LinkStats {
+    uint32_t cand = 0, hit = 0, core = 0, same = 0, find_same = 0, unions = 0;
+};
+
+template <bool ST>
 struct Linker {
     uint32_t* par;
     uint32_t rr;
+    LinkStats st;
     __device__ __forceinline__ void edge(uint32_t j) { edge(j, ld_l1(par + j)); }
     // pj: parent[j] read ahead of the distance test (stale is fine: an older
     // ancestor still proves membership, and a mismatch falls through to find)
     __device__ __forceinline__ void edge(uint32_t j, uint32_t pj) {
+        if constexpr (ST) {
+            ++st.hit;
+            st.core += pj != kNone;
+            st.same += pj == rr;
+        }
         if (pj == kNone || pj == rr) return;   // non-core, or already under our root
         const uint32_t rj = uf_find_l1(par, pj);
+        if constexpr (ST) st.find_same += rj == rr;
         if (rj == rr) return;
+        if constexpr (ST) ++st.unions;
         rr = uf_link_roots(par, rr, rj);
     }
 };
 
-template <typename T, int D, int M>
+template <typename T, int D, int M, bool ST>
 __global__ __launch_bounds__(kBlock) void link_kernel(const T* __restrict__ Xs, uint32_t NL,
                                                       const uint32_t* __restrict__ list, Cells C,
                                                       double eps, double eps2, float lo, float hi,
-                                                      uint32_t* __restrict__ par) {
+                                                      uint32_t* __restrict__ par,
+                                                      unsigned long long* __restrict__ stats) {
     constexpr int NR = NRows<D>::v;
     const uint32_t i = rec_index();
     if (i >= NL) return;
@@ -703,7 +724,7 @@ __global__ __launch_bounds__(kBlock) void link_kernel(const T* __restrict__ Xs, 
     uint32_t s[NR], e[NR];
     row_ranges<D, M>(C, a, L, eps, s, e);
     const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
-    Linker lk{par, uf_find_l1(par, r)};
+    Linker<ST> lk{par, uf_find_l1(par, r), {}};
 #pragma unroll
     for (int q = 0; q < NR; ++q) {
         uint32_t j = s[q] > r + 1 ? s[q] : r + 1;
@@ -717,6 +738,7 @@ __global__ __launch_bounds__(kBlock) void link_kernel(const T* __restrict__ Xs, 
             load_raw<T, D>(Xs, j + 3, b3);
             const uint32_t p0 = ld_l1(par + j), p1 = ld_l1(par + j + 1), p2 = ld_l1(par + j + 2),
                            p3 = ld_l1(par + j + 3);
+            if constexpr (ST) lk.st.cand += 4;
             if (pr(b0)) lk.edge(j, p0);
             if (pr(b1)) lk.edge(j + 1, p1);
             if (pr(b2)) lk.edge(j + 2, p2);
@@ -726,8 +748,17 @@ __global__ __launch_bounds__(kBlock) void link_kernel(const T* __restrict__ Xs, 
             T b0[D];
             load_raw<T, D>(Xs, j, b0);
             const uint32_t p0 = ld_l1(par + j);
+            if constexpr (ST) ++lk.st.cand;
             if (pr(b0)) lk.edge(j, p0);
         }
+    }
+    if constexpr (ST) {
+        atomicAdd(stats + 1, (unsigned long long)lk.st.cand);
+        atomicAdd(stats + 2, (unsigned long long)lk.st.hit);
+        atomicAdd(stats + 3, (unsigned long long)lk.st.core);
+        atomicAdd(stats + 4, (unsigned long long)lk.st.same);
+        atomicAdd(stats + 5, (unsigned long long)lk.st.find_same);
+        atomicAdd(stats + 6, (unsigned long long)lk.st.unions);
     }
 }
 
@@ -1100,11 +1131,21 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     uint8_t* core = ctx.arena.get<uint8_t>("core", R);
     uint32_t* mn = ctx.arena.get<uint32_t>("minnbr", R);
     uint32_t* cnt_rec = a.counts ? ctx.arena.get<uint32_t>("cnt_rec", R) : nullptr;
-    if (R)
-        hipLaunchKernelGGL((count_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R, C,
-                           eps, eps2, slo, shi, (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
-                           core, mn,
-                           cnt_rec);
+    unsigned long long* sst = nullptr;
+    if (ctx.sweep_stats) {
+        sst = ctx.arena.get<unsigned long long>("sweep_stats", 8);
+        PD_HIP(hipMemsetAsync(sst, 0, sizeof(unsigned long long) * 8, s));
+    }
+    if (R) {
+        if (sst)
+            hipLaunchKernelGGL((count_kernel<T, D, M, true>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                               Xs, R, C, eps, eps2, slo, shi, (uint32_t)a.min_samples,
+                               ctx.full_counts ? 1 : 0, core, mn, cnt_rec, sst);
+        else
+            hipLaunchKernelGGL((count_kernel<T, D, M, false>), dim3(blocks(R)), dim3(kBlock), 0,
+                               s, Xs, R, C, eps, eps2, slo, shi, (uint32_t)a.min_samples,
+                               ctx.full_counts ? 1 : 0, core, mn, cnt_rec, sst);
+    }
     PD_HIP(hipGetLastError());
     tm.mark();   // 5
 
@@ -1121,9 +1162,12 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
             uint32_t* clist = nullptr;
             const uint32_t NC = select_records(ctx, "core_list", R, IsCore{core}, &clist, s);
             ctx.t.core_records = NC;
-            if (NC)
-                hipLaunchKernelGGL((link_kernel<T, D, M>), dim3(blocks(NC)), dim3(kBlock), 0, s,
-                                   Xs, NC, clist, C, eps, eps2, slo, shi, par);
+            if (NC && sst)
+                hipLaunchKernelGGL((link_kernel<T, D, M, true>), dim3(blocks(NC)), dim3(kBlock), 0,
+                                   s, Xs, NC, clist, C, eps, eps2, slo, shi, par, sst);
+            else if (NC)
+                hipLaunchKernelGGL((link_kernel<T, D, M, false>), dim3(blocks(NC)), dim3(kBlock),
+                                   0, s, Xs, NC, clist, C, eps, eps2, slo, shi, par, sst);
         }
     }
     PD_HIP(hipGetLastError());
@@ -1264,6 +1308,13 @@ void finish(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
                                   hipMemcpyDeviceToHost, s));
         sync(s);
         ctx.t.cells_n = *hnc;
+        if (ctx.sweep_stats && ctx.st.R) {
+            unsigned long long* hs = (unsigned long long*)pinned(ctx, 8 * sizeof(unsigned long long));
+            PD_HIP(hipMemcpyAsync(hs, ctx.arena.get<unsigned long long>("sweep_stats", 8),
+                                  8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+            sync(s);
+            for (int k = 0; k < 7; ++k) ctx.t.sweep[k] = (int64_t)hs[k];
+        }
         ctx.t.grid_cells = (int64_t)ctx.st.G;
         ctx.t.key_bits = ctx.st.key_bits;
     } else {

@@ -46,6 +46,9 @@ struct Timings {
     float halo = 0, sort = 0, gather = 0, cells = 0, count = 0, link = 0, merge = 0,
           roots = 0, border = 0, label = 0, total = 0;
     int64_t records = 0, cells_n = 0, grid_cells = 0, core_records = 0, key_bits = 0;
+    // PD_OPT_SWEEP_STATS: count candidates; link candidates, predicate hits,
+    // core hits, hits already under the root, finds that met the root, unions
+    int64_t sweep[7] = {0, 0, 0, 0, 0, 0, 0};
 };
 
 // Device state carried from phase A (local clustering) to phase B (border
@@ -85,6 +88,7 @@ struct Ctx {
     int jump_rounds = 4;
     int xsub = 2;                // axis-0 sub-cells per eps
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
+    bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
     Timings t;
     PhaseState st;
     hipEvent_t ev[16] = {};

@@ -15,6 +15,8 @@
  *   pd_kd_moments    R:dbscan/partition.py:86-89    min_var_split moments aggregate
  *   pd_kd_counts     R:dbscan/partition.py:60-63    mean_var_split 7-bound counts aggregate
  *   pd_kd_split      R:dbscan/partition.py:66-68    filter(v[axis] >= boundary) relabel
+ *                    (also :27-29, the median_search_split filters)
+ *   pd_kd_radix_hist R:dbscan/partition.py:23-26    sortBy(v[axis]).collect()[len/2] (rotation)
  *   pd_halo_members  R:dbscan/dbscan.py:136-151     _create_neighborhoods filter(contains)
  *   pd_cluster       R:dbscan/dbscan.py:28-30       skc.DBSCAN(**params).fit_predict(x),
  *                                                   core_sample_indices_  (SK:cluster/_dbscan.py:369-446)
@@ -113,6 +115,17 @@ int32_t pd_kd_split(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_
                     int32_t* labels, int32_t n_sel, const int32_t* sel_host,
                     const int32_t* axis_host, const double* boundary_host,
                     const int32_t* new_host, void* stream);
+
+/* One pass of the radix select behind split_method='rotation'
+ * (median_search_split, R:dbscan/partition.py:8-30: the value at index len/2
+ * of sortBy(v[axis])).  key(v) = order-preserving u64 of (double)v[axis_host[s]]
+ * (-0.0 taken as +0.0).  hist_host[s][b] = #points of label sel_host[s] with
+ * key >> (shift + 8) == prefix_host[s] (no condition when shift == 56) and
+ * (key >> shift) & 255 == b.  shift in {56, 48, .., 0}. */
+int32_t pd_kd_radix_hist(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                         const int32_t* labels, int32_t n_sel, const int32_t* sel_host,
+                         const int32_t* axis_host, const uint64_t* prefix_host, int32_t shift,
+                         int64_t* hist_host, void* stream);
 
 /* ebox_host: P x [lo[d], hi[d]] (inclusive).  counts_host[P] = members per
  * box; if members != NULL it receives the ascending point ids of box 0, then

@@ -32,7 +32,8 @@ EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
            "pd_ctx_set_option", "pd_ctx_timings", "pd_bbox", "pd_kd_moments", "pd_kd_counts",
            "pd_kd_split", "pd_halo_members", "pd_cluster", "pd_train", "pd_kd_moments_dd",
            "pd_route", "pd_pack", "pd_train_begin", "pd_train_exports", "pd_merge_exports",
-           "pd_train_end", "pd_select_roots", "pd_sort_u32", "pd_rank_labels"]
+           "pd_train_end", "pd_select_roots", "pd_sort_u32", "pd_rank_labels",
+           "pd_kd_radix_hist"]
 
 
 class PardisError(RuntimeError):
@@ -86,6 +87,7 @@ def load():
             "pd_select_roots": ([P, P, P, I64, P, P, P], I32),
             "pd_sort_u32": ([P, P, I64, P], I32),
             "pd_rank_labels": ([P, P, I64, P, I64, P, P], I32),
+            "pd_kd_radix_hist": ([P, P, I32, I64, I32, P, I32, P, P, P, I32, P, P], I32),
         }
         for name, (args, res) in sig.items():
             f = getattr(lib, name)
@@ -229,6 +231,22 @@ def kd_split(X, labels, sel, axis, boundary, new, ctx=None):
     _check(load().pd_kd_split(ctx.ptr, X.data_ptr(), dt, X.shape[0], X.shape[1],
                               labels.data_ptr(), len(sel), sel.ctypes.data, axis.ctypes.data,
                               boundary.ctypes.data, new.ctypes.data, _stream(X.device)))
+
+
+def kd_radix_hist(X, labels, sel, axis, prefix, shift, ctx=None):
+    """One radix-select pass (pd_kd_radix_hist): (n_sel, 256) int64 digit
+    histogram of the order keys of v[axis] under each slot's prefix."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    sel = np.ascontiguousarray(sel, np.int32)
+    axis = np.ascontiguousarray(axis, np.int32)
+    prefix = np.ascontiguousarray(prefix, np.uint64)
+    out = np.zeros((len(sel), 256), np.int64)
+    _check(load().pd_kd_radix_hist(ctx.ptr, X.data_ptr(), dt, X.shape[0], X.shape[1],
+                                   labels.data_ptr(), len(sel), sel.ctypes.data,
+                                   axis.ctypes.data, prefix.ctypes.data, int(shift),
+                                   out.ctypes.data, _stream(X.device)))
+    return out
 
 
 def halo_members(X, ebox, ctx=None):

@@ -202,6 +202,26 @@ int32_t pd_kd_split(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_
     });
 }
 
+int32_t pd_kd_radix_hist(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                         const int32_t* labels, int32_t n_sel, const int32_t* sel,
+                         const int32_t* axis, const uint64_t* prefix, int32_t shift,
+                         int64_t* hist, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (n_sel < 0 || (n_sel && (!sel || !axis || !prefix || !hist)) || (n && !labels))
+            throw Error(PD_EINVAL, "bad selection");
+        if (shift < 0 || shift > 56 || shift % 8) throw Error(PD_EINVAL, "shift must be 0, 8, .., 56");
+        for (int s = 0; s < n_sel; ++s)
+            if (axis[s] < 0 || axis[s] >= d || sel[s] < 0) throw Error(PD_EINVAL, "bad axis/label");
+        if (n == 0) {
+            std::memset(hist, 0, sizeof(int64_t) * 256 * n_sel);
+            return;
+        }
+        kd_radix_hist(ctx->c, X, dtype, n, d, labels, n_sel, sel, axis, prefix, shift, hist,
+                      (hipStream_t)stream);
+    });
+}
+
 int32_t pd_halo_members(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
                         int32_t P, const double* ebox, int64_t* counts, int64_t* members,
                         int64_t capacity, void* stream) {

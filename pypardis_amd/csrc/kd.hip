@@ -284,6 +284,49 @@ __global__ __launch_bounds__(kBlock) void split_kernel(
     }
 }
 
+// ---------------------------------------------------------------- radix select
+// One pass of an MSD radix select over v[axis] of each selected label
+// (median_search_split, R:dbscan/partition.py:23-26: sortBy(v[axis]) then
+// sorted_values[len/2]).  Values are widened to fp64 and mapped to an
+// order-preserving u64 key (-0.0 folded onto +0.0: the reference's sort
+// compares them equal).  hist[slot][b] = #points whose key agrees with the
+// slot's prefix above bit (shift + 8) and whose digit at `shift` is b.
+__device__ __forceinline__ uint64_t order_key(double v) {
+    uint64_t b = (uint64_t)__double_as_longlong(v);
+    if (b == 0x8000000000000000ull) b = 0;   // -0.0 == +0.0
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void radix_hist_kernel(
+    const T* __restrict__ X, uint64_t n, const int32_t* __restrict__ labels,
+    const int32_t* __restrict__ slot_of, int n_label_tab, const int32_t* __restrict__ axis,
+    const uint64_t* __restrict__ prefix, int shift, int n_sel, int lds,
+    unsigned int* __restrict__ out) {
+    extern __shared__ unsigned int lh[];   // n_sel * 256 when lds
+    if (lds) {
+        for (int k = threadIdx.x; k < n_sel * 256; k += kBlock) lh[k] = 0;
+        __syncthreads();
+    }
+    unsigned int* h = lds ? lh : out;
+    const int top = shift + 8;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kBlock) {
+        const int lab = labels[i];
+        if (lab < 0 || lab >= n_label_tab) continue;
+        const int sl = slot_of[lab];
+        if (sl < 0) continue;
+        const uint64_t key = order_key((double)X[i * D + axis[sl]]);
+        if (top < 64 && (key >> top) != prefix[sl]) continue;
+        atomicAdd(&h[sl * 256 + (int)((key >> shift) & 255u)], 1u);
+    }
+    if (lds) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < n_sel * 256; k += kBlock)
+            if (lh[k]) atomicAdd(&out[k], lh[k]);
+    }
+}
+
 // ---------------------------------------------------------------- halo membership
 template <typename T, int D>
 struct InBox {
@@ -501,6 +544,32 @@ void kd_split(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
     });
     PD_HIP(hipGetLastError());
     sync(s);
+}
+
+void kd_radix_hist(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
+                   int n_sel, const int32_t* sel, const int32_t* axis, const uint64_t* prefix,
+                   int shift, int64_t* out, hipStream_t s) {
+    if (n_sel <= 0) return;
+    // the u64 prefixes travel in the tables' fp64 slots (bit copies)
+    LabelTables t = upload_tables(ctx, n_sel, sel, axis, reinterpret_cast<const double*>(prefix),
+                                  1, nullptr, s);
+    unsigned int* dh = ctx.arena.get<unsigned int>("kd_rhist", (size_t)n_sel * 256);
+    PD_HIP(hipMemsetAsync(dh, 0, sizeof(unsigned int) * n_sel * 256, s));
+    const int lds = n_sel <= 48 ? 1 : 0;   // <= 48 KiB of LDS histograms per block
+    const unsigned nb = grid_for(n, 2048);
+    dispatch(dtype, d, [&](auto tp, auto Dc) {
+        using T = std::remove_pointer_t<decltype(tp)>;
+        constexpr int D = decltype(Dc)::value;
+        hipLaunchKernelGGL((radix_hist_kernel<T, D>), dim3(nb), dim3(kBlock),
+                           lds ? sizeof(unsigned int) * n_sel * 256 : 0, s, (const T*)X,
+                           (uint64_t)n, labels, t.slot_of, t.ntab, t.axis,
+                           reinterpret_cast<const uint64_t*>(t.dbl), shift, n_sel, lds, dh);
+    });
+    PD_HIP(hipGetLastError());
+    unsigned int* h = (unsigned int*)pinned(ctx, sizeof(unsigned int) * n_sel * 256);
+    PD_HIP(hipMemcpyAsync(h, dh, sizeof(unsigned int) * n_sel * 256, hipMemcpyDeviceToHost, s));
+    sync(s);
+    for (int k = 0; k < n_sel * 256; ++k) out[k] = (int64_t)h[k];
 }
 
 void halo_members(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P,

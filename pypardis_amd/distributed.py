@@ -42,7 +42,8 @@ import torch.distributed as dist
 
 from . import _native
 from .geometry import BoundingBox
-from .partition import _split_schedule, apply_level, level_axes, level_boundaries
+from .partition import (_split_schedule, apply_level, apply_rotation_level, level_axes,
+                        level_boundaries, level_medians)
 
 
 class NativeOps(object):
@@ -69,6 +70,9 @@ class NativeOps(object):
 
     def counts(self, X, labels, sel, axes, bounds):
         return _native.kd_counts(X, labels, sel, axes, bounds, ctx=self.ctx)
+
+    def radix_hist(self, X, labels, sel, axes, prefix, shift):
+        return _native.kd_radix_hist(X, labels, sel, axes, prefix, shift, ctx=self.ctx)
 
     def split(self, X, labels, sel, axes, boundary, new):
         _native.kd_split(X, labels, sel, axes, boundary, new, ctx=self.ctx)
@@ -218,13 +222,16 @@ class ShardedResult(object):
 
 
 def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitions=None,
-                  group=None, ops=None):
+                  group=None, ops=None, split_method='min_var'):
     """Sharded DBSCAN train over the ranks of ``group`` (default: world).
 
     X: this rank's (n_i, d) slice (float32/float64, on this rank's GPU for
     NativeOps); the global id of row j is sum(n_0 .. n_{i-1}) + j.
     ``max_partitions`` defaults to the world size (one KD partition per GPU).
+    ``split_method``: 'min_var' (default) or 'rotation' (KDPartitioner's).
     """
+    if split_method not in ('min_var', 'rotation'):
+        split_method = 'min_var'   # the reference's fallback (R:dbscan/partition.py:129-130)
     ops = ops or NativeOps(X.device)
     comm = _Comm(group, getattr(ops, "device", X.device))
     W, rank = comm.world, comm.rank
@@ -268,9 +275,25 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     kdlab = ops.zeros(n, torch.int32)
     boxes = {0: box}
     splits = []
-    for level in _split_schedule(P):
+    fp32 = X.dtype == torch.float32
+    for depth, level in enumerate(_split_schedule(P)):
         sel = [c for c, _ in level]
         new = [nl for _, nl in level]
+        if split_method == 'rotation':
+            # median per split from all-reduced digit histograms: the same
+            # sorted_values[len/2] as one device (R:dbscan/partition.py:23-26)
+            axes = [depth % d] * len(sel)
+
+            def hist(prefix, shift):
+                h = ops.radix_hist(X, kdlab, sel, axes, prefix, shift) if n else \
+                    np.zeros((len(sel), 256), np.int64)
+                return comm.all_reduce(np.asarray(h, np.int64), dist.ReduceOp.SUM)
+
+            med, less, tot = level_medians(hist, len(sel), fp32)
+            if n:
+                ops.split(X, kdlab, sel, axes, med, new)
+            apply_rotation_level(boxes, splits, level, axes, med, less, tot)
+            continue
         part = ops.moments_dd(X, kdlab, sel) if n else np.zeros((len(sel), 1 + 4 * d))
         mom = dd_combine(comm.all_gather_np(part))
         axes, means, vars_, bounds = level_axes(mom)

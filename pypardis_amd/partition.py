@@ -10,6 +10,9 @@ the points run as HIP kernels through the C ABI:
     counts   Σ 2·[v < b_i] − 1        pd_kd_counts    (R:dbscan/partition.py:60-63)
     split    v >= boundary → relabel  pd_kd_split     (R:dbscan/partition.py:66-68)
     bbox     union of all points      pd_bbox         (R:dbscan/partition.py:135-137)
+    median   sorted v[axis][len/2]    pd_kd_radix_hist (R:dbscan/partition.py:23-26;
+             split_method='rotation': MSD radix select, one histogram pass
+             per 8-bit digit of the order key, all splits of a level at once)
 
 All splits of one BFS level run in the same passes (each split only reads its
 own label's points, so batching cannot change a result).  The sums are
@@ -133,11 +136,58 @@ def min_var_split(partition, k, next_label, sums='exact'):
     return mean_var_split(partition, k, axis, next_label, means[axis], variances[axis]), axis
 
 
+def _from_key(key):
+    """Inverse of the device's order key (kd.hip order_key) -> fp64 value."""
+    key = int(key)
+    bits = key & 0x7FFFFFFFFFFFFFFF if key >> 63 else (~key) & 0xFFFFFFFFFFFFFFFF
+    return np.array([bits], np.uint64).view(np.float64)[0]
+
+
+def level_medians(hist_fn, S, fp32):
+    """Radix select of sorted_values[len // 2] for the S splits of a level
+    (R:dbscan/partition.py:23-26).  hist_fn(prefix, shift) -> (S, 256) digit
+    histograms (pd_kd_radix_hist, or its all-reduced sum over devices).
+    Returns (median fp64 values, #points strictly below each median, #points).
+    fp32 inputs widen to doubles whose low 29 mantissa bits are zero, so their
+    select stops after the digit at bit 24.  An empty partition raises
+    IndexError, as the reference's list index does."""
+    less = np.zeros(S, np.int64)
+    prefix = np.zeros(S, np.uint64)
+    last = 24 if fp32 else 0
+    totals = target = None
+    for shift in range(56, last - 1, -8):
+        h = np.asarray(hist_fn(prefix, shift), np.int64).reshape(S, 256)
+        if totals is None:   # the top digit has no prefix condition: all points
+            totals = h.sum(axis=1)
+            if np.any(totals == 0):
+                raise IndexError("list index out of range (median of an empty partition, "
+                                 "R:dbscan/partition.py:25-26)")
+            target = totals // 2
+        cum = np.cumsum(h, axis=1)
+        b = np.argmax(cum > target[:, None], axis=1)
+        below = np.where(b > 0, cum[np.arange(S), b - 1], 0)
+        less += below
+        target -= below
+        prefix = (prefix << np.uint64(8)) | b.astype(np.uint64)
+    # the undecided low bits are zero in the value: zeros in the key of a
+    # positive value, ones in the (complemented) key of a negative one
+    low = (1 << last) - 1
+    keys = [(int(p) << last) | (low if not (int(p) << last) >> 63 else 0) for p in prefix]
+    return np.array([_from_key(k) for k in keys]), less, totals
+
+
 def median_search_split(partition, axis, next_part):
-    """R:dbscan/partition.py:8-30 (split_method='rotation').  Not built yet:
-    the reference itself cannot run it on Python 3 (float list index, :26);
-    SURVEY.md §8(f) item 2 ranks the GPU radix-select version after (a)-(e)."""
-    raise NotImplementedError("split_method='rotation' (median_search_split) is not built yet")
+    """R:dbscan/partition.py:8-30 (split_method='rotation'): split at the
+    value of index len/2 of the sorted v[axis] (radix select on the GPU,
+    pd_kd_radix_hist); part1 = v < median keeps the label, part2 = v >= median
+    becomes ``next_part``.  Returns (part1, part2, median)."""
+    X, labels = _labels_of(partition)
+    med, _, _ = level_medians(
+        lambda prefix, shift: _native.kd_radix_hist(X, labels, [partition.label], [axis],
+                                                    prefix, shift),
+        1, X.dtype == torch.float32)
+    _native.kd_split(X, labels, [partition.label], [axis], [med[0]], [next_part])
+    return (partition, PartitionView(partition.points, labels, next_part), float(med[0]))
 
 
 def level_axes(mom):
@@ -183,6 +233,17 @@ def apply_level(boxes, splits, level, axes, means, vars_, cnt, cand, boundary):
                        float(means[s]), float(vars_[s]), float(boundary[s])))
 
 
+def apply_rotation_level(boxes, splits, level, axes, medians, less, totals):
+    """Box splits of one 'rotation' level (R:dbscan/partition.py:168-176);
+    trace entries as apply_level's with cand = -1 and mean = var = NaN."""
+    for s, (cur, nl) in enumerate(level):
+        left, right = boxes[cur].split(axes[s], medians[s])
+        boxes[cur] = left
+        boxes[nl] = right
+        splits.append((cur, nl, axes[s], -1, int(less[s]), int(totals[s] - less[s]),
+                       float('nan'), float('nan'), float(medians[s])))
+
+
 class KDPartitioner(object):
     """R:dbscan/partition.py:98-183.
 
@@ -202,8 +263,6 @@ class KDPartitioner(object):
 
     def __init__(self, data, max_partitions=None, k=None, split_method='min_var', sums='exact'):
         self.split_method = split_method if split_method in ['min_var', 'rotation'] else 'min_var'
-        if self.split_method == 'rotation':
-            raise NotImplementedError("split_method='rotation' is not built yet")
         if sums not in ('exact', 'sequential'):
             raise ValueError("sums must be 'exact' or 'sequential'")
         self.sums = sums
@@ -228,9 +287,19 @@ class KDPartitioner(object):
     def _create_partitions(self, box):
         X, labels = self.points.X, self.labels
         self.bounding_boxes = {0: box}
-        for level in _split_schedule(self.max_partitions):
+        for depth, level in enumerate(_split_schedule(self.max_partitions)):
             sel = [c for c, _ in level]
             new = [nl for _, nl in level]
+            if self.split_method == 'rotation':
+                # the axis cycles once per BFS level (R:dbscan/partition.py:152,180-183)
+                axes = [depth % self.k] * len(sel)
+                med, less, tot = level_medians(
+                    lambda prefix, shift: _native.kd_radix_hist(X, labels, sel, axes, prefix,
+                                                                shift),
+                    len(sel), X.dtype == torch.float32)
+                _native.kd_split(X, labels, sel, axes, med, new)
+                apply_rotation_level(self.bounding_boxes, self.splits, level, axes, med, less, tot)
+                continue
             mom = _native.kd_moments(X, labels, sel, sequential=(self.sums == 'sequential'))
             axes, means, vars_, bounds = level_axes(mom)
             cnt = _native.kd_counts(X, labels, sel, axes, bounds)

@@ -19,7 +19,12 @@ def golden_names():
     return sorted(f[4:-4] for f in os.listdir(GOLDEN) if f.startswith("ref_") and f.endswith(".npz"))
 
 
-def load_golden(name):
+def load_golden(name, prefix="ref"):
     import numpy as np
-    z = np.load(os.path.join(GOLDEN, f"ref_{name}.npz"))
+    z = np.load(os.path.join(GOLDEN, f"{prefix}_{name}.npz"))
     return {k: z[k] for k in z.files}
+
+
+def rotation_names():
+    """Goldens of KDPartitioner(split_method='rotation') (make_golden_rotation.py)."""
+    return sorted(f[4:-4] for f in os.listdir(GOLDEN) if f.startswith("rot_") and f.endswith(".npz"))

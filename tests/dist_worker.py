@@ -19,7 +19,8 @@ def cut_points(n, world):
     return (c * n).astype(np.int64)
 
 
-def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native):
+def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native,
+             split_method='min_var'):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -38,7 +39,8 @@ def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native)
             sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
             from sharded_ops import OracleOps
             ops = OracleOps()
-        res = train_sharded(Xi, eps, min_samples, metric=metric, max_partitions=P, ops=ops)
+        res = train_sharded(Xi, eps, min_samples, metric=metric, max_partitions=P, ops=ops,
+                            split_method=split_method)
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), gid=res.gid.cpu().numpy(),
                  labels=res.labels.cpu().numpy(), core=res.core.cpu().numpy(),
                  ncl=np.int64(res.n_clusters), splits=np.array(res.splits, np.float64),
@@ -48,7 +50,8 @@ def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native)
         dist.destroy_process_group()
 
 
-def run_world(world, X, eps, min_samples, metric, P, out_dir, native=False, timeout=600):
+def run_world(world, X, eps, min_samples, metric, P, out_dir, native=False, timeout=600,
+              split_method='min_var'):
     """Spawn `world` ranks; return the assembled (labels, core, n_clusters,
     splits) over all points."""
     import socket
@@ -60,7 +63,8 @@ def run_world(world, X, eps, min_samples, metric, P, out_dir, native=False, time
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     procs = [ctx.Process(target=run_rank,
-                         args=(r, world, port, X, eps, min_samples, metric, P, out_dir, native))
+                         args=(r, world, port, X, eps, min_samples, metric, P, out_dir, native,
+                               split_method))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -62,6 +62,20 @@ class OracleOps(object):
             out[s, 7] = len(v)
         return out
 
+    def radix_hist(self, X, labels, sel, axes, prefix, shift):
+        """pd_kd_radix_hist restated: digit histograms of the fp64 order keys."""
+        x = X.numpy().astype(np.float64)
+        lab = labels.numpy()
+        out = np.zeros((len(sel), 256), np.int64)
+        for s, L in enumerate(sel):
+            b = np.ascontiguousarray(x[lab == L, axes[s]]).view(np.uint64).copy()
+            b[b == np.uint64(1 << 63)] = 0
+            k = np.where((b >> np.uint64(63)) == 1, ~b, b | np.uint64(1 << 63))
+            if shift + 8 < 64:
+                k = k[(k >> np.uint64(shift + 8)) == np.uint64(prefix[s])]
+            np.add.at(out[s], ((k >> np.uint64(shift)) & np.uint64(255)).astype(np.int64), 1)
+        return out
+
     def split(self, X, labels, sel, axes, boundary, new):
         x = X.numpy().astype(np.float64)
         lab = labels.numpy()

@@ -38,6 +38,21 @@ def test_sharded_labels_equal_sklearn(tmp_path, name, world, P):
         np.testing.assert_array_equal(sp, np.array(kd["splits"], np.float64))
 
 
+@pytest.mark.parametrize("name,world,P", [("b3d_20k", 2, 8), ("c0", 3, 5)])
+def test_sharded_rotation_split(tmp_path, name, world, P):
+    """split_method='rotation' over ranks: the all-reduced digit histograms
+    give the same medians as one process (oracle sort), labels stay sklearn's."""
+    g = load_golden(name)
+    X = g["X"]
+    out = run_world(world, X, float(g["eps"]), int(g["min_samples"]), 0, P, str(tmp_path),
+                    split_method="rotation")
+    np.testing.assert_array_equal(out["labels"], g["sk_labels"])
+    kd = oracle.kd_partition(X, P, split_method="rotation")
+    want = np.array(kd["splits"], np.float64)
+    for sp in out["splits"]:
+        np.testing.assert_array_equal(sp, want)
+
+
 def test_dd_combine_matches_exact_sum():
     rng = np.random.default_rng(3)
     v = rng.normal(size=(3, 1000)) * 10.0 ** rng.integers(-8, 8, size=(3, 1000))

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 import oracle
-from conftest import GOLDEN, golden_names, load_golden
+from conftest import GOLDEN, golden_names, load_golden, rotation_names
 
 pytestmark = pytest.mark.gpu
 
@@ -115,6 +115,36 @@ def test_kd_partitioner_exact_sums_match_oracle(native, name):
     assert np.array_equal(sf, rf)
     assert np.array_equal(kd.box_array()[:, 0], ref["box_lo"])
     assert np.array_equal(kd.box_array()[:, 1], ref["box_hi"])
+    assert np.array_equal(kd.labels.cpu().numpy(), ref["owner"])
+
+
+@pytest.mark.parametrize("name", rotation_names())
+def test_kd_partitioner_rotation_matches_reference(native, name):
+    """split_method='rotation': the GPU radix-select medians, split sizes,
+    boxes and owner labels are bit-identical to the reference's
+    median_search_split (R:dbscan/partition.py:8-30) run on the same points."""
+    from pypardis_amd import KDPartitioner
+    g = load_golden(name, "rot")
+    kd = KDPartitioner(_dev(g["X"]), int(g["max_partitions"]), split_method="rotation")
+    sp = np.array([[s[0], s[1], s[2], s[4], s[5]] for s in kd.splits], np.int64)
+    assert np.array_equal(sp, g["splits"])
+    assert np.array_equal(np.array([s[8] for s in kd.splits]), g["medians"])
+    assert np.array_equal(kd.box_array()[:, 0], g["box_lo"])
+    assert np.array_equal(kd.box_array()[:, 1], g["box_hi"])
+    assert np.array_equal(kd.labels.cpu().numpy(), g["owner"])
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_kd_rotation_large_matches_oracle(native, dtype):
+    """2M points with heavy ties and negative values, P=13: GPU medians vs the
+    oracle's sort (fp32 and fp64 inputs)."""
+    from pypardis_amd import KDPartitioner
+    rng = np.random.default_rng(31)
+    X = np.round(rng.normal(size=(2_000_000, 3)) * 50.0, 1).astype(dtype)
+    kd = KDPartitioner(_dev(X), 13, split_method="rotation")
+    ref = oracle.kd_partition(X, 13, split_method="rotation")
+    assert np.array_equal(np.array([s[8] for s in kd.splits]),
+                          np.array([s[8] for s in ref["splits"]]))
     assert np.array_equal(kd.labels.cpu().numpy(), ref["owner"])
 
 

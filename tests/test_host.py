@@ -55,6 +55,42 @@ def test_expanded_boxes_from_golden_boxes(name):
         assert np.array_equal(e.lower, g["ebox_lo"][L]) and np.array_equal(e.upper, g["ebox_hi"][L])
 
 
+def _order_keys(v):
+    """numpy twin of kd.hip order_key (fp64 bits -> order-preserving u64)."""
+    b = np.ascontiguousarray(v, np.float64).view(np.uint64).copy()
+    b[b == np.uint64(1 << 63)] = 0
+    neg = (b >> np.uint64(63)) == 1
+    return np.where(neg, ~b, b | np.uint64(1 << 63))
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_level_medians_radix_select(dtype):
+    """Host side of split_method='rotation': the digit walk over emulated
+    pd_kd_radix_hist histograms returns sorted(v)[len // 2] exactly, with
+    ties, negative values and signed zeros, for several splits at once."""
+    rng = np.random.default_rng(5)
+    groups = [rng.normal(size=1001), np.round(rng.normal(size=64), 1),
+              np.array([-0.0, 0.0, -0.0, 1.0, -2.5]), np.full(7, 3.25), np.array([-7.0])]
+    groups = [g.astype(dtype) for g in groups]
+    keys = [_order_keys(g.astype(np.float64)) for g in groups]
+
+    def hist_fn(prefix, shift):
+        h = np.zeros((len(groups), 256), np.int64)
+        for s, k in enumerate(keys):
+            if shift + 8 < 64:
+                k = k[(k >> np.uint64(shift + 8)) == np.uint64(prefix[s])]
+            np.add.at(h[s], ((k >> np.uint64(shift)) & np.uint64(255)).astype(np.int64), 1)
+        return h
+
+    med, less, tot = part.level_medians(hist_fn, len(groups), dtype == np.float32)
+    for s, g in enumerate(groups):
+        want = np.sort(g.astype(np.float64))[len(g) // 2]
+        assert med[s] == want, s
+        assert less[s] == int((g.astype(np.float64) < want).sum()) and tot[s] == len(g)
+    with pytest.raises(IndexError):
+        part.level_medians(lambda p, s: np.zeros((1, 256), np.int64), 1, False)
+
+
 def test_cluster_aggregator_links_core_labels_only():
     agg = ClusterAggregator()
     agg + (0, ["0:0", "1:3"])          # core in two neighbourhoods: link

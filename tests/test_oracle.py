@@ -6,9 +6,24 @@ import numpy as np
 import pytest
 
 import oracle
-from conftest import GOLDEN, golden_names, load_golden
+from conftest import GOLDEN, golden_names, load_golden, rotation_names
 
 NAMES = golden_names()
+ROT = rotation_names()
+
+
+@pytest.mark.parametrize("name", ROT)
+def test_rotation_partition_matches_reference(name):
+    """split_method='rotation' (median_search_split, R:dbscan/partition.py:8-30):
+    medians, split sizes, boxes and owner labels equal the reference's."""
+    g = load_golden(name, "rot")
+    kd = oracle.kd_partition(g["X"], int(g["max_partitions"]), split_method="rotation")
+    sp = np.array([[s[0], s[1], s[2], s[4], s[5]] for s in kd["splits"]], np.int64)
+    assert np.array_equal(sp, g["splits"])
+    assert np.array_equal(np.array([s[8] for s in kd["splits"]]), g["medians"])
+    assert np.array_equal(kd["box_lo"], g["box_lo"])
+    assert np.array_equal(kd["box_hi"], g["box_hi"])
+    assert np.array_equal(kd["owner"], g["owner"])
 
 
 def _metric(g):

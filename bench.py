@@ -17,7 +17,8 @@ routing + all-to-all-v of the halo records, per-GPU clustering of its
 max_partitions/N neighbourhoods, all-gather label merge, global ranks):
 strong scaling, value = total points / max-over-ranks time.
 
-Roofline object: the neighbour-count kernel (count_kernel in engine.hip).
+Roofline object: the neighbour-count kernel (count2_kernel in engine.hip, or
+count_kernel with --sweep-variant bit 0 clear).
 achieved = B_nc / t, B_nc = records * (3^d*4d + 4d + 4) + (cells + 1) * 4 bytes
 (340 B per record in 3-D), t = the kernel's HIP-event time on
 its own stream, averaged over the timed steps.  traffic = FETCH_SIZE*2 +
@@ -51,6 +52,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-n", type=int, default=1_000_000, help="CPU baseline sample size")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--sweep-variant", type=int, default=None,
+                    help="PD_OPT_SWEEP_VARIANT override (bit 0 count, 1 link, 2 border)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
@@ -118,6 +121,8 @@ def main():
     n, d = X.shape
     eps, ms, P = cfg["eps"], cfg["min_samples"], cfg.get("max_partitions") or 1
     ctx = _native.context(local_rank)
+    if args.sweep_variant is not None:
+        ctx.set_option(_native.PD_OPT_SWEEP_VARIANT, args.sweep_variant)
     if world > 1:
         from pypardis_amd.distributed import NativeOps, train_sharded
         lo, hi = rank * n // world, (rank + 1) * n // world
@@ -176,7 +181,10 @@ def main():
         t_cnt = float(np.mean(count_ms))
         alg_bytes, per = b_nc(rec, cells, d)
         achieved = alg_bytes / (t_cnt * 1e-3) / 1e9
-        pmc = load_pmc()
+        variant = args.sweep_variant if args.sweep_variant is not None \
+            else _native.SWEEP_VARIANT_DEFAULT
+        kname = "count2_kernel" if variant & 1 else "count_kernel"
+        pmc = load_pmc(kname)
         traffic = pmc["bytes_per_launch"] if pmc else None
         stages = {k: round(v / args.steps, 3) for k, v in stage_sum.items()
                   if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records")
@@ -207,7 +215,7 @@ def main():
                        "parallelism": f"kd-sharded{world}" if world > 1 else "single"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "kernel": "count_kernel",
+                         "traffic": traffic, "kernel": kname,
                          "kernel_ms": t_cnt, "bytes_per_record": per, "records": rec,
                          "cells": cells, "algorithmic_bytes": alg_bytes},
             "cpu_baseline": cpu,

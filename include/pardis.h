@@ -66,8 +66,13 @@ enum pd_option {
     PD_OPT_FP32_SCREEN = 7, /* fp32 inputs: decide pairs outside a 2^-18 band around eps with
                                fp32 arithmetic, the rest with the exact fp64 predicate
                                (default 1; results are identical with 0) */
-    PD_OPT_SWEEP_STATS = 8  /* tally the neighbour sweeps' candidates and union-find outcomes
+    PD_OPT_SWEEP_STATS = 8, /* tally the neighbour sweeps' candidates and union-find outcomes
                                into the PD_T_S_* slots (instrumented kernels; default 0) */
+    PD_OPT_SWEEP_VARIANT = 9 /* kernel variant per neighbour sweep (tuning; results are
+                               identical): bit 0 count, bit 1 link, bit 2 border; a set bit
+                               selects the batched lane kernel (wave-uniform grid in scalar
+                               registers, three rows swept as one list), a clear bit the
+                               row-by-row kernel.  Default 5 (the measured best on MI355X). */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -22,6 +22,8 @@ PD_EUCLIDEAN, PD_CITYBLOCK = 0, 1
 PD_OPT_TIMING, PD_OPT_FULL_COUNTS, PD_OPT_SEQUENTIAL_MOMENTS = 1, 2, 3
 PD_OPT_LINK_MODE, PD_OPT_JUMP_ROUNDS, PD_OPT_XSUB, PD_OPT_FP32_SCREEN = 4, 5, 6, 7
 PD_OPT_SWEEP_STATS = 8
+PD_OPT_SWEEP_VARIANT = 9
+SWEEP_VARIANT_DEFAULT = 5
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
                 "s_count_cand", "s_link_cand", "s_link_hit", "s_link_core", "s_link_same",

@@ -118,7 +118,10 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.screen = value != 0;
         else if (option == PD_OPT_SWEEP_STATS)
             ctx->c.sweep_stats = value != 0;
-        else if (option == PD_OPT_XSUB) {
+        else if (option == PD_OPT_SWEEP_VARIANT) {
+            if (value < 0 || value > 7) throw Error(PD_EINVAL, "sweep variant is a 3-bit mask");
+            ctx->c.variant = (int)value;
+        } else if (option == PD_OPT_XSUB) {
             if (value < 1 || value > 16) throw Error(PD_EINVAL, "xsub must be in [1, 16]");
             ctx->c.xsub = (int)value;
         }

@@ -369,81 +369,105 @@ struct NRows {
 // together, then its cstart words — two round trips per batch instead of
 // two per row (the compiler otherwise serialises them behind the per-row
 // branches: ~36 dependent loads per record).
+// The query point's cell and in-cell fractions in its neighbourhood's grid
+// (grid fields copied to registers once).
+template <int D>
+struct QueryCell {
+    double lo[D], inv[D], cs[D], f[D];
+    int64_t nc[D], c[D];
+    uint64_t base;
+};
+
+template <int D>
+__device__ __forceinline__ QueryCell<D> query_cell(const PartGrid* gp, const double (&a)[D]) {
+    QueryCell<D> Q;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        Q.lo[j] = gp->lo[j];
+        Q.inv[j] = gp->inv[j];
+        Q.cs[j] = gp->cs[j];
+        Q.nc[j] = gp->nc[j];
+    }
+    Q.base = gp->base;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const double u = (a[j] - Q.lo[j]) * Q.inv[j];
+        int64_t q = (int64_t)floor(u);
+        q = q < 0 ? 0 : q;
+        q = q >= Q.nc[j] ? Q.nc[j] - 1 : q;
+        Q.c[j] = q;
+        const double fr = u - (double)q;
+        Q.f[j] = fr < 0.0 ? 0.0 : (fr > 1.0 ? 1.0 : fr);
+    }
+    return Q;
+}
+
+// Key range [k0, k1) of candidate row q (offsets of axes 1.. in base 3, axis
+// 1 fastest), clipped to the eps-ball's chord; false if the ball misses it.
+template <int D, int M>
+__device__ __forceinline__ bool row_keys(const QueryCell<D>& Q, const double (&a)[D], double eps,
+                                         int q, uint64_t& k0, uint64_t& k1) {
+    const double slack = eps * (1.0 / 1048576.0);
+    int t = q;
+    bool okq = true;
+    double d2 = 0.0, d1 = 0.0;
+    int64_t cc[D];
+#pragma unroll
+    for (int j = 1; j < D; ++j) {
+        const int o = (t % 3) - 1;
+        t /= 3;
+        const int64_t v = Q.c[j] + o;
+        okq &= (v >= 0) & (v < Q.nc[j]);
+        cc[j] = v;
+        double dist = o == 0 ? 0.0 : (o < 0 ? Q.f[j] : 1.0 - Q.f[j]) * Q.cs[j] - slack;
+        dist = dist > 0.0 ? dist : 0.0;
+        d2 += dist * dist;
+        d1 += dist;
+    }
+    double w;
+    if constexpr (M == 0) {
+        okq &= d2 <= eps * eps;
+        w = sqrt(fmax(eps * eps - d2, 0.0));
+    } else {
+        okq &= d1 <= eps;
+        w = eps - d1;
+    }
+    w = w * (1.0 + 1.0 / 1048576.0) + slack;
+    int64_t x0 = (int64_t)floor((a[0] - w - Q.lo[0]) * Q.inv[0]);
+    int64_t x1 = (int64_t)floor((a[0] + w - Q.lo[0]) * Q.inv[0]);
+    x0 = x0 < 0 ? 0 : x0;
+    x1 = x1 >= Q.nc[0] ? Q.nc[0] - 1 : x1;
+    cc[0] = x0;
+    uint64_t lin = 0;
+#pragma unroll
+    for (int j = D - 1; j >= 0; --j) lin = lin * (uint64_t)Q.nc[j] + (uint64_t)cc[j];
+    const uint64_t kk0 = Q.base + lin;
+    k0 = okq ? kk0 : 0;
+    k1 = okq ? kk0 + (uint64_t)(x1 - x0) + 1 : 0;
+    return okq;
+}
+
+// Occupied cells with key < k, from the key's directory word.
+__device__ __forceinline__ uint32_t dir_rank(const uint4& w, uint64_t k) {
+    const uint64_t bits = ((uint64_t)w.y << 32) | (uint64_t)w.x;
+    const uint32_t sh = (uint32_t)(k & 63);
+    const uint64_t m = sh ? (bits & ((~0ull) >> (64 - sh))) : 0ull;
+    return w.z + (uint32_t)__popcll(m);
+}
+
 template <int D, int M>
 __device__ __forceinline__ void row_ranges(const Cells& C, const double (&a)[D], int L, double eps,
                                            uint32_t (&s)[NRows<D>::v],
                                            uint32_t (&e)[NRows<D>::v]) {
     constexpr int NR = NRows<D>::v;
     constexpr int B = NR < 3 ? NR : 3;   // rows per batch
-    const PartGrid* gp = C.parts + L;
-    double lo[D], inv[D], cs[D];
-    int64_t nc[D];
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        lo[j] = gp->lo[j];
-        inv[j] = gp->inv[j];
-        cs[j] = gp->cs[j];
-        nc[j] = gp->nc[j];
-    }
-    const uint64_t base = gp->base;
-    int64_t c[D];
-    double f[D];
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        const double u = (a[j] - lo[j]) * inv[j];
-        int64_t q = (int64_t)floor(u);
-        q = q < 0 ? 0 : q;
-        q = q >= nc[j] ? nc[j] - 1 : q;
-        c[j] = q;
-        const double fr = u - (double)q;
-        f[j] = fr < 0.0 ? 0.0 : (fr > 1.0 ? 1.0 : fr);
-    }
-    const double slack = eps * (1.0 / 1048576.0);
+    const QueryCell<D> Q = query_cell<D>(C.parts + L, a);
 #pragma unroll
     for (int q0 = 0; q0 < NR; q0 += B) {
         uint64_t k0[B], k1[B];
         bool ok[B];
 #pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const int q = q0 + b;
-            int t = q;
-            bool okq = true;
-            double d2 = 0.0, d1 = 0.0;
-            int64_t cc[D];
-#pragma unroll
-            for (int j = 1; j < D; ++j) {
-                const int o = (t % 3) - 1;
-                t /= 3;
-                const int64_t v = c[j] + o;
-                okq &= (v >= 0) & (v < nc[j]);
-                cc[j] = v;
-                double dist = o == 0 ? 0.0 : (o < 0 ? f[j] : 1.0 - f[j]) * cs[j] - slack;
-                dist = dist > 0.0 ? dist : 0.0;
-                d2 += dist * dist;
-                d1 += dist;
-            }
-            double w;
-            if constexpr (M == 0) {
-                okq &= d2 <= eps * eps;
-                w = sqrt(fmax(eps * eps - d2, 0.0));
-            } else {
-                okq &= d1 <= eps;
-                w = eps - d1;
-            }
-            w = w * (1.0 + 1.0 / 1048576.0) + slack;
-            int64_t x0 = (int64_t)floor((a[0] - w - lo[0]) * inv[0]);
-            int64_t x1 = (int64_t)floor((a[0] + w - lo[0]) * inv[0]);
-            x0 = x0 < 0 ? 0 : x0;
-            x1 = x1 >= nc[0] ? nc[0] - 1 : x1;
-            cc[0] = x0;
-            uint64_t lin = 0;
-#pragma unroll
-            for (int j = D - 1; j >= 0; --j) lin = lin * (uint64_t)nc[j] + (uint64_t)(j == 0 ? x0 : cc[j]);
-            const uint64_t kk0 = base + lin;
-            k0[b] = okq ? kk0 : 0;
-            k1[b] = okq ? kk0 + (uint64_t)(x1 - x0) + 1 : 0;
-            ok[b] = okq;
-        }
+        for (int b = 0; b < B; ++b) ok[b] = row_keys<D, M>(Q, a, eps, q0 + b, k0[b], k1[b]);
         uint4 w0[B], w1[B];
 #pragma unroll
         for (int b = 0; b < B; ++b) {
@@ -453,14 +477,8 @@ __device__ __forceinline__ void row_ranges(const Cells& C, const double (&a)[D],
         uint32_t i0[B], i1[B];
 #pragma unroll
         for (int b = 0; b < B; ++b) {
-            auto rk = [](const uint4& w, uint64_t k) {
-                const uint64_t bits = ((uint64_t)w.y << 32) | (uint64_t)w.x;
-                const uint32_t sh = (uint32_t)(k & 63);
-                const uint64_t m = sh ? (bits & ((~0ull) >> (64 - sh))) : 0ull;
-                return w.z + (uint32_t)__popcll(m);
-            };
-            i0[b] = rk(w0[b], k0[b]);
-            i1[b] = rk(w1[b], k1[b]);
+            i0[b] = dir_rank(w0[b], k0[b]);
+            i1[b] = dir_rank(w1[b], k1[b]);
         }
 #pragma unroll
         for (int b = 0; b < B; ++b) {
@@ -653,7 +671,7 @@ done:
     // the border pass skips it)
     core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
     mn_out[r] = mn;
-    if (cnt_out) cnt_out[r] = cnt;
+    if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
     if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
 }
 
@@ -946,6 +964,261 @@ __global__ __launch_bounds__(kBlock) void border_kernel(
     key_out[pt] = best;
 }
 
+// ------------------------------------------------------------------ batched lane sweeps
+// One lane per record (as above), restructured for latency (PD_OPT_SWEEP_VARIANT
+// bits): the neighbourhood index is made wave-uniform (a waterfall over the
+// wave's distinct neighbourhoods — almost always one), so the grid parameters
+// sit in scalar registers; rows are taken three at a time and the three
+// ranges are swept as ONE virtual list, four candidates per round trip with
+// no per-row remainder loops.  Fewer live registers, more waves in flight.
+__device__ __forceinline__ double uniform_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xFFFFFFFFll));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ int64_t uniform_i64(int64_t v) {
+    const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xFFFFFFFFll));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return ((int64_t)hi << 32) | (unsigned int)lo;
+}
+
+// Grid of neighbourhood L (wave-uniform L) in scalar registers + the query's cell.
+template <int D>
+__device__ __forceinline__ QueryCell<D> query_cell_u(const PartGrid* gp, const double (&a)[D]) {
+    QueryCell<D> Q;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        Q.lo[j] = uniform_f64(gp->lo[j]);
+        Q.inv[j] = uniform_f64(gp->inv[j]);
+        Q.cs[j] = uniform_f64(gp->cs[j]);
+        Q.nc[j] = uniform_i64(gp->nc[j]);
+    }
+    Q.base = (uint64_t)uniform_i64((int64_t)gp->base);
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        const double u = (a[j] - Q.lo[j]) * Q.inv[j];
+        int64_t q = (int64_t)floor(u);
+        q = q < 0 ? 0 : q;
+        q = q >= Q.nc[j] ? Q.nc[j] - 1 : q;
+        Q.c[j] = q;
+        const double fr = u - (double)q;
+        Q.f[j] = fr < 0.0 ? 0.0 : (fr > 1.0 ? 1.0 : fr);
+    }
+    return Q;
+}
+
+// Runs body(L, uniform): when the whole wave lies in one neighbourhood (all
+// but at most P - 1 waves of a sweep) with L wave-uniform, so the grid
+// parameters sit in scalar registers; otherwise with each lane's own L.
+template <typename F>
+__device__ __forceinline__ void with_part(const uint32_t* __restrict__ ps, int P, uint32_t r,
+                                          F&& body) {
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane(r);
+    const int L0 = part_of(ps, P, r0);
+    const uint32_t lo = ps[L0], hi = ps[L0 + 1];
+    if (__all(r >= lo && r < hi))
+        body(__builtin_amdgcn_readfirstlane(L0), std::true_type{});
+    else
+        body(part_of(ps, P, r), std::false_type{});
+}
+
+template <int D>
+struct RowBatch {
+    static constexpr int NR = NRows<D>::v;
+    static constexpr int B = NR < 3 ? NR : 3;   // rows per batch
+    static constexpr int NB = NR / B;           // batches
+};
+
+// Ranges of the rows of batch `bt` (row order within the batch: centre row
+// first when centre_first), clipped below at clip, as one virtual list:
+// position v < tot maps to record v + off[k] for v in [pre[k], pre[k+1]).
+template <int D, int M>
+__device__ __forceinline__ uint32_t batch_list(const Cells& C, const QueryCell<D>& Q,
+                                               const double (&a)[D], double eps, int bt,
+                                               bool centre_first, uint32_t clip,
+                                               uint32_t (&pre)[RowBatch<D>::B],
+                                               uint32_t (&off)[RowBatch<D>::B]) {
+    constexpr int B = RowBatch<D>::B;
+    uint64_t k0[B], k1[B];
+    bool ok[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const int bb = (centre_first && B == 3) ? (b == 0 ? 1 : (b == 1 ? 0 : 2)) : b;
+        ok[b] = row_keys<D, M>(Q, a, eps, bt * B + bb, k0[b], k1[b]);
+    }
+    uint4 w0[B], w1[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        w0[b] = C.dir[k0[b] >> 6];
+        w1[b] = C.dir[k1[b] >> 6];
+    }
+    uint32_t i0[B], i1[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        i0[b] = dir_rank(w0[b], k0[b]);
+        i1[b] = dir_rank(w1[b], k1[b]);
+    }
+    uint32_t tot = 0;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const uint32_t sv = C.cstart[i0[b]], ev = C.cstart[i1[b]];
+        uint32_t st = ok[b] ? sv : 0u;
+        const uint32_t en = ok[b] ? ev : 0u;
+        st = st > clip ? st : clip;
+        const uint32_t len = en > st ? en - st : 0u;
+        pre[b] = tot;
+        off[b] = st - tot;
+        tot += len;
+    }
+    return tot;
+}
+
+template <int B>
+__device__ __forceinline__ uint32_t bpos(uint32_t v, const uint32_t (&pre)[B],
+                                         const uint32_t (&off)[B]) {
+    uint32_t o = off[0];
+#pragma unroll
+    for (int b = 1; b < B; ++b) o = v >= pre[b] ? off[b] : o;
+    return v + o;
+}
+
+template <typename T, int D, int M, bool ST>
+__global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs, uint32_t R,
+                                                        Cells C, double eps, double eps2,
+                                                        float lo, float hi, uint32_t ms, int full,
+                                                        uint8_t* __restrict__ core,
+                                                        uint32_t* __restrict__ mn_out,
+                                                        uint32_t* __restrict__ cnt_out,
+                                                        unsigned long long* __restrict__ stats) {
+    constexpr int B = RowBatch<D>::B, NB = RowBatch<D>::NB;
+    const uint32_t r = rec_index();
+    if (r >= R) return;
+    double a[D];
+    load_rec<T, D>(Xs, r, a);
+    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
+    const uint32_t stop = full ? 0xFFFFFFFFu : ms;
+    uint32_t cnt = 0, mn = r, n_cand = 0;
+    with_part(C.part_start, C.P, r, [&](int L, auto U) {
+        const QueryCell<D> Q = decltype(U)::value ? query_cell_u<D>(C.parts + L, a)
+                                                  : query_cell<D>(C.parts + L, a);
+        for (int bq = 0; bq < NB; ++bq) {
+            const int bt = (bq + NB / 2) % NB;   // centre batch first
+            uint32_t pre[B], off[B];
+            const uint32_t tot = batch_list<D, M>(C, Q, a, eps, bt, true, 0u, pre, off);
+            for (uint32_t v = 0; v < tot; v += 4) {
+                uint32_t j[4];
+                T b[4][D];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    j[u] = v + u < tot ? bpos<B>(v + u, pre, off) : r;
+                    load_raw<T, D>(Xs, j[u], b[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const bool w = (v + u < tot) && pr(b[u]);
+                    cnt += w ? 1u : 0u;
+                    mn = (w && j[u] < mn) ? j[u] : mn;
+                }
+                if constexpr (ST) n_cand += (tot - v < 4u ? tot - v : 4u);
+                if (cnt >= stop) return;
+            }
+        }
+    });
+    core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
+    mn_out[r] = mn;
+    if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
+    if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
+}
+
+template <typename T, int D, int M, bool ST>
+__global__ __launch_bounds__(kBlock) void link2_kernel(const T* __restrict__ Xs, uint32_t NL,
+                                                       const uint32_t* __restrict__ list, Cells C,
+                                                       double eps, double eps2, float lo, float hi,
+                                                       uint32_t* __restrict__ par,
+                                                       unsigned long long* __restrict__ stats) {
+    constexpr int B = RowBatch<D>::B, NB = RowBatch<D>::NB;
+    const uint32_t i = rec_index();
+    if (i >= NL) return;
+    const uint32_t r = list[i];   // core records, ascending
+    double a[D];
+    load_rec<T, D>(Xs, r, a);
+    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
+    Linker<ST> lk{par, uf_find_l1(par, r), {}};
+    with_part(C.part_start, C.P, r, [&](int L, auto U) {
+        const QueryCell<D> Q = decltype(U)::value ? query_cell_u<D>(C.parts + L, a)
+                                                  : query_cell<D>(C.parts + L, a);
+        for (int bt = 0; bt < NB; ++bt) {
+            uint32_t pre[B], off[B];
+            // edges j > r only (the predicate is symmetric)
+            const uint32_t tot = batch_list<D, M>(C, Q, a, eps, bt, false, r + 1, pre, off);
+            for (uint32_t v = 0; v < tot; v += 4) {
+                uint32_t j[4], pj[4];
+                T b[4][D];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    j[u] = v + u < tot ? bpos<B>(v + u, pre, off) : r;
+                    load_raw<T, D>(Xs, j[u], b[u]);
+                    pj[u] = ld_l1(par + j[u]);
+                }
+                if constexpr (ST) lk.st.cand += (tot - v < 4u ? tot - v : 4u);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (v + u < tot && pr(b[u])) lk.edge(j[u], pj[u]);
+            }
+        }
+    });
+    if constexpr (ST) {
+        atomicAdd(stats + 1, (unsigned long long)lk.st.cand);
+        atomicAdd(stats + 2, (unsigned long long)lk.st.hit);
+        atomicAdd(stats + 3, (unsigned long long)lk.st.core);
+        atomicAdd(stats + 4, (unsigned long long)lk.st.same);
+        atomicAdd(stats + 5, (unsigned long long)lk.st.find_same);
+        atomicAdd(stats + 6, (unsigned long long)lk.st.unions);
+    }
+}
+
+template <typename T, int D, int M>
+__global__ __launch_bounds__(kBlock) void border2_kernel(
+    const T* __restrict__ Xs, uint32_t NL, const uint32_t* __restrict__ list, Cells C, double eps,
+    double eps2, float lo, float hi, const uint32_t* __restrict__ vals,
+    const uint32_t* __restrict__ par, const uint32_t* __restrict__ gmin,
+    uint32_t* __restrict__ key_out) {
+    constexpr int B = RowBatch<D>::B, NB = RowBatch<D>::NB;
+    const uint32_t i = rec_index();
+    if (i >= NL) return;
+    const uint32_t r = list[i];   // owner, non-core records with a neighbour, ascending
+    double a[D];
+    load_rec<T, D>(Xs, r, a);
+    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
+    uint32_t best = kNone;
+    with_part(C.part_start, C.P, r, [&](int L, auto U) {
+        const QueryCell<D> Q = decltype(U)::value ? query_cell_u<D>(C.parts + L, a)
+                                                  : query_cell<D>(C.parts + L, a);
+        for (int bt = 0; bt < NB; ++bt) {
+            uint32_t pre[B], off[B];
+            const uint32_t tot = batch_list<D, M>(C, Q, a, eps, bt, false, 0u, pre, off);
+            for (uint32_t v = 0; v < tot; v += 4) {
+                uint32_t j[4], pj[4];
+                T b[4][D];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    j[u] = v + u < tot ? bpos<B>(v + u, pre, off) : r;
+                    load_raw<T, D>(Xs, j[u], b[u]);
+                    pj[u] = par[j[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (v + u < tot && pj[u] != kNone && pr(b[u])) {
+                        const uint32_t k = gmin[pj[u]];
+                        best = k < best ? k : best;
+                    }
+            }
+        }
+    });
+    key_out[vals[r] & kIdMask] = best;
+}
+
 __global__ __launch_bounds__(kBlock) void root_flag_kernel(const uint32_t* __restrict__ key,
                                                            uint64_t n,
                                                            uint32_t* __restrict__ flag) {
@@ -991,6 +1264,46 @@ struct EvTimer {
 };
 
 inline unsigned blocks(uint64_t n) { return n ? (unsigned)((n + kBlock - 1) / kBlock) : 1u; }
+
+// Launch helpers for the three neighbour sweeps: bit k of `variant`
+// (PD_OPT_SWEEP_VARIANT) selects the batched lane kernel for sweep k (0
+// count, 1 link, 2 border) instead of the row-by-row one.
+template <typename T, int D, int M, bool ST>
+void launch_count(int variant, hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double eps,
+                  double eps2, float lo, float hi, uint32_t ms, int full, uint8_t* core,
+                  uint32_t* mn, uint32_t* cnt, unsigned long long* st) {
+    if (variant & 1)
+        hipLaunchKernelGGL((count2_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
+                           C, eps, eps2, lo, hi, ms, full, core, mn, cnt, st);
+    else
+        hipLaunchKernelGGL((count_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
+                           C, eps, eps2, lo, hi, ms, full, core, mn, cnt, st);
+}
+
+template <typename T, int D, int M, bool ST>
+void launch_link(int variant, hipStream_t s, const T* Xs, uint32_t NL, const uint32_t* list,
+                 const Cells& C, double eps, double eps2, float lo, float hi, uint32_t* par,
+                 unsigned long long* st) {
+    if (variant & 2)
+        hipLaunchKernelGGL((link2_kernel<T, D, M, ST>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs,
+                           NL, list, C, eps, eps2, lo, hi, par, st);
+    else
+        hipLaunchKernelGGL((link_kernel<T, D, M, ST>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs,
+                           NL, list, C, eps, eps2, lo, hi, par, st);
+}
+
+template <typename T, int D, int M>
+void launch_border(int variant, hipStream_t s, const T* Xs, uint32_t NL, const uint32_t* list,
+                   const Cells& C, double eps, double eps2, float lo, float hi,
+                   const uint32_t* vals, const uint32_t* par, const uint32_t* gmin,
+                   uint32_t* key_out) {
+    if (variant & 4)
+        hipLaunchKernelGGL((border2_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
+                           list, C, eps, eps2, lo, hi, vals, par, gmin, key_out);
+    else
+        hipLaunchKernelGGL((border_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
+                           list, C, eps, eps2, lo, hi, vals, par, gmin, key_out);
+}
 
 // Ordered compaction of record ids satisfying `pred` (keeps the spatial
 // order, so a wave's records stay neighbours).  Returns the count (syncs).
@@ -1138,13 +1451,13 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     }
     if (R) {
         if (sst)
-            hipLaunchKernelGGL((count_kernel<T, D, M, true>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                               Xs, R, C, eps, eps2, slo, shi, (uint32_t)a.min_samples,
-                               ctx.full_counts ? 1 : 0, core, mn, cnt_rec, sst);
+            launch_count<T, D, M, true>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
+                                        (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0, core,
+                                        mn, cnt_rec, sst);
         else
-            hipLaunchKernelGGL((count_kernel<T, D, M, false>), dim3(blocks(R)), dim3(kBlock), 0,
-                               s, Xs, R, C, eps, eps2, slo, shi, (uint32_t)a.min_samples,
-                               ctx.full_counts ? 1 : 0, core, mn, cnt_rec, sst);
+            launch_count<T, D, M, false>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
+                                         (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0, core,
+                                         mn, cnt_rec, sst);
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 5
@@ -1163,11 +1476,11 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
             const uint32_t NC = select_records(ctx, "core_list", R, IsCore{core}, &clist, s);
             ctx.t.core_records = NC;
             if (NC && sst)
-                hipLaunchKernelGGL((link_kernel<T, D, M, true>), dim3(blocks(NC)), dim3(kBlock), 0,
-                                   s, Xs, NC, clist, C, eps, eps2, slo, shi, par, sst);
+                launch_link<T, D, M, true>(ctx.variant, s, Xs, NC, clist, C, eps, eps2, slo, shi,
+                                           par, sst);
             else if (NC)
-                hipLaunchKernelGGL((link_kernel<T, D, M, false>), dim3(blocks(NC)), dim3(kBlock),
-                                   0, s, Xs, NC, clist, C, eps, eps2, slo, shi, par, sst);
+                launch_link<T, D, M, false>(ctx.variant, s, Xs, NC, clist, C, eps, eps2, slo, shi,
+                                            par, sst);
         }
     }
     PD_HIP(hipGetLastError());
@@ -1264,8 +1577,8 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         const uint32_t NB =
             select_records(ctx, "border_list", R, IsBorderCandidate{core, vals}, &blist, s);
         if (NB)
-            hipLaunchKernelGGL((border_kernel<T, D, M>), dim3(blocks(NB)), dim3(kBlock), 0, s, Xs,
-                               NB, blist, C, eps, eps2, slo, shi, vals, par, gmin, key_out);
+            launch_border<T, D, M>(ctx.variant, s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par,
+                                   gmin, key_out);
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 9 (phase 2: 1)

@@ -89,6 +89,7 @@ struct Ctx {
     int xsub = 2;                // axis-0 sub-cells per eps
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
+    int variant = 5;             // PD_OPT_SWEEP_VARIANT: batched count + border, row-wise link
     Timings t;
     PhaseState st;
     hipEvent_t ev[16] = {};
@@ -137,7 +138,7 @@ void kd_split(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
 void kd_radix_hist(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                    int n_sel, const int32_t* sel_host, const int32_t* axis_host,
                    const uint64_t* prefix_host, int shift, int64_t* hist_host, hipStream_t s);
-void kd_moments_dd(Ctx& ctx,const void* X, int dtype, int64_t n, int d, const int32_t* labels,
+void kd_moments_dd(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                    int n_sel, const int32_t* sel_host, double* out_host, hipStream_t s);
 void route(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P, const double* ebox_host,
            const int32_t* part_rank_host, int n_ranks, uint64_t* mask, int64_t* counts_host,

@@ -228,6 +228,45 @@ def test_train_matches_oracle(native, case):
     assert m.n_clusters_ == ncl
 
 
+@pytest.mark.parametrize("variant", [0, 7])
+def test_sweep_variants_exact(native, variant):
+    """PD_OPT_SWEEP_VARIANT: the row-by-row and the batched sweep kernels
+    (every stage in one or the other) give identical counts, core flags and
+    labels (= oracle) on every case: 1-D..4-D, cityblock, fp64, exact ties,
+    min_samples 1, several neighbourhoods (waves straddling two)."""
+    from pypardis_amd import DBSCAN, synth
+    ctx = native.context()
+    ctx.set_option(native.PD_OPT_SWEEP_VARIANT, variant)
+    try:
+        for _, kw, eps, ms, metric, P in CASES:
+            X = synth.blobs_noise(**kw)
+            lab_o, core_o, cnt_o, _ = oracle.dbscan(X, eps, ms, metric)
+            lab, core, ncl, cnt = _cluster(native, X, eps, ms, metric, full=True)
+            assert np.array_equal(cnt, cnt_o), kw
+            assert np.array_equal(lab, lab_o), kw
+            m = DBSCAN(eps=eps, min_samples=ms, metric=metric, max_partitions=P).train(_dev(X))
+            assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o), kw
+            assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_o), kw
+        g = np.arange(60, dtype=np.float32) * np.float32(0.05)
+        lattice = np.stack(np.meshgrid(g, g, indexing="ij"), -1).reshape(-1, 2)
+        lab_o, _, cnt_o, _ = oracle.dbscan(lattice, float(np.float32(0.05)), 5)
+        lab, _, _, cnt = _cluster(native, lattice, float(np.float32(0.05)), 5, full=True)
+        assert np.array_equal(cnt, cnt_o) and np.array_equal(lab, lab_o)
+        X = synth.blobs_noise(30_000, 3, side=5.0, n_centers=4, sigma=0.3, seed=61)
+        X64 = X.astype(np.float64) + np.random.default_rng(2).uniform(-1e-9, 1e-9, X.shape)
+        for Y, ms in ((X, 1), (X, 30), (X64, 6)):
+            lab_o, core_o, _, _ = oracle.dbscan(Y, 0.06, ms)
+            m = DBSCAN(eps=0.06, min_samples=ms, max_partitions=6).train(_dev(Y))
+            assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o), ms
+        for name in ("b3d_20k", "c0_p5_cityblock", "dup_1d"):
+            gd = load_golden(name)
+            lab, core, _ = _cluster(native, gd["X"], float(gd["eps"]), int(gd["min_samples"]),
+                                    _metric(gd))
+            assert np.array_equal(lab, gd["sk_labels"]) and np.array_equal(core, gd["sk_core"])
+    finally:
+        ctx.set_option(native.PD_OPT_SWEEP_VARIANT, native.SWEEP_VARIANT_DEFAULT)
+
+
 def test_fp64_input_exact(native):
     from pypardis_amd import synth
     X = synth.blobs_noise(40_000, 2, side=10.0, n_centers=5, sigma=0.3, seed=31).astype(np.float64)

@@ -3,6 +3,7 @@
 
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "internal.hpp"
 
@@ -231,7 +232,6 @@ int32_t pd_halo_members(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, in
     return guard(ctx, [&] {
         check_common(ctx, X, n, d);
         if (P < 1 || !ebox || !counts) throw Error(PD_EINVAL, "bad boxes");
-        if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "d > 4");
         if (n == 0) {
             std::memset(counts, 0, sizeof(int64_t) * P);
             return;
@@ -288,15 +288,14 @@ int32_t pd_cluster(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t
         a.core = core;
         a.counts = counts;
         a.stream = (hipStream_t)stream;
-        double box[2 * kMaxDim] = {0};
+        std::vector<double> box(2 * (size_t)d, 0.0);
         if (n > 0) {
-            if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "d > 4: the dense-tile path is not built yet");
             int64_t bad = 0;
-            bbox(ctx->c, X, dtype, n, d, box, &bad, a.stream);
+            bbox(ctx->c, X, dtype, n, d, box.data(), &bad, a.stream);
             if (bad) throw Error(PD_EINVAL, "input contains NaN or infinity");
         }
-        a.ebox = box;
-        a.data_box = box;
+        a.ebox = box.data();
+        a.data_box = box.data();
         train(ctx->c, a);
         if (n_clusters) *n_clusters = a.n_clusters;
     });

@@ -1,0 +1,550 @@
+// The high-dimensional path (d > 4): DBSCAN from dense distance tiles on the
+// matrix cores (BASELINE config C3, 64-D embeddings).  An eps-grid is useless
+// there (3^d neighbour cells), so the neighbour test of sklearn's radius query
+// (SK:cluster/_dbscan.py:410-434; the reference calls it per partition in
+// R:dbscan/dbscan.py:28-30) becomes a Gram-matrix tile:
+//
+//   d2~(i, j) = |x_i|^2 + |x_j|^2 - 2 <x_i, x_j>
+//
+// with <.,.> from split-bf16 MFMA (x = hi + lo, hi = bf16(x), lo = bf16(x -
+// hi); hi.hi + hi.lo + lo.hi on v_mfma_f32_32x32x16_bf16, fp32 accumulation)
+// and a rigorous error band |d2~ - d2| <= c (|x_i|^2 + |x_j|^2), c = 2^-13:
+// the split drops <= 3 * 2^-18 |x||y|, the fp32 accumulation over K <= 128
+// adds <= 2^-17 |x||y|, fp32 rounding of the coordinates and of d2~ itself
+// < 2^-21 (|x|^2 + |y|^2), and 2|x||y| <= |x|^2 + |y|^2 — a > 4x margin.
+// Pairs outside the band are decided exactly by the bound; pairs inside it
+// are re-tested with sklearn's kd_tree leaf predicate (fp64, per axis in
+// order, no FMA; SK:metrics/_dist_metrics.pxd.tp:39-49).  So counts, core
+// flags and labels are bit-exact, as on the grid path (engine.hip).
+//
+// Stages (sklearn DBSCAN.fit semantics, same keys and numbering as engine.hip):
+//   count   all x all tiles              -> neighbour counts (self included)
+//   link    core x core tiles, j > i     -> union-find -> components
+//   border  non-core-with-neighbour x core tiles -> smallest adjacent key
+//   labels  rank of the keys (rank_labels_async, engine.hip)
+// Cityblock, and d > 128, take an exact fp64 VALU tile instead of the MFMA.
+//
+// Layout in HBM: points centred on the bbox midpoint and scaled by a power of
+// two (the exact recheck reads the caller's X), split into bf16 hi / lo
+// arrays in "fragment-major" order so one 16-byte load per lane is an MFMA
+// operand: row group g (32 rows), k-step s (16 dims) is a 1 KiB block of 64
+// lanes x 8 bf16 where lane 32h + r holds dims 16s + 8h .. 16s + 8h + 7 of
+// row 32g + r — the A[row][k] / B[k][col] maps of 32x32x16 (the Gram matrix
+// needs the same layout for both operands).  Norms |x|^2 in fp32.  Per wave:
+// 64 query points (B operand, held in registers) against a stream of 64-point
+// tiles of the other set (A operand); C/D: col = lane & 31 is the query,
+// rows = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5) the streamed points.
+#include <cstring>   // before rocprim (its texture_cache_iterator uses memset)
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "internal.hpp"
+#include "uf.hpp"
+
+namespace pd {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum { kCount = 0, kLink = 1, kBorder = 2 };
+constexpr int kTile = 64;                 // points per wave tile (2 MFMA tiles of 32)
+constexpr float kBandC = 1.0f / 8192.0f;  // error band c (see header)
+constexpr float kPadNorm = 1.0e30f;       // norm of padding rows: never a neighbour
+
+inline unsigned nblocks(uint64_t n, unsigned per = kBlock) {
+    return n ? (unsigned)((n + per - 1) / per) : 1u;
+}
+inline uint32_t pad_rows(uint32_t m) { return (m + kTile - 1) / kTile * kTile; }
+
+// A point set in MFMA fragment layout.
+struct FragSet {
+    const bf16x8* hi;
+    const bf16x8* lo;
+    const float* norm;     // [rows_pad]
+    const uint32_t* idx;   // row -> point id (null: identity)
+    uint32_t m;            // valid rows
+};
+
+// sklearn kd_tree leaf predicate (exact, as engine.hip's `within`), any d.
+template <typename T, int M>
+__device__ __noinline__ bool exact_within(const T* __restrict__ X, int d, uint32_t p, uint32_t q,
+                                          double eps, double eps2) {
+    const T* a = X + (uint64_t)p * d;
+    const T* b = X + (uint64_t)q * d;
+    double acc = 0.0;
+    for (int k = 0; k < d; ++k) {
+        const double t = __dadd_rn((double)a[k], -(double)b[k]);
+        acc = M == 0 ? __dadd_rn(acc, __dmul_rn(t, t)) : __dadd_rn(acc, fabs(t));
+    }
+    return M == 0 ? (acc <= eps2) : (acc <= eps);
+}
+
+// ---------------------------------------------------------------- data prep
+// One thread per (row, k-step, lane half): 8 dims -> bf16 hi and lo.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void prep_kernel(const T* __restrict__ X, int d,
+                                                      const uint32_t* __restrict__ idx, uint32_t m,
+                                                      uint32_t rows_pad, int KS,
+                                                      const double* __restrict__ center,
+                                                      double scale, bf16x8* __restrict__ Fh,
+                                                      bf16x8* __restrict__ Fl) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= (uint64_t)rows_pad * KS * 2) return;
+    const int h = (int)(t & 1);
+    const int s = (int)((t >> 1) % KS);
+    const uint32_t r = (uint32_t)((t >> 1) / KS);
+    bf16x8 vh, vl;
+    const uint32_t p = r < m ? (idx ? idx[r] : r) : 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = 16 * s + 8 * h + j;
+        float v = 0.0f;
+        if (r < m && k < d) v = (float)(((double)X[(uint64_t)p * d + k] - center[k]) * scale);
+        const __bf16 bh = (__bf16)v;
+        vh[j] = bh;
+        vl[j] = (__bf16)(v - (float)bh);
+    }
+    const uint64_t o = ((uint64_t)(r >> 5) * KS + s) * 64 + 32 * h + (r & 31);
+    Fh[o] = vh;
+    Fl[o] = vl;
+}
+
+// |v|^2 of the scaled fp32 coordinates (the values the fragments split).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void norm_kernel(const T* __restrict__ X, int d,
+                                                      const uint32_t* __restrict__ idx, uint32_t m,
+                                                      uint32_t rows_pad,
+                                                      const double* __restrict__ center,
+                                                      double scale, float* __restrict__ norm) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= rows_pad) return;
+    if (r >= m) {
+        norm[r] = kPadNorm;
+        return;
+    }
+    const uint32_t p = idx ? idx[r] : r;
+    double acc = 0.0;
+    for (int k = 0; k < d; ++k) {
+        const double v = (double)(float)(((double)X[(uint64_t)p * d + k] - center[k]) * scale);
+        acc += v * v;
+    }
+    norm[r] = (float)acc;
+}
+
+// ---------------------------------------------------------------- tiles
+template <typename T>
+struct TileArgs {
+    FragSet I, J;
+    const T* X;
+    int d;
+    double eps, eps2;      // exact predicate, caller's units
+    float elo, ehi;        // scaled eps^2 thresholds, rounded outward
+    uint32_t* cnt;         // kCount: neighbours per I row
+    uint32_t* par;         // kLink: union-find over the (I = J) rows
+    const uint32_t* keyJ;  // kBorder: cluster key per J row
+    uint32_t* best;        // kBorder: smallest adjacent key per I row
+};
+
+template <typename T, int MODE>
+__device__ __forceinline__ void tile_hit(const TileArgs<T>& A, uint32_t i, uint32_t j, uint32_t& cnt,
+                                         uint32_t& best) {
+    if constexpr (MODE == kCount) {
+        ++cnt;
+    } else if constexpr (MODE == kLink) {
+        uf_unite(A.par, i, j);
+    } else {
+        const uint32_t k = A.keyJ[j];
+        best = k < best ? k : best;
+    }
+}
+
+template <typename T, int MODE, int KS>
+__global__ __launch_bounds__(kBlock) void tile_kernel(TileArgs<T> A) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t i0 = (xcd_block(blockIdx.x, gridDim.x) * (kBlock / 64) + wave) * kTile;
+    if (i0 >= A.I.m) return;
+    const int col = lane & 31, h = lane >> 5;
+    // the wave's 64 query points: B operand fragments, kept in registers
+    bf16x8 bh[2][KS], bl[2][KS];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const uint64_t o = ((uint64_t)(i0 / 32 + t) * KS + s) * 64 + lane;
+            bh[t][s] = A.I.hi[o];
+            bl[t][s] = A.I.lo[o];
+        }
+    uint32_t iq[2];
+    float nI[2];
+    bool ok[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        iq[t] = i0 + 32 * t + col;
+        nI[t] = A.I.norm[iq[t]];
+        ok[t] = iq[t] < A.I.m;
+    }
+    uint32_t cnt[2] = {0u, 0u}, best[2] = {kNone, kNone};
+    // link: only j > i, so start at the diagonal tile
+    const uint32_t jbeg = MODE == kLink ? i0 : 0u;
+    for (uint32_t j0 = jbeg; j0 < A.J.m; j0 += kTile) {
+        f32x16 acc[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[u][t][e] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            bf16x8 ah[2], al[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint64_t o = ((uint64_t)(j0 / 32 + u) * KS + s) * 64 + lane;
+                ah[u] = A.J.hi[o];
+                al[u] = A.J.lo[o];
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bh[t][s], acc[u][t],
+                                                                        0, 0, 0);
+                    acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bl[t][s], acc[u][t],
+                                                                        0, 0, 0);
+                    acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[u], bh[t][s], acc[u][t],
+                                                                        0, 0, 0);
+                }
+        }
+        // epilogue: decide each pair from d2~ and the band; recheck the band
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t jr = j0 + 32 * u + 8 * q + 4 * h;
+                const float4 nj = *reinterpret_cast<const float4*>(A.J.norm + jr);
+                const float njv[4] = {nj.x, nj.y, nj.z, nj.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint32_t j = jr + e;
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const float sn = nI[t] + njv[e];
+                        const float d2 = sn - 2.0f * acc[u][t][4 * q + e];
+                        const float dl = kBandC * sn;
+                        bool in = d2 + dl <= A.elo;
+                        const bool maybe = d2 - dl <= A.ehi;
+                        if (MODE == kLink && j <= iq[t]) in = false;
+                        else if (maybe && !in && ok[t] && j < A.J.m) {
+                            const uint32_t p = A.I.idx ? A.I.idx[iq[t]] : iq[t];
+                            const uint32_t qj = A.J.idx ? A.J.idx[j] : j;
+                            in = exact_within<T, 0>(A.X, A.d, p, qj, A.eps, A.eps2);
+                        }
+                        if (in) tile_hit<T, MODE>(A, iq[t], j, cnt[t], best[t]);
+                    }
+                }
+            }
+    }
+    // lanes l and l + 32 hold the same query column
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        if constexpr (MODE == kCount) {
+            cnt[t] += (uint32_t)__shfl_xor((int)cnt[t], 32, 64);
+            if (h == 0 && ok[t]) A.cnt[iq[t]] = cnt[t];
+        } else if constexpr (MODE == kBorder) {
+            const uint32_t o = (uint32_t)__shfl_xor((int)best[t], 32, 64);
+            best[t] = o < best[t] ? o : best[t];
+            if (h == 0 && ok[t]) A.best[iq[t]] = best[t];
+        }
+    }
+}
+
+// Exact fp64 VALU tiles (cityblock; euclidean with d > 128 or an extreme
+// scale): one lane per query, the streamed point broadcast to the wave.
+template <typename T, int MODE, int M>
+__global__ __launch_bounds__(kBlock) void brute_kernel(TileArgs<T> A) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const bool ok = i < A.I.m;
+    const uint32_t p = ok ? (A.I.idx ? A.I.idx[i] : i) : 0u;
+    uint32_t cnt = 0, best = kNone;
+    const uint32_t jbeg = MODE == kLink ? __builtin_amdgcn_readfirstlane(blockIdx.x * kBlock) : 0u;
+    for (uint32_t j = jbeg; j < A.J.m; ++j) {
+        if (!ok || (MODE == kLink && j <= i)) continue;
+        const uint32_t q = A.J.idx ? A.J.idx[j] : j;
+        if (exact_within<T, M>(A.X, A.d, p, q, A.eps, A.eps2)) tile_hit<T, MODE>(A, i, j, cnt, best);
+    }
+    if (!ok) return;
+    if constexpr (MODE == kCount) A.cnt[i] = cnt;
+    if constexpr (MODE == kBorder) A.best[i] = best;
+}
+
+// ---------------------------------------------------------------- small kernels
+__global__ __launch_bounds__(kBlock) void iota_kernel(uint32_t* __restrict__ p, uint32_t m) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k < m) p[k] = k;
+}
+
+__global__ __launch_bounds__(kBlock) void flatten_keys_kernel(uint32_t* __restrict__ par,
+                                                              const uint32_t* __restrict__ list,
+                                                              uint32_t m,
+                                                              uint32_t* __restrict__ keyc,
+                                                              uint32_t* __restrict__ key_out) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= m) return;
+    // root = smallest core row of the component = smallest core point id
+    // (the list is ascending): sklearn's cluster order (engine.hip gmin)
+    const uint32_t key = list[uf_find(par, k)];
+    keyc[k] = key;
+    key_out[list[k]] = key;
+}
+
+__global__ __launch_bounds__(kBlock) void scatter_best_kernel(const uint32_t* __restrict__ best,
+                                                              const uint32_t* __restrict__ list,
+                                                              uint32_t m,
+                                                              uint32_t* __restrict__ key_out) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    if (b < m) key_out[list[b]] = best[b];
+}
+
+__global__ __launch_bounds__(kBlock) void outputs_kernel(const uint32_t* __restrict__ cnt,
+                                                         uint64_t n, uint32_t ms, int full,
+                                                         uint8_t* __restrict__ core,
+                                                         uint32_t* __restrict__ counts) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = cnt[i];
+    if (core) core[i] = c >= ms ? 1 : 0;
+    if (counts) counts[i] = full ? c : (c < ms ? c : ms);
+}
+
+struct CntAtLeast {
+    const uint32_t* cnt;
+    uint32_t v;
+    __device__ bool operator()(uint32_t i) const { return cnt[i] >= v; }
+};
+struct BorderCand {   // not core, a neighbour besides itself
+    const uint32_t* cnt;
+    uint32_t ms;
+    __device__ bool operator()(uint32_t i) const { return cnt[i] >= 2 && cnt[i] < ms; }
+};
+
+template <typename Pred>
+uint32_t select_ids(Ctx& ctx, const char* name, uint32_t n, Pred pred, uint32_t** out,
+                    hipStream_t s) {
+    uint32_t* list = ctx.arena.get<uint32_t>(name, n);
+    uint32_t* dcount = ctx.arena.get<uint32_t>("dsel_count", 4);
+    rocprim::counting_iterator<uint32_t> it(0u);
+    size_t tb = 0;
+    PD_HIP(rocprim::select(nullptr, tb, it, list, dcount, (size_t)n, pred, s));
+    void* tmp = ctx.arena.get<char>("dsel_tmp", tb);
+    PD_HIP(rocprim::select(tmp, tb, it, list, dcount, (size_t)n, pred, s));
+    uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+    PD_HIP(hipMemcpyAsync(h, dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    sync(s);
+    *out = list;
+    return *h;
+}
+
+// ---------------------------------------------------------------- driver
+struct Geometry {
+    int KS = 1;            // k-steps of 16 dims (1, 2, 4 or 8)
+    double* center = nullptr;
+    double scale = 1.0;
+    float elo = 0, ehi = 0;
+    bool mfma = false;
+};
+
+template <typename T>
+FragSet make_frags(Ctx& ctx, const std::string& tag, const T* X, int d, const uint32_t* idx,
+                   uint32_t m, const Geometry& G, hipStream_t s) {
+    const uint32_t rp = pad_rows(m ? m : 1);
+    FragSet F;
+    F.m = m;
+    F.idx = idx;
+    if (!G.mfma) {
+        F.hi = F.lo = nullptr;
+        F.norm = nullptr;
+        return F;
+    }
+    const size_t nfrag = (size_t)(rp / 32) * G.KS * 64;
+    bf16x8* hi = ctx.arena.get<bf16x8>(tag + "_hi", nfrag);
+    bf16x8* lo = ctx.arena.get<bf16x8>(tag + "_lo", nfrag);
+    float* nrm = ctx.arena.get<float>(tag + "_norm", rp);
+    hipLaunchKernelGGL(prep_kernel<T>, dim3(nblocks((uint64_t)rp * G.KS * 2)), dim3(kBlock), 0, s,
+                       X, d, idx, m, rp, G.KS, G.center, G.scale, hi, lo);
+    hipLaunchKernelGGL(norm_kernel<T>, dim3(nblocks(rp)), dim3(kBlock), 0, s, X, d, idx, m, rp,
+                       G.center, G.scale, nrm);
+    PD_HIP(hipGetLastError());
+    F.hi = hi;
+    F.lo = lo;
+    F.norm = nrm;
+    return F;
+}
+
+template <typename T, int MODE>
+void run_tiles(const TileArgs<T>& A, const Geometry& G, int metric, hipStream_t s) {
+    if (A.I.m == 0 || A.J.m == 0) return;
+    if (G.mfma) {
+        const unsigned waves = (A.I.m + kTile - 1) / kTile;
+        const dim3 grid(nblocks(waves, kBlock / 64));
+        switch (G.KS) {
+            case 1: hipLaunchKernelGGL((tile_kernel<T, MODE, 1>), grid, dim3(kBlock), 0, s, A); break;
+            case 2: hipLaunchKernelGGL((tile_kernel<T, MODE, 2>), grid, dim3(kBlock), 0, s, A); break;
+            case 4: hipLaunchKernelGGL((tile_kernel<T, MODE, 4>), grid, dim3(kBlock), 0, s, A); break;
+            default: hipLaunchKernelGGL((tile_kernel<T, MODE, 8>), grid, dim3(kBlock), 0, s, A);
+        }
+    } else if (metric == 0) {
+        hipLaunchKernelGGL((brute_kernel<T, MODE, 0>), dim3(nblocks(A.I.m)), dim3(kBlock), 0, s, A);
+    } else {
+        hipLaunchKernelGGL((brute_kernel<T, MODE, 1>), dim3(nblocks(A.I.m)), dim3(kBlock), 0, s, A);
+    }
+    PD_HIP(hipGetLastError());
+}
+
+struct Ev {
+    Ctx& ctx;
+    hipStream_t s;
+    int k = 0;
+    Ev(Ctx& c, hipStream_t st) : ctx(c), s(st) {}
+    void mark() {
+        if (!ctx.timing) return;
+        if (!ctx.ev[k]) PD_HIP(hipEventCreate(&ctx.ev[k]));
+        PD_HIP(hipEventRecord(ctx.ev[k], s));
+        ++k;
+    }
+    float span(int a, int b) {
+        if (!ctx.timing || b >= k) return 0;
+        float ms = 0;
+        PD_HIP(hipEventElapsedTime(&ms, ctx.ev[a], ctx.ev[b]));
+        return ms;
+    }
+};
+
+template <typename T>
+void run_dense(Ctx& ctx, TrainArgs& a) {
+    hipStream_t s = a.stream;
+    const T* X = (const T*)a.X;
+    const uint32_t n = (uint32_t)a.n;
+    const int d = a.d;
+    const uint32_t ms = (uint32_t)a.min_samples;
+    Ev ev(ctx, s);
+    ev.mark();   // 0
+
+    // geometry: centre on the bbox midpoint, scale by a power of two
+    Geometry G;
+    G.KS = d <= 16 ? 1 : d <= 32 ? 2 : d <= 64 ? 4 : 8;
+    std::vector<double> hc(d);
+    double span = 0.0;
+    for (int k = 0; k < d; ++k) {
+        const double lo = a.data_box[k], hi = a.data_box[d + k];
+        hc[k] = 0.5 * lo + 0.5 * hi;
+        span = std::max(span, std::max(std::fabs(lo - hc[k]), std::fabs(hi - hc[k])));
+    }
+    int e2 = 0;
+    if (span > 0.0) std::frexp(span, &e2);
+    G.scale = std::ldexp(1.0, -e2);   // max |scaled coordinate| in [0.5, 1]
+    const double eps2 = a.eps * a.eps;
+    const double eps2s = eps2 * G.scale * G.scale;
+    G.mfma = a.metric == 0 && d <= 128 && std::isfinite(eps2s) && eps2s > 1e-30 && eps2s < 1e30;
+    if (G.mfma) {
+        G.elo = std::nextafter((float)(eps2s * (1.0 - 1.0 / 1048576.0)), 0.0f);
+        G.ehi = std::nextafter((float)(eps2s * (1.0 + 1.0 / 1048576.0)), INFINITY);
+        G.center = ctx.arena.get<double>("dn_center", d);
+        double* h = (double*)pinned(ctx, sizeof(double) * d);
+        std::memcpy(h, hc.data(), sizeof(double) * d);
+        PD_HIP(hipMemcpyAsync(G.center, h, sizeof(double) * d, hipMemcpyHostToDevice, s));
+    }
+    TileArgs<T> A{};
+    A.X = X;
+    A.d = d;
+    A.eps = a.eps;
+    A.eps2 = eps2;
+    A.elo = G.elo;
+    A.ehi = G.ehi;
+
+    // ---- neighbour counts (all x all)
+    const FragSet Fall = make_frags<T>(ctx, "dn_all", X, d, nullptr, n, G, s);
+    uint32_t* cnt = ctx.arena.get<uint32_t>("dn_cnt", n);
+    A.I = A.J = Fall;
+    A.cnt = cnt;
+    run_tiles<T, kCount>(A, G, a.metric, s);
+    ev.mark();   // 1
+
+    // ---- core-core components
+    uint32_t* clist = nullptr;
+    const uint32_t mc = select_ids(ctx, "dn_core", n, CntAtLeast{cnt, ms}, &clist, s);
+    uint32_t* par = ctx.arena.get<uint32_t>("dn_par", mc + 1);
+    uint32_t* keyc = ctx.arena.get<uint32_t>("dn_keyc", mc + 1);
+    uint32_t* key_out = ctx.arena.get<uint32_t>("dn_key", n);
+    PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
+    FragSet Fcore{};
+    if (mc) {
+        hipLaunchKernelGGL(iota_kernel, dim3(nblocks(mc)), dim3(kBlock), 0, s, par, mc);
+        Fcore = make_frags<T>(ctx, "dn_cf", X, d, clist, mc, G, s);
+        A.I = A.J = Fcore;
+        A.par = par;
+        run_tiles<T, kLink>(A, G, a.metric, s);
+        hipLaunchKernelGGL(flatten_keys_kernel, dim3(nblocks(mc)), dim3(kBlock), 0, s, par, clist,
+                           mc, keyc, key_out);
+        PD_HIP(hipGetLastError());
+    }
+    ev.mark();   // 2
+
+    // ---- border points: smallest key among the core neighbours
+    if (mc) {
+        uint32_t* blist = nullptr;
+        const uint32_t mb = select_ids(ctx, "dn_border", n, BorderCand{cnt, ms}, &blist, s);
+        if (mb) {
+            uint32_t* best = ctx.arena.get<uint32_t>("dn_best", mb);
+            A.I = make_frags<T>(ctx, "dn_bf", X, d, blist, mb, G, s);
+            A.J = Fcore;
+            A.keyJ = keyc;
+            A.best = best;
+            run_tiles<T, kBorder>(A, G, a.metric, s);
+            hipLaunchKernelGGL(scatter_best_kernel, dim3(nblocks(mb)), dim3(kBlock), 0, s, best,
+                               blist, mb, key_out);
+            PD_HIP(hipGetLastError());
+        }
+    }
+    ev.mark();   // 3
+
+    // ---- outputs and labels
+    hipLaunchKernelGGL(outputs_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, cnt, (uint64_t)n, ms,
+                       ctx.full_counts ? 1 : 0, a.core, a.counts);
+    rank_labels_async(ctx, key_out, n, a.labels, s);
+    ev.mark();   // 4
+    a.n_clusters = rank_labels_count(ctx, s);
+    ctx.t.records = n;
+    ctx.t.core_records = mc;
+    ctx.t.cells_n = 0;
+    ctx.t.grid_cells = 0;
+    if (ctx.timing) {
+        ctx.t.count = ev.span(0, 1);
+        ctx.t.link = ev.span(1, 2);
+        ctx.t.border = ev.span(2, 3);
+        ctx.t.label = ev.span(3, 4);
+        ctx.t.total = ev.span(0, 4);
+    }
+}
+
+}  // namespace
+
+void dense_train(Ctx& ctx, TrainArgs& a) {
+    if (a.phase != 0)
+        throw Error(-5, "the sharded train is built for d <= 4 only (dense tiles are single-device)");
+    if (!a.data_box) throw Error(-1, "dense path needs the data bbox");
+    if (a.n >= 0xFFFFFFFFll) throw Error(-5, "dense path: n must be < 2^32 - 1");
+    ctx.st.valid = false;
+    if (a.dtype == 0)
+        run_dense<float>(ctx, a);
+    else if (a.dtype == 1)
+        run_dense<double>(ctx, a);
+    else
+        throw Error(-1, "dtype must be 0 (float32) or 1 (float64)");
+}
+
+}  // namespace pd

@@ -39,51 +39,13 @@
 #include <vector>
 
 #include "internal.hpp"
+#include "uf.hpp"
 
 namespace pd {
 namespace {
 
 // ------------------------------------------------------------------ helpers
-__device__ __forceinline__ uint32_t ld_rlx(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_rlx(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Union-find with the invariant parent[x] <= x; links always hook the larger
-// root under the smaller, so a component's root is its minimum record and
-// every stale (older) parent value is still an ancestor — plain path halving
-// is safe without locks (ECL-CC style).
-__device__ __forceinline__ uint32_t uf_find(uint32_t* par, uint32_t x) {
-    uint32_t p = ld_rlx(par + x);
-    while (p != x) {
-        uint32_t g = ld_rlx(par + p);
-        if (g == p) return p;
-        st_rlx(par + x, g);
-        x = g;
-        p = ld_rlx(par + x);
-    }
-    return x;
-}
-
-__device__ __forceinline__ void uf_unite(uint32_t* par, uint32_t a, uint32_t b) {
-    a = uf_find(par, a);
-    b = uf_find(par, b);
-    while (a != b) {
-        if (a > b) {
-            uint32_t t = a;
-            a = b;
-            b = t;
-        }
-        uint32_t expected = b;
-        if (__hip_atomic_compare_exchange_strong(par + b, &expected, a, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            return;
-        b = uf_find(par, expected);
-        a = uf_find(par, a);
-    }
-}
+// (union-find primitives: uf.hpp)
 
 // L1-cacheable variant for the hot link loop: workgroup-scope relaxed loads
 // compile to plain global_loads; stale values are older ancestors, which the
@@ -1587,27 +1549,9 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         return;
     }
 
-    uint32_t* rflag = ctx.arena.get<uint32_t>("rflag", n);
-    uint32_t* rnk = ctx.arena.get<uint32_t>("rnk", n);
-    int64_t* dncl = ctx.arena.get<int64_t>("ncl", 2);
-    PD_HIP(hipMemsetAsync(dncl, 0, sizeof(int64_t), s));
-    if (n) {
-        hipLaunchKernelGGL(root_flag_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key_out, n, rflag);
-        size_t tb = 0;
-        PD_HIP(rocprim::exclusive_scan(nullptr, tb, rflag, rnk, 0u, (size_t)n,
-                                       rocprim::plus<uint32_t>(), s));
-        void* tmp = ctx.arena.get<char>("scan_tmp", tb);
-        PD_HIP(rocprim::exclusive_scan(tmp, tb, rflag, rnk, 0u, (size_t)n,
-                                       rocprim::plus<uint32_t>(), s));
-        hipLaunchKernelGGL(label_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key_out, rnk, rflag,
-                           n, a.labels, dncl);
-    }
-    PD_HIP(hipGetLastError());
+    rank_labels_async(ctx, key_out, n, a.labels, s);
     tm.mark();   // 10
-    int64_t* hres = (int64_t*)pinned(ctx, sizeof(int64_t));
-    PD_HIP(hipMemcpyAsync(hres, dncl, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    sync(s);
-    a.n_clusters = hres[0];
+    a.n_clusters = rank_labels_count(ctx, s);
 }
 
 // Host-side bookkeeping after phase A (and B): cell count, stage times.
@@ -1708,6 +1652,38 @@ void run_d(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& p, uint64_t G, i
 
 }  // namespace
 
+// Labels from cluster keys (key[i] = smallest core point id of i's cluster,
+// 0xFFFFFFFF noise): a key's rank among the cluster roots (points whose key
+// is their own id) is the label — sklearn's numbering.  Async on s; the
+// cluster count is read back by rank_labels_count.
+void rank_labels_async(Ctx& ctx, const uint32_t* key, uint64_t n, int32_t* labels,
+                       hipStream_t s) {
+    uint32_t* rflag = ctx.arena.get<uint32_t>("rflag", n);
+    uint32_t* rnk = ctx.arena.get<uint32_t>("rnk", n);
+    int64_t* dncl = ctx.arena.get<int64_t>("ncl", 2);
+    PD_HIP(hipMemsetAsync(dncl, 0, sizeof(int64_t), s));
+    if (n) {
+        hipLaunchKernelGGL(root_flag_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key, n, rflag);
+        size_t tb = 0;
+        PD_HIP(rocprim::exclusive_scan(nullptr, tb, rflag, rnk, 0u, (size_t)n,
+                                       rocprim::plus<uint32_t>(), s));
+        void* tmp = ctx.arena.get<char>("scan_tmp", tb);
+        PD_HIP(rocprim::exclusive_scan(tmp, tb, rflag, rnk, 0u, (size_t)n,
+                                       rocprim::plus<uint32_t>(), s));
+        hipLaunchKernelGGL(label_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key, rnk, rflag, n,
+                           labels, dncl);
+    }
+    PD_HIP(hipGetLastError());
+}
+
+int64_t rank_labels_count(Ctx& ctx, hipStream_t s) {
+    int64_t* hres = (int64_t*)pinned(ctx, sizeof(int64_t));
+    PD_HIP(hipMemcpyAsync(hres, ctx.arena.get<int64_t>("ncl", 2), sizeof(int64_t),
+                          hipMemcpyDeviceToHost, s));
+    sync(s);
+    return hres[0];
+}
+
 void train(Ctx& ctx, TrainArgs& a) {
     if (a.phase == 2) {   // resume a sharded train after the global key merge
         PhaseState& st = ctx.st;
@@ -1725,7 +1701,6 @@ void train(Ctx& ctx, TrainArgs& a) {
     }
     ctx.st.valid = false;
     if (a.n < 0 || a.d < 1) throw Error(-1, "invalid shape");
-    if (a.d > kMaxDim) throw Error(-5, "d > 4: the dense-tile path is not built yet");
     if (!(a.eps > 0) || !std::isfinite(a.eps)) throw Error(-1, "eps must be a finite value > 0");
     if (a.min_samples < 1) throw Error(-1, "min_samples must be >= 1");
     if (a.metric != 0 && a.metric != 1) throw Error(-1, "metric must be 0 (euclidean) or 1 (cityblock)");
@@ -1733,6 +1708,27 @@ void train(Ctx& ctx, TrainArgs& a) {
     if (a.n > (int64_t)kIdMask) throw Error(-5, "n must be < 2^30 points per device");
     if (a.phase == 0 && !a.labels && a.n) throw Error(-1, "labels output is required");
     ctx.t = Timings{};
+    if (a.d > kMaxDim) {
+        // dense tiles (dense.hip): one pass over all points; the halo + merge
+        // of the neighbourhoods would reproduce exactly this global answer
+        std::vector<double> dbox(2 * (size_t)a.d);
+        if (a.data_box) {
+            std::memcpy(dbox.data(), a.data_box, sizeof(double) * 2 * a.d);
+        } else if (a.n) {
+            int64_t bad = 0;
+            bbox(ctx, a.X, a.dtype, a.n, a.d, dbox.data(), &bad, a.stream);
+            if (bad) throw Error(-1, "input contains NaN or infinity");
+        }
+        if (a.n == 0) {
+            if (a.phase == 1) throw Error(-5, "the sharded train is built for d <= 4 only");
+            a.n_clusters = 0;
+            return;
+        }
+        a.data_box = dbox.data();
+        dense_train(ctx, a);
+        a.data_box = nullptr;
+        return;
+    }
     const int d = a.d;
     double box[2 * kMaxDim];
     if (a.data_box) {

@@ -123,6 +123,11 @@ struct TrainArgs {
 };
 
 void train(Ctx& ctx, TrainArgs& a);
+// d > kMaxDim: dense distance tiles on the matrix cores (dense.hip)
+void dense_train(Ctx& ctx, TrainArgs& a);
+// labels from cluster keys (engine.hip): async, then the cluster count (syncs)
+void rank_labels_async(Ctx& ctx, const uint32_t* key, uint64_t n, int32_t* labels, hipStream_t s);
+int64_t rank_labels_count(Ctx& ctx, hipStream_t s);
 
 // KD partition stages (kd.hip)
 void bbox(Ctx& ctx, const void* X, int dtype, int64_t n, int d, double* lohi_host,

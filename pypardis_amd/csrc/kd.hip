@@ -25,10 +25,13 @@ namespace {
 constexpr int kRedBlocks = 1024;
 constexpr int kGroup = 4;   // labels per moments pass (register budget)
 
+// Point i's D consecutive coordinates starting at X (row stride ld): the
+// passes below see a d-dimensional input as chunks of <= 4 axes.
 template <typename T, int D>
-__device__ __forceinline__ void load_pt(const T* __restrict__ X, uint64_t i, double (&v)[D]) {
+__device__ __forceinline__ void load_pt(const T* __restrict__ X, uint64_t i, uint32_t ld,
+                                        double (&v)[D]) {
 #pragma unroll
-    for (int j = 0; j < D; ++j) v[j] = (double)X[i * D + j];
+    for (int j = 0; j < D; ++j) v[j] = (double)X[i * ld + j];
 }
 
 __device__ __forceinline__ double wave_sum(double x) {
@@ -50,7 +53,7 @@ __device__ __forceinline__ double wave_max(double x) {
 // ---------------------------------------------------------------- bbox
 template <typename T, int D>
 __global__ __launch_bounds__(kBlock) void bbox_kernel(const T* __restrict__ X, uint64_t n,
-                                                      double* __restrict__ part) {
+                                                      uint32_t ld, double* __restrict__ part) {
     double lo[D], hi[D];
     double bad = 0;
 #pragma unroll
@@ -61,7 +64,7 @@ __global__ __launch_bounds__(kBlock) void bbox_kernel(const T* __restrict__ X, u
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * kBlock) {
         double v[D];
-        load_pt<T, D>(X, i, v);
+        load_pt<T, D>(X, i, ld, v);
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             if (!isfinite(v[j])) bad += 1;
@@ -146,6 +149,7 @@ __device__ __forceinline__ DD wave_dd(DD a) {
 
 template <typename T, int D>
 __global__ __launch_bounds__(kBlock) void moments_kernel(const T* __restrict__ X, uint64_t n,
+                                                         uint32_t ld,
                                                          const int32_t* __restrict__ labels,
                                                          int4 sel, double* __restrict__ part) {
     double c[kGroup];
@@ -166,7 +170,7 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(const T* __restrict__ X
                 c[g] += 1.0;
 #pragma unroll
                 for (int j = 0; j < D; ++j) {
-                    const T v = X[i * D + j];
+                    const T v = X[i * ld + j];
                     const T vv = v * v;
                     dd_acc(s[g][j], (double)v);
                     dd_acc(q[g][j], (double)vv);
@@ -219,7 +223,7 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(const T* __restrict__ X
 // single slice (R:dbscan/partition.py:86-89).  O(n) serial per lane: a
 // compatibility mode for bit-identical split boundaries, not the fast path.
 template <typename T, int D>
-__global__ void moments_seq_kernel(const T* __restrict__ X, uint64_t n,
+__global__ void moments_seq_kernel(const T* __restrict__ X, uint64_t n, uint32_t ld,
                                    const int32_t* __restrict__ labels, int4 sel,
                                    double* __restrict__ out) {
     const int lane = threadIdx.x;
@@ -229,7 +233,7 @@ __global__ void moments_seq_kernel(const T* __restrict__ X, uint64_t n,
     double acc = 0.0, cnt = 0.0;
     for (uint64_t i = 0; i < n; ++i) {
         if (labels[i] != want) continue;
-        const T v = X[i * D + j];
+        const T v = X[i * ld + j];
         const T vv = v * v;
         acc = acc + (sq ? (double)vv : (double)v);
         cnt += 1.0;
@@ -242,35 +246,54 @@ __global__ void moments_seq_kernel(const T* __restrict__ X, uint64_t n,
 }
 
 // ---------------------------------------------------------------- counts
-// counts[slot][i] = #points of the slot's label with v[axis] < bounds[slot][i]
-template <typename T, int D>
+// counts[slot][i] = #points of the slot's label with v[axis] < bounds[slot][i].
+// mono (every slot's bounds non-decreasing, as mean + (i-3)*0.3*std is for
+// std >= 0, or all NaN): v < b_i holds exactly for i >= 7 - c with c = #true,
+// so one histogram bump of c per point carries all seven answers (the host
+// sums the tail); the histograms are replicated per lane & (kRep-1) so a wave
+// spreads its LDS atomics.  !mono: one atomic per true compare.
+constexpr int kRep = 8;
+
+template <typename T>
 __global__ __launch_bounds__(kBlock) void counts_kernel(
-    const T* __restrict__ X, uint64_t n, const int32_t* __restrict__ labels,
+    const T* __restrict__ X, uint64_t n, uint32_t ld, const int32_t* __restrict__ labels,
     const int32_t* __restrict__ slot_of, int n_label_tab, const int32_t* __restrict__ axis,
-    const double* __restrict__ bounds, int n_sel, unsigned long long* __restrict__ out) {
-    extern __shared__ unsigned int lcnt[];   // n_sel * 8
-    for (int k = threadIdx.x; k < n_sel * 8; k += kBlock) lcnt[k] = 0;
+    const double* __restrict__ bounds, int n_sel, int mono, int rep,
+    unsigned long long* __restrict__ out) {
+    extern __shared__ unsigned int lcnt[];   // rep * n_sel * 8
+    for (int k = threadIdx.x; k < rep * n_sel * 8; k += kBlock) lcnt[k] = 0;
     __syncthreads();
+    unsigned int* mine = lcnt + (threadIdx.x & (rep - 1)) * n_sel * 8;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * kBlock) {
         const int lab = labels[i];
         if (lab < 0 || lab >= n_label_tab) continue;
         const int sl = slot_of[lab];
         if (sl < 0) continue;
-        const double v = (double)X[i * D + axis[sl]];
-        for (int b = 0; b < 7; ++b)
-            if (v < bounds[sl * 7 + b]) atomicAdd(&lcnt[sl * 8 + b], 1u);
-        atomicAdd(&lcnt[sl * 8 + 7], 1u);
+        const double v = (double)X[i * ld + axis[sl]];
+        if (mono) {
+            int c = 0;
+#pragma unroll
+            for (int b = 0; b < 7; ++b) c += v < bounds[sl * 7 + b] ? 1 : 0;
+            atomicAdd(&mine[sl * 8 + c], 1u);
+        } else {
+            for (int b = 0; b < 7; ++b)
+                if (v < bounds[sl * 7 + b]) atomicAdd(&mine[sl * 8 + b], 1u);
+            atomicAdd(&mine[sl * 8 + 7], 1u);
+        }
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < n_sel * 8; k += kBlock)
-        if (lcnt[k]) atomicAdd(&out[k], (unsigned long long)lcnt[k]);
+    for (int k = threadIdx.x; k < n_sel * 8; k += kBlock) {
+        unsigned int v = 0;
+        for (int q = 0; q < rep; ++q) v += lcnt[q * n_sel * 8 + k];
+        if (v) atomicAdd(&out[k], (unsigned long long)v);
+    }
 }
 
 // ---------------------------------------------------------------- split
-template <typename T, int D>
+template <typename T>
 __global__ __launch_bounds__(kBlock) void split_kernel(
-    const T* __restrict__ X, uint64_t n, int32_t* __restrict__ labels,
+    const T* __restrict__ X, uint64_t n, uint32_t ld, int32_t* __restrict__ labels,
     const int32_t* __restrict__ slot_of, int n_label_tab, const int32_t* __restrict__ axis,
     const double* __restrict__ boundary, const int32_t* __restrict__ newlab) {
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
@@ -279,7 +302,7 @@ __global__ __launch_bounds__(kBlock) void split_kernel(
         if (lab < 0 || lab >= n_label_tab) continue;
         const int sl = slot_of[lab];
         if (sl < 0) continue;
-        const double v = (double)X[i * D + axis[sl]];
+        const double v = (double)X[i * ld + axis[sl]];
         if (v >= boundary[sl]) labels[i] = newlab[sl];
     }
 }
@@ -297,9 +320,9 @@ __device__ __forceinline__ uint64_t order_key(double v) {
     return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
 
-template <typename T, int D>
+template <typename T>
 __global__ __launch_bounds__(kBlock) void radix_hist_kernel(
-    const T* __restrict__ X, uint64_t n, const int32_t* __restrict__ labels,
+    const T* __restrict__ X, uint64_t n, uint32_t ld, const int32_t* __restrict__ labels,
     const int32_t* __restrict__ slot_of, int n_label_tab, const int32_t* __restrict__ axis,
     const uint64_t* __restrict__ prefix, int shift, int n_sel, int lds,
     unsigned int* __restrict__ out) {
@@ -316,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void radix_hist_kernel(
         if (lab < 0 || lab >= n_label_tab) continue;
         const int sl = slot_of[lab];
         if (sl < 0) continue;
-        const uint64_t key = order_key((double)X[i * D + axis[sl]]);
+        const uint64_t key = order_key((double)X[i * ld + axis[sl]]);
         if (top < 64 && (key >> top) != prefix[sl]) continue;
         atomicAdd(&h[sl * 256 + (int)((key >> shift) & 255u)], 1u);
     }
@@ -343,25 +366,50 @@ struct InBox {
     }
 };
 
-template <int D, typename F>
+// Any d (the dense high-dimensional path): runtime loop over the axes.
+template <typename T>
+struct InBoxDyn {
+    const T* X;
+    const double* box;   // lo[d], hi[d]
+    int d;
+    __device__ bool operator()(int64_t i) const {
+        bool in = true;
+        for (int j = 0; j < d; ++j) {
+            const double v = (double)X[i * d + j];
+            in &= (box[j] <= v) & (box[d + j] >= v);
+        }
+        return in;
+    }
+};
+
+template <typename F>
 void dispatch_d(int d, F&& f) {
     switch (d) {
         case 1: f(std::integral_constant<int, 1>{}); break;
         case 2: f(std::integral_constant<int, 2>{}); break;
         case 3: f(std::integral_constant<int, 3>{}); break;
         case 4: f(std::integral_constant<int, 4>{}); break;
-        default: throw Error(-5, "dimension " + std::to_string(d) + " > 4 not supported yet");
+        default: throw Error(-1, "axis chunk must have 1..4 axes");
     }
 }
 
 template <typename F>
-void dispatch(int dtype, int d, F&& f) {
+void dispatch_t(int dtype, F&& f) {
     if (dtype == 0)
-        dispatch_d<0>(d, [&](auto D) { f((float*)nullptr, D); });
+        f((float*)nullptr);
     else if (dtype == 1)
-        dispatch_d<0>(d, [&](auto D) { f((double*)nullptr, D); });
+        f((double*)nullptr);
     else
         throw Error(-1, "dtype must be 0 (float32) or 1 (float64)");
+}
+
+// f(T*, D, a0) for each chunk of <= 4 consecutive axes [a0, a0 + D).
+template <typename F>
+void dispatch_chunks(int dtype, int d, F&& f) {
+    dispatch_t(dtype, [&](auto tp) {
+        for (int a0 = 0; a0 < d; a0 += 4)
+            dispatch_d(std::min(4, d - a0), [&](auto Dc) { f(tp, Dc, a0); });
+    });
 }
 
 struct LabelTables {
@@ -410,86 +458,94 @@ LabelTables upload_tables(Ctx& ctx, int n_sel, const int32_t* sel, const int32_t
 void bbox(Ctx& ctx, const void* X, int dtype, int64_t n, int d, double* lohi, int64_t* bad,
           hipStream_t s) {
     const int nb = (int)std::min<int64_t>(kRedBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
-    const int W = 2 * d + 1;
-    double* part = ctx.arena.get<double>("bbox_part", (size_t)nb * W);
-    dispatch(dtype, d, [&](auto tp, auto Dc) {
+    double* part = ctx.arena.get<double>("bbox_part", (size_t)nb * 9);
+    double nbad = 0;
+    dispatch_chunks(dtype, d, [&](auto tp, auto Dc, int a0) {
         using T = std::remove_pointer_t<decltype(tp)>;
         constexpr int D = decltype(Dc)::value;
-        hipLaunchKernelGGL((bbox_kernel<T, D>), dim3(nb), dim3(kBlock), 0, s, (const T*)X,
-                           (uint64_t)n, part);
-    });
-    PD_HIP(hipGetLastError());
-    double* h = (double*)pinned(ctx, sizeof(double) * nb * W);
-    PD_HIP(hipMemcpyAsync(h, part, sizeof(double) * nb * W, hipMemcpyDeviceToHost, s));
-    sync(s);
-    double nbad = 0;
-    for (int j = 0; j < d; ++j) {
-        double a = INFINITY, b = -INFINITY;
-        for (int k = 0; k < nb; ++k) {
-            a = std::fmin(a, h[k * W + j]);
-            b = std::fmax(b, h[k * W + d + j]);
+        constexpr int W = 2 * D + 1;
+        hipLaunchKernelGGL((bbox_kernel<T, D>), dim3(nb), dim3(kBlock), 0, s, (const T*)X + a0,
+                           (uint64_t)n, (uint32_t)d, part);
+        PD_HIP(hipGetLastError());
+        double* h = (double*)pinned(ctx, sizeof(double) * nb * W);
+        PD_HIP(hipMemcpyAsync(h, part, sizeof(double) * nb * W, hipMemcpyDeviceToHost, s));
+        sync(s);
+        for (int j = 0; j < D; ++j) {
+            double lo = INFINITY, hi = -INFINITY;
+            for (int k = 0; k < nb; ++k) {
+                lo = std::fmin(lo, h[k * W + j]);
+                hi = std::fmax(hi, h[k * W + D + j]);
+            }
+            lohi[a0 + j] = lo;
+            lohi[d + a0 + j] = hi;
         }
-        lohi[j] = a;
-        lohi[d + j] = b;
-    }
-    for (int k = 0; k < nb; ++k) nbad += h[k * W + 2 * d];
+        for (int k = 0; k < nb; ++k) nbad += h[k * W + 2 * D];
+    });
     if (bad) *bad = (int64_t)nbad;
 }
 
 namespace {
+// Moments of the selected labels, kGroup labels x <= 4 axes per pass.
 void moments_impl(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                   int n_sel, const int32_t* sel, double* out, bool dd_out, hipStream_t s) {
     const int nb = (int)std::min<int64_t>(kRedBlocks, std::max<int64_t>(1, (n + kBlock - 1) / kBlock));
-    const int G = 1 + 4 * d;
-    const int W = kGroup * G;
+    const int nbk = ctx.seq_moments ? 1 : nb;
+    const int Gd = 1 + 4 * d;
+    double* part = ctx.arena.get<double>("mom_part", (size_t)nb * kGroup * (1 + 4 * 4));
     for (int g0 = 0; g0 < n_sel; g0 += kGroup) {
         int4 sl = make_int4(-2, -2, -2, -2);
         int* sp = &sl.x;
         for (int g = 0; g < kGroup && g0 + g < n_sel; ++g) sp[g] = sel[g0 + g];
-        double* part = ctx.arena.get<double>("mom_part", (size_t)nb * W);
-        const int nbk = ctx.seq_moments ? 1 : nb;
-        dispatch(dtype, d, [&](auto tp, auto Dc) {
+        // per label of the group: count, dd sums and dd sums of squares per axis
+        std::vector<double> cnt(kGroup, 0.0);
+        std::vector<DD> sum((size_t)kGroup * d, DD{0.0, 0.0}), sq((size_t)kGroup * d, DD{0.0, 0.0});
+        dispatch_chunks(dtype, d, [&](auto tp, auto Dc, int a0) {
             using T = std::remove_pointer_t<decltype(tp)>;
             constexpr int D = decltype(Dc)::value;
+            constexpr int G = 1 + 4 * D;
+            constexpr int W = kGroup * G;
             if (ctx.seq_moments)
                 hipLaunchKernelGGL((moments_seq_kernel<T, D>), dim3(1), dim3(64), 0, s,
-                                   (const T*)X, (uint64_t)n, labels, sl, part);
+                                   (const T*)X + a0, (uint64_t)n, (uint32_t)d, labels, sl, part);
             else
                 hipLaunchKernelGGL((moments_kernel<T, D>), dim3(nb), dim3(kBlock), 0, s,
-                                   (const T*)X, (uint64_t)n, labels, sl, part);
+                                   (const T*)X + a0, (uint64_t)n, (uint32_t)d, labels, sl, part);
+            PD_HIP(hipGetLastError());
+            double* h = (double*)pinned(ctx, sizeof(double) * nbk * W);
+            PD_HIP(hipMemcpyAsync(h, part, sizeof(double) * nbk * W, hipMemcpyDeviceToHost, s));
+            sync(s);
+            for (int g = 0; g < kGroup; ++g)
+                for (int k = 0; k < nbk; ++k) {
+                    const double* p = h + (size_t)k * W + g * G;
+                    if (a0 == 0) cnt[g] += p[0];
+                    for (int j = 0; j < D; ++j) {
+                        DD& su = sum[(size_t)g * d + a0 + j];
+                        DD& sqq = sq[(size_t)g * d + a0 + j];
+                        su = dd_add(su, DD{p[1 + 2 * j], p[2 + 2 * j]});
+                        sqq = dd_add(sqq, DD{p[1 + 2 * D + 2 * j], p[2 + 2 * D + 2 * j]});
+                    }
+                }
         });
-        PD_HIP(hipGetLastError());
-        double* h = (double*)pinned(ctx, sizeof(double) * nbk * W);
-        PD_HIP(hipMemcpyAsync(h, part, sizeof(double) * nbk * W, hipMemcpyDeviceToHost, s));
-        sync(s);
         for (int g = 0; g < kGroup && g0 + g < n_sel; ++g) {
             // out layout per selected label: [3][d] = count row, sum row, sumsq row;
             // dd_out: [1 + 4d] = count, (hi, lo) per axis of the sums, then of the squares
-            double* o = out + (size_t)(g0 + g) * (dd_out ? G : 3 * d);
-            double cnt = 0;
-            std::vector<DD> sum(d, DD{0.0, 0.0}), sq(d, DD{0.0, 0.0});
-            for (int k = 0; k < nbk; ++k) {
-                const double* p = h + (size_t)k * W + g * G;
-                cnt += p[0];
-                for (int j = 0; j < d; ++j) {
-                    sum[j] = dd_add(sum[j], DD{p[1 + 2 * j], p[2 + 2 * j]});
-                    sq[j] = dd_add(sq[j], DD{p[1 + 2 * d + 2 * j], p[2 + 2 * d + 2 * j]});
-                }
-            }
+            double* o = out + (size_t)(g0 + g) * (dd_out ? Gd : 3 * d);
+            const DD* su = &sum[(size_t)g * d];
+            const DD* sqq = &sq[(size_t)g * d];
             if (dd_out) {
-                o[0] = cnt;
+                o[0] = cnt[g];
                 for (int j = 0; j < d; ++j) {
-                    o[1 + 2 * j] = sum[j].hi;
-                    o[2 + 2 * j] = sum[j].lo;
-                    o[1 + 2 * d + 2 * j] = sq[j].hi;
-                    o[2 + 2 * d + 2 * j] = sq[j].lo;
+                    o[1 + 2 * j] = su[j].hi;
+                    o[2 + 2 * j] = su[j].lo;
+                    o[1 + 2 * d + 2 * j] = sqq[j].hi;
+                    o[2 + 2 * d + 2 * j] = sqq[j].lo;
                 }
                 continue;
             }
             for (int j = 0; j < d; ++j) {
-                o[j] = cnt;
-                o[d + j] = sum[j].hi + sum[j].lo;
-                o[2 * d + j] = sq[j].hi + sq[j].lo;
+                o[j] = cnt[g];
+                o[d + j] = su[j].hi + su[j].lo;
+                o[2 * d + j] = sqq[j].hi + sqq[j].lo;
             }
         }
     }
@@ -514,20 +570,48 @@ void kd_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32
     LabelTables t = upload_tables(ctx, n_sel, sel, axis, bounds, 7, nullptr, s);
     unsigned long long* dcnt = ctx.arena.get<unsigned long long>("kd_cnt", (size_t)n_sel * 8);
     PD_HIP(hipMemsetAsync(dcnt, 0, sizeof(unsigned long long) * n_sel * 8, s));
+    bool mono = true;
+    for (int k = 0; k < n_sel; ++k) {
+        const double* b = bounds + (size_t)k * 7;
+        bool all_nan = true, ordered = true;
+        for (int i = 0; i < 7; ++i) {
+            all_nan &= std::isnan(b[i]);
+            if (i) ordered &= b[i - 1] <= b[i];
+        }
+        mono &= all_nan || ordered;
+    }
+    int rep = kRep;
+    while (rep > 1 && (size_t)rep * n_sel * 8 * sizeof(unsigned int) > 48 * 1024) rep >>= 1;
+    if ((size_t)n_sel * 8 * sizeof(unsigned int) > 60 * 1024)
+        throw Error(-5, "too many splits in one KD level (> 1920)");
     const unsigned nb = grid_for(n, 2048);
-    dispatch(dtype, d, [&](auto tp, auto Dc) {
+    dispatch_t(dtype, [&](auto tp) {
         using T = std::remove_pointer_t<decltype(tp)>;
-        constexpr int D = decltype(Dc)::value;
-        hipLaunchKernelGGL((counts_kernel<T, D>), dim3(nb), dim3(kBlock),
-                           sizeof(unsigned int) * n_sel * 8, s, (const T*)X, (uint64_t)n, labels,
-                           t.slot_of, t.ntab, t.axis, t.dbl, n_sel, dcnt);
+        hipLaunchKernelGGL((counts_kernel<T>), dim3(nb), dim3(kBlock),
+                           sizeof(unsigned int) * rep * n_sel * 8, s, (const T*)X, (uint64_t)n,
+                           (uint32_t)d, labels, t.slot_of, t.ntab, t.axis, t.dbl, n_sel,
+                           mono ? 1 : 0, rep, dcnt);
     });
     PD_HIP(hipGetLastError());
     unsigned long long* h = (unsigned long long*)pinned(ctx, sizeof(unsigned long long) * n_sel * 8);
     PD_HIP(hipMemcpyAsync(h, dcnt, sizeof(unsigned long long) * n_sel * 8, hipMemcpyDeviceToHost, s));
     sync(s);
     // out[slot][0..6] = n_less per bound, out[slot][7] = n_total
-    for (int k = 0; k < n_sel * 8; ++k) out[k] = (int64_t)h[k];
+    if (!mono) {
+        for (int k = 0; k < n_sel * 8; ++k) out[k] = (int64_t)h[k];
+        return;
+    }
+    for (int k = 0; k < n_sel; ++k) {   // h[k][c] = #points with c true compares
+        const unsigned long long* hc = h + (size_t)k * 8;
+        int64_t tot = 0;
+        for (int c = 0; c < 8; ++c) tot += (int64_t)hc[c];
+        for (int i = 0; i < 7; ++i) {
+            int64_t less = 0;
+            for (int c = 7 - i; c < 8; ++c) less += (int64_t)hc[c];
+            out[(size_t)k * 8 + i] = less;
+        }
+        out[(size_t)k * 8 + 7] = tot;
+    }
 }
 
 void kd_split(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels, int n_sel,
@@ -536,11 +620,11 @@ void kd_split(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
     if (n_sel <= 0) return;
     LabelTables t = upload_tables(ctx, n_sel, sel, axis, boundary, 1, newlab, s);
     const unsigned nb = grid_for(n, 4096);
-    dispatch(dtype, d, [&](auto tp, auto Dc) {
+    dispatch_t(dtype, [&](auto tp) {
         using T = std::remove_pointer_t<decltype(tp)>;
-        constexpr int D = decltype(Dc)::value;
-        hipLaunchKernelGGL((split_kernel<T, D>), dim3(nb), dim3(kBlock), 0, s, (const T*)X,
-                           (uint64_t)n, labels, t.slot_of, t.ntab, t.axis, t.dbl, t.newlab);
+        hipLaunchKernelGGL((split_kernel<T>), dim3(nb), dim3(kBlock), 0, s, (const T*)X,
+                           (uint64_t)n, (uint32_t)d, labels, t.slot_of, t.ntab, t.axis, t.dbl,
+                           t.newlab);
     });
     PD_HIP(hipGetLastError());
     sync(s);
@@ -557,12 +641,11 @@ void kd_radix_hist(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const i
     PD_HIP(hipMemsetAsync(dh, 0, sizeof(unsigned int) * n_sel * 256, s));
     const int lds = n_sel <= 48 ? 1 : 0;   // <= 48 KiB of LDS histograms per block
     const unsigned nb = grid_for(n, 2048);
-    dispatch(dtype, d, [&](auto tp, auto Dc) {
+    dispatch_t(dtype, [&](auto tp) {
         using T = std::remove_pointer_t<decltype(tp)>;
-        constexpr int D = decltype(Dc)::value;
-        hipLaunchKernelGGL((radix_hist_kernel<T, D>), dim3(nb), dim3(kBlock),
+        hipLaunchKernelGGL((radix_hist_kernel<T>), dim3(nb), dim3(kBlock),
                            lds ? sizeof(unsigned int) * n_sel * 256 : 0, s, (const T*)X,
-                           (uint64_t)n, labels, t.slot_of, t.ntab, t.axis,
+                           (uint64_t)n, (uint32_t)d, labels, t.slot_of, t.ntab, t.axis,
                            reinterpret_cast<const uint64_t*>(t.dbl), shift, n_sel, lds, dh);
     });
     PD_HIP(hipGetLastError());
@@ -584,15 +667,22 @@ void halo_members(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P,
     int64_t used = 0;
     for (int L = 0; L < P; ++L) {
         int64_t* outp = members ? members + used : scratch;
-        dispatch(dtype, d, [&](auto tp, auto Dc) {
-            using T = std::remove_pointer_t<decltype(tp)>;
-            constexpr int D = decltype(Dc)::value;
-            InBox<T, D> pred{(const T*)X, dbox + (size_t)L * 2 * D};
+        auto run_select = [&](auto pred) {
             rocprim::counting_iterator<int64_t> it(0);
             size_t tb = 0;
             PD_HIP(rocprim::select(nullptr, tb, it, outp, dsel, (size_t)n, pred, s));
             void* tmp = ctx.arena.get<char>("halo_tmp", tb);
             PD_HIP(rocprim::select(tmp, tb, it, outp, dsel, (size_t)n, pred, s));
+        };
+        dispatch_t(dtype, [&](auto tp) {
+            using T = std::remove_pointer_t<decltype(tp)>;
+            if (d <= kMaxDim)
+                dispatch_d(d, [&](auto Dc) {
+                    constexpr int D = decltype(Dc)::value;
+                    run_select(InBox<T, D>{(const T*)X, dbox + (size_t)L * 2 * D});
+                });
+            else
+                run_select(InBoxDyn<T>{(const T*)X, dbox + (size_t)L * 2 * d, d});
         });
         int64_t* h = (int64_t*)pinned(ctx, sizeof(int64_t));
         PD_HIP(hipMemcpyAsync(h, dsel, sizeof(int64_t), hipMemcpyDeviceToHost, s));

@@ -232,6 +232,9 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     """
     if split_method not in ('min_var', 'rotation'):
         split_method = 'min_var'   # the reference's fallback (R:dbscan/partition.py:129-130)
+    if X.dim() != 2 or X.shape[1] > 4:
+        raise NotImplementedError("the sharded train is built for d <= 4 (the dense "
+                                  "high-dimensional path runs on one device)")
     ops = ops or NativeOps(X.device)
     comm = _Comm(group, getattr(ops, "device", X.device))
     W, rank = comm.world, comm.rank

@@ -272,6 +272,11 @@ class KDPartitioner(object):
         self.max_partitions = int(max_partitions) if max_partitions is not None else 4 ** self.k
         if self.max_partitions < 1:
             raise ValueError("max_partitions must be >= 1")
+        if self.max_partitions > 1 << 16:
+            # the reference's default 4**k (R:dbscan/partition.py:132-133) is
+            # astronomically large in high dimension; it would never finish
+            raise ValueError(f"max_partitions={self.max_partitions} (> 65536; the default is "
+                             "4**k): pass max_partitions explicitly")
         lo, hi, bad = _native.bbox(X)
         if bad:
             raise ValueError("Input contains NaN or infinity.")

@@ -46,6 +46,29 @@ def c0_demo():
     return np.ascontiguousarray(StandardScaler().fit_transform(X))
 
 
+def embeddings(n, d=64, n_clusters=2000, clustered_frac=0.10, spread=0.1, seed=3,
+               dtype=np.float32, chunk=1 << 20):
+    """unit-norm embeddings.  clustered_frac·n points are
+    normalize(c_j + spread·g) around n_clusters centres c_j ~ N(0, I_d); the
+    rest are normalize(g), g ~ N(0, I_d).  Rows shuffled."""
+    n = int(n)
+    rng = np.random.default_rng(seed)
+    centers = rng.normal(size=(n_clusters, d))
+    n_cl = int(round(clustered_frac * n))
+    out = np.empty((n, d), dtype=dtype)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        g = rng.normal(size=(e - s, d))
+        k = np.arange(s, e) < n_cl
+        if k.any():
+            g[k] = centers[rng.integers(0, n_clusters, size=int(k.sum()))] + spread * g[k]
+        out[s:e] = g / np.linalg.norm(g, axis=1, keepdims=True)
+    perm = rng.permutation(n)
+    return np.ascontiguousarray(out[perm])
+
+
+C3_EPS = 0.114028   # tools/c3_eps.py: 0.11402826147489717, rounded to 6 digits
+
 # BASELINE.json configs (sizes, eps, min_samples, max_partitions)
 CONFIGS = {
     "C0": dict(n=750, d=2, eps=0.3, min_samples=10, max_partitions=None),
@@ -55,6 +78,11 @@ CONFIGS = {
     "C2": dict(n=100_000_000, d=3, side=100.0, n_centers=256, sigma=1.0,
                noise_frac=0.10, seed=2, eps=0.1, min_samples=10,
                max_partitions=8),
+    # eps: the 1st percentile over 50k sampled points of the distance to the
+    # 10th neighbour (self included) in the full 1M set, so ~1% of points are
+    # core; computed once by tools/c3_eps.py
+    "C3": dict(n=1_000_000, d=64, n_clusters=2000, clustered_frac=0.10, spread=0.1,
+               seed=3, eps=C3_EPS, min_samples=10, max_partitions=1),
 }
 
 
@@ -66,6 +94,14 @@ def make_config(name, n=None):
     cfg = dict(CONFIGS[name])
     if name == "C0":
         return c0_demo(), cfg
+    if name == "C3":   # slices keep the points per cluster: fewer clusters
+        N = cfg["n"]
+        n = N if n is None else int(n)
+        k = max(1, int(round(cfg["n_clusters"] * n / N)))
+        X = embeddings(n, cfg["d"], n_clusters=k, clustered_frac=cfg["clustered_frac"],
+                       spread=cfg["spread"], seed=cfg["seed"])
+        cfg.update(n=n, n_clusters=k)
+        return X, cfg
     N = cfg["n"]
     n = N if n is None else int(n)
     side = cfg["side"] * (n / N) ** (1.0 / cfg["d"])

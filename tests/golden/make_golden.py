@@ -24,7 +24,7 @@ Two sources of truth:
    on the fp64 upcast of each dataset, and the known-answer cases of
    SK:cluster/tests/test_dbscan.py:297-305, 376-403.
 
-Usage:  PYTHONHASHSEED=0 python tests/golden/make_golden.py
+Usage:  PYTHONHASHSEED=0 python tests/golden/make_golden.py [dataset ...]
 """
 from __future__ import annotations
 
@@ -302,6 +302,9 @@ def datasets():
     Xd = np.repeat(rng.uniform(0, 5, size=(200, 1)).astype(np.float32), 3, axis=0)
     rng.shuffle(Xd)
     out["dup_1d"] = (Xd, 0.05, 4, 4, "euclidean")
+    # 64-D unit embeddings (config C3 at 5k points: 10 clusters of ~50)
+    X6, c6 = synth.make_config("C3", n=5000)
+    out["c3_5k"] = (X6, c6["eps"], c6["min_samples"], 2, "euclidean")
     return out
 
 
@@ -343,11 +346,14 @@ def sklearn_kats():
     return res
 
 
-def main():
+def main(only=()):
     if os.environ.get("PYTHONHASHSEED") != "0":
         print("warning: run with PYTHONHASHSEED=0 for a reproducible ref_assign artefact")
-    np.savez_compressed(os.path.join(HERE, "sklearn_kat.npz"), **sklearn_kats())
+    if not only:
+        np.savez_compressed(os.path.join(HERE, "sklearn_kat.npz"), **sklearn_kats())
     for name, (X, eps, ms, P, metric) in datasets().items():
+        if only and name not in only:
+            continue
         sk_metric = "euclidean" if metric == "callable" else metric
         rec = dict(X=X, eps=np.float64(eps), min_samples=np.int64(ms),
                    max_partitions=np.int64(-1 if P is None else P),
@@ -362,4 +368,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

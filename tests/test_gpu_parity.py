@@ -468,3 +468,69 @@ def test_sharded_native_large(native, tmp_path):
     assert out["exports"] > 0
     np.testing.assert_array_equal(out["labels"], lab1.cpu().numpy().astype(np.int64))
     np.testing.assert_array_equal(out["core"], core1.cpu().numpy())
+
+
+# ------------------------------------------------------------ dense (d > 4) path
+DENSE = [
+    # (name, X builder, eps, min_samples, metric, max_partitions)
+    ("c3_30k", lambda: __import__("pypardis_amd").synth.make_config("C3", n=30_000)[0],
+     0.114028, 10, "euclidean", 1),
+    ("c3_wide_eps", lambda: __import__("pypardis_amd").synth.make_config("C3", n=8_000)[0],
+     0.9, 25, "euclidean", 3),
+    ("d5_blobs", lambda: __import__("pypardis_amd").synth.blobs_noise(
+        20_000, 5, side=6.0, n_centers=8, sigma=0.4, seed=71), 0.3, 8, "euclidean", 1),
+    ("d100_f64", lambda: __import__("pypardis_amd").synth.blobs_noise(
+        6_000, 100, side=4.0, n_centers=6, sigma=0.15, seed=72).astype(np.float64) + 1e3,
+     1.6, 5, "euclidean", 1),
+    ("d200_brute", lambda: __import__("pypardis_amd").synth.blobs_noise(
+        3_000, 200, side=3.0, n_centers=4, sigma=0.1, seed=73), 2.0, 5, "euclidean", 1),
+    ("d8_cityblock", lambda: __import__("pypardis_amd").synth.blobs_noise(
+        8_000, 8, side=5.0, n_centers=6, sigma=0.3, seed=74), 1.2, 6, "cityblock", 1),
+]
+
+
+@pytest.mark.parametrize("case", DENSE, ids=[c[0] for c in DENSE])
+def test_dense_path_matches_oracle(native, case):
+    """d > 4: split-bf16 MFMA Gram tiles with the exact fp64 band recheck (or
+    the exact VALU tile for cityblock / d > 128): neighbour counts, core flags
+    and labels bit-identical to the oracle (sklearn kd_tree semantics)."""
+    from pypardis_amd import DBSCAN
+    _, build, eps, ms, metric, P = case
+    X = np.ascontiguousarray(build())
+    lab_o, core_o, cnt_o, nc_o = oracle.dbscan(X, eps, ms, metric)
+    lab, core, ncl, cnt = _cluster(native, X, eps, ms, metric, full=True)
+    assert np.array_equal(cnt, cnt_o)
+    assert np.array_equal(core, core_o)
+    assert np.array_equal(lab, lab_o) and ncl == nc_o
+    m = DBSCAN(eps=eps, min_samples=ms, metric=metric, max_partitions=P).train(_dev(X))
+    assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)
+    assert 0 < int(core_o.sum()) < len(X)   # the case exercises core, border and noise
+
+
+def test_dense_exact_ties(native):
+    """A 6-D fp32 lattice with eps equal to the spacing: every axis neighbour
+    is an exact tie (inside the MFMA error band), decided by the fp64 recheck."""
+    g = np.arange(6, dtype=np.float32) * np.float32(0.05)
+    X = np.stack(np.meshgrid(*([g] * 6), indexing="ij"), -1).reshape(-1, 6).astype(np.float32)
+    for eps in (float(np.float32(0.05)), 0.05):
+        lab_o, core_o, cnt_o, _ = oracle.dbscan(X, eps, 7)
+        lab, core, _, cnt = _cluster(native, X, eps, 7, full=True)
+        assert np.array_equal(cnt, cnt_o), eps
+        assert np.array_equal(lab, lab_o), eps
+
+
+def test_dense_edge_cases(native):
+    from pypardis_amd import DBSCAN
+    X = np.full((300, 16), 0.25, np.float32)   # identical points
+    m = DBSCAN(eps=0.1, min_samples=5, max_partitions=2).train(_dev(X))
+    assert np.all(m.labels_.cpu().numpy() == 0)
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(700, 12)).astype(np.float32)
+    for ms in (1, 2):
+        lab_o, _, _, _ = oracle.dbscan(X, 2.5, ms)
+        lab, _, _ = _cluster(native, X, 2.5, ms)
+        assert np.array_equal(lab, lab_o), ms
+    lab, core, ncl = _cluster(native, X[:1], 0.5, 2)
+    assert ncl == 0 and lab[0] == -1
+    lab, core, ncl = _cluster(native, np.zeros((0, 12), np.float32), 0.5, 2)
+    assert ncl == 0 and len(lab) == 0

@@ -40,6 +40,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0
+MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md; no sparsity)
 
 
 def parse():
@@ -50,7 +51,8 @@ def parse():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--points", type=int, default=None, help="override point count")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-n", type=int, default=1_000_000, help="CPU baseline sample size")
+    ap.add_argument("--cpu-n", type=int, default=None,
+                    help="CPU baseline sample size (default 1M points; 20k for d > 15)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--sweep-variant", type=int, default=None,
                     help="PD_OPT_SWEEP_VARIANT override (bit 0 count, 1 link, 2 border)")
@@ -58,6 +60,10 @@ def parse():
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
     return ap.parse_args()
+
+
+def default_cpu_n(d):
+    return 20_000 if d > 15 else 1_000_000
 
 
 def b_nc(records, cells, d):
@@ -79,7 +85,7 @@ def load_pmc(kernel="count_kernel"):
         return None
 
 
-def cpu_baseline(cfg_name, n_sample):
+def cpu_baseline(cfg_name, n_sample, n_full):
     import oracle
     from oracle import cpu_ref
     from pypardis_amd import synth
@@ -87,12 +93,17 @@ def cpu_baseline(cfg_name, n_sample):
     oracle.build()
     labels, secs, workers = cpu_ref.run(X, cfg["eps"], cfg["min_samples"],
                                         cfg.get("max_partitions") or 1)
-    return {"value": n_sample / secs, "unit": "points/s", "cores": workers, "kind": "port",
-            "seconds": secs,
-            "sample": (f"{cfg_name} density-preserving slice, {n_sample} pts, "
-                       f"max_partitions={cfg.get('max_partitions')}: numpy KD + halo, "
-                       f"sklearn 1.7.2 kd_tree DBSCAN per neighbourhood in a {workers}-process "
-                       "pool (Spark local[*] emulation), owner-rule merge")}
+    out = {"value": n_sample / secs, "unit": "points/s", "cores": workers, "kind": "port",
+           "seconds": secs,
+           "sample": (f"{cfg_name} density-preserving slice, {n_sample} pts, "
+                      f"max_partitions={cfg.get('max_partitions')}: numpy KD + halo, "
+                      f"sklearn 1.7.2 DBSCAN (algorithm='auto') per neighbourhood in a "
+                      f"{workers}-process pool, 1 BLAS thread each (Spark local[*] emulation), "
+                      "owner-rule merge")}
+    if X.shape[1] > 15:   # brute force: O(n^2) work, the rate falls as 1/n
+        out["extrapolated_full_value"] = out["value"] * n_sample / n_full
+        out["sample"] += f"; brute O(n^2): at the full {n_full} pts x{n_sample / n_full:.3g}"
+    return out
 
 
 def main():
@@ -179,20 +190,44 @@ def main():
 
     if rank == 0:
         t_cnt = float(np.mean(count_ms))
-        alg_bytes, per = b_nc(rec, cells, d)
-        achieved = alg_bytes / (t_cnt * 1e-3) / 1e9
-        variant = args.sweep_variant if args.sweep_variant is not None \
-            else _native.SWEEP_VARIANT_DEFAULT
-        kname = "count2_kernel" if variant & 1 else "count_kernel"
-        pmc = load_pmc(kname)
-        traffic = pmc["bytes_per_launch"] if pmc else None
+        if d <= 4:
+            alg_bytes, per = b_nc(rec, cells, d)
+            achieved = alg_bytes / (t_cnt * 1e-3) / 1e9
+            variant = args.sweep_variant if args.sweep_variant is not None \
+                else _native.SWEEP_VARIANT_DEFAULT
+            kname = "count2_kernel" if variant & 1 else "count_kernel"
+            pmc = load_pmc(kname)
+            roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS,
+                    "traffic": pmc["bytes_per_launch"] if pmc else None, "kernel": kname,
+                    "kernel_ms": t_cnt, "bytes_per_record": per, "records": rec,
+                    "cells": cells, "algorithmic_bytes": alg_bytes}
+            dtype = "f64"
+        else:
+            # dense tiles (dense.hip): the all-pairs Gram matrix of the count
+            # pass, 2 n^2 d algorithmic flops; the MFMA executes 3 split-bf16
+            # products over the padded shape
+            ks = 1 if d <= 16 else 2 if d <= 32 else 4 if d <= 64 else 8
+            n_pad = -(-n // 64) * 64
+            alg = 2.0 * n * n * d
+            exe = 3 * 2.0 * n_pad * n_pad * 16 * ks
+            achieved = alg / (t_cnt * 1e-3) / 1e12
+            pmc = load_pmc("tile_kernel")
+            roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS,
+                    "traffic": pmc["bytes_per_launch"] if pmc else None,
+                    "kernel": "tile_kernel (count pass)", "kernel_ms": t_cnt,
+                    "algorithmic_flops": alg, "mfma_executed_flops": exe,
+                    "mfma_executed_tflops": exe / (t_cnt * 1e-3) / 1e12,
+                    "mfma_utilisation": exe / (t_cnt * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS}
+            dtype = "bf16x3 (split bf16 MFMA, fp32 accumulate) + f64 recheck"
         stages = {k: round(v / args.steps, 3) for k, v in stage_sum.items()
                   if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records")
                   and not k.startswith("s_")}
         cpu = None
         if world == 1 and not args.no_cpu:
             try:
-                cpu = cpu_baseline(args.config, min(args.cpu_n, n))
+                cpu = cpu_baseline(args.config, min(args.cpu_n or default_cpu_n(d), n), n)
             except Exception as e:   # report, never fake
                 cpu = {"value": None, "error": repr(e)}
         out = {
@@ -206,18 +241,14 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": dtype,
             "data": "synthetic",
-            "config": {"workload": f"{args.config}: blobs_noise n={n} d={d} eps={eps} "
-                                   f"min_samples={ms} max_partitions={P}",
+            "config": {"workload": f"{args.config}: {'blobs_noise' if d <= 4 else 'embeddings'} "
+                                   f"n={n} d={d} eps={eps} min_samples={ms} max_partitions={P}",
                        "n_points": n, "d": d, "eps": eps, "min_samples": ms,
                        "max_partitions": P, "input": "fp32 device-resident",
                        "parallelism": f"kd-sharded{world}" if world > 1 else "single"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "kernel": kname,
-                         "kernel_ms": t_cnt, "bytes_per_record": per, "records": rec,
-                         "cells": cells, "algorithmic_bytes": alg_bytes},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "stages_ms": stages,
             "n_clusters": ncl,

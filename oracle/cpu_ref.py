@@ -8,10 +8,12 @@ the GPU box: no JVM, and the reference never travels):
      R:dbscan/partition.py:33-183)
   2. 2·eps halo                                            (oracle.halo,
      R:dbscan/dbscan.py:136-151)
-  3. per-neighbourhood ``sklearn.cluster.DBSCAN(eps, min_samples, metric,
-     algorithm='kd_tree')`` — the reference's arithmetic engine
+  3. per-neighbourhood ``sklearn.cluster.DBSCAN(eps, min_samples, metric)``
+     with the reference's default algorithm='auto' (kd_tree for d <= 15,
+     brute GEMM above) — the reference's arithmetic engine
      (R:dbscan/dbscan.py:28-29) — one task per neighbourhood in a process
-     pool, as Spark ``local[*]`` runs ``mapPartitions``
+     pool, as Spark ``local[*]`` runs ``mapPartitions``; BLAS held to one
+     thread per task, so ``workers`` is the core count used
   4. merge: local clusters linked through points core in two neighbourhoods;
      a point takes its owner neighbourhood's label (R:dbscan/dbscan.py:153-165
      intent).
@@ -32,7 +34,9 @@ from . import halo, kd_partition
 def _sk_task(args):
     X, eps, ms, metric = args
     from sklearn.cluster import DBSCAN
-    db = DBSCAN(eps=eps, min_samples=ms, metric=metric, algorithm="kd_tree", n_jobs=1).fit(X)
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(1):
+        db = DBSCAN(eps=eps, min_samples=ms, metric=metric, algorithm="auto", n_jobs=1).fit(X)
     core = np.zeros(len(X), bool)
     core[db.core_sample_indices_] = True
     return db.labels_.astype(np.int64), core

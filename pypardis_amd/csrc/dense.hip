@@ -163,91 +163,176 @@ __device__ __forceinline__ void tile_hit(const TileArgs<T>& A, uint32_t i, uint3
     }
 }
 
+// One block = 4 waves x 64 query points; the streamed 64-point tiles of the
+// other set are shared by the 4 waves through LDS (double-buffered, the next
+// tile prefetched into registers while the current one is computed).
+//
+// Epilogue: with s = |x_i|^2 + |x_j|^2 and acc = <x_i, x_j>~,
+//   in    <=>  d2~ + c s <= elo  <=>  acc >= ((1+c)|x_i|^2 - elo)/2 + (1+c)|x_j|^2/2
+//   maybe <=>  d2~ - c s <= ehi  <=>  acc >= ((1-c)|x_i|^2 - ehi)/2 + (1-c)|x_j|^2/2
+// (column terms per lane, row terms per tile row from LDS: one add and one
+// compare each; the fp32 rounding of the rearrangement is < 2^-22 s, inside
+// the band's margin).  Band pairs (maybe && !in) are rare: collected as bits
+// and re-tested exactly after the tile.
+template <int KS>
+struct TileLds {
+    bf16x8 hi[2][2][KS][64];   // [buffer][row group][k-step][lane]
+    bf16x8 lo[2][2][KS][64];
+    float ta[2][kTile];        // (1+c)|x_j|^2 / 2
+    float tb[2][kTile];        // (1-c)|x_j|^2 / 2
+};
+
 template <typename T, int MODE, int KS>
 __global__ __launch_bounds__(kBlock) void tile_kernel(TileArgs<T> A) {
+    constexpr int NCH = 2 * 2 * KS * 64 / kBlock;   // 16-byte chunks per thread (hi + lo)
+    static_assert(NCH >= 1 && NCH * kBlock == 2 * 2 * KS * 64, "tile staging split");
+    __shared__ TileLds<KS> S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t i0 = (xcd_block(blockIdx.x, gridDim.x) * (kBlock / 64) + wave) * kTile;
-    if (i0 >= A.I.m) return;
+    const uint32_t blk_i0 = xcd_block(blockIdx.x, gridDim.x) * (kBlock / 64) * kTile;
+    const uint32_t i0 = blk_i0 + wave * kTile;
+    const bool wave_ok = i0 < A.I.m;
     const int col = lane & 31, h = lane >> 5;
     // the wave's 64 query points: B operand fragments, kept in registers
     bf16x8 bh[2][KS], bl[2][KS];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const uint64_t o = ((uint64_t)(i0 / 32 + t) * KS + s) * 64 + lane;
-            bh[t][s] = A.I.hi[o];
-            bl[t][s] = A.I.lo[o];
-        }
     uint32_t iq[2];
-    float nI[2];
+    float ai[2], bi[2];
     bool ok[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-        iq[t] = i0 + 32 * t + col;
-        nI[t] = A.I.norm[iq[t]];
-        ok[t] = iq[t] < A.I.m;
-    }
-    uint32_t cnt[2] = {0u, 0u}, best[2] = {kNone, kNone};
-    // link: only j > i, so start at the diagonal tile
-    const uint32_t jbeg = MODE == kLink ? i0 : 0u;
-    for (uint32_t j0 = jbeg; j0 < A.J.m; j0 += kTile) {
-        f32x16 acc[2][2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) acc[u][t][e] = 0.0f;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-            bf16x8 ah[2], al[2];
+            const uint64_t o = ((uint64_t)((wave_ok ? i0 : 0) / 32 + t) * KS + s) * 64 + lane;
+            bh[t][s] = A.I.hi[o];
+            bl[t][s] = A.I.lo[o];
+        }
+        iq[t] = i0 + 32 * t + col;
+        ok[t] = wave_ok && iq[t] < A.I.m;
+        const float nI = wave_ok ? A.I.norm[iq[t]] : kPadNorm;
+        ai[t] = ((1.0f + kBandC) * nI - A.elo) * 0.5f;
+        bi[t] = ((1.0f - kBandC) * nI - A.ehi) * 0.5f;
+    }
+    uint32_t cnt[2] = {0u, 0u}, best[2] = {kNone, kNone};
+
+    // staging: thread k moves 16-byte chunks c = k + q * kBlock of the tile
+    // (hi then lo), plus one norm per thread < 64
+    const uint32_t jbeg = MODE == kLink ? blk_i0 : 0u;
+    bf16x8 stg[NCH];
+    float stn = 0.0f;
+    auto fetch = [&](uint32_t j0) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const uint64_t o = ((uint64_t)(j0 / 32 + u) * KS + s) * 64 + lane;
-                ah[u] = A.J.hi[o];
-                al[u] = A.J.lo[o];
-            }
+        for (int q = 0; q < NCH; ++q) {
+            const int c = threadIdx.x + q * kBlock;        // [0, 2 * 2 * KS * 64)
+            const int half = c / (2 * KS * 64);            // 0 hi, 1 lo
+            const int w = c % (2 * KS * 64);               // (row group, k-step, lane)
+            const uint64_t o = (uint64_t)(j0 / 32) * KS * 64 + w;
+            stg[q] = half ? A.J.lo[o] : A.J.hi[o];
+        }
+        if (threadIdx.x < kTile) stn = A.J.norm[j0 + threadIdx.x];
+    };
+    auto commit = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < NCH; ++q) {
+            const int c = threadIdx.x + q * kBlock;
+            const int half = c / (2 * KS * 64);
+            const int w = c % (2 * KS * 64);
+            bf16x8* dst = half ? &S.lo[buf][0][0][0] : &S.hi[buf][0][0][0];
+            dst[w] = stg[q];
+        }
+        if (threadIdx.x < kTile) {
+            S.ta[buf][threadIdx.x] = (1.0f + kBandC) * 0.5f * stn;
+            S.tb[buf][threadIdx.x] = (1.0f - kBandC) * 0.5f * stn;
+        }
+    };
+    if (jbeg < A.J.m) {
+        fetch(jbeg);
+        commit(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (uint32_t j0 = jbeg; j0 < A.J.m; j0 += kTile, buf ^= 1) {
+        const bool more = j0 + kTile < A.J.m;
+        if (more) fetch(j0 + kTile);
+        // link: only j > i; tiles wholly below this wave's diagonal are skipped
+        const bool compute = wave_ok && !(MODE == kLink && j0 + kTile <= i0);
+        if (compute) {
+            f32x16 acc[2][2];
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int t = 0; t < 2; ++t) {
-                    acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bh[t][s], acc[u][t],
-                                                                        0, 0, 0);
-                    acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bl[t][s], acc[u][t],
-                                                                        0, 0, 0);
-                    acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[u], bh[t][s], acc[u][t],
-                                                                        0, 0, 0);
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) acc[u][t][e] = 0.0f;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                bf16x8 ah[2], al[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    ah[u] = S.hi[buf][u][s][lane];
+                    al[u] = S.lo[buf][u][s][lane];
                 }
-        }
-        // epilogue: decide each pair from d2~ and the band; recheck the band
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t jr = j0 + 32 * u + 8 * q + 4 * h;
-                const float4 nj = *reinterpret_cast<const float4*>(A.J.norm + jr);
-                const float njv[4] = {nj.x, nj.y, nj.z, nj.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const uint32_t j = jr + e;
+                for (int u = 0; u < 2; ++u)
 #pragma unroll
                     for (int t = 0; t < 2; ++t) {
-                        const float sn = nI[t] + njv[e];
-                        const float d2 = sn - 2.0f * acc[u][t][4 * q + e];
-                        const float dl = kBandC * sn;
-                        bool in = d2 + dl <= A.elo;
-                        const bool maybe = d2 - dl <= A.ehi;
-                        if (MODE == kLink && j <= iq[t]) in = false;
-                        else if (maybe && !in && ok[t] && j < A.J.m) {
-                            const uint32_t p = A.I.idx ? A.I.idx[iq[t]] : iq[t];
-                            const uint32_t qj = A.J.idx ? A.J.idx[j] : j;
-                            in = exact_within<T, 0>(A.X, A.d, p, qj, A.eps, A.eps2);
-                        }
-                        if (in) tile_hit<T, MODE>(A, iq[t], j, cnt[t], best[t]);
+                        acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bh[t][s],
+                                                                            acc[u][t], 0, 0, 0);
+                        acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bl[t][s],
+                                                                            acc[u][t], 0, 0, 0);
+                        acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[u], bh[t][s],
+                                                                            acc[u][t], 0, 0, 0);
                     }
+            }
+            // element e of block q of m-tile u: row j = j0 + 32u + 8q + 4h + e
+            uint64_t band[2] = {0ull, 0ull};
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int rb = 32 * u + 8 * q + 4 * h;
+                    const float4 ta = *reinterpret_cast<const float4*>(&S.ta[buf][rb]);
+                    const float4 tb = *reinterpret_cast<const float4*>(&S.tb[buf][rb]);
+                    const float tav[4] = {ta.x, ta.y, ta.z, ta.w};
+                    const float tbv[4] = {tb.x, tb.y, tb.z, tb.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t) {
+                            const float v = acc[u][t][4 * q + e];
+                            const bool in = v >= ai[t] + tav[e];
+                            const bool maybe = v >= bi[t] + tbv[e];
+                            const int bit = 16 * u + 4 * q + e;
+                            if constexpr (MODE == kCount) {
+                                cnt[t] += in ? 1u : 0u;
+                                band[t] |= (maybe && !in) ? (1ull << bit) : 0ull;
+                            } else {
+                                band[t] |= maybe ? (1ull << bit) : 0ull;   // hits + band
+                                if (in) band[t] |= 1ull << (32 + bit);
+                            }
+                        }
+                }
+            // hits (link / border) and band pairs (all modes), lane-divergent
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                uint32_t m = (uint32_t)band[t];
+                while (m) {
+                    const int bit = __builtin_ctz(m);
+                    m &= m - 1;
+                    const int u = bit >> 4, q = (bit >> 2) & 3, e = bit & 3;
+                    const uint32_t j = j0 + 32 * u + 8 * q + 4 * h + e;
+                    if (!ok[t] || j >= A.J.m) continue;
+                    if (MODE == kLink && j <= iq[t]) continue;
+                    bool in = MODE != kCount && ((band[t] >> (32 + bit)) & 1ull);
+                    if (!in) {
+                        const uint32_t p = A.I.idx ? A.I.idx[iq[t]] : iq[t];
+                        const uint32_t qj = A.J.idx ? A.J.idx[j] : j;
+                        in = exact_within<T, 0>(A.X, A.d, p, qj, A.eps, A.eps2);
+                    }
+                    if (in) tile_hit<T, MODE>(A, iq[t], j, cnt[t], best[t]);
                 }
             }
+        }
+        if (more) commit(buf ^ 1);
+        __syncthreads();
     }
     // lanes l and l + 32 hold the same query column
 #pragma unroll

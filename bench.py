@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--cpu-n", type=int, default=None,
                     help="CPU baseline sample size (default 1M points; 20k for d > 15)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--link-mode", type=int, default=None, help="PD_OPT_LINK_MODE override")
     ap.add_argument("--sweep-variant", type=int, default=None,
                     help="PD_OPT_SWEEP_VARIANT override (bit 0 count, 1 link, 2 border)")
     ap.add_argument("--rehearse", action="store_true",
@@ -134,6 +135,8 @@ def main():
     ctx = _native.context(local_rank)
     if args.sweep_variant is not None:
         ctx.set_option(_native.PD_OPT_SWEEP_VARIANT, args.sweep_variant)
+    if args.link_mode is not None:
+        ctx.set_option(_native.PD_OPT_LINK_MODE, args.link_mode)
     if world > 1:
         from pypardis_amd.distributed import NativeOps, train_sharded
         lo, hi = rank * n // world, (rank + 1) * n // world

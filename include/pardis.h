@@ -56,9 +56,12 @@ enum pd_option {
                                       the reference's single-slice aggregate (slow; for
                                       bit-identical split boundaries).  Default: correctly
                                       rounded, order-independent double-double sums. */
-    PD_OPT_LINK_MODE = 4,  /* union strategy (tuning): 0 (default) initial forest from the count
-                              pass's smallest neighbour + pointer jumping, then lock-free union
-                              over core-core edges; 2 the union pass alone */
+    PD_OPT_LINK_MODE = 4,  /* union strategy (tuning; labels identical): 3 (default) union
+                              sweep over each core record's own row only, then one pass over
+                              neighbouring cells that tests record pairs only where the
+                              cells' roots differ; 0 initial forest from the count pass's
+                              smallest neighbour + pointer jumping, then a lock-free union
+                              sweep over all core-core edges; 2 that sweep alone */
     PD_OPT_JUMP_ROUNDS = 5, /* pointer-jumping rounds for link mode 0 (default 4) */
     PD_OPT_XSUB = 6,        /* sub-cells per eps along axis 0 (default 2): finer rows follow
                                the eps-ball's chord more tightly, at 1/xsub the directory
@@ -82,7 +85,7 @@ enum pd_timing_slot {
     PD_T_KEY_BITS, PD_T_CORE_RECORDS,
     /* PD_OPT_SWEEP_STATS counters */
     PD_T_S_COUNT_CAND, PD_T_S_LINK_CAND, PD_T_S_LINK_HIT, PD_T_S_LINK_CORE, PD_T_S_LINK_SAME,
-    PD_T_S_LINK_FIND_SAME, PD_T_S_LINK_UNIONS, PD_T_NSLOTS
+    PD_T_S_LINK_FIND_SAME, PD_T_S_LINK_UNIONS, PD_T_S_VERIFY_PAIRS, PD_T_NSLOTS
 };
 
 typedef struct pd_ctx pd_ctx;

@@ -24,10 +24,11 @@ PD_OPT_LINK_MODE, PD_OPT_JUMP_ROUNDS, PD_OPT_XSUB, PD_OPT_FP32_SCREEN = 4, 5, 6,
 PD_OPT_SWEEP_STATS = 8
 PD_OPT_SWEEP_VARIANT = 9
 SWEEP_VARIANT_DEFAULT = 5
+LINK_MODE_DEFAULT = 3
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
                 "s_count_cand", "s_link_cand", "s_link_hit", "s_link_core", "s_link_same",
-                "s_link_find_same", "s_link_unions"]
+                "s_link_find_same", "s_link_unions", "s_verify_pairs"]
 
 # every symbol include/pardis.h declares (tests/test_abi.py checks the .so)
 EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",

@@ -1093,6 +1093,203 @@ __global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs
     if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
 }
 
+// ------------------------------------------------------------------ link mode 3
+// (1) on the forest of the count pass's smallest neighbours (init_kernel),
+// union over the centre row only (each core record with the core records of
+// its own row within eps, j > r): the densest part of every neighbourhood,
+// and nearly every cluster is one tree after it (tools/forest_sim.py: 99.9 %
+// of the core-core edges of a C2 slice already join one root); (2) flatten;
+// (3) per cell, the common root of its core records (kNone: no core record,
+// kMixed: several roots); (4) per cell, its forward neighbour cells (higher
+// index, within the eps stencil): a pair of cells whose roots agree — in the
+// snapshot or, re-read live, after earlier unions — is already connected and
+// skipped (a directory-word summary lets whole neighbour rows go unread);
+// only the rest test their core records against each other.  Every
+// core-core edge lies in one cell or two neighbouring cells, so every edge is
+// either proven connected or tested: the same guarantee as link_kernel.
+constexpr uint32_t kMixed = 0xFFFFFFFEu;
+
+template <typename T, int D, int M>
+__global__ __launch_bounds__(kBlock) void centre_link_kernel(const T* __restrict__ Xs, uint32_t R,
+                                                             Cells C, double eps, double eps2,
+                                                             float lo, float hi,
+                                                             uint32_t* __restrict__ par) {
+    const uint32_t r = rec_index();
+    if (r >= R || par[r] == kNone) return;   // not core
+    double a[D];
+    load_rec<T, D>(Xs, r, a);
+    const int L = part_of_wave(C.part_start, C.P, r);
+    const QueryCell<D> Q = query_cell<D>(C.parts + L, a);
+    uint64_t k0, k1;
+    const bool ok = row_keys<D, M>(Q, a, eps, NRows<D>::v / 2, k0, k1);
+    const uint32_t s0 = C.cstart[dir_rank(C.dir[k0 >> 6], k0)];
+    const uint32_t e0 = C.cstart[dir_rank(C.dir[k1 >> 6], k1)];
+    const uint32_t end = ok ? e0 : 0u;
+    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
+    Linker<false> lk{par, uf_find_l1(par, r), {}};
+    uint32_t j = s0 > r + 1 ? s0 : r + 1;
+    for (; j + 4 <= end; j += 4) {
+        T b0[D], b1[D], b2[D], b3[D];
+        load_raw<T, D>(Xs, j, b0);
+        load_raw<T, D>(Xs, j + 1, b1);
+        load_raw<T, D>(Xs, j + 2, b2);
+        load_raw<T, D>(Xs, j + 3, b3);
+        const uint32_t p0 = ld_l1(par + j), p1 = ld_l1(par + j + 1), p2 = ld_l1(par + j + 2),
+                       p3 = ld_l1(par + j + 3);
+        if (pr(b0)) lk.edge(j, p0);
+        if (pr(b1)) lk.edge(j + 1, p1);
+        if (pr(b2)) lk.edge(j + 2, p2);
+        if (pr(b3)) lk.edge(j + 3, p3);
+    }
+    for (; j < end; ++j) {
+        T b0[D];
+        load_raw<T, D>(Xs, j, b0);
+        const uint32_t p0 = ld_l1(par + j);
+        if (pr(b0)) lk.edge(j, p0);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void cell_root_kernel(const uint32_t* __restrict__ cstart,
+                                                           const uint32_t* __restrict__ ncells,
+                                                           const uint32_t* __restrict__ par,
+                                                           uint32_t* __restrict__ croot) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= *ncells) return;
+    const uint32_t e = cstart[c + 1];
+    uint32_t v = kNone;
+    for (uint32_t r = cstart[c]; r < e; ++r) {
+        const uint32_t p = par[r];   // flattened: the root, or kNone (not core)
+        if (p == kNone) continue;
+        if (v == kNone) {
+            v = p;
+        } else if (p != v) {
+            v = kMixed;
+            break;
+        }
+    }
+    croot[c] = v;
+}
+
+// Per directory word (64 consecutive cell keys of a row): the common root of
+// its cells' core records (kNone: none, kMixed: several) — lets a cell skip a
+// whole neighbour row whose words hold no other root.
+__global__ __launch_bounds__(kBlock) void word_root_kernel(const uint4* __restrict__ dir,
+                                                           uint64_t W,
+                                                           const uint32_t* __restrict__ croot,
+                                                           uint32_t* __restrict__ wroot) {
+    const uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (w >= W) return;
+    const uint4 d = dir[w];
+    const int nc = __popc(d.x) + __popc(d.y);
+    uint32_t v = kNone;
+    for (int i = 0; i < nc; ++i) {
+        const uint32_t cr = croot[d.z + i];
+        if (cr == kNone) continue;
+        if (v == kNone) {
+            v = cr;
+        } else if (cr != v) {
+            v = kMixed;
+            break;
+        }
+    }
+    wroot[w] = v;
+}
+
+// Test the core records of [s0, e0) against those of [s1, e1) (b > a when the
+// ranges are the same cell) and unite the pairs within eps; pairs already
+// under one root (live) skip the distance test.
+template <typename T, int D, int M>
+__device__ __noinline__ void pair_block(const T* __restrict__ Xs, uint32_t s0, uint32_t e0,
+                                        uint32_t s1, uint32_t e1, bool same, double eps,
+                                        double eps2, float lo, float hi, uint32_t* par) {
+    for (uint32_t a = s0; a < e0; ++a) {
+        if (ld_rlx(par + a) == kNone) continue;
+        double av[D];
+        load_rec<T, D>(Xs, a, av);
+        const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, a, av, eps, eps2, lo, hi);
+        for (uint32_t b = same ? a + 1 : s1; b < e1; ++b) {
+            if (ld_rlx(par + b) == kNone) continue;
+            if (uf_find(par, a) == uf_find(par, b)) continue;
+            T bv[D];
+            load_raw<T, D>(Xs, b, bv);
+            if (pr(bv)) uf_unite(par, a, b);
+        }
+    }
+}
+
+template <typename T, int D, int M, typename K>
+__global__ __launch_bounds__(kBlock) void cell_verify_kernel(
+    const T* __restrict__ Xs, const K* __restrict__ keys, const uint32_t* __restrict__ ncells,
+    const uint32_t* __restrict__ croot, const uint32_t* __restrict__ wroot, Cells C, int xsub,
+    double eps, double eps2, float lo, float hi, uint32_t* __restrict__ par,
+    unsigned long long* __restrict__ stats) {
+    constexpr int NR = NRows<D>::v;
+    const uint32_t c = xcd_block(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
+    if (c >= *ncells) return;
+    const uint32_t rc = croot[c];
+    if (rc == kNone) return;
+    const uint32_t s0 = C.cstart[c], e0 = C.cstart[c + 1];
+    uint32_t pairs = 0;
+    if (rc == kMixed) {
+        pair_block<T, D, M>(Xs, s0, e0, s0, e0, true, eps, eps2, lo, hi, par);
+        ++pairs;
+    }
+    // the cell's grid coordinates
+    const int L = part_of(C.part_start, C.P, s0);
+    const PartGrid* gp = C.parts + L;
+    int64_t nc[D], cc[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) nc[j] = gp->nc[j];
+    const uint64_t base = gp->base;
+    uint64_t lin = (uint64_t)keys[s0] - base;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        cc[j] = (int64_t)(lin % (uint64_t)nc[j]);
+        lin /= (uint64_t)nc[j];
+    }
+    for (int q = 0; q < NR; ++q) {
+        // row offsets o_j in {-1, 0, 1} (axis 1 fastest, as row_keys); key
+        // order is lexicographic from the last axis: skip rows before ours
+        int t = q, o[D];
+        o[0] = 0;
+        bool okq = true;
+#pragma unroll
+        for (int j = 1; j < D; ++j) {
+            o[j] = (t % 3) - 1;
+            t /= 3;
+            okq &= (cc[j] + o[j] >= 0) & (cc[j] + o[j] < nc[j]);
+        }
+        int dir = 0;
+#pragma unroll
+        for (int j = D - 1; j >= 1; --j)
+            if (dir == 0) dir = o[j];
+        if (dir < 0 || !okq) continue;
+        const int64_t x0 = dir == 0 ? cc[0] : (cc[0] - xsub < 0 ? 0 : cc[0] - xsub);
+        const int64_t x1 = cc[0] + xsub >= nc[0] ? nc[0] - 1 : cc[0] + xsub;
+        uint64_t k0 = 0;
+#pragma unroll
+        for (int j = D - 1; j >= 0; --j)
+            k0 = k0 * (uint64_t)nc[j] + (uint64_t)(j == 0 ? x0 : cc[j] + o[j]);
+        k0 += base;
+        const uint64_t k1 = k0 + (uint64_t)(x1 - x0) + 1;
+        if (rc != kMixed) {   // the row's words hold no root but ours: nothing to test
+            const uint32_t wa = wroot[k0 >> 6], wb = wroot[(k1 - 1) >> 6];
+            if ((wa == kNone || wa == rc) && (wb == kNone || wb == rc)) continue;
+        }
+        const uint32_t i0 = dir_rank(C.dir[k0 >> 6], k0), i1 = dir_rank(C.dir[k1 >> 6], k1);
+        for (uint32_t c2 = i0 > c + 1 ? i0 : c + 1; c2 < i1; ++c2) {
+            const uint32_t r2 = croot[c2];
+            if (r2 == kNone || (r2 == rc && rc != kMixed)) continue;
+            // two uniform cells: one live root comparison may settle it
+            if (rc != kMixed && r2 != kMixed && uf_find(par, rc) == uf_find(par, r2)) continue;
+            pair_block<T, D, M>(Xs, s0, e0, C.cstart[c2], C.cstart[c2 + 1], false, eps, eps2, lo,
+                                hi, par);
+            ++pairs;
+        }
+    }
+    if (stats && pairs) atomicAdd(stats + 7, (unsigned long long)pairs);
+}
+
 template <typename T, int D, int M, bool ST>
 __global__ __launch_bounds__(kBlock) void link2_kernel(const T* __restrict__ Xs, uint32_t NL,
                                                        const uint32_t* __restrict__ list, Cells C,
@@ -1226,6 +1423,7 @@ struct EvTimer {
 };
 
 inline unsigned blocks(uint64_t n) { return n ? (unsigned)((n + kBlock - 1) / kBlock) : 1u; }
+inline int xsub_of(const Ctx& ctx) { return ctx.xsub < 1 ? 1 : ctx.xsub; }
 
 // Launch helpers for the three neighbour sweeps: bit k of `variant`
 // (PD_OPT_SWEEP_VARIANT) selects the batched lane kernel for sweep k (0
@@ -1411,6 +1609,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         sst = ctx.arena.get<unsigned long long>("sweep_stats", 8);
         PD_HIP(hipMemsetAsync(sst, 0, sizeof(unsigned long long) * 8, s));
     }
+    const int mode = ctx.link_mode;
     if (R) {
         if (sst)
             launch_count<T, D, M, true>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
@@ -1425,8 +1624,23 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     tm.mark();   // 5
 
     uint32_t* par = ctx.arena.get<uint32_t>("parent", R);
-    if (R) {
-        const int mode = ctx.link_mode;
+    if (R && mode == 3) {
+        // forest from the count pass's smallest neighbour (links across rows)
+        hipLaunchKernelGGL(init_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, mn, 1, par);
+        hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
+        hipLaunchKernelGGL((centre_link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs,
+                           R, C, eps, eps2, slo, shi, par);
+        hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
+        uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
+        hipLaunchKernelGGL(cell_root_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, cstart, dncells,
+                           par, croot);
+        uint32_t* wroot = ctx.arena.get<uint32_t>("word_root", W);
+        hipLaunchKernelGGL(word_root_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, W, croot,
+                           wroot);
+        hipLaunchKernelGGL((cell_verify_kernel<T, D, M, K>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                           Xs, keys, dncells, croot, wroot, C, xsub_of(ctx), eps, eps2, slo, shi,
+                           par, sst);
+    } else if (R) {
         hipLaunchKernelGGL(init_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, mn,
                            mode == 0 ? 1 : 0, par);
         {
@@ -1570,7 +1784,7 @@ void finish(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
             PD_HIP(hipMemcpyAsync(hs, ctx.arena.get<unsigned long long>("sweep_stats", 8),
                                   8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
             sync(s);
-            for (int k = 0; k < 7; ++k) ctx.t.sweep[k] = (int64_t)hs[k];
+            for (int k = 0; k < 8; ++k) ctx.t.sweep[k] = (int64_t)hs[k];
         }
         ctx.t.grid_cells = (int64_t)ctx.st.G;
         ctx.t.key_bits = ctx.st.key_bits;

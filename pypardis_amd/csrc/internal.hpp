@@ -47,8 +47,9 @@ struct Timings {
           roots = 0, border = 0, label = 0, total = 0;
     int64_t records = 0, cells_n = 0, grid_cells = 0, core_records = 0, key_bits = 0;
     // PD_OPT_SWEEP_STATS: count candidates; link candidates, predicate hits,
-    // core hits, hits already under the root, finds that met the root, unions
-    int64_t sweep[7] = {0, 0, 0, 0, 0, 0, 0};
+    // core hits, hits already under the root, finds that met the root, unions;
+    // cell pairs tested record by record (link mode 3)
+    int64_t sweep[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 // Device state carried from phase A (local clustering) to phase B (border
@@ -84,7 +85,7 @@ struct Ctx {
     bool timing = false;
     bool full_counts = false;    // debug: count every neighbour (no early exit)
     bool seq_moments = false;    // reference-order (sequential) KD moment sums
-    int link_mode = 0;           // 0 init forest + jumps + union; 2 union only; 1 diagnostic
+    int link_mode = 3;           // 3 samples + cell verify; 0 init forest + jumps + union sweep; 2 union sweep only
     int jump_rounds = 4;
     int xsub = 2;                // axis-0 sub-cells per eps
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)

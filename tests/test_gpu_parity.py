@@ -228,15 +228,17 @@ def test_train_matches_oracle(native, case):
     assert m.n_clusters_ == ncl
 
 
-@pytest.mark.parametrize("variant", [0, 7])
-def test_sweep_variants_exact(native, variant):
-    """PD_OPT_SWEEP_VARIANT: the row-by-row and the batched sweep kernels
-    (every stage in one or the other) give identical counts, core flags and
-    labels (= oracle) on every case: 1-D..4-D, cityblock, fp64, exact ties,
+@pytest.mark.parametrize("variant,link_mode", [(0, 3), (7, 3), (5, 0), (7, 2)])
+def test_sweep_variants_exact(native, variant, link_mode):
+    """PD_OPT_SWEEP_VARIANT x PD_OPT_LINK_MODE: the row-by-row and the
+    batched sweep kernels, and the sampled-union + cell-verify link (3) or the
+    full union sweeps (0, 2), give identical counts, core flags and labels
+    (= oracle) on every case: 1-D..4-D, cityblock, fp64, exact ties,
     min_samples 1, several neighbourhoods (waves straddling two)."""
     from pypardis_amd import DBSCAN, synth
     ctx = native.context()
     ctx.set_option(native.PD_OPT_SWEEP_VARIANT, variant)
+    ctx.set_option(native.PD_OPT_LINK_MODE, link_mode)
     try:
         for _, kw, eps, ms, metric, P in CASES:
             X = synth.blobs_noise(**kw)
@@ -265,6 +267,7 @@ def test_sweep_variants_exact(native, variant):
             assert np.array_equal(lab, gd["sk_labels"]) and np.array_equal(core, gd["sk_core"])
     finally:
         ctx.set_option(native.PD_OPT_SWEEP_VARIANT, native.SWEEP_VARIANT_DEFAULT)
+        ctx.set_option(native.PD_OPT_LINK_MODE, native.LINK_MODE_DEFAULT)
 
 
 def test_fp64_input_exact(native):

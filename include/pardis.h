@@ -71,11 +71,14 @@ enum pd_option {
                                (default 1; results are identical with 0) */
     PD_OPT_SWEEP_STATS = 8, /* tally the neighbour sweeps' candidates and union-find outcomes
                                into the PD_T_S_* slots (instrumented kernels; default 0) */
-    PD_OPT_SWEEP_VARIANT = 9 /* kernel variant per neighbour sweep (tuning; results are
+    PD_OPT_SWEEP_VARIANT = 9, /* kernel variant per neighbour sweep (tuning; results are
                                identical): bit 0 count, bit 1 link, bit 2 border; a set bit
                                selects the batched lane kernel (wave-uniform grid in scalar
                                registers, three rows swept as one list), a clear bit the
                                row-by-row kernel.  Default 5 (the measured best on MI355X). */
+    PD_OPT_BORDER_ROOTS = 10 /* batched border sweep: skip or stop early where the stencil's
+                                directory words hold at most one cluster root (tuning; same
+                                labels; default 0 — slower on C2) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -23,6 +23,7 @@ PD_OPT_TIMING, PD_OPT_FULL_COUNTS, PD_OPT_SEQUENTIAL_MOMENTS = 1, 2, 3
 PD_OPT_LINK_MODE, PD_OPT_JUMP_ROUNDS, PD_OPT_XSUB, PD_OPT_FP32_SCREEN = 4, 5, 6, 7
 PD_OPT_SWEEP_STATS = 8
 PD_OPT_SWEEP_VARIANT = 9
+PD_OPT_BORDER_ROOTS = 10
 SWEEP_VARIANT_DEFAULT = 5
 LINK_MODE_DEFAULT = 3
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",

@@ -532,16 +532,33 @@ __global__ void part_start_kernel(const K* __restrict__ keys, uint64_t R,
     ps[L] = (uint32_t)lo;
 }
 
+// Cell starts: flag[r] = 1 where a new key begins, and the key's occupancy
+// bit in its directory word.  Keys are sorted, so a wave's starts fall in a
+// few consecutive words: one atomicOr per distinct word per wave (the bits of
+// different lanes are distinct, so their OR is their sum).
 template <typename K>
 __global__ __launch_bounds__(kBlock) void run_flag_kernel(const K* __restrict__ keys, uint64_t R,
                                                           uint32_t* __restrict__ flag,
                                                           uint4* __restrict__ dir) {
     const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R) return;
-    const uint64_t k = keys[r];
-    const bool start = (r == 0) || ((uint64_t)keys[r - 1] != k);
-    flag[r] = start ? 1u : 0u;
-    if (start) atomicOr(reinterpret_cast<unsigned long long*>(dir + (k >> 6)), 1ull << (k & 63));
+    const bool in = r < R;
+    const uint64_t k = in ? (uint64_t)keys[r] : 0ull;
+    const bool start = in && ((r == 0) || ((uint64_t)keys[r - 1] != k));
+    if (in) flag[r] = start ? 1u : 0u;
+    const uint64_t word = k >> 6;
+    const unsigned long long bit = start ? (1ull << (k & 63)) : 0ull;
+    const int lane = threadIdx.x & 63;
+    unsigned long long active = __ballot(start);
+    while (active) {
+        const int leader = __ffsll(active) - 1;
+        const uint64_t lw = (uint64_t)__shfl((long long)word, leader, 64);
+        const bool mine = start && word == lw;
+        unsigned long long v = mine ? bit : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v |= (unsigned long long)__shfl_xor((long long)v, o, 64);
+        if (lane == leader) atomicOr(reinterpret_cast<unsigned long long*>(dir + lw), v);
+        active &= ~__ballot(mine);
+    }
 }
 
 struct DirPopc {
@@ -842,12 +859,17 @@ __global__ __launch_bounds__(kBlock) void remap_kernel(uint32_t R, const uint8_t
 }
 
 // Owner records: publish core flag / count, and the cluster key of core
-// points (their component's smallest core point).
+// points (their component's smallest core point).  core_bit (single device,
+// ids < 2^30): the core flag rides in bit 30 of the key instead of a byte
+// scattered to core_out — the label pass writes the core mask coalesced.
+constexpr uint32_t kKeyCoreBit = 0x40000000u;
+
 __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_t* __restrict__ vals,
                                                        const uint8_t* __restrict__ core,
                                                        const uint32_t* __restrict__ par,
                                                        const uint32_t* __restrict__ gmin,
                                                        const uint32_t* __restrict__ cnt_rec,
+                                                       int core_bit,
                                                        uint32_t* __restrict__ key_out,
                                                        uint8_t* __restrict__ core_out,
                                                        uint32_t* __restrict__ cnt_out) {
@@ -857,9 +879,9 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
     if (!(v & kOwnerBit)) return;
     const uint32_t pt = v & kIdMask;
     const uint8_t fl = core[r];
-    if (core_out) core_out[pt] = fl & 1;
+    if (core_out && !core_bit) core_out[pt] = fl & 1;
     if (cnt_out) cnt_out[pt] = cnt_rec[r];
-    if (fl & 1) key_out[pt] = gmin[par[r]];
+    if (fl & 1) key_out[pt] = gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u);
 }
 
 struct IsCore {
@@ -1337,13 +1359,18 @@ __global__ __launch_bounds__(kBlock) void link2_kernel(const T* __restrict__ Xs,
     }
 }
 
+// wroot (nullable; directory-word roots of the final forest): when every word
+// of the stencil holds no root but one, R, the smallest adjacent key can only
+// be R's — one core neighbour within eps proves it, so the sweep stops at the
+// first (centre row first); no root at all means noise, without a sweep.
 template <typename T, int D, int M>
 __global__ __launch_bounds__(kBlock) void border2_kernel(
     const T* __restrict__ Xs, uint32_t NL, const uint32_t* __restrict__ list, Cells C, double eps,
     double eps2, float lo, float hi, const uint32_t* __restrict__ vals,
     const uint32_t* __restrict__ par, const uint32_t* __restrict__ gmin,
-    uint32_t* __restrict__ key_out) {
+    const uint32_t* __restrict__ wroot, uint32_t* __restrict__ key_out) {
     constexpr int B = RowBatch<D>::B, NB = RowBatch<D>::NB;
+    constexpr int NR = NRows<D>::v;
     const uint32_t i = rec_index();
     if (i >= NL) return;
     const uint32_t r = list[i];   // owner, non-core records with a neighbour, ascending
@@ -1354,6 +1381,48 @@ __global__ __launch_bounds__(kBlock) void border2_kernel(
     with_part(C.part_start, C.P, r, [&](int L, auto U) {
         const QueryCell<D> Q = decltype(U)::value ? query_cell_u<D>(C.parts + L, a)
                                                   : query_cell<D>(C.parts + L, a);
+        if (wroot) {
+            uint32_t R = kNone;
+            bool mixed = false;
+            for (int q = 0; q < NR; ++q) {
+                uint64_t k0, k1;
+                if (!row_keys<D, M>(Q, a, eps, q, k0, k1)) continue;
+                const uint32_t w2[2] = {wroot[k0 >> 6], wroot[(k1 - 1) >> 6]};
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t w = w2[h];
+                    if (w == kMixed || (w != kNone && R != kNone && w != R)) mixed = true;
+                    if (w != kNone && w != kMixed) R = w;
+                }
+            }
+            if (!mixed) {
+                if (R == kNone) return;   // no core record anywhere near: noise
+                for (int bq = 0; bq < NB; ++bq) {
+                    const int bt = (bq + NB / 2) % NB;
+                    uint32_t pre[B], off[B];
+                    const uint32_t tot = batch_list<D, M>(C, Q, a, eps, bt, true, 0u, pre, off);
+                    for (uint32_t v = 0; v < tot; v += 4) {
+                        uint32_t j[4], pj[4];
+                        T b[4][D];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            j[u] = v + u < tot ? bpos<B>(v + u, pre, off) : r;
+                            load_raw<T, D>(Xs, j[u], b[u]);
+                            pj[u] = par[j[u]];
+                        }
+                        bool hit = false;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            hit |= v + u < tot && pj[u] != kNone && pr(b[u]);
+                        if (hit) {
+                            best = gmin[R];
+                            return;
+                        }
+                    }
+                }
+                return;
+            }
+        }
         for (int bt = 0; bt < NB; ++bt) {
             uint32_t pre[B], off[B];
             const uint32_t tot = batch_list<D, M>(C, Q, a, eps, bt, false, 0u, pre, off);
@@ -1378,22 +1447,31 @@ __global__ __launch_bounds__(kBlock) void border2_kernel(
     key_out[vals[r] & kIdMask] = best;
 }
 
+// Keys may carry kKeyCoreBit (owner_kernel core_bit mode): strip it.
+__device__ __forceinline__ uint32_t key_id(uint32_t k, int core_bit) {
+    return (core_bit && k != kNone) ? (k & ~kKeyCoreBit) : k;
+}
+
 __global__ __launch_bounds__(kBlock) void root_flag_kernel(const uint32_t* __restrict__ key,
-                                                           uint64_t n,
+                                                           uint64_t n, int core_bit,
                                                            uint32_t* __restrict__ flag) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) flag[i] = key[i] == (uint32_t)i ? 1u : 0u;
+    if (i < n) flag[i] = key_id(key[i], core_bit) == (uint32_t)i ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(kBlock) void label_kernel(const uint32_t* __restrict__ key,
                                                        const uint32_t* __restrict__ rnk,
                                                        const uint32_t* __restrict__ flag,
-                                                       uint64_t n, int32_t* __restrict__ labels,
+                                                       uint64_t n, int core_bit,
+                                                       int32_t* __restrict__ labels,
+                                                       uint8_t* __restrict__ core_out,
                                                        int64_t* __restrict__ ncl) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = key[i];
-    labels[i] = k == kNone ? -1 : (int32_t)rnk[k];
+    const uint32_t id = key_id(k, core_bit);
+    labels[i] = k == kNone ? -1 : (int32_t)rnk[id];
+    if (core_bit && core_out) core_out[i] = (k != kNone && (k & kKeyCoreBit)) ? 1 : 0;
     if (i == n - 1) *ncl = (int64_t)rnk[i] + flag[i];
 }
 
@@ -1456,10 +1534,10 @@ template <typename T, int D, int M>
 void launch_border(int variant, hipStream_t s, const T* Xs, uint32_t NL, const uint32_t* list,
                    const Cells& C, double eps, double eps2, float lo, float hi,
                    const uint32_t* vals, const uint32_t* par, const uint32_t* gmin,
-                   uint32_t* key_out) {
+                   const uint32_t* wroot, uint32_t* key_out) {
     if (variant & 4)
         hipLaunchKernelGGL((border2_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
-                           list, C, eps, eps2, lo, hi, vals, par, gmin, key_out);
+                           list, C, eps, eps2, lo, hi, vals, par, gmin, wroot, key_out);
     else
         hipLaunchKernelGGL((border_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
                            list, C, eps, eps2, lo, hi, vals, par, gmin, key_out);
@@ -1676,6 +1754,18 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         hipLaunchKernelGGL(gmin_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, vals, R, core, par,
                            a.gid, gmin);
     }
+    // final cell / word roots for the border sweep's single-root fast path
+    // (PD_OPT_BORDER_ROOTS; off by default: on C2 the extra root passes and
+    // the 9-row word checks cost more than the sweep they save)
+    uint32_t* wroot_final = nullptr;
+    if (R && (ctx.variant & 4) && ctx.border_roots) {
+        uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
+        hipLaunchKernelGGL(cell_root_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, cstart, dncells,
+                           par, croot);
+        wroot_final = ctx.arena.get<uint32_t>("word_root", W);
+        hipLaunchKernelGGL(word_root_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, W, croot,
+                           wroot_final);
+    }
     PD_HIP(hipGetLastError());
     tm.mark();   // 8
 
@@ -1702,6 +1792,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     st.par = par;
     st.gmin = gmin;
     st.cnt_rec = cnt_rec;
+    st.wroot = wroot_final;
     st.n_exports = 0;
     if (a.phase == 1 && R && a.xr) {
         uint32_t* elist = nullptr;
@@ -1743,18 +1834,20 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
                                a.keymap, gmin);
     }
     uint32_t* key_out = a.phase == 2 ? a.keys_out : ctx.arena.get<uint32_t>("key_out", n);
+    // single device: core flags travel in the keys (ids < 2^30); sharded: global ids
+    const int core_bit = a.phase == 2 ? 0 : 1;
     PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
-    if (a.core) PD_HIP(hipMemsetAsync(a.core, 0, n, s));
+    if (a.core && !core_bit) PD_HIP(hipMemsetAsync(a.core, 0, n, s));
     if (R)
     {
         hipLaunchKernelGGL(owner_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, vals, core, par,
-                           gmin, st.cnt_rec, key_out, a.core, a.counts);
+                           gmin, st.cnt_rec, core_bit, key_out, a.core, a.counts);
         uint32_t* blist = nullptr;
         const uint32_t NB =
             select_records(ctx, "border_list", R, IsBorderCandidate{core, vals}, &blist, s);
         if (NB)
             launch_border<T, D, M>(ctx.variant, s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par,
-                                   gmin, key_out);
+                                   gmin, st.wroot, key_out);
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 9 (phase 2: 1)
@@ -1763,7 +1856,7 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         return;
     }
 
-    rank_labels_async(ctx, key_out, n, a.labels, s);
+    rank_labels_async(ctx, key_out, n, a.labels, s, core_bit, a.core);
     tm.mark();   // 10
     a.n_clusters = rank_labels_count(ctx, s);
 }
@@ -1871,13 +1964,14 @@ void run_d(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& p, uint64_t G, i
 // is their own id) is the label — sklearn's numbering.  Async on s; the
 // cluster count is read back by rank_labels_count.
 void rank_labels_async(Ctx& ctx, const uint32_t* key, uint64_t n, int32_t* labels,
-                       hipStream_t s) {
+                       hipStream_t s, int core_bit, uint8_t* core_from_key) {
     uint32_t* rflag = ctx.arena.get<uint32_t>("rflag", n);
     uint32_t* rnk = ctx.arena.get<uint32_t>("rnk", n);
     int64_t* dncl = ctx.arena.get<int64_t>("ncl", 2);
     PD_HIP(hipMemsetAsync(dncl, 0, sizeof(int64_t), s));
     if (n) {
-        hipLaunchKernelGGL(root_flag_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key, n, rflag);
+        hipLaunchKernelGGL(root_flag_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key, n, core_bit,
+                           rflag);
         size_t tb = 0;
         PD_HIP(rocprim::exclusive_scan(nullptr, tb, rflag, rnk, 0u, (size_t)n,
                                        rocprim::plus<uint32_t>(), s));
@@ -1885,7 +1979,7 @@ void rank_labels_async(Ctx& ctx, const uint32_t* key, uint64_t n, int32_t* label
         PD_HIP(rocprim::exclusive_scan(tmp, tb, rflag, rnk, 0u, (size_t)n,
                                        rocprim::plus<uint32_t>(), s));
         hipLaunchKernelGGL(label_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key, rnk, rflag, n,
-                           labels, dncl);
+                           core_bit, labels, core_from_key, dncl);
     }
     PD_HIP(hipGetLastError());
 }

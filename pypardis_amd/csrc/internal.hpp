@@ -74,6 +74,7 @@ struct PhaseState {
     uint32_t* par = nullptr;
     uint32_t* gmin = nullptr;
     uint32_t* cnt_rec = nullptr;
+    uint32_t* wroot = nullptr;   // directory-word roots of the final forest (border fast path)
     uint32_t* exp_gid = nullptr;
     uint32_t* exp_key = nullptr;
 };
@@ -90,6 +91,7 @@ struct Ctx {
     int xsub = 2;                // axis-0 sub-cells per eps
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
+    bool border_roots = false;   // border sweep's single-root fast path (tuning)
     int variant = 5;             // PD_OPT_SWEEP_VARIANT: batched count + border, row-wise link
     Timings t;
     PhaseState st;
@@ -127,7 +129,10 @@ void train(Ctx& ctx, TrainArgs& a);
 // d > kMaxDim: dense distance tiles on the matrix cores (dense.hip)
 void dense_train(Ctx& ctx, TrainArgs& a);
 // labels from cluster keys (engine.hip): async, then the cluster count (syncs)
-void rank_labels_async(Ctx& ctx, const uint32_t* key, uint64_t n, int32_t* labels, hipStream_t s);
+// core_bit: keys carry the core flag in bit 30 (stripped; written to
+// core_from_key when not null)
+void rank_labels_async(Ctx& ctx, const uint32_t* key, uint64_t n, int32_t* labels, hipStream_t s,
+                       int core_bit = 0, uint8_t* core_from_key = nullptr);
 int64_t rank_labels_count(Ctx& ctx, hipStream_t s);
 
 // KD partition stages (kd.hip)

@@ -228,8 +228,9 @@ def test_train_matches_oracle(native, case):
     assert m.n_clusters_ == ncl
 
 
-@pytest.mark.parametrize("variant,link_mode", [(0, 3), (7, 3), (5, 0), (7, 2)])
-def test_sweep_variants_exact(native, variant, link_mode):
+@pytest.mark.parametrize("variant,link_mode,border_roots",
+                         [(0, 3, 0), (7, 3, 1), (5, 0, 0), (7, 2, 0)])
+def test_sweep_variants_exact(native, variant, link_mode, border_roots):
     """PD_OPT_SWEEP_VARIANT x PD_OPT_LINK_MODE: the row-by-row and the
     batched sweep kernels, and the sampled-union + cell-verify link (3) or the
     full union sweeps (0, 2), give identical counts, core flags and labels
@@ -239,6 +240,7 @@ def test_sweep_variants_exact(native, variant, link_mode):
     ctx = native.context()
     ctx.set_option(native.PD_OPT_SWEEP_VARIANT, variant)
     ctx.set_option(native.PD_OPT_LINK_MODE, link_mode)
+    ctx.set_option(native.PD_OPT_BORDER_ROOTS, border_roots)
     try:
         for _, kw, eps, ms, metric, P in CASES:
             X = synth.blobs_noise(**kw)
@@ -268,6 +270,7 @@ def test_sweep_variants_exact(native, variant, link_mode):
     finally:
         ctx.set_option(native.PD_OPT_SWEEP_VARIANT, native.SWEEP_VARIANT_DEFAULT)
         ctx.set_option(native.PD_OPT_LINK_MODE, native.LINK_MODE_DEFAULT)
+        ctx.set_option(native.PD_OPT_BORDER_ROOTS, 0)
 
 
 def test_fp64_input_exact(native):

@@ -1244,20 +1244,37 @@ __global__ __launch_bounds__(kBlock) void cell_verify_kernel(
     const T* __restrict__ Xs, const K* __restrict__ keys, const uint32_t* __restrict__ ncells,
     const uint32_t* __restrict__ croot, const uint32_t* __restrict__ wroot, Cells C, int xsub,
     double eps, double eps2, float lo, float hi, uint32_t* __restrict__ par,
+    uint2* __restrict__ plist, uint32_t pcap, uint32_t* __restrict__ pcount,
     unsigned long long* __restrict__ stats) {
     constexpr int NR = NRows<D>::v;
+    constexpr uint32_t kBuf = 1024;
+    // cell pairs whose roots differ go to a list, resolved by pair_kernel, so
+    // the rare record-level work does not stall this kernel's waves: staged
+    // per block in LDS, one global reservation per block (overflow of the
+    // block buffer or of the list: resolved in place)
+    __shared__ uint2 lbuf[kBuf];
+    __shared__ uint32_t lcnt, lbase;
+    if (threadIdx.x == 0) lcnt = 0;
+    __syncthreads();
     const uint32_t c = xcd_block(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
-    if (c >= *ncells) return;
-    const uint32_t rc = croot[c];
-    if (rc == kNone) return;
-    const uint32_t s0 = C.cstart[c], e0 = C.cstart[c + 1];
+    const uint32_t rc = c < *ncells ? croot[c] : kNone;
     uint32_t pairs = 0;
-    if (rc == kMixed) {
-        pair_block<T, D, M>(Xs, s0, e0, s0, e0, true, eps, eps2, lo, hi, par);
+    if (rc != kNone) {
+    const uint32_t s0 = C.cstart[c], e0 = C.cstart[c + 1];
+    auto defer = [&](uint32_t c2) {
         ++pairs;
-    }
-    // the cell's grid coordinates
-    const int L = part_of(C.part_start, C.P, s0);
+        const uint32_t slot = atomicAdd(&lcnt, 1u);
+        if (slot < kBuf) {
+            lbuf[slot] = make_uint2(c, c2);
+        } else {
+            const bool same = c2 == c;
+            pair_block<T, D, M>(Xs, s0, e0, same ? s0 : C.cstart[c2], same ? e0 : C.cstart[c2 + 1],
+                                same, eps, eps2, lo, hi, par);
+        }
+    };
+    if (rc == kMixed) defer(c);
+    // the cell's grid coordinates (wave-uniform neighbourhood in the common case)
+    const int L = part_of_wave(C.part_start, C.P, s0);
     const PartGrid* gp = C.parts + L;
     int64_t nc[D], cc[D];
 #pragma unroll
@@ -1266,12 +1283,34 @@ __global__ __launch_bounds__(kBlock) void cell_verify_kernel(
     uint64_t lin = (uint64_t)keys[s0] - base;
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-        cc[j] = (int64_t)(lin % (uint64_t)nc[j]);
-        lin /= (uint64_t)nc[j];
+        uint64_t qt;
+        if (lin < (1ull << 52) && nc[j] < (1ll << 31)) {
+            // exact via fp64 (both operands exact), one-step correction
+            qt = (uint64_t)floor((double)lin / (double)nc[j]);
+            int64_t rem = (int64_t)(lin - qt * (uint64_t)nc[j]);
+            if (rem < 0) {
+                --qt;
+                rem += nc[j];
+            } else if (rem >= nc[j]) {
+                ++qt;
+                rem -= nc[j];
+            }
+            cc[j] = rem;
+        } else {
+            qt = lin / (uint64_t)nc[j];
+            cc[j] = (int64_t)(lin - qt * (uint64_t)nc[j]);
+        }
+        lin = qt;
     }
-    for (int q = 0; q < NR; ++q) {
-        // row offsets o_j in {-1, 0, 1} (axis 1 fastest, as row_keys); key
-        // order is lexicographic from the last axis: skip rows before ours
+    // forward rows (key order is lexicographic from the last axis; row q's
+    // offsets o_j = digit j-1 of q in base 3, minus 1): their key ranges, and
+    // a first look at their directory-word roots, all issued together
+    constexpr int NF = (NR + 1) / 2;   // the own row and the rows after it
+    uint64_t k0[NF], k1[NF];
+    bool okr[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        const int q = NR / 2 + f;   // rows NR/2 .. NR-1 are the own row and those after
         int t = q, o[D];
         o[0] = 0;
         bool okq = true;
@@ -1281,35 +1320,77 @@ __global__ __launch_bounds__(kBlock) void cell_verify_kernel(
             t /= 3;
             okq &= (cc[j] + o[j] >= 0) & (cc[j] + o[j] < nc[j]);
         }
-        int dir = 0;
-#pragma unroll
-        for (int j = D - 1; j >= 1; --j)
-            if (dir == 0) dir = o[j];
-        if (dir < 0 || !okq) continue;
-        const int64_t x0 = dir == 0 ? cc[0] : (cc[0] - xsub < 0 ? 0 : cc[0] - xsub);
+        const int64_t x0 = f == 0 ? cc[0] : (cc[0] - xsub < 0 ? 0 : cc[0] - xsub);
         const int64_t x1 = cc[0] + xsub >= nc[0] ? nc[0] - 1 : cc[0] + xsub;
-        uint64_t k0 = 0;
+        uint64_t kk = 0;
 #pragma unroll
         for (int j = D - 1; j >= 0; --j)
-            k0 = k0 * (uint64_t)nc[j] + (uint64_t)(j == 0 ? x0 : cc[j] + o[j]);
-        k0 += base;
-        const uint64_t k1 = k0 + (uint64_t)(x1 - x0) + 1;
-        if (rc != kMixed) {   // the row's words hold no root but ours: nothing to test
-            const uint32_t wa = wroot[k0 >> 6], wb = wroot[(k1 - 1) >> 6];
-            if ((wa == kNone || wa == rc) && (wb == kNone || wb == rc)) continue;
-        }
-        const uint32_t i0 = dir_rank(C.dir[k0 >> 6], k0), i1 = dir_rank(C.dir[k1 >> 6], k1);
+            kk = kk * (uint64_t)nc[j] + (uint64_t)(j == 0 ? x0 : cc[j] + o[j]);
+        k0[f] = okq ? kk + base : 0;
+        k1[f] = okq ? kk + base + (uint64_t)(x1 - x0) + 1 : 1;
+        okr[f] = okq;
+    }
+    uint32_t wa[NF], wb[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        wa[f] = wroot[k0[f] >> 6];
+        wb[f] = wroot[(k1[f] - 1) >> 6];
+    }
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+        if (!okr[f]) continue;
+        // the row's words hold no root but ours: nothing to test
+        if (rc != kMixed && (wa[f] == kNone || wa[f] == rc) && (wb[f] == kNone || wb[f] == rc))
+            continue;
+        const uint32_t i0 = dir_rank(C.dir[k0[f] >> 6], k0[f]);
+        const uint32_t i1 = dir_rank(C.dir[k1[f] >> 6], k1[f]);
         for (uint32_t c2 = i0 > c + 1 ? i0 : c + 1; c2 < i1; ++c2) {
             const uint32_t r2 = croot[c2];
             if (r2 == kNone || (r2 == rc && rc != kMixed)) continue;
-            // two uniform cells: one live root comparison may settle it
-            if (rc != kMixed && r2 != kMixed && uf_find(par, rc) == uf_find(par, r2)) continue;
-            pair_block<T, D, M>(Xs, s0, e0, C.cstart[c2], C.cstart[c2 + 1], false, eps, eps2, lo,
-                                hi, par);
-            ++pairs;
+            defer(c2);
+        }
+    }
+    }   // rc != kNone
+    __syncthreads();
+    const uint32_t nb = lcnt < kBuf ? lcnt : kBuf;
+    if (threadIdx.x == 0) lbase = nb ? atomicAdd(pcount, nb) : 0u;
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nb; k += kBlock) {
+        const uint2 pr = lbuf[k];
+        if (lbase + k < pcap) {
+            plist[lbase + k] = pr;
+        } else {
+            const bool same = pr.x == pr.y;
+            pair_block<T, D, M>(Xs, C.cstart[pr.x], C.cstart[pr.x + 1], C.cstart[pr.y],
+                                C.cstart[pr.y + 1], same, eps, eps2, lo, hi, par);
         }
     }
     if (stats && pairs) atomicAdd(stats + 7, (unsigned long long)pairs);
+}
+
+// The deferred cell pairs: a live root comparison of two uniform cells may
+// settle a pair (earlier unions merged their trees); otherwise their core
+// records are tested against each other.
+template <typename T, int D, int M>
+__global__ __launch_bounds__(kBlock) void pair_kernel(const T* __restrict__ Xs,
+                                                      const uint2* __restrict__ plist,
+                                                      const uint32_t* __restrict__ pcount,
+                                                      uint32_t pcap,
+                                                      const uint32_t* __restrict__ cstart,
+                                                      const uint32_t* __restrict__ croot, double eps,
+                                                      double eps2, float lo, float hi,
+                                                      uint32_t* __restrict__ par) {
+    const uint32_t np0 = *pcount;
+    const uint32_t np = np0 < pcap ? np0 : pcap;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < np; i += gridDim.x * kBlock) {
+        const uint2 pr = plist[i];
+        const uint32_t ra = croot[pr.x], rb = croot[pr.y];
+        if (pr.x != pr.y && ra != kMixed && rb != kMixed && uf_find(par, ra) == uf_find(par, rb))
+            continue;
+        const bool same = pr.x == pr.y;
+        pair_block<T, D, M>(Xs, cstart[pr.x], cstart[pr.x + 1], cstart[pr.y], cstart[pr.y + 1],
+                            same, eps, eps2, lo, hi, par);
+    }
 }
 
 template <typename T, int D, int M, bool ST>
@@ -1715,9 +1796,15 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         uint32_t* wroot = ctx.arena.get<uint32_t>("word_root", W);
         hipLaunchKernelGGL(word_root_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, W, croot,
                            wroot);
+        const uint32_t pcap = (uint32_t)std::min<uint64_t>(R, 64ull << 20);
+        uint2* plist = ctx.arena.get<uint2>("pair_list", pcap);
+        uint32_t* pcount = ctx.arena.get<uint32_t>("pair_count", 4);
+        PD_HIP(hipMemsetAsync(pcount, 0, sizeof(uint32_t), s));
         hipLaunchKernelGGL((cell_verify_kernel<T, D, M, K>), dim3(blocks(R)), dim3(kBlock), 0, s,
                            Xs, keys, dncells, croot, wroot, C, xsub_of(ctx), eps, eps2, slo, shi,
-                           par, sst);
+                           par, plist, pcap, pcount, sst);
+        hipLaunchKernelGGL((pair_kernel<T, D, M>), dim3(std::min(blocks(pcap), 4096u)), dim3(kBlock), 0, s, Xs, plist,
+                           pcount, pcap, cstart, croot, eps, eps2, slo, shi, par);
     } else if (R) {
         hipLaunchKernelGGL(init_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, mn,
                            mode == 0 ? 1 : 0, par);

@@ -73,17 +73,23 @@ def b_nc(records, cells, d):
 
 
 def load_pmc(kernel="count_kernel"):
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*pmc*.json")))
-    if not files:
-        return None
-    try:
-        z = json.load(open(files[-1]))
-        k = z.get(kernel)
-        if not k:
-            return None
-        return dict(bytes_per_launch=k["hbm_bytes_per_launch"], source=os.path.basename(files[-1]))
-    except Exception:
-        return None
+    """Per-launch HBM bytes of `kernel` from the newest PMC summary that has it
+    (profiles/rNN_vMM_pmc_summary.json, newest = highest (round, version))."""
+    import re
+
+    def order(f):
+        m = re.search(r"r(\d+)_v(\d+)", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*pmc*.json")), key=order,
+                    reverse=True):
+        try:
+            k = json.load(open(f)).get(kernel)
+        except Exception:
+            continue
+        if k and "hbm_bytes_per_launch" in k:
+            return dict(bytes_per_launch=k["hbm_bytes_per_launch"], source=os.path.basename(f))
+    return None
 
 
 def cpu_baseline(cfg_name, n_sample, n_full):

@@ -66,6 +66,7 @@ struct FragSet {
     const bf16x8* hi;
     const bf16x8* lo;
     const float* norm;     // [rows_pad]
+    const float* nmax;     // max norm over the valid rows (device scalar)
     const uint32_t* idx;   // row -> point id (null: identity)
     uint32_t m;            // valid rows
 };
@@ -120,20 +121,26 @@ __global__ __launch_bounds__(kBlock) void norm_kernel(const T* __restrict__ X, i
                                                       const uint32_t* __restrict__ idx, uint32_t m,
                                                       uint32_t rows_pad,
                                                       const double* __restrict__ center,
-                                                      double scale, float* __restrict__ norm) {
+                                                      double scale, float* __restrict__ norm,
+                                                      uint32_t* __restrict__ nmax) {
     const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= rows_pad) return;
-    if (r >= m) {
+    float nr = 0.0f;   // norms are >= 0: their bits order as uint32
+    if (r < m) {
+        const uint32_t p = idx ? idx[r] : r;
+        double acc = 0.0;
+        for (int k = 0; k < d; ++k) {
+            const double v = (double)(float)(((double)X[(uint64_t)p * d + k] - center[k]) * scale);
+            acc += v * v;
+        }
+        nr = (float)acc;
+        norm[r] = nr;
+    } else if (r < rows_pad) {
         norm[r] = kPadNorm;
-        return;
     }
-    const uint32_t p = idx ? idx[r] : r;
-    double acc = 0.0;
-    for (int k = 0; k < d; ++k) {
-        const double v = (double)(float)(((double)X[(uint64_t)p * d + k] - center[k]) * scale);
-        acc += v * v;
-    }
-    norm[r] = (float)acc;
+    uint32_t w = __float_as_uint(nr);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) w = max(w, (uint32_t)__shfl_xor((int)w, o, 64));
+    if ((threadIdx.x & 63) == 0 && w) atomicMax(nmax, w);
 }
 
 // ---------------------------------------------------------------- tiles
@@ -168,22 +175,24 @@ __device__ __forceinline__ void tile_hit(const TileArgs<T>& A, uint32_t i, uint3
 // tile prefetched into registers while the current one is computed).
 //
 // Epilogue: with s = |x_i|^2 + |x_j|^2 and acc = <x_i, x_j>~,
-//   in    <=>  d2~ + c s <= elo  <=>  acc >= ((1+c)|x_i|^2 - elo)/2 + (1+c)|x_j|^2/2
-//   maybe <=>  d2~ - c s <= ehi  <=>  acc >= ((1-c)|x_i|^2 - ehi)/2 + (1-c)|x_j|^2/2
-// (column terms per lane, row terms per tile row from LDS: one add and one
-// compare each; the fp32 rounding of the rearrangement is < 2^-22 s, inside
-// the band's margin).  Band pairs (maybe && !in) are rare: collected as bits
-// and re-tested exactly after the tile.
+//   in    <=>  d2~ + c s <= elo  <=>  acc - ta_j >= ai := ((1+c)|x_i|^2 - elo)/2
+//   maybe <=>  d2~ - c s <= ehi  <=>  acc - ta_j >= ((1-c)|x_i|^2 - ehi)/2 - c |x_j|^2
+// with ta_j = (1+c)|x_j|^2/2.  The row term -ta_j is the MFMA's C operand
+// (the accumulation starts from it), so `in` is one compare against a column
+// constant; `maybe` is widened to the column constant bi := ((1-c)|x_i|^2 -
+// ehi)/2 - c max_j |x_j|^2 (a superset: more pairs re-tested, none missed).
+// The fp32 rounding of the rearrangement is < 2^-22 s, inside the band's
+// margin.  The count pass tallies in and maybe per lane and builds the band
+// bits (maybe && !in, re-tested exactly) only for tiles where they differ.
 template <int KS>
 struct TileLds {
     bf16x8 hi[2][2][KS][64];   // [buffer][row group][k-step][lane]
     bf16x8 lo[2][2][KS][64];
-    float ta[2][kTile];        // (1+c)|x_j|^2 / 2
-    float tb[2][kTile];        // (1-c)|x_j|^2 / 2
+    float nta[2][kTile];       // -ta_j = -(1+c)|x_j|^2 / 2
 };
 
 template <typename T, int MODE, int KS>
-__global__ __launch_bounds__(kBlock) void tile_kernel(TileArgs<T> A) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS >= 8 ? 1 : 2))) void tile_kernel(TileArgs<T> A) {
     constexpr int NCH = 2 * 2 * KS * 64 / kBlock;   // 16-byte chunks per thread (hi + lo)
     static_assert(NCH >= 1 && NCH * kBlock == 2 * 2 * KS * 64, "tile staging split");
     __shared__ TileLds<KS> S;
@@ -192,6 +201,7 @@ __global__ __launch_bounds__(kBlock) void tile_kernel(TileArgs<T> A) {
     const uint32_t i0 = blk_i0 + wave * kTile;
     const bool wave_ok = i0 < A.I.m;
     const int col = lane & 31, h = lane >> 5;
+    const float nJmax = *A.J.nmax;
     // the wave's 64 query points: B operand fragments, kept in registers
     bf16x8 bh[2][KS], bl[2][KS];
     uint32_t iq[2];
@@ -209,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void tile_kernel(TileArgs<T> A) {
         ok[t] = wave_ok && iq[t] < A.I.m;
         const float nI = wave_ok ? A.I.norm[iq[t]] : kPadNorm;
         ai[t] = ((1.0f + kBandC) * nI - A.elo) * 0.5f;
-        bi[t] = ((1.0f - kBandC) * nI - A.ehi) * 0.5f;
+        bi[t] = ((1.0f - kBandC) * nI - A.ehi) * 0.5f - kBandC * 1.001f * nJmax;
     }
     uint32_t cnt[2] = {0u, 0u}, best[2] = {kNone, kNone};
 
@@ -238,10 +248,7 @@ __global__ __launch_bounds__(kBlock) void tile_kernel(TileArgs<T> A) {
             bf16x8* dst = half ? &S.lo[buf][0][0][0] : &S.hi[buf][0][0][0];
             dst[w] = stg[q];
         }
-        if (threadIdx.x < kTile) {
-            S.ta[buf][threadIdx.x] = (1.0f + kBandC) * 0.5f * stn;
-            S.tb[buf][threadIdx.x] = (1.0f - kBandC) * 0.5f * stn;
-        }
+        if (threadIdx.x < kTile) S.nta[buf][threadIdx.x] = -((1.0f + kBandC) * 0.5f) * stn;
     };
     if (jbeg < A.J.m) {
         fetch(jbeg);
@@ -255,13 +262,20 @@ __global__ __launch_bounds__(kBlock) void tile_kernel(TileArgs<T> A) {
         // link: only j > i; tiles wholly below this wave's diagonal are skipped
         const bool compute = wave_ok && !(MODE == kLink && j0 + kTile <= i0);
         if (compute) {
-            f32x16 acc[2][2];
+            // C operand: -ta of the tile's rows, element 4q + e = row 32u + 8q + 4h + e
+            f32x16 nt[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int t = 0; t < 2; ++t)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) acc[u][t][e] = 0.0f;
+                for (int q = 0; q < 4; ++q) {
+                    const float4 v =
+                        *reinterpret_cast<const float4*>(&S.nta[buf][32 * u + 8 * q + 4 * h]);
+                    nt[u][4 * q + 0] = v.x;
+                    nt[u][4 * q + 1] = v.y;
+                    nt[u][4 * q + 2] = v.z;
+                    nt[u][4 * q + 3] = v.w;
+                }
+            f32x16 acc[2][2];
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 bf16x8 ah[2], al[2];
@@ -274,8 +288,8 @@ __global__ __launch_bounds__(kBlock) void tile_kernel(TileArgs<T> A) {
                 for (int u = 0; u < 2; ++u)
 #pragma unroll
                     for (int t = 0; t < 2; ++t) {
-                        acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bh[t][s],
-                                                                            acc[u][t], 0, 0, 0);
+                        acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                            ah[u], bh[t][s], s == 0 ? nt[u] : acc[u][t], 0, 0, 0);
                         acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bl[t][s],
                                                                             acc[u][t], 0, 0, 0);
                         acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[u], bh[t][s],
@@ -284,35 +298,54 @@ __global__ __launch_bounds__(kBlock) void tile_kernel(TileArgs<T> A) {
             }
             // element e of block q of m-tile u: row j = j0 + 32u + 8q + 4h + e
             uint64_t band[2] = {0ull, 0ull};
+            bool walk = true;
+            if constexpr (MODE == kCount) {
+                uint32_t ci[2] = {0u, 0u}, cm[2] = {0u, 0u};
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+                for (int r = 0; r < 16; ++r)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int rb = 32 * u + 8 * q + 4 * h;
-                    const float4 ta = *reinterpret_cast<const float4*>(&S.ta[buf][rb]);
-                    const float4 tb = *reinterpret_cast<const float4*>(&S.tb[buf][rb]);
-                    const float tav[4] = {ta.x, ta.y, ta.z, ta.w};
-                    const float tbv[4] = {tb.x, tb.y, tb.z, tb.w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
+                    for (int u = 0; u < 2; ++u)
 #pragma unroll
                         for (int t = 0; t < 2; ++t) {
-                            const float v = acc[u][t][4 * q + e];
-                            const bool in = v >= ai[t] + tav[e];
-                            const bool maybe = v >= bi[t] + tbv[e];
-                            const int bit = 16 * u + 4 * q + e;
-                            if constexpr (MODE == kCount) {
-                                cnt[t] += in ? 1u : 0u;
-                                band[t] |= (maybe && !in) ? (1ull << bit) : 0ull;
-                            } else {
-                                band[t] |= maybe ? (1ull << bit) : 0ull;   // hits + band
-                                if (in) band[t] |= 1ull << (32 + bit);
-                            }
+                            ci[t] += acc[u][t][r] >= ai[t] ? 1u : 0u;
+                            cm[t] += acc[u][t][r] >= bi[t] ? 1u : 0u;
                         }
+                cnt[0] += ci[0];
+                cnt[1] += ci[1];
+                walk = __any((ci[0] != cm[0]) || (ci[1] != cm[1]));
+                if (walk) {
+                    // fresh compares (keeps the masks above from living across)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t) asm volatile("" : "+v"(acc[u][t]));
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+#pragma unroll
+                        for (int u = 0; u < 2; ++u)
+#pragma unroll
+                            for (int t = 0; t < 2; ++t) {
+                                const float v = acc[u][t][r];
+                                const bool b = v >= bi[t] && !(v >= ai[t]);
+                                band[t] |= b ? (1ull << (16 * u + r)) : 0ull;
+                            }
                 }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t) {
+                            const float v = acc[u][t][r];
+                            const int bit = 16 * u + r;
+                            band[t] |= v >= bi[t] ? (1ull << bit) : 0ull;   // hits + band
+                            if (v >= ai[t]) band[t] |= 1ull << (32 + bit);
+                        }
+            }
             // hits (link / border) and band pairs (all modes), lane-divergent
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
+            for (int t = 0; t < 2 && walk; ++t) {
                 uint32_t m = (uint32_t)band[t];
                 while (m) {
                     const int bit = __builtin_ctz(m);
@@ -452,21 +485,24 @@ FragSet make_frags(Ctx& ctx, const std::string& tag, const T* X, int d, const ui
     F.idx = idx;
     if (!G.mfma) {
         F.hi = F.lo = nullptr;
-        F.norm = nullptr;
+        F.norm = F.nmax = nullptr;
         return F;
     }
     const size_t nfrag = (size_t)(rp / 32) * G.KS * 64;
     bf16x8* hi = ctx.arena.get<bf16x8>(tag + "_hi", nfrag);
     bf16x8* lo = ctx.arena.get<bf16x8>(tag + "_lo", nfrag);
     float* nrm = ctx.arena.get<float>(tag + "_norm", rp);
+    uint32_t* nmax = ctx.arena.get<uint32_t>(tag + "_nmax", 1);
+    PD_HIP(hipMemsetAsync(nmax, 0, sizeof(uint32_t), s));
     hipLaunchKernelGGL(prep_kernel<T>, dim3(nblocks((uint64_t)rp * G.KS * 2)), dim3(kBlock), 0, s,
                        X, d, idx, m, rp, G.KS, G.center, G.scale, hi, lo);
     hipLaunchKernelGGL(norm_kernel<T>, dim3(nblocks(rp)), dim3(kBlock), 0, s, X, d, idx, m, rp,
-                       G.center, G.scale, nrm);
+                       G.center, G.scale, nrm, nmax);
     PD_HIP(hipGetLastError());
     F.hi = hi;
     F.lo = lo;
     F.norm = nrm;
+    F.nmax = (const float*)nmax;
     return F;
 }
 

@@ -533,32 +533,32 @@ __global__ void part_start_kernel(const K* __restrict__ keys, uint64_t R,
 }
 
 // Cell starts: flag[r] = 1 where a new key begins, and the key's occupancy
-// bit in its directory word.  Keys are sorted, so a wave's starts fall in a
-// few consecutive words: one atomicOr per distinct word per wave (the bits of
-// different lanes are distinct, so their OR is their sum).
+// bit in its directory word.  Keys are sorted, so the lanes of one word are
+// contiguous: a segmented OR-scan across the wave (Hillis-Steele, equal words
+// at distance o imply equal words in between) leaves each word's bits in its
+// last lane, which adds them with one atomicOr (the bits of different lanes
+// are distinct, and a word can continue into the neighbouring waves).
 template <typename K>
 __global__ __launch_bounds__(kBlock) void run_flag_kernel(const K* __restrict__ keys, uint64_t R,
                                                           uint32_t* __restrict__ flag,
                                                           uint4* __restrict__ dir) {
     const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const bool in = r < R;
-    const uint64_t k = in ? (uint64_t)keys[r] : 0ull;
+    const uint64_t k = in ? (uint64_t)keys[r] : ~0ull;
     const bool start = in && ((r == 0) || ((uint64_t)keys[r - 1] != k));
     if (in) flag[r] = start ? 1u : 0u;
     const uint64_t word = k >> 6;
-    const unsigned long long bit = start ? (1ull << (k & 63)) : 0ull;
+    unsigned long long v = start ? (1ull << (k & 63)) : 0ull;
     const int lane = threadIdx.x & 63;
-    unsigned long long active = __ballot(start);
-    while (active) {
-        const int leader = __ffsll(active) - 1;
-        const uint64_t lw = (uint64_t)__shfl((long long)word, leader, 64);
-        const bool mine = start && word == lw;
-        unsigned long long v = mine ? bit : 0ull;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v |= (unsigned long long)__shfl_xor((long long)v, o, 64);
-        if (lane == leader) atomicOr(reinterpret_cast<unsigned long long*>(dir + lw), v);
-        active &= ~__ballot(mine);
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t wo = (uint64_t)__shfl_up((long long)word, o, 64);
+        const unsigned long long vo = (unsigned long long)__shfl_up((long long)v, o, 64);
+        if (lane >= o && wo == word) v |= vo;
     }
+    const uint64_t wn = (uint64_t)__shfl_down((long long)word, 1, 64);
+    const bool last = lane == 63 || wn != word;
+    if (in && last && v) atomicOr(reinterpret_cast<unsigned long long*>(dir + word), v);
 }
 
 struct DirPopc {
@@ -794,15 +794,21 @@ __global__ __launch_bounds__(kBlock) void merge_kernel(const uint32_t* __restric
 __global__ __launch_bounds__(kBlock) void flatten_kernel(uint32_t R,
                                                          const uint8_t* __restrict__ core,
                                                          uint32_t* __restrict__ par) {
+    // par doubles as the core flag (kNone: not core, init_kernel), so the
+    // core array is not read; records already under their root are not
+    // written (most of them, after the first flatten)
+    (void)core;
     const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R || !(core[r] & 1)) return;
-    uint32_t x = par[r];
+    if (r >= R) return;
+    const uint32_t x0 = par[r];
+    if (x0 == kNone) return;
+    uint32_t x = x0;
     while (true) {
         const uint32_t p = par[x];
         if (p == x) break;
         x = p;
     }
-    par[r] = x;
+    if (x != x0) par[r] = x;
 }
 
 // Component key = smallest (global) id of its core points.  gid maps local

@@ -1179,21 +1179,26 @@ __global__ __launch_bounds__(kBlock) void centre_link_kernel(const T* __restrict
 
 __global__ __launch_bounds__(kBlock) void cell_root_kernel(const uint32_t* __restrict__ cstart,
                                                            const uint32_t* __restrict__ ncells,
-                                                           const uint32_t* __restrict__ par,
+                                                           uint32_t* __restrict__ par,
                                                            uint32_t* __restrict__ croot) {
+    // also flattens: each core record (all lie in one cell) gets its root
+    // written back, so no separate flatten pass runs before (no unions run
+    // concurrently, so a chain read by another cell stays valid)
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= *ncells) return;
     const uint32_t e = cstart[c + 1];
     uint32_t v = kNone;
     for (uint32_t r = cstart[c]; r < e; ++r) {
-        const uint32_t p = par[r];   // flattened: the root, or kNone (not core)
-        if (p == kNone) continue;
-        if (v == kNone) {
-            v = p;
-        } else if (p != v) {
-            v = kMixed;
-            break;
+        const uint32_t p0 = par[r];
+        if (p0 == kNone) continue;   // not core
+        uint32_t p = p0;
+        while (true) {
+            const uint32_t q = par[p];
+            if (q == p) break;
+            p = q;
         }
+        if (p != p0) par[r] = p;
+        v = v == kNone ? p : (p != v ? kMixed : v);
     }
     croot[c] = v;
 }
@@ -1795,7 +1800,6 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
         hipLaunchKernelGGL((centre_link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs,
                            R, C, eps, eps2, slo, shi, par);
-        hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
         uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
         hipLaunchKernelGGL(cell_root_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, cstart, dncells,
                            par, croot);

@@ -213,13 +213,16 @@ def main():
                     "cells": cells, "algorithmic_bytes": alg_bytes}
             dtype = "f64"
         else:
-            # dense tiles (dense.hip): the all-pairs Gram matrix of the count
-            # pass, 2 n^2 d algorithmic flops; the MFMA executes 3 split-bf16
-            # products over the padded shape
+            # dense tiles (dense.hip): the count pass's Gram tiles, 2 d flops
+            # per pair over the 64 x 64 wave tiles it computes (the engine
+            # reports them in cells_n; the projection window prunes the rest
+            # of the n^2 pairs); the MFMA executes 3 split-bf16 products
+            # with d padded to 16 ks
             ks = 1 if d <= 16 else 2 if d <= 32 else 4 if d <= 64 else 8
             n_pad = -(-n // 64) * 64
-            alg = 2.0 * n * n * d
-            exe = 3 * 2.0 * n_pad * n_pad * 16 * ks
+            tiles = cells if cells > 0 else (n_pad // 64) ** 2
+            alg = 2.0 * d * 64 * 64 * tiles
+            exe = 3 * 2.0 * 64 * 64 * 16 * ks * tiles
             achieved = alg / (t_cnt * 1e-3) / 1e12
             pmc = load_pmc("tile_kernel")
             roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
@@ -227,6 +230,8 @@ def main():
                     "traffic": pmc["bytes_per_launch"] if pmc else None,
                     "kernel": "tile_kernel (count pass)", "kernel_ms": t_cnt,
                     "algorithmic_flops": alg, "mfma_executed_flops": exe,
+                    "wave_tiles": tiles, "tiles_all_pairs": (n_pad // 64) ** 2,
+                    "tile_fraction": tiles / (n_pad // 64) ** 2,
                     "mfma_executed_tflops": exe / (t_cnt * 1e-3) / 1e12,
                     "mfma_utilisation": exe / (t_cnt * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS}
             dtype = "bf16x3 (split bf16 MFMA, fp32 accumulate) + f64 recheck"

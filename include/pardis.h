@@ -76,9 +76,11 @@ enum pd_option {
                                selects the batched lane kernel (wave-uniform grid in scalar
                                registers, three rows swept as one list), a clear bit the
                                row-by-row kernel.  Default 5 (the measured best on MI355X). */
-    PD_OPT_BORDER_ROOTS = 10 /* batched border sweep: skip or stop early where the stencil's
+    PD_OPT_BORDER_ROOTS = 10, /* batched border sweep: skip or stop early where the stencil's
                                 directory words hold at most one cluster root (tuning; same
                                 labels; default 0 — slower on C2) */
+    PD_OPT_DENSE_PRUNE = 11   /* d > 4 count pass: stream only the tiles inside the two-axis
+                                projection window (exact; default 1; 0 = all n^2 pairs) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

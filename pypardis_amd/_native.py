@@ -24,6 +24,7 @@ PD_OPT_LINK_MODE, PD_OPT_JUMP_ROUNDS, PD_OPT_XSUB, PD_OPT_FP32_SCREEN = 4, 5, 6,
 PD_OPT_SWEEP_STATS = 8
 PD_OPT_SWEEP_VARIANT = 9
 PD_OPT_BORDER_ROOTS = 10
+PD_OPT_DENSE_PRUNE = 11
 SWEEP_VARIANT_DEFAULT = 5
 LINK_MODE_DEFAULT = 3
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",

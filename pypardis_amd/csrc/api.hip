@@ -119,6 +119,8 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.screen = value != 0;
         else if (option == PD_OPT_SWEEP_STATS)
             ctx->c.sweep_stats = value != 0;
+        else if (option == PD_OPT_DENSE_PRUNE)
+            ctx->c.dense_prune = value != 0;
         else if (option == PD_OPT_BORDER_ROOTS)
             ctx->c.border_roots = value != 0;
         else if (option == PD_OPT_SWEEP_VARIANT) {

@@ -38,6 +38,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -155,7 +156,34 @@ struct TileArgs {
     uint32_t* par;         // kLink: union-find over the (I = J) rows
     const uint32_t* keyJ;  // kBorder: cluster key per J row
     uint32_t* best;        // kBorder: smallest adjacent key per I row
+    // projection pruning (count pass, I = J): rows grouped into bands of
+    // `band` rows by their rank in coordinate p1, sorted by coordinate p2
+    // within a band.  A pair whose p1 or p2 differ by more than win cannot
+    // be within eps (|x_k - y_k| <= |x - y|), so a block streams, per band
+    // whose p1 range meets its own widened by win, only the run of rows whose
+    // p2 lies within win of its rows' p2 range.  p2: null = no pruning.
+    const double* p2;           // [m] p2 of each row
+    const double* bp1;          // [2 * nband] p1 range (lo, hi) of each band
+    uint32_t band, nband;
+    double win;
+    unsigned long long* tiles;  // wave tiles computed (null: not counted)
 };
+
+constexpr int kMaxSeg = 256;   // bands a block can stream (host keeps nband <= this)
+
+// First index in the ascending p[lo, hi) with p[k] >= v (upper: > v).
+__device__ __forceinline__ uint32_t p_bound(const double* __restrict__ p, uint32_t lo, uint32_t hi,
+                                            double v, bool upper) {
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const double x = p[mid];
+        if (upper ? (x <= v) : (x < v))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
 
 template <typename T, int MODE>
 __device__ __forceinline__ void tile_hit(const TileArgs<T>& A, uint32_t i, uint32_t j, uint32_t& cnt,
@@ -223,9 +251,60 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS >= 8 
     }
     uint32_t cnt[2] = {0u, 0u}, best[2] = {kNone, kNone};
 
+    // streamed segments [seg_lo, seg_hi) of J rows (tile-aligned starts):
+    // all of J, from the diagonal (link), or one per band in the window
+    __shared__ uint32_t seg_lo[kMaxSeg], seg_hi[kMaxSeg];
+    __shared__ uint32_t nseg_s;
+    if (A.p2 && blk_i0 < A.I.m) {
+        const uint32_t b = blk_i0 / A.band;   // a block lies in one band
+        const uint32_t last = min(blk_i0 + (uint32_t)(kBlock / 64) * kTile, A.I.m) - 1u;
+        const double lo1 = A.bp1[2 * b] - A.win, hi1 = A.bp1[2 * b + 1] + A.win;
+        const double lo2 = A.p2[blk_i0] - A.win, hi2 = A.p2[last] + A.win;
+        // bands are p1-ordered: both ends of their ranges ascend
+        uint32_t blo = 0, bhi = A.nband;
+        {
+            uint32_t l = 0, h = A.nband;
+            while (l < h) {
+                const uint32_t mid = (l + h) >> 1;
+                if (A.bp1[2 * mid + 1] < lo1) l = mid + 1; else h = mid;
+            }
+            blo = l;
+            l = blo;
+            h = A.nband;
+            while (l < h) {
+                const uint32_t mid = (l + h) >> 1;
+                if (A.bp1[2 * mid] <= hi1) l = mid + 1; else h = mid;
+            }
+            bhi = l;
+        }
+        const uint32_t ns = bhi - blo;   // <= nband <= kMaxSeg
+        for (uint32_t t = threadIdx.x; t < ns; t += kBlock) {
+            const uint32_t bb = blo + t;
+            const uint32_t r0 = bb * A.band, r1 = min(r0 + A.band, A.J.m);
+            const uint32_t sl = p_bound(A.p2, r0, r1, lo2, false);
+            const uint32_t sh = p_bound(A.p2, sl, r1, hi2, true);
+            seg_lo[t] = sl < sh ? (sl & ~(uint32_t)(kTile - 1)) : sh;
+            seg_hi[t] = sh;
+        }
+        if (threadIdx.x == 0) nseg_s = ns;
+    } else if (threadIdx.x == 0) {
+        seg_lo[0] = MODE == kLink ? blk_i0 : 0u;
+        seg_hi[0] = A.J.m;
+        nseg_s = 1;
+    }
+    __syncthreads();
+    const uint32_t nseg = nseg_s;
+    uint32_t ntiles = 0;
+    // cursor over the tiles of the segments; false at the end
+    auto seek = [&](uint32_t& sg, uint32_t& j) -> bool {
+        while (sg < nseg) {
+            if (j < seg_hi[sg]) return true;
+            if (++sg < nseg) j = seg_lo[sg];
+        }
+        return false;
+    };
     // staging: thread k moves 16-byte chunks c = k + q * kBlock of the tile
     // (hi then lo), plus one norm per thread < 64
-    const uint32_t jbeg = MODE == kLink ? blk_i0 : 0u;
     bf16x8 stg[NCH];
     float stn = 0.0f;
     auto fetch = [&](uint32_t j0) {
@@ -250,18 +329,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS >= 8 
         }
         if (threadIdx.x < kTile) S.nta[buf][threadIdx.x] = -((1.0f + kBandC) * 0.5f) * stn;
     };
-    if (jbeg < A.J.m) {
-        fetch(jbeg);
+    uint32_t sg = 0, j0 = seg_lo[0];
+    bool have = seek(sg, j0);
+    if (have) {
+        fetch(j0);
         commit(0);
     }
     __syncthreads();
     int buf = 0;
-    for (uint32_t j0 = jbeg; j0 < A.J.m; j0 += kTile, buf ^= 1) {
-        const bool more = j0 + kTile < A.J.m;
-        if (more) fetch(j0 + kTile);
+    while (have) {
+        uint32_t sn = sg, jn = j0 + kTile;
+        const bool more = seek(sn, jn);
+        if (more) fetch(jn);
         // link: only j > i; tiles wholly below this wave's diagonal are skipped
         const bool compute = wave_ok && !(MODE == kLink && j0 + kTile <= i0);
         if (compute) {
+            ++ntiles;
             // C operand: -ta of the tile's rows, element 4q + e = row 32u + 8q + 4h + e
             f32x16 nt[2];
 #pragma unroll
@@ -366,7 +449,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS >= 8 
         }
         if (more) commit(buf ^ 1);
         __syncthreads();
+        sg = sn;
+        j0 = jn;
+        have = more;
+        buf ^= 1;
     }
+    if (A.tiles && lane == 0 && ntiles) atomicAdd(A.tiles, (unsigned long long)ntiles);
     // lanes l and l + 32 hold the same query column
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -437,6 +525,64 @@ __global__ __launch_bounds__(kBlock) void outputs_kernel(const uint32_t* __restr
     const uint32_t c = cnt[i];
     if (core) core[i] = c >= ms ? 1 : 0;
     if (counts) counts[i] = full ? c : (c < ms ? c : ms);
+}
+
+// Projection pruning: sort rows by one coordinate (order-preserving u64 of
+// its fp64 value, -0.0 folded onto +0.0).
+__device__ __forceinline__ unsigned long long proj_okey(double v) {
+    unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    if (b == 0x8000000000000000ull) b = 0ull;
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void proj_key_kernel(const T* __restrict__ X, int d, int ax,
+                                                          uint32_t n,
+                                                          unsigned long long* __restrict__ key,
+                                                          uint32_t* __restrict__ id) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    key[i] = proj_okey((double)X[(uint64_t)i * d + ax]);
+    id[i] = i;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void proj_gather_kernel(const T* __restrict__ X, int d, int ax,
+                                                             const uint32_t* __restrict__ sid,
+                                                             uint32_t n, double* __restrict__ p) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r < n) p[r] = (double)X[(uint64_t)sid[r] * d + ax];
+}
+
+// band of each point = its p1 rank / band; band p1 ranges from the p1 order
+__global__ __launch_bounds__(kBlock) void band_of_kernel(const uint32_t* __restrict__ sid1, uint32_t n,
+                                                         uint32_t band,
+                                                         uint32_t* __restrict__ band_of) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r < n) band_of[sid1[r]] = r / band;
+}
+
+__global__ __launch_bounds__(kBlock) void band_key_kernel(const uint32_t* __restrict__ band_of,
+                                                          const uint32_t* __restrict__ sid2,
+                                                          uint32_t n, uint32_t* __restrict__ key) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r < n) key[r] = band_of[sid2[r]];
+}
+
+__global__ __launch_bounds__(kBlock) void band_range_kernel(const double* __restrict__ p1s, uint32_t n,
+                                                            uint32_t band, uint32_t nband,
+                                                            double* __restrict__ bp1) {
+    const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= nband) return;
+    bp1[2 * b] = p1s[b * band];
+    bp1[2 * b + 1] = p1s[min((b + 1) * band, n) - 1u];
+}
+
+__global__ __launch_bounds__(kBlock) void scatter_cnt_kernel(const uint32_t* __restrict__ cs,
+                                                             const uint32_t* __restrict__ sid,
+                                                             uint32_t n, uint32_t* __restrict__ cnt) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r < n) cnt[sid[r]] = cs[r];
 }
 
 struct CntAtLeast {
@@ -588,11 +734,108 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
     A.ehi = G.ehi;
 
     // ---- neighbour counts (all x all)
-    const FragSet Fall = make_frags<T>(ctx, "dn_all", X, d, nullptr, n, G, s);
     uint32_t* cnt = ctx.arena.get<uint32_t>("dn_cnt", n);
-    A.I = A.J = Fall;
+    unsigned long long* dtiles = nullptr;
+    if (G.mfma && ctx.dense_prune) {
+        // rows in bands of the widest axis' rank, sorted by the second
+        // widest within a band; each block streams only the tiles of its
+        // projection window (TileArgs::p2).  The margin covers the fp64
+        // predicate: a pruned pair has one squared term above eps^2 by
+        // 2^-20, so sklearn's rounded sum exceeds eps^2 too.
+        int ax1 = 0, ax2 = d > 1 ? 1 : 0;
+        double amax = 0.0;
+        {
+            std::vector<std::pair<double, int>> wd;
+            for (int k = 0; k < d; ++k) {
+                const double lo = a.data_box[k], hi = a.data_box[d + k];
+                wd.push_back({-(hi - lo), k});
+                amax = std::max(amax, std::max(std::fabs(lo), std::fabs(hi)));
+            }
+            std::stable_sort(wd.begin(), wd.end());
+            ax1 = wd[0].second;
+            if (d > 1) ax2 = wd[1].second;
+        }
+        uint32_t band = 16384;
+        while ((n + band - 1) / band > (uint32_t)kMaxSeg) band *= 2;
+        const uint32_t nband = (n + band - 1) / band;
+        unsigned long long* k0 = ctx.arena.get<unsigned long long>("dn_pk0", n);
+        unsigned long long* k1 = ctx.arena.get<unsigned long long>("dn_pk1", n);
+        uint32_t* i0 = ctx.arena.get<uint32_t>("dn_pi0", n);
+        uint32_t* i1 = ctx.arena.get<uint32_t>("dn_pi1", n);
+        uint32_t* bof = ctx.arena.get<uint32_t>("dn_band_of", n);
+        uint32_t* bk0 = ctx.arena.get<uint32_t>("dn_bk0", n);
+        uint32_t* bk1 = ctx.arena.get<uint32_t>("dn_bk1", n);
+        uint32_t* i2 = ctx.arena.get<uint32_t>("dn_pi2", n);
+        uint32_t* i3 = ctx.arena.get<uint32_t>("dn_pi3", n);
+        double* p1s = ctx.arena.get<double>("dn_p1s", n);
+        double* bp1 = ctx.arena.get<double>("dn_bp1", 2 * nband);
+        auto sort64 = [&](uint32_t*& sid) {
+            rocprim::double_buffer<unsigned long long> kb(k0, k1);
+            rocprim::double_buffer<uint32_t> vb(i0, i1);
+            size_t tb = 0;
+            PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)n, 0u, 64u, s));
+            void* tmp = ctx.arena.get<char>("dn_sort_tmp", tb);
+            PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)n, 0u, 64u, s));
+            sid = vb.current();
+        };
+        // (1) p1 order -> band of each point, band p1 ranges
+        uint32_t* sid1 = nullptr;
+        hipLaunchKernelGGL(proj_key_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d, ax1, n,
+                           k0, i0);
+        sort64(sid1);
+        hipLaunchKernelGGL(band_of_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, sid1, n, band, bof);
+        hipLaunchKernelGGL(proj_gather_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d, ax1,
+                           sid1, n, p1s);
+        hipLaunchKernelGGL(band_range_kernel, dim3(nblocks(nband)), dim3(kBlock), 0, s, p1s, n,
+                           band, nband, bp1);
+        // (2) p2 order, then stably by band
+        uint32_t* sid2 = nullptr;
+        hipLaunchKernelGGL(proj_key_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d, ax2, n,
+                           k0, i0);
+        sort64(sid2);
+        hipLaunchKernelGGL(band_key_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, bof, sid2, n, bk0);
+        PD_HIP(hipMemcpyAsync(i2, sid2, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, s));
+        unsigned bbits = 1;
+        while ((1u << bbits) < nband) ++bbits;
+        const uint32_t* sid = nullptr;
+        {
+            rocprim::double_buffer<uint32_t> kb(bk0, bk1);
+            rocprim::double_buffer<uint32_t> vb(i2, i3);
+            size_t tb = 0;
+            PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)n, 0u, bbits, s));
+            void* tmp = ctx.arena.get<char>("dn_sort_tmp2", tb);
+            PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)n, 0u, bbits, s));
+            sid = vb.current();
+        }
+        double* ps = ctx.arena.get<double>("dn_proj", n);
+        hipLaunchKernelGGL(proj_gather_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d, ax2,
+                           sid, n, ps);
+        PD_HIP(hipGetLastError());
+        const FragSet Fs = make_frags<T>(ctx, "dn_all", X, d, sid, n, G, s);
+        uint32_t* cs = ctx.arena.get<uint32_t>("dn_cnt_sorted", n);
+        dtiles = ctx.arena.get<unsigned long long>("dn_tiles", 1);
+        PD_HIP(hipMemsetAsync(dtiles, 0, sizeof(unsigned long long), s));
+        A.I = A.J = Fs;
+        A.p2 = ps;
+        A.bp1 = bp1;
+        A.band = band;
+        A.nband = nband;
+        A.win = a.eps * (1.0 + 1.0 / 1048576.0) + 16.0 * amax * DBL_EPSILON;
+        A.tiles = dtiles;
+        A.cnt = cs;
+        run_tiles<T, kCount>(A, G, a.metric, s);
+        hipLaunchKernelGGL(scatter_cnt_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, cs, sid, n,
+                           cnt);
+        PD_HIP(hipGetLastError());
+        A.p2 = nullptr;
+        A.tiles = nullptr;
+    } else {
+        const FragSet Fall = make_frags<T>(ctx, "dn_all", X, d, nullptr, n, G, s);
+        A.I = A.J = Fall;
+        A.cnt = cnt;
+        run_tiles<T, kCount>(A, G, a.metric, s);
+    }
     A.cnt = cnt;
-    run_tiles<T, kCount>(A, G, a.metric, s);
     ev.mark();   // 1
 
     // ---- core-core components
@@ -641,7 +884,12 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
     a.n_clusters = rank_labels_count(ctx, s);
     ctx.t.records = n;
     ctx.t.core_records = mc;
-    ctx.t.cells_n = 0;
+    ctx.t.cells_n = 0;   // dense: wave tiles computed by the count pass (timing on)
+    if (dtiles && ctx.timing) {
+        unsigned long long nt = 0;
+        PD_HIP(hipMemcpy(&nt, dtiles, sizeof(nt), hipMemcpyDeviceToHost));
+        ctx.t.cells_n = (int64_t)nt;
+    }
     ctx.t.grid_cells = 0;
     if (ctx.timing) {
         ctx.t.count = ev.span(0, 1);

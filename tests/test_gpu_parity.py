@@ -525,6 +525,28 @@ def test_dense_exact_ties(native):
         assert np.array_equal(lab, lab_o), eps
 
 
+@pytest.mark.parametrize("n,eps", [(1_000_000, 0.114028), (300_000, 0.3), (60_000, 0.02)])
+def test_dense_prune_full_size(native, n, eps):
+    """Projection pruning of the count pass is exact: at C3's full size (and
+    with wide / tiny windows over many bands) the pruned and the all-pairs
+    runs give identical counts, core flags and labels — a size-independent
+    property where the CPU oracle is too slow to run."""
+    from pypardis_amd import synth
+    X = synth.make_config("C3", n=n)[0]
+    ctx = native.context()
+    lab0, core0, ncl0, cnt0 = _cluster(native, X, eps, 10, full=True)
+    ctx.set_option(native.PD_OPT_DENSE_PRUNE, 0)
+    try:
+        lab1, core1, ncl1, cnt1 = _cluster(native, X, eps, 10, full=True)
+    finally:
+        ctx.set_option(native.PD_OPT_DENSE_PRUNE, 1)
+    assert np.array_equal(cnt0, cnt1)
+    assert np.array_equal(core0, core1)
+    assert np.array_equal(lab0, lab1) and ncl0 == ncl1
+    if eps > 0.1:   # the tiny window has no core points, only counts
+        assert int(core0.sum()) > 0
+
+
 def test_dense_edge_cases(native):
     from pypardis_amd import DBSCAN
     X = np.full((300, 16), 0.25, np.float32)   # identical points

@@ -212,6 +212,11 @@ __device__ __forceinline__ void tile_hit(const TileArgs<T>& A, uint32_t i, uint3
 // The fp32 rounding of the rearrangement is < 2^-22 s, inside the band's
 // margin.  The count pass tallies in and maybe per lane and builds the band
 // bits (maybe && !in, re-tested exactly) only for tiles where they differ.
+// Threads per tile block: 4 waves share each streamed tile.  (8 waves per
+// block halve the streamed bytes per MFMA but measured slower on C3: 125 vs
+// 110 ms — an 8-wave barrier per tile, one block per CU.)
+constexpr int tile_threads(int) { return 256; }
+
 template <int KS>
 struct TileLds {
     bf16x8 hi[2][2][KS][64];   // [buffer][row group][k-step][lane]
@@ -220,12 +225,13 @@ struct TileLds {
 };
 
 template <typename T, int MODE, int KS>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS >= 8 ? 1 : 2))) void tile_kernel(TileArgs<T> A) {
-    constexpr int NCH = 2 * 2 * KS * 64 / kBlock;   // 16-byte chunks per thread (hi + lo)
-    static_assert(NCH >= 1 && NCH * kBlock == 2 * 2 * KS * 64, "tile staging split");
+__global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_eu(KS >= 8 ? 1 : 2))) void tile_kernel(TileArgs<T> A) {
+    constexpr int TB = tile_threads(KS);
+    constexpr int NC = 2 * 2 * KS * 64;          // 16-byte chunks per tile (hi + lo)
+    constexpr int NCH = (NC + TB - 1) / TB;      // per thread
     __shared__ TileLds<KS> S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t blk_i0 = xcd_block(blockIdx.x, gridDim.x) * (kBlock / 64) * kTile;
+    const uint32_t blk_i0 = xcd_block(blockIdx.x, gridDim.x) * (TB / 64) * kTile;
     const uint32_t i0 = blk_i0 + wave * kTile;
     const bool wave_ok = i0 < A.I.m;
     const int col = lane & 31, h = lane >> 5;
@@ -257,7 +263,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS >= 8 
     __shared__ uint32_t nseg_s;
     if (A.p2 && blk_i0 < A.I.m) {
         const uint32_t b = blk_i0 / A.band;   // a block lies in one band
-        const uint32_t last = min(blk_i0 + (uint32_t)(kBlock / 64) * kTile, A.I.m) - 1u;
+        const uint32_t last = min(blk_i0 + (uint32_t)(TB / 64) * kTile, A.I.m) - 1u;
         const double lo1 = A.bp1[2 * b] - A.win, hi1 = A.bp1[2 * b + 1] + A.win;
         const double lo2 = A.p2[blk_i0] - A.win, hi2 = A.p2[last] + A.win;
         // bands are p1-ordered: both ends of their ranges ascend
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS >= 8 
             bhi = l;
         }
         const uint32_t ns = bhi - blo;   // <= nband <= kMaxSeg
-        for (uint32_t t = threadIdx.x; t < ns; t += kBlock) {
+        for (uint32_t t = threadIdx.x; t < ns; t += TB) {
             const uint32_t bb = blo + t;
             const uint32_t r0 = bb * A.band, r1 = min(r0 + A.band, A.J.m);
             const uint32_t sl = p_bound(A.p2, r0, r1, lo2, false);
@@ -303,14 +309,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS >= 8 
         }
         return false;
     };
-    // staging: thread k moves 16-byte chunks c = k + q * kBlock of the tile
+    // staging: thread k moves 16-byte chunks c = k + q * TB of the tile
     // (hi then lo), plus one norm per thread < 64
     bf16x8 stg[NCH];
     float stn = 0.0f;
     auto fetch = [&](uint32_t j0) {
 #pragma unroll
         for (int q = 0; q < NCH; ++q) {
-            const int c = threadIdx.x + q * kBlock;        // [0, 2 * 2 * KS * 64)
+            const int c = threadIdx.x + q * TB;        // [0, 2 * 2 * KS * 64)
+            if (NC % TB != 0 && c >= NC) break;
             const int half = c / (2 * KS * 64);            // 0 hi, 1 lo
             const int w = c % (2 * KS * 64);               // (row group, k-step, lane)
             const uint64_t o = (uint64_t)(j0 / 32) * KS * 64 + w;
@@ -321,7 +328,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KS >= 8 
     auto commit = [&](int buf) {
 #pragma unroll
         for (int q = 0; q < NCH; ++q) {
-            const int c = threadIdx.x + q * kBlock;
+            const int c = threadIdx.x + q * TB;
+            if (NC % TB != 0 && c >= NC) break;
             const int half = c / (2 * KS * 64);
             const int w = c % (2 * KS * 64);
             bf16x8* dst = half ? &S.lo[buf][0][0][0] : &S.hi[buf][0][0][0];
@@ -657,12 +665,16 @@ void run_tiles(const TileArgs<T>& A, const Geometry& G, int metric, hipStream_t 
     if (A.I.m == 0 || A.J.m == 0) return;
     if (G.mfma) {
         const unsigned waves = (A.I.m + kTile - 1) / kTile;
-        const dim3 grid(nblocks(waves, kBlock / 64));
+        auto launch = [&](auto ks) {
+            constexpr int KS = decltype(ks)::value, TB = tile_threads(KS);
+            hipLaunchKernelGGL((tile_kernel<T, MODE, KS>), dim3(nblocks(waves, TB / 64)), dim3(TB),
+                               0, s, A);
+        };
         switch (G.KS) {
-            case 1: hipLaunchKernelGGL((tile_kernel<T, MODE, 1>), grid, dim3(kBlock), 0, s, A); break;
-            case 2: hipLaunchKernelGGL((tile_kernel<T, MODE, 2>), grid, dim3(kBlock), 0, s, A); break;
-            case 4: hipLaunchKernelGGL((tile_kernel<T, MODE, 4>), grid, dim3(kBlock), 0, s, A); break;
-            default: hipLaunchKernelGGL((tile_kernel<T, MODE, 8>), grid, dim3(kBlock), 0, s, A);
+            case 1: launch(std::integral_constant<int, 1>{}); break;
+            case 2: launch(std::integral_constant<int, 2>{}); break;
+            case 4: launch(std::integral_constant<int, 4>{}); break;
+            default: launch(std::integral_constant<int, 8>{});
         }
     } else if (metric == 0) {
         hipLaunchKernelGGL((brute_kernel<T, MODE, 0>), dim3(nblocks(A.I.m)), dim3(kBlock), 0, s, A);
@@ -755,7 +767,7 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
             ax1 = wd[0].second;
             if (d > 1) ax2 = wd[1].second;
         }
-        uint32_t band = 16384;
+        uint32_t band = 16384;   // a multiple of every tile block's rows
         while ((n + band - 1) / band > (uint32_t)kMaxSeg) band *= 2;
         const uint32_t nband = (n + band - 1) / band;
         unsigned long long* k0 = ctx.arena.get<unsigned long long>("dn_pk0", n);

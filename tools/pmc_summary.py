@@ -15,6 +15,9 @@ from collections import defaultdict
 
 
 def short(name):
+    m = re.search(r"tile_kernel<\w+, (\d)", name)   # dense tiles: one entry per mode
+    if m:
+        return "tile_kernel_m" + m.group(1)
     m = re.search(r"(\w+_kernel)\b", name)
     if m:
         return m.group(1)

@@ -231,7 +231,22 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
     constexpr int NCH = (NC + TB - 1) / TB;      // per thread
     __shared__ TileLds<KS> S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t blk_i0 = xcd_block(blockIdx.x, gridDim.x) * (TB / 64) * kTile;
+    // block -> query rows.  Pruned count: bands are dealt round-robin to the
+    // 8 XCDs (dispatch puts block id b on XCD b % 8), a band's blocks kept
+    // together on one XCD (its L2 serves their overlapping windows); bands
+    // near the middle of the first axis have larger windows, so contiguous
+    // runs of bands per XCD would leave the XCDs unbalanced (106 -> 88 ms on
+    // C3; handing bands out centre-first measured 91 ms).
+    uint32_t lblk;
+    if (A.p2) {
+        const uint32_t bpb = A.band / ((TB / 64) * kTile);   // blocks per band
+        const uint32_t x = blockIdx.x % 8u, k = blockIdx.x / 8u;
+        lblk = (x + 8u * (k / bpb)) * bpb + k % bpb;
+    } else {
+        lblk = xcd_block(blockIdx.x, gridDim.x);
+    }
+    const uint32_t blk_i0 = lblk * (TB / 64) * kTile;
+    if (blk_i0 >= A.I.m) return;   // spare block of the pruned grid (whole block, no barrier yet)
     const uint32_t i0 = blk_i0 + wave * kTile;
     const bool wave_ok = i0 < A.I.m;
     const int col = lane & 31, h = lane >> 5;
@@ -311,9 +326,14 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
     };
     // staging: thread k moves 16-byte chunks c = k + q * TB of the tile
     // (hi then lo), plus one norm per thread < 64
-    bf16x8 stg[NCH];
-    float stn = 0.0f;
-    auto fetch = [&](uint32_t j0) {
+    // Two register stages: the tile two ahead is in flight while the next
+    // one is committed (a streamed tile often misses L2 under pruning)
+    struct Stage {
+        bf16x8 v[NCH];
+        float n;
+    };
+    Stage stA, stB;
+    auto fetch = [&](Stage& st, uint32_t j0) {
 #pragma unroll
         for (int q = 0; q < NCH; ++q) {
             const int c = threadIdx.x + q * TB;        // [0, 2 * 2 * KS * 64)
@@ -321,11 +341,11 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
             const int half = c / (2 * KS * 64);            // 0 hi, 1 lo
             const int w = c % (2 * KS * 64);               // (row group, k-step, lane)
             const uint64_t o = (uint64_t)(j0 / 32) * KS * 64 + w;
-            stg[q] = half ? A.J.lo[o] : A.J.hi[o];
+            st.v[q] = half ? A.J.lo[o] : A.J.hi[o];
         }
-        if (threadIdx.x < kTile) stn = A.J.norm[j0 + threadIdx.x];
+        if (threadIdx.x < kTile) st.n = A.J.norm[j0 + threadIdx.x];
     };
-    auto commit = [&](int buf) {
+    auto commit = [&](const Stage& st, int buf) {
 #pragma unroll
         for (int q = 0; q < NCH; ++q) {
             const int c = threadIdx.x + q * TB;
@@ -333,22 +353,26 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
             const int half = c / (2 * KS * 64);
             const int w = c % (2 * KS * 64);
             bf16x8* dst = half ? &S.lo[buf][0][0][0] : &S.hi[buf][0][0][0];
-            dst[w] = stg[q];
+            dst[w] = st.v[q];
         }
-        if (threadIdx.x < kTile) S.nta[buf][threadIdx.x] = -((1.0f + kBandC) * 0.5f) * stn;
+        if (threadIdx.x < kTile) S.nta[buf][threadIdx.x] = -((1.0f + kBandC) * 0.5f) * st.n;
     };
+    // cursors: current tile (in LDS buf), next (in `ready`), the one after
     uint32_t sg = 0, j0 = seg_lo[0];
     bool have = seek(sg, j0);
     if (have) {
-        fetch(j0);
-        commit(0);
+        fetch(stA, j0);
+        commit(stA, 0);
     }
+    uint32_t sn = sg, jn = j0 + kTile;
+    bool more = have && seek(sn, jn);
+    if (more) fetch(stB, jn);
     __syncthreads();
     int buf = 0;
-    while (have) {
-        uint32_t sn = sg, jn = j0 + kTile;
-        const bool more = seek(sn, jn);
-        if (more) fetch(jn);
+    auto step = [&](Stage& ready, Stage& spare) {
+        uint32_t sf = sn, jf = jn + kTile;
+        const bool far = more && seek(sf, jf);
+        if (far) fetch(spare, jf);
         // link: only j > i; tiles wholly below this wave's diagonal are skipped
         const bool compute = wave_ok && !(MODE == kLink && j0 + kTile <= i0);
         if (compute) {
@@ -455,12 +479,20 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
                 }
             }
         }
-        if (more) commit(buf ^ 1);
+        if (more) commit(ready, buf ^ 1);
         __syncthreads();
         sg = sn;
         j0 = jn;
         have = more;
+        sn = sf;
+        jn = jf;
+        more = far;
         buf ^= 1;
+    };
+    while (have) {
+        step(stB, stA);
+        if (!have) break;
+        step(stA, stB);
     }
     if (A.tiles && lane == 0 && ntiles) atomicAdd(A.tiles, (unsigned long long)ntiles);
     // lanes l and l + 32 hold the same query column
@@ -667,8 +699,10 @@ void run_tiles(const TileArgs<T>& A, const Geometry& G, int metric, hipStream_t 
         const unsigned waves = (A.I.m + kTile - 1) / kTile;
         auto launch = [&](auto ks) {
             constexpr int KS = decltype(ks)::value, TB = tile_threads(KS);
-            hipLaunchKernelGGL((tile_kernel<T, MODE, KS>), dim3(nblocks(waves, TB / 64)), dim3(TB),
-                               0, s, A);
+            // pruned count: 8 x ceil(bands / 8) x blocks per band (tile_kernel)
+            const unsigned grid = A.p2 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (TB / 64 * kTile))
+                                       : nblocks(waves, TB / 64);
+            hipLaunchKernelGGL((tile_kernel<T, MODE, KS>), dim3(grid), dim3(TB), 0, s, A);
         };
         switch (G.KS) {
             case 1: launch(std::integral_constant<int, 1>{}); break;

@@ -156,20 +156,23 @@ struct TileArgs {
     uint32_t* par;         // kLink: union-find over the (I = J) rows
     const uint32_t* keyJ;  // kBorder: cluster key per J row
     uint32_t* best;        // kBorder: smallest adjacent key per I row
-    // projection pruning (count pass, I = J): rows grouped into bands of
-    // `band` rows by their rank in coordinate p1, sorted by coordinate p2
-    // within a band.  A pair whose p1 or p2 differ by more than win cannot
-    // be within eps (|x_k - y_k| <= |x - y|), so a block streams, per band
-    // whose p1 range meets its own widened by win, only the run of rows whose
-    // p2 lies within win of its rows' p2 range.  p2: null = no pruning.
-    const double* p2;           // [m] p2 of each row
+    // projection pruning (count pass, I = J) over three coordinates p1, p2,
+    // p3: rows in bands of `band` rows by their p1 rank, each band in
+    // sub-bands of `sub` rows by p2 rank, sorted by p3 within a sub-band.  A
+    // pair whose p1, p2 or p3 differ by more than win cannot be within eps
+    // (|x_k - y_k| <= |x - y|), so a block streams, per sub-band whose p1
+    // and p2 ranges meet its own widened by win, only the run of rows whose
+    // p3 lies within win of its rows' p3 range.  p3: null = no pruning.
+    const double* p3;           // [m] p3 of each row
     const double* bp1;          // [2 * nband] p1 range (lo, hi) of each band
-    uint32_t band, nband;
+    const double* bp2;          // [2 * nband * nsub] p2 range of each sub-band
+    uint32_t band, nband, sub, nsub;
     double win;
     unsigned long long* tiles;  // wave tiles computed (null: not counted)
 };
 
-constexpr int kMaxSeg = 256;   // bands a block can stream (host keeps nband <= this)
+constexpr int kMaxBand = 256;   // bands (host keeps nband <= this)
+constexpr int kMaxSeg = 1024;   // sub-band segments a block keeps (else one per band)
 
 // First index in the ascending p[lo, hi) with p[k] >= v (upper: > v).
 __device__ __forceinline__ uint32_t p_bound(const double* __restrict__ p, uint32_t lo, uint32_t hi,
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
     // runs of bands per XCD would leave the XCDs unbalanced (106 -> 88 ms on
     // C3; handing bands out centre-first measured 91 ms).
     uint32_t lblk;
-    if (A.p2) {
+    if (A.p3) {
         const uint32_t bpb = A.band / ((TB / 64) * kTile);   // blocks per band
         const uint32_t x = blockIdx.x % 8u, k = blockIdx.x / 8u;
         lblk = (x + 8u * (k / bpb)) * bpb + k % bpb;
@@ -276,13 +279,19 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
     // all of J, from the diagonal (link), or one per band in the window
     __shared__ uint32_t seg_lo[kMaxSeg], seg_hi[kMaxSeg];
     __shared__ uint32_t nseg_s;
-    if (A.p2 && blk_i0 < A.I.m) {
-        const uint32_t b = blk_i0 / A.band;   // a block lies in one band
+    __shared__ uint32_t bk_lo[kMaxBand], bk_off[kMaxBand + 1];
+    __shared__ uint32_t fallback_s;
+    if (A.p3 && blk_i0 < A.I.m) {
+        const uint32_t b = blk_i0 / A.band;                 // a block lies in one band
+        const uint32_t k = (blk_i0 - b * A.band) / A.sub;   // ... and one sub-band
         const uint32_t last = min(blk_i0 + (uint32_t)(TB / 64) * kTile, A.I.m) - 1u;
         const double lo1 = A.bp1[2 * b] - A.win, hi1 = A.bp1[2 * b + 1] + A.win;
-        const double lo2 = A.p2[blk_i0] - A.win, hi2 = A.p2[last] + A.win;
-        // bands are p1-ordered: both ends of their ranges ascend
-        uint32_t blo = 0, bhi = A.nband;
+        const uint64_t kb = (uint64_t)b * A.nsub + k;
+        const double lo2 = A.bp2[2 * kb] - A.win, hi2 = A.bp2[2 * kb + 1] + A.win;
+        const double lo3 = A.p3[blk_i0] - A.win, hi3 = A.p3[last] + A.win;
+        // bands are p1-ordered, sub-bands p2-ordered: both ends of their
+        // ranges ascend
+        uint32_t blo, bhi;
         {
             uint32_t l = 0, h = A.nband;
             while (l < h) {
@@ -290,7 +299,6 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
                 if (A.bp1[2 * mid + 1] < lo1) l = mid + 1; else h = mid;
             }
             blo = l;
-            l = blo;
             h = A.nband;
             while (l < h) {
                 const uint32_t mid = (l + h) >> 1;
@@ -298,16 +306,67 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
             }
             bhi = l;
         }
-        const uint32_t ns = bhi - blo;   // <= nband <= kMaxSeg
+        const uint32_t ns = bhi - blo;   // <= nband <= kMaxBand
+        // (1) per candidate band: its candidate sub-bands [klo, khi)
         for (uint32_t t = threadIdx.x; t < ns; t += TB) {
             const uint32_t bb = blo + t;
             const uint32_t r0 = bb * A.band, r1 = min(r0 + A.band, A.J.m);
-            const uint32_t sl = p_bound(A.p2, r0, r1, lo2, false);
-            const uint32_t sh = p_bound(A.p2, sl, r1, hi2, true);
-            seg_lo[t] = sl < sh ? (sl & ~(uint32_t)(kTile - 1)) : sh;
-            seg_hi[t] = sh;
+            const uint32_t nsb = (r1 - r0 + A.sub - 1) / A.sub;
+            const double* q = A.bp2 + 2ull * bb * A.nsub;
+            uint32_t l = 0, h = nsb;
+            while (l < h) {
+                const uint32_t mid = (l + h) >> 1;
+                if (q[2 * mid + 1] < lo2) l = mid + 1; else h = mid;
+            }
+            const uint32_t klo = l;
+            h = nsb;
+            while (l < h) {
+                const uint32_t mid = (l + h) >> 1;
+                if (q[2 * mid] <= hi2) l = mid + 1; else h = mid;
+            }
+            bk_lo[t] = klo;
+            bk_off[t + 1] = l - klo;
         }
-        if (threadIdx.x == 0) nseg_s = ns;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            bk_off[0] = 0;
+            for (uint32_t t = 0; t < ns; ++t) {
+                acc += bk_off[t + 1];
+                bk_off[t + 1] = acc;
+            }
+            fallback_s = acc > (uint32_t)kMaxSeg ? 1u : 0u;
+            nseg_s = acc > (uint32_t)kMaxSeg ? ns : acc;
+        }
+        __syncthreads();
+        if (!fallback_s) {
+            // (2) one segment per candidate sub-band: its rows within the p3 window
+            const uint32_t total = nseg_s;
+            for (uint32_t sg = threadIdx.x; sg < total; sg += TB) {
+                uint32_t l = 0, h = ns;   // band slot t: bk_off[t] <= sg < bk_off[t + 1]
+                while (l < h) {
+                    const uint32_t mid = (l + h) >> 1;
+                    if (bk_off[mid + 1] <= sg) l = mid + 1; else h = mid;
+                }
+                const uint32_t bb = blo + l, kk = bk_lo[l] + (sg - bk_off[l]);
+                const uint32_t bend = min(bb * A.band + A.band, A.J.m);
+                const uint32_t r0 = bb * A.band + kk * A.sub, r1 = min(r0 + A.sub, bend);
+                const uint32_t sl = p_bound(A.p3, r0, r1, lo3, false);
+                const uint32_t sh = p_bound(A.p3, sl, r1, hi3, true);
+                seg_lo[sg] = sl < sh ? (sl & ~(uint32_t)(kTile - 1)) : sh;
+                seg_hi[sg] = sh;
+            }
+        } else {
+            // too many: the candidate sub-bands of each band as one run
+            for (uint32_t t = threadIdx.x; t < ns; t += TB) {
+                const uint32_t bb = blo + t, n_k = bk_off[t + 1] - bk_off[t];
+                const uint32_t bend = min(bb * A.band + A.band, A.J.m);
+                const uint32_t r0 = bb * A.band + bk_lo[t] * A.sub;
+                const uint32_t r1 = min(r0 + n_k * A.sub, bend);
+                seg_lo[t] = n_k ? r0 : r1;
+                seg_hi[t] = r1;
+            }
+        }
     } else if (threadIdx.x == 0) {
         seg_lo[0] = MODE == kLink ? blk_i0 : 0u;
         seg_hi[0] = A.J.m;
@@ -618,6 +677,34 @@ __global__ __launch_bounds__(kBlock) void band_range_kernel(const double* __rest
     bp1[2 * b + 1] = p1s[min((b + 1) * band, n) - 1u];
 }
 
+// group (band * nsub + sub-band) of each point from its position in the
+// (band, p2) order; sub-band p2 ranges from the same order
+__global__ __launch_bounds__(kBlock) void sub_of_kernel(const uint32_t* __restrict__ sid, uint32_t n,
+                                                        uint32_t band, uint32_t sub, uint32_t nsub,
+                                                        uint32_t* __restrict__ grp) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t b = r / band;
+    grp[sid[r]] = b * nsub + (r - b * band) / sub;
+}
+
+__global__ __launch_bounds__(kBlock) void sub_range_kernel(const double* __restrict__ p2s, uint32_t n,
+                                                           uint32_t band, uint32_t sub,
+                                                           uint32_t nsub, uint32_t nband,
+                                                           double* __restrict__ bp2) {
+    const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+    if (g >= nband * nsub) return;
+    const uint32_t b = g / nsub, k = g % nsub;
+    const uint32_t r0 = b * band + k * sub, bend = min(b * band + band, n);
+    if (r0 >= bend) {   // past the last band's rows: never a candidate
+        bp2[2 * g] = 0.0;
+        bp2[2 * g + 1] = 0.0;
+        return;
+    }
+    bp2[2 * g] = p2s[r0];
+    bp2[2 * g + 1] = p2s[min(r0 + sub, bend) - 1u];
+}
+
 __global__ __launch_bounds__(kBlock) void scatter_cnt_kernel(const uint32_t* __restrict__ cs,
                                                              const uint32_t* __restrict__ sid,
                                                              uint32_t n, uint32_t* __restrict__ cnt) {
@@ -700,7 +787,7 @@ void run_tiles(const TileArgs<T>& A, const Geometry& G, int metric, hipStream_t 
         auto launch = [&](auto ks) {
             constexpr int KS = decltype(ks)::value, TB = tile_threads(KS);
             // pruned count: 8 x ceil(bands / 8) x blocks per band (tile_kernel)
-            const unsigned grid = A.p2 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (TB / 64 * kTile))
+            const unsigned grid = A.p3 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (TB / 64 * kTile))
                                        : nblocks(waves, TB / 64);
             hipLaunchKernelGGL((tile_kernel<T, MODE, KS>), dim3(grid), dim3(TB), 0, s, A);
         };
@@ -783,12 +870,12 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
     uint32_t* cnt = ctx.arena.get<uint32_t>("dn_cnt", n);
     unsigned long long* dtiles = nullptr;
     if (G.mfma && ctx.dense_prune) {
-        // rows in bands of the widest axis' rank, sorted by the second
-        // widest within a band; each block streams only the tiles of its
-        // projection window (TileArgs::p2).  The margin covers the fp64
-        // predicate: a pruned pair has one squared term above eps^2 by
-        // 2^-20, so sklearn's rounded sum exceeds eps^2 too.
-        int ax1 = 0, ax2 = d > 1 ? 1 : 0;
+        // rows in bands of the widest axis' rank, sub-bands of the second
+        // widest's rank, sorted by the third within a sub-band; each block
+        // streams only the tiles of its projection window (TileArgs::p3).
+        // The margin covers the fp64 predicate: a pruned pair has one squared
+        // term above eps^2 by 2^-20, so sklearn's rounded sum exceeds eps^2 too.
+        int ax[3] = {0, 1, 2};
         double amax = 0.0;
         {
             std::vector<std::pair<double, int>> wd;
@@ -798,63 +885,75 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
                 amax = std::max(amax, std::max(std::fabs(lo), std::fabs(hi)));
             }
             std::stable_sort(wd.begin(), wd.end());
-            ax1 = wd[0].second;
-            if (d > 1) ax2 = wd[1].second;
+            for (int q = 0; q < 3; ++q) ax[q] = wd[q].second;   // d > 4
         }
         uint32_t band = 16384;   // a multiple of every tile block's rows
-        while ((n + band - 1) / band > (uint32_t)kMaxSeg) band *= 2;
+        while ((n + band - 1) / band > (uint32_t)kMaxBand) band *= 2;
         const uint32_t nband = (n + band - 1) / band;
+        // sub-band rows: C3 sweep 256 / 512 / 1024 / 2048 / 4096 -> 89.1 / 82.0 /
+        // 81.9 / 77.3 / 85.1 ms (a narrower p2 range vs shorter p3 runs)
+        const uint32_t subr = 2048, nsub = band / subr;
         unsigned long long* k0 = ctx.arena.get<unsigned long long>("dn_pk0", n);
         unsigned long long* k1 = ctx.arena.get<unsigned long long>("dn_pk1", n);
         uint32_t* i0 = ctx.arena.get<uint32_t>("dn_pi0", n);
         uint32_t* i1 = ctx.arena.get<uint32_t>("dn_pi1", n);
         uint32_t* bof = ctx.arena.get<uint32_t>("dn_band_of", n);
+        uint32_t* grp = ctx.arena.get<uint32_t>("dn_grp", n);
         uint32_t* bk0 = ctx.arena.get<uint32_t>("dn_bk0", n);
         uint32_t* bk1 = ctx.arena.get<uint32_t>("dn_bk1", n);
         uint32_t* i2 = ctx.arena.get<uint32_t>("dn_pi2", n);
         uint32_t* i3 = ctx.arena.get<uint32_t>("dn_pi3", n);
-        double* p1s = ctx.arena.get<double>("dn_p1s", n);
+        double* pv = ctx.arena.get<double>("dn_p1s", n);
         double* bp1 = ctx.arena.get<double>("dn_bp1", 2 * nband);
-        auto sort64 = [&](uint32_t*& sid) {
+        double* bp2 = ctx.arena.get<double>("dn_bp2", 2ull * nband * nsub);
+        auto sort64 = [&](int axis) {   // ids in the order of coordinate `axis`
+            hipLaunchKernelGGL(proj_key_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d,
+                               axis, n, k0, i0);
             rocprim::double_buffer<unsigned long long> kb(k0, k1);
             rocprim::double_buffer<uint32_t> vb(i0, i1);
             size_t tb = 0;
             PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)n, 0u, 64u, s));
             void* tmp = ctx.arena.get<char>("dn_sort_tmp", tb);
             PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)n, 0u, 64u, s));
-            sid = vb.current();
+            return (const uint32_t*)vb.current();
         };
-        // (1) p1 order -> band of each point, band p1 ranges
-        uint32_t* sid1 = nullptr;
-        hipLaunchKernelGGL(proj_key_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d, ax1, n,
-                           k0, i0);
-        sort64(sid1);
-        hipLaunchKernelGGL(band_of_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, sid1, n, band, bof);
-        hipLaunchKernelGGL(proj_gather_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d, ax1,
-                           sid1, n, p1s);
-        hipLaunchKernelGGL(band_range_kernel, dim3(nblocks(nband)), dim3(kBlock), 0, s, p1s, n,
-                           band, nband, bp1);
-        // (2) p2 order, then stably by band
-        uint32_t* sid2 = nullptr;
-        hipLaunchKernelGGL(proj_key_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d, ax2, n,
-                           k0, i0);
-        sort64(sid2);
-        hipLaunchKernelGGL(band_key_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, bof, sid2, n, bk0);
-        PD_HIP(hipMemcpyAsync(i2, sid2, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, s));
-        unsigned bbits = 1;
-        while ((1u << bbits) < nband) ++bbits;
-        const uint32_t* sid = nullptr;
-        {
+        // stable re-sort of `ids` by key[id] (`bits` wide): the group order
+        auto regroup = [&](const uint32_t* ids, const uint32_t* key, unsigned bits) {
+            hipLaunchKernelGGL(band_key_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, key, ids, n,
+                               bk0);
+            PD_HIP(hipMemcpyAsync(i2, ids, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, s));
             rocprim::double_buffer<uint32_t> kb(bk0, bk1);
             rocprim::double_buffer<uint32_t> vb(i2, i3);
             size_t tb = 0;
-            PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)n, 0u, bbits, s));
+            PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)n, 0u, bits, s));
             void* tmp = ctx.arena.get<char>("dn_sort_tmp2", tb);
-            PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)n, 0u, bbits, s));
-            sid = vb.current();
-        }
+            PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)n, 0u, bits, s));
+            return (const uint32_t*)vb.current();
+        };
+        auto bits_for = [](uint32_t v) {
+            unsigned b = 1;
+            while ((1ull << b) < v) ++b;
+            return b;
+        };
+        // (1) p1 order -> band of each point, band p1 ranges
+        const uint32_t* sid1 = sort64(ax[0]);
+        hipLaunchKernelGGL(band_of_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, sid1, n, band, bof);
+        hipLaunchKernelGGL(proj_gather_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d, ax[0],
+                           sid1, n, pv);
+        hipLaunchKernelGGL(band_range_kernel, dim3(nblocks(nband)), dim3(kBlock), 0, s, pv, n,
+                           band, nband, bp1);
+        // (2) p2 order within bands -> sub-band (group) of each point, p2 ranges
+        const uint32_t* sid2 = regroup(sort64(ax[1]), bof, bits_for(nband));
+        hipLaunchKernelGGL(sub_of_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, sid2, n, band, subr,
+                           nsub, grp);
+        hipLaunchKernelGGL(proj_gather_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d, ax[1],
+                           sid2, n, pv);
+        hipLaunchKernelGGL(sub_range_kernel, dim3(nblocks(nband * nsub)), dim3(kBlock), 0, s, pv,
+                           n, band, subr, nsub, nband, bp2);
+        // (3) p3 order within groups: the final row order
+        const uint32_t* sid = regroup(sort64(ax[2]), grp, bits_for(nband * nsub));
         double* ps = ctx.arena.get<double>("dn_proj", n);
-        hipLaunchKernelGGL(proj_gather_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d, ax2,
+        hipLaunchKernelGGL(proj_gather_kernel<T>, dim3(nblocks(n)), dim3(kBlock), 0, s, X, d, ax[2],
                            sid, n, ps);
         PD_HIP(hipGetLastError());
         const FragSet Fs = make_frags<T>(ctx, "dn_all", X, d, sid, n, G, s);
@@ -862,10 +961,13 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
         dtiles = ctx.arena.get<unsigned long long>("dn_tiles", 1);
         PD_HIP(hipMemsetAsync(dtiles, 0, sizeof(unsigned long long), s));
         A.I = A.J = Fs;
-        A.p2 = ps;
+        A.p3 = ps;
         A.bp1 = bp1;
+        A.bp2 = bp2;
         A.band = band;
         A.nband = nband;
+        A.sub = subr;
+        A.nsub = nsub;
         A.win = a.eps * (1.0 + 1.0 / 1048576.0) + 16.0 * amax * DBL_EPSILON;
         A.tiles = dtiles;
         A.cnt = cs;
@@ -873,7 +975,7 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
         hipLaunchKernelGGL(scatter_cnt_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, cs, sid, n,
                            cnt);
         PD_HIP(hipGetLastError());
-        A.p2 = nullptr;
+        A.p3 = nullptr;
         A.tiles = nullptr;
     } else {
         const FragSet Fall = make_frags<T>(ctx, "dn_all", X, d, nullptr, n, G, s);

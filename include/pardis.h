@@ -79,8 +79,10 @@ enum pd_option {
     PD_OPT_BORDER_ROOTS = 10, /* batched border sweep: skip or stop early where the stencil's
                                 directory words hold at most one cluster root (tuning; same
                                 labels; default 0 — slower on C2) */
-    PD_OPT_DENSE_PRUNE = 11   /* d > 4 count pass: stream only the tiles inside the two-axis
-                                projection window (exact; default 1; 0 = all n^2 pairs) */
+    PD_OPT_DENSE_PRUNE = 11   /* d > 4 count pass: stream only the tiles inside the three-axis
+                                projection window (exact; default 1; 0 = all n^2 pairs;
+                                2 = per-band runs, the path a block takes when its segment
+                                list overflows — for tests) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -119,9 +119,10 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.screen = value != 0;
         else if (option == PD_OPT_SWEEP_STATS)
             ctx->c.sweep_stats = value != 0;
-        else if (option == PD_OPT_DENSE_PRUNE)
-            ctx->c.dense_prune = value != 0;
-        else if (option == PD_OPT_BORDER_ROOTS)
+        else if (option == PD_OPT_DENSE_PRUNE) {
+            if (value < 0 || value > 2) throw Error(PD_EINVAL, "dense prune is 0, 1 or 2");
+            ctx->c.dense_prune = (int)value;
+        } else if (option == PD_OPT_BORDER_ROOTS)
             ctx->c.border_roots = value != 0;
         else if (option == PD_OPT_SWEEP_VARIANT) {
             if (value < 0 || value > 7) throw Error(PD_EINVAL, "sweep variant is a 3-bit mask");

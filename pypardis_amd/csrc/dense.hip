@@ -167,6 +167,7 @@ struct TileArgs {
     const double* bp1;          // [2 * nband] p1 range (lo, hi) of each band
     const double* bp2;          // [2 * nband * nsub] p2 range of each sub-band
     uint32_t band, nband, sub, nsub;
+    uint32_t whole_bands;       // 1: one run per band (the overflow path), for tests
     double win;
     unsigned long long* tiles;  // wave tiles computed (null: not counted)
 };
@@ -335,8 +336,9 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
                 acc += bk_off[t + 1];
                 bk_off[t + 1] = acc;
             }
-            fallback_s = acc > (uint32_t)kMaxSeg ? 1u : 0u;
-            nseg_s = acc > (uint32_t)kMaxSeg ? ns : acc;
+            const bool fb = acc > (uint32_t)kMaxSeg || A.whole_bands;
+            fallback_s = fb ? 1u : 0u;
+            nseg_s = fb ? ns : acc;
         }
         __syncthreads();
         if (!fallback_s) {
@@ -968,6 +970,7 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
         A.nband = nband;
         A.sub = subr;
         A.nsub = nsub;
+        A.whole_bands = ctx.dense_prune == 2 ? 1u : 0u;
         A.win = a.eps * (1.0 + 1.0 / 1048576.0) + 16.0 * amax * DBL_EPSILON;
         A.tiles = dtiles;
         A.cnt = cs;

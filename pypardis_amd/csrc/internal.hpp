@@ -92,7 +92,7 @@ struct Ctx {
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
     bool border_roots = false;   // border sweep's single-root fast path (tuning)
-    bool dense_prune = true;     // dense count pass: projection-window tiles only
+    int dense_prune = 1;         // dense count pass: projection-window tiles only (2: per-band runs)
     int variant = 5;             // PD_OPT_SWEEP_VARIANT: batched count + border, row-wise link
     Timings t;
     PhaseState st;

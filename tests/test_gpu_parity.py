@@ -535,14 +535,15 @@ def test_dense_prune_full_size(native, n, eps):
     X = synth.make_config("C3", n=n)[0]
     ctx = native.context()
     lab0, core0, ncl0, cnt0 = _cluster(native, X, eps, 10, full=True)
-    ctx.set_option(native.PD_OPT_DENSE_PRUNE, 0)
-    try:
-        lab1, core1, ncl1, cnt1 = _cluster(native, X, eps, 10, full=True)
-    finally:
-        ctx.set_option(native.PD_OPT_DENSE_PRUNE, 1)
-    assert np.array_equal(cnt0, cnt1)
-    assert np.array_equal(core0, core1)
-    assert np.array_equal(lab0, lab1) and ncl0 == ncl1
+    for mode in (0, 2):   # all pairs; per-band runs (the segment-overflow path)
+        ctx.set_option(native.PD_OPT_DENSE_PRUNE, mode)
+        try:
+            lab1, core1, ncl1, cnt1 = _cluster(native, X, eps, 10, full=True)
+        finally:
+            ctx.set_option(native.PD_OPT_DENSE_PRUNE, 1)
+        assert np.array_equal(cnt0, cnt1), mode
+        assert np.array_equal(core0, core1), mode
+        assert np.array_equal(lab0, lab1) and ncl0 == ncl1, mode
     if eps > 0.1:   # the tiny window has no core points, only counts
         assert int(core0.sum()) > 0
 

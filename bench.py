@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--link-mode", type=int, default=None, help="PD_OPT_LINK_MODE override")
     ap.add_argument("--sweep-variant", type=int, default=None,
                     help="PD_OPT_SWEEP_VARIANT override (bit 0 count, 1 link, 2 border)")
+    ap.add_argument("--count-rotate", type=int, default=None,
+                    help="PD_OPT_COUNT_ROTATE override (0 = count sweeps always start at the row)")
+    ap.add_argument("--centre-window", type=int, default=None,
+                    help="PD_OPT_CENTRE_WINDOW override (link mode 3 centre-row union)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
@@ -72,17 +76,24 @@ def b_nc(records, cells, d):
     return records * per + (cells + 1) * 4, per
 
 
-def load_pmc(kernel="count_kernel"):
-    """Per-launch HBM bytes of `kernel` from the newest PMC summary that has it
-    (profiles/rNN_vMM_pmc_summary.json, newest = highest (round, version))."""
+def load_pmc(kernel="count_kernel", config="C2"):
+    """Per-launch HBM bytes of `kernel` from the newest PMC summary of the same
+    config that has it (profiles/rNN_vMM_pmc[_cK]_summary.json; no _cK tag =
+    C2; newest = highest (round, version))."""
     import re
 
     def order(f):
         m = re.search(r"r(\d+)_v(\d+)", os.path.basename(f))
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
 
+    def tag(f):
+        m = re.search(r"pmc_(c\d)_", os.path.basename(f))
+        return m.group(1).upper() if m else "C2"
+
     for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*pmc*.json")), key=order,
                     reverse=True):
+        if tag(f) != config:
+            continue
         try:
             k = json.load(open(f)).get(kernel)
         except Exception:
@@ -102,7 +113,8 @@ def cpu_baseline(cfg_name, n_sample, n_full):
                                         cfg.get("max_partitions") or 1)
     out = {"value": n_sample / secs, "unit": "points/s", "cores": workers, "kind": "port",
            "seconds": secs,
-           "sample": (f"{cfg_name} density-preserving slice, {n_sample} pts, "
+           "sample": (f"{cfg_name} {'sample of the same distribution (NOT density-preserving: ' if cfg_name == 'C4' else 'density-preserving slice'}"
+                      f"{'sparser than the full set, so the CPU rate is optimistic)' if cfg_name == 'C4' else ''}, {n_sample} pts, "
                       f"max_partitions={cfg.get('max_partitions')}: numpy KD + halo, "
                       f"sklearn 1.7.2 DBSCAN (algorithm='auto') per neighbourhood in a "
                       f"{workers}-process pool, 1 BLAS thread each (Spark local[*] emulation), "
@@ -135,24 +147,32 @@ def main():
 
     from pypardis_amd import DBSCAN, _native, synth
 
-    X, cfg = synth.make_config(args.config, n=args.points)
+    # C4 (1B points) is generated on the device: a host-side build of 1B
+    # points would dominate the run; the other configs are numpy
+    X, cfg = synth.make_config(args.config, n=args.points,
+                               device=dev if args.config == "C4" else "cpu")
     n, d = X.shape
     eps, ms, P = cfg["eps"], cfg["min_samples"], cfg.get("max_partitions") or 1
     ctx = _native.context(local_rank)
     if args.sweep_variant is not None:
         ctx.set_option(_native.PD_OPT_SWEEP_VARIANT, args.sweep_variant)
+    if args.centre_window is not None:
+        ctx.set_option(_native.PD_OPT_CENTRE_WINDOW, args.centre_window)
+    if args.count_rotate is not None:
+        ctx.set_option(_native.PD_OPT_COUNT_ROTATE, args.count_rotate)
     if args.link_mode is not None:
         ctx.set_option(_native.PD_OPT_LINK_MODE, args.link_mode)
     if world > 1:
         from pypardis_amd.distributed import NativeOps, train_sharded
         lo, hi = rank * n // world, (rank + 1) * n // world
-        Xd = torch.from_numpy(np.ascontiguousarray(X[lo:hi])).to(dev)
+        Xd = X[lo:hi].clone() if torch.is_tensor(X) else \
+            torch.from_numpy(np.ascontiguousarray(X[lo:hi])).to(dev)
         ops = NativeOps(dev)
 
         def step():
             return train_sharded(Xd, eps, ms, max_partitions=max(P, world), ops=ops)
     else:
-        Xd = torch.from_numpy(X).to(dev)
+        Xd = X if torch.is_tensor(X) else torch.from_numpy(X).to(dev)
 
         def step():
             return DBSCAN(eps=eps, min_samples=ms, max_partitions=P).train(Xd)
@@ -205,7 +225,7 @@ def main():
             variant = args.sweep_variant if args.sweep_variant is not None \
                 else _native.SWEEP_VARIANT_DEFAULT
             kname = "count2_kernel" if variant & 1 else "count_kernel"
-            pmc = load_pmc(kname)
+            pmc = load_pmc(kname, args.config)
             roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS,
                     "traffic": pmc["bytes_per_launch"] if pmc else None, "kernel": kname,
@@ -224,7 +244,7 @@ def main():
             alg = 2.0 * d * 64 * 64 * tiles
             exe = 3 * 2.0 * 64 * 64 * 16 * ks * tiles
             achieved = alg / (t_cnt * 1e-3) / 1e12
-            pmc = load_pmc("tile_kernel_m0")   # the count-pass launch
+            pmc = load_pmc("tile_kernel_m0", args.config)   # the count-pass launch
             roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS,
                     "traffic": pmc["bytes_per_launch"] if pmc else None,
@@ -257,7 +277,8 @@ def main():
             "vs_baseline": None,
             "dtype": dtype,
             "data": "synthetic",
-            "config": {"workload": f"{args.config}: {'blobs_noise' if d <= 4 else 'embeddings'} "
+            "config": {"workload": f"{args.config}: "
+                                   f"{'gps_skew' if args.config == 'C4' else 'blobs_noise' if d <= 4 else 'embeddings'} "
                                    f"n={n} d={d} eps={eps} min_samples={ms} max_partitions={P}",
                        "n_points": n, "d": d, "eps": eps, "min_samples": ms,
                        "max_partitions": P, "input": "fp32 device-resident",

@@ -82,7 +82,14 @@ enum pd_option {
     PD_OPT_DENSE_PRUNE = 11   /* d > 4 count pass: stream only the tiles inside the three-axis
                                 projection window (exact; default 1; 0 = all n^2 pairs;
                                 2 = per-band runs, the path a block takes when its segment
-                                list overflows — for tests) */
+                                list overflows — for tests) */,
+    PD_OPT_COUNT_ROTATE = 12  /* count sweep: a candidate list longer than this starts at
+                                record (r & ~255) when that lies in the query's own row, and
+                                wraps (dense cells: spreads the row-start hot spot; same
+                                counts, same labels); default 1024, 0 = never */,
+    PD_OPT_CENTRE_WINDOW = 13 /* link mode 3: forward candidates each core record tests in the
+                                centre-row union (a heuristic: the cell verify proves or tests
+                                every edge, so labels are the same); default 64, 0 = all */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -25,6 +25,8 @@ PD_OPT_SWEEP_STATS = 8
 PD_OPT_SWEEP_VARIANT = 9
 PD_OPT_BORDER_ROOTS = 10
 PD_OPT_DENSE_PRUNE = 11
+PD_OPT_COUNT_ROTATE = 12
+PD_OPT_CENTRE_WINDOW = 13
 SWEEP_VARIANT_DEFAULT = 5
 LINK_MODE_DEFAULT = 3
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",

@@ -1073,10 +1073,13 @@ __device__ __forceinline__ uint32_t bpos(uint32_t v, const uint32_t (&pre)[B],
     return v + o;
 }
 
+constexpr uint32_t kRotAlign = 256;
+
 template <typename T, int D, int M, bool ST>
 __global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs, uint32_t R,
                                                         Cells C, double eps, double eps2,
                                                         float lo, float hi, uint32_t ms, int full,
+                                                        uint32_t rot_min,
                                                         uint8_t* __restrict__ core,
                                                         uint32_t* __restrict__ mn_out,
                                                         uint32_t* __restrict__ cnt_out,
@@ -1096,12 +1099,29 @@ __global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs
             const int bt = (bq + NB / 2) % NB;   // centre batch first
             uint32_t pre[B], off[B];
             const uint32_t tot = batch_list<D, M>(C, Q, a, eps, bt, true, 0u, pre, off);
+            // a long list (dense cells): start at record r & ~(kRotAlign-1)
+            // when it lies in the query's centre row (the first row of the
+            // centre batch), and wrap.  The records of a dense row then do
+            // not all stream the same first lines (one hot L2 channel per
+            // row start), the early exit comes sooner (the block's records
+            // are in the query's own cell), and the smallest neighbour
+            // found is still near a shared record, so the initial forest
+            // stays shallow (one tree per aligned block, joined by the
+            // centre-row union)
+            uint32_t v0 = 0;
+            if (bq == 0 && tot > rot_min) {
+                const uint32_t vr = (r & ~(kRotAlign - 1u)) - off[0];
+                const uint32_t clen = B > 1 ? pre[B > 1 ? 1 : 0] : tot;   // centre row
+                v0 = vr < clen ? vr : 0u;
+            }
             for (uint32_t v = 0; v < tot; v += 4) {
                 uint32_t j[4];
                 T b[4][D];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    j[u] = v + u < tot ? bpos<B>(v + u, pre, off) : r;
+                    uint32_t w = v0 + v + u;
+                    w = w >= tot ? w - tot : w;
+                    j[u] = v + u < tot ? bpos<B>(w, pre, off) : r;
                     load_raw<T, D>(Xs, j[u], b[u]);
                 }
 #pragma unroll
@@ -1140,7 +1160,7 @@ constexpr uint32_t kMixed = 0xFFFFFFFEu;
 template <typename T, int D, int M>
 __global__ __launch_bounds__(kBlock) void centre_link_kernel(const T* __restrict__ Xs, uint32_t R,
                                                              Cells C, double eps, double eps2,
-                                                             float lo, float hi,
+                                                             float lo, float hi, uint32_t window,
                                                              uint32_t* __restrict__ par) {
     const uint32_t r = rec_index();
     if (r >= R || par[r] == kNone) return;   // not core
@@ -1152,10 +1172,15 @@ __global__ __launch_bounds__(kBlock) void centre_link_kernel(const T* __restrict
     const bool ok = row_keys<D, M>(Q, a, eps, NRows<D>::v / 2, k0, k1);
     const uint32_t s0 = C.cstart[dir_rank(C.dir[k0 >> 6], k0)];
     const uint32_t e0 = C.cstart[dir_rank(C.dir[k1 >> 6], k1)];
-    const uint32_t end = ok ? e0 : 0u;
     const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
     Linker<false> lk{par, uf_find_l1(par, r), {}};
     uint32_t j = s0 > r + 1 ? s0 : r + 1;
+    // at most `window` forward candidates: the union is only a
+    // heuristic (cell_verify proves or tests every core-core edge), and in a
+    // dense cell overlapping windows already join the whole row — an
+    // uncapped sweep is quadratic in the occupancy (C4 city centres)
+    const uint32_t cap = window > 0xFFFFFFFFu - j ? 0xFFFFFFFFu : j + window;
+    const uint32_t end = ok ? (e0 < cap ? e0 : cap) : 0u;
     for (; j + 4 <= end; j += 4) {
         T b0[D], b1[D], b2[D], b3[D];
         load_raw<T, D>(Xs, j, b0);
@@ -1233,19 +1258,33 @@ __global__ __launch_bounds__(kBlock) void word_root_kernel(const uint4* __restri
 // under one root (live) skip the distance test.
 template <typename T, int D, int M>
 __device__ __noinline__ void pair_block(const T* __restrict__ Xs, uint32_t s0, uint32_t e0,
-                                        uint32_t s1, uint32_t e1, bool same, double eps,
-                                        double eps2, float lo, float hi, uint32_t* par) {
+                                        uint32_t s1, uint32_t e1, bool same, bool uniform,
+                                        double eps, double eps2, float lo, float hi,
+                                        uint32_t* par) {
+    // uniform: two different cells, each under one root (the cell_root
+    // snapshot; later unions only merge trees), so the first pair found
+    // connected settles the whole block — a dense cell pair costs a few
+    // tests, not occupancy^2.  ra may go stale under concurrent unions: a
+    // match still proves a and b share a tree (trees only merge).
     for (uint32_t a = s0; a < e0; ++a) {
         if (ld_rlx(par + a) == kNone) continue;
         double av[D];
         load_rec<T, D>(Xs, a, av);
         const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, a, av, eps, eps2, lo, hi);
+        uint32_t ra = uf_find(par, a);
         for (uint32_t b = same ? a + 1 : s1; b < e1; ++b) {
             if (ld_rlx(par + b) == kNone) continue;
-            if (uf_find(par, a) == uf_find(par, b)) continue;
+            if (uf_find(par, b) == ra) {
+                if (uniform) return;
+                continue;
+            }
             T bv[D];
             load_raw<T, D>(Xs, b, bv);
-            if (pr(bv)) uf_unite(par, a, b);
+            if (pr(bv)) {
+                uf_unite(par, a, b);
+                if (uniform) return;
+                ra = uf_find(par, a);
+            }
         }
     }
 }
@@ -1279,8 +1318,9 @@ __global__ __launch_bounds__(kBlock) void cell_verify_kernel(
             lbuf[slot] = make_uint2(c, c2);
         } else {
             const bool same = c2 == c;
+            const bool uni = !same && rc != kMixed && croot[c2] != kMixed;
             pair_block<T, D, M>(Xs, s0, e0, same ? s0 : C.cstart[c2], same ? e0 : C.cstart[c2 + 1],
-                                same, eps, eps2, lo, hi, par);
+                                same, uni, eps, eps2, lo, hi, par);
         }
     };
     if (rc == kMixed) defer(c);
@@ -1372,8 +1412,9 @@ __global__ __launch_bounds__(kBlock) void cell_verify_kernel(
             plist[lbase + k] = pr;
         } else {
             const bool same = pr.x == pr.y;
+            const bool uni = !same && croot[pr.x] != kMixed && croot[pr.y] != kMixed;
             pair_block<T, D, M>(Xs, C.cstart[pr.x], C.cstart[pr.x + 1], C.cstart[pr.y],
-                                C.cstart[pr.y + 1], same, eps, eps2, lo, hi, par);
+                                C.cstart[pr.y + 1], same, uni, eps, eps2, lo, hi, par);
         }
     }
     if (stats && pairs) atomicAdd(stats + 7, (unsigned long long)pairs);
@@ -1399,8 +1440,9 @@ __global__ __launch_bounds__(kBlock) void pair_kernel(const T* __restrict__ Xs,
         if (pr.x != pr.y && ra != kMixed && rb != kMixed && uf_find(par, ra) == uf_find(par, rb))
             continue;
         const bool same = pr.x == pr.y;
+        const bool uni = !same && ra != kMixed && rb != kMixed;
         pair_block<T, D, M>(Xs, cstart[pr.x], cstart[pr.x + 1], cstart[pr.y], cstart[pr.y + 1],
-                            same, eps, eps2, lo, hi, par);
+                            same, uni, eps, eps2, lo, hi, par);
     }
 }
 
@@ -1600,11 +1642,11 @@ inline int xsub_of(const Ctx& ctx) { return ctx.xsub < 1 ? 1 : ctx.xsub; }
 // count, 1 link, 2 border) instead of the row-by-row one.
 template <typename T, int D, int M, bool ST>
 void launch_count(int variant, hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double eps,
-                  double eps2, float lo, float hi, uint32_t ms, int full, uint8_t* core,
-                  uint32_t* mn, uint32_t* cnt, unsigned long long* st) {
+                  double eps2, float lo, float hi, uint32_t ms, int full, uint32_t rot_min,
+                  uint8_t* core, uint32_t* mn, uint32_t* cnt, unsigned long long* st) {
     if (variant & 1)
         hipLaunchKernelGGL((count2_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
-                           C, eps, eps2, lo, hi, ms, full, core, mn, cnt, st);
+                           C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
     else
         hipLaunchKernelGGL((count_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
                            C, eps, eps2, lo, hi, ms, full, core, mn, cnt, st);
@@ -1783,11 +1825,15 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     if (R) {
         if (sst)
             launch_count<T, D, M, true>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
-                                        (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0, core,
+                                        (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
+                                        ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu,
+                                        core,
                                         mn, cnt_rec, sst);
         else
             launch_count<T, D, M, false>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
-                                         (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0, core,
+                                         (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
+                                        ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu,
+                                        core,
                                          mn, cnt_rec, sst);
     }
     PD_HIP(hipGetLastError());
@@ -1799,7 +1845,8 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         hipLaunchKernelGGL(init_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, mn, 1, par);
         hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
         hipLaunchKernelGGL((centre_link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs,
-                           R, C, eps, eps2, slo, shi, par);
+                           R, C, eps, eps2, slo, shi,
+                           ctx.centre_window ? (uint32_t)ctx.centre_window : 0xFFFFFFFFu, par);
         uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
         hipLaunchKernelGGL(cell_root_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, cstart, dncells,
                            par, croot);

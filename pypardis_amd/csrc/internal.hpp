@@ -89,6 +89,8 @@ struct Ctx {
     int link_mode = 3;           // 3 samples + cell verify; 0 init forest + jumps + union sweep; 2 union sweep only
     int jump_rounds = 4;
     int xsub = 2;                // axis-0 sub-cells per eps
+    int centre_window = 64;     // link mode 3: forward candidates per centre-row union (0: all)
+    int count_rotate = 1024;     // count sweep: lists longer than this start near the query (0: off)
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
     bool border_roots = false;   // border sweep's single-root fast path (tuning)

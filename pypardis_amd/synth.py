@@ -67,6 +67,56 @@ def embeddings(n, d=64, n_clusters=2000, clustered_frac=0.10, spread=0.1, seed=3
     return np.ascontiguousarray(out[perm])
 
 
+def gps_skew(n, seed=4, n_cities=10_000, zipf=1.1, sigma0=0.02, sigma_pow=0.3,
+             noise_frac=0.05, lon=(-180.0, 180.0), lat=(-60.0, 75.0), device="cpu",
+             chunk=1 << 25):
+    """GPS-like skewed 2-D density (lon, lat in degrees).
+
+    ``n_cities`` centres ~ U(box); city of rank r (1-based) has Zipf weight
+    r^-zipf and spread sigma0·r^sigma_pow degrees; (1 - noise_frac) of the
+    points are centre + N(0, sigma²I) (longitude wrapped, latitude clamped
+    into the box), the rest uniform in the box.  Each row independently is
+    noise or a city point, so rows are already interleaved.
+
+    Generated with torch on ``device`` in chunks (a 1B-point set is built on
+    the GPU in seconds); the stream is deterministic in (seed, device type),
+    so tests that compare against the oracle build the points on the CPU.
+    Returns a float32 torch tensor (n, 2) on ``device``.
+    """
+    import torch
+    n = int(n)
+    dev = torch.device(device)
+    g = torch.Generator(device=dev)
+    g.manual_seed(int(seed))
+    f64 = torch.float64
+    lo = torch.tensor([lon[0], lat[0]], dtype=f64, device=dev)
+    span = torch.tensor([lon[1] - lon[0], lat[1] - lat[0]], dtype=f64, device=dev)
+    centres = lo + span * torch.rand(n_cities, 2, generator=g, dtype=f64, device=dev)
+    r = torch.arange(1, n_cities + 1, dtype=f64, device=dev)
+    cdf = torch.cumsum(r ** -zipf, 0)
+    cdf = cdf / cdf[-1]
+    sig = sigma0 * r ** sigma_pow
+    out = torch.empty(n, 2, dtype=torch.float32, device=dev)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        m = e - s
+        u = torch.rand(m, generator=g, dtype=f64, device=dev)
+        city = torch.searchsorted(cdf, u).clamp_(max=n_cities - 1)
+        pts = centres[city] + sig[city, None] * torch.randn(m, 2, generator=g, dtype=f64,
+                                                             device=dev)
+        pts[:, 0] = torch.remainder(pts[:, 0] - lon[0], span[0]) + lon[0]
+        pts[:, 1].clamp_(lat[0], lat[1])
+        noise = torch.rand(m, generator=g, dtype=f64, device=dev) < noise_frac
+        uni = lo + span * torch.rand(m, 2, generator=g, dtype=f64, device=dev)
+        pts = torch.where(noise[:, None], uni, pts)
+        out[s:e] = pts.to(torch.float32)
+        # fp32 rounding can land a wrapped longitude on +180: keep it in [lo, hi)
+        col = out[s:e, 0]
+        col[col >= lon[1]] = lon[0]
+        del u, city, pts, noise, uni
+    return out
+
+
 C3_EPS = 0.114028   # tools/c3_eps.py: 0.11402826147489717, rounded to 6 digits
 
 # BASELINE.json configs (sizes, eps, min_samples, max_partitions)
@@ -83,10 +133,12 @@ CONFIGS = {
     # core; computed once by tools/c3_eps.py
     "C3": dict(n=1_000_000, d=64, n_clusters=2000, clustered_frac=0.10, spread=0.1,
                seed=3, eps=C3_EPS, min_samples=10, max_partitions=1),
+    # 1B points is the 8-GPU config; one MI355X holds it too (n < 2^30)
+    "C4": dict(n=1_000_000_000, d=2, seed=4, eps=0.001, min_samples=20, max_partitions=8),
 }
 
 
-def make_config(name, n=None):
+def make_config(name, n=None, device="cpu"):
     """Points for config ``name``; ``n`` < full size gives a density-preserving
     slice: side scaled by (n/N)^(1/d) and the number of centres by n/N, so
     both the noise density and the points per blob stay those of the full
@@ -94,6 +146,11 @@ def make_config(name, n=None):
     cfg = dict(CONFIGS[name])
     if name == "C0":
         return c0_demo(), cfg
+    if name == "C4":   # a sample of the same distribution (not density-preserving)
+        n = cfg["n"] if n is None else int(n)
+        cfg.update(n=n)
+        return gps_skew(n, seed=cfg["seed"], device=device).numpy() if device == "cpu" \
+            else gps_skew(n, seed=cfg["seed"], device=device), cfg
     if name == "C3":   # slices keep the points per cluster: fewer clusters
         N = cfg["n"]
         n = N if n is None else int(n)

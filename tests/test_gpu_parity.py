@@ -563,3 +563,63 @@ def test_dense_edge_cases(native):
     assert ncl == 0 and lab[0] == -1
     lab, core, ncl = _cluster(native, np.zeros((0, 12), np.float32), 0.5, 2)
     assert ncl == 0 and len(lab) == 0
+
+
+# ------------------------------------------------------------ C4: GPS-like skew
+@pytest.mark.parametrize("case", ["sample_200k", "dense_tile_100k"])
+def test_c4_skew_vs_oracle(native, case):
+    """C4 (SURVEY.md §8(d), 2-D GPS-like Zipf skew, eps=0.001°, min_samples=20):
+    a 200k sample of the 1B distribution (10k cities over the globe; mostly
+    sparse), and a dense tile (40 cities in 2°x1°, sigma0=0.002°: ~1000 points
+    per eps-cell at the densest city) — labels and core flags bit-exact
+    against the oracle at max_partitions=8 and 1."""
+    from pypardis_amd import DBSCAN, synth
+    if case == "sample_200k":
+        X, cfg = synth.make_config("C4", n=200_000)
+    else:
+        cfg = dict(synth.CONFIGS["C4"])
+        X = synth.gps_skew(100_000, seed=6, n_cities=40, sigma0=0.002, lon=(-1.0, 1.0),
+                           lat=(-0.5, 0.5)).numpy()
+    eps, ms = cfg["eps"], cfg["min_samples"]
+    want, core_w, _, nc = oracle.dbscan(X, eps, ms)
+    Xd = _dev(X)
+    for P in (8, 1):
+        m = DBSCAN(eps=eps, min_samples=ms, max_partitions=P).train(Xd)
+        assert m.n_clusters_ == nc, P
+        assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), want), P
+        assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_w), P
+    # dense-cell tuning knobs change the work order, never the answer:
+    # rotated count starts on every long list / never; centre-row union
+    # window of 1 candidate / unbounded
+    ctx = native.context()
+    for opt, val, default in ((native.PD_OPT_COUNT_ROTATE, 16, 1024),
+                              (native.PD_OPT_COUNT_ROTATE, 0, 1024),
+                              (native.PD_OPT_CENTRE_WINDOW, 1, 64),
+                              (native.PD_OPT_CENTRE_WINDOW, 0, 64)):
+        ctx.set_option(opt, val)
+        try:
+            m = DBSCAN(eps=eps, min_samples=ms, max_partitions=8).train(Xd)
+        finally:
+            ctx.set_option(opt, default)
+        assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), want), (opt, val)
+        assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_w), (opt, val)
+
+
+def test_c4_partition_invariance_large(native):
+    """Size-independent property on a 20M C4 sample (skewed density, up to
+    ~1000 points per eps-cell): labels and core flags do not depend on
+    max_partitions, and clusters are numbered in sklearn's order."""
+    from pypardis_amd import DBSCAN, synth
+    cfg = synth.CONFIGS["C4"]
+    Xd = synth.gps_skew(20_000_000, seed=cfg["seed"], device="cuda")
+    eps, ms = cfg["eps"], cfg["min_samples"]
+    ref = DBSCAN(eps=eps, min_samples=ms, max_partitions=1).train(Xd)
+    m = DBSCAN(eps=eps, min_samples=ms, max_partitions=8).train(Xd)
+    assert m.n_clusters_ == ref.n_clusters_
+    assert torch.equal(m.labels_, ref.labels_)
+    assert torch.equal(m.core_sample_mask_, ref.core_sample_mask_)
+    lab = ref.labels_.cpu().numpy()
+    idx = np.nonzero(ref.core_sample_mask_.cpu().numpy())[0]
+    u, fi = np.unique(lab[idx], return_index=True)
+    assert np.array_equal(u, np.arange(ref.n_clusters_))
+    assert np.all(np.diff(idx[fi]) > 0)

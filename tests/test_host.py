@@ -123,3 +123,20 @@ def test_as_points_forms_cpu():
     assert list(p.keys) == list(range(10, 0, -1))
     p = as_points((np.arange(10) * 2, X), device="cpu")
     assert p.keys[1] == 2
+
+
+def test_c4_generator():
+    """C4 GPS-like skew: deterministic in the seed, float32, inside the
+    lon/lat box, 5% uniform noise, heavy Zipf skew (the densest eps-cell of
+    a 2M sample holds > 50 points)."""
+    from pypardis_amd import synth
+    X, cfg = synth.make_config("C4", n=2_000_000)
+    Y, _ = synth.make_config("C4", n=2_000_000)
+    assert X.dtype == np.float32 and X.shape == (2_000_000, 2)
+    assert np.array_equal(X, Y)
+    assert X[:, 0].min() >= -180 and X[:, 0].max() < 180
+    assert X[:, 1].min() >= -60 and X[:, 1].max() <= 75
+    k = np.floor(X.astype(np.float64) / cfg["eps"]).astype(np.int64)
+    _, c = np.unique(k[:, 0] * 1_000_000 + k[:, 1], return_counts=True)
+    assert c.max() > 50
+    assert cfg["eps"] == 0.001 and cfg["min_samples"] == 20 and cfg["max_partitions"] == 8

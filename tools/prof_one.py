@@ -8,8 +8,9 @@ import torch
 from pypardis_amd import DBSCAN, synth
 
 n = int(os.environ.get("PROF_N", "100000000"))
-X, cfg = synth.make_config(os.environ.get("PROF_CFG", "C2"), n=n)
-Xd = torch.from_numpy(X).cuda()
+name = os.environ.get("PROF_CFG", "C2")
+X, cfg = synth.make_config(name, n=n, device="cuda" if name == "C4" else "cpu")
+Xd = X if torch.is_tensor(X) else torch.from_numpy(X).cuda()
 del X
 for _ in range(int(os.environ.get("PROF_REPS", "2"))):
     m = DBSCAN(eps=cfg["eps"], min_samples=cfg["min_samples"],

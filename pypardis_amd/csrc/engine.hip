@@ -107,7 +107,10 @@ __device__ __forceinline__ void wave_atomic_min(uint32_t* base, bool valid, uint
         const uint32_t lk = (uint32_t)__shfl((int)key, leader, 64);
         const bool mine = valid && ((active >> lane) & 1ull) && key == lk;
         const uint32_t m = wave_min_u32(mine ? val : kNone);
-        if (lane == leader) atomicMin(base + lk, m);
+        // keys only decrease: a stale read is >= the current minimum, so
+        // skipping when it is already <= m is exact; a hot root (a city of
+        // 1e8 records) then takes reads, not a queue of atomics
+        if (lane == leader && m < ld_rlx(base + lk)) atomicMin(base + lk, m);
         active &= ~__ballot(mine);
     }
 }
@@ -1202,30 +1205,74 @@ __global__ __launch_bounds__(kBlock) void centre_link_kernel(const T* __restrict
     }
 }
 
+// Per cell, the common root of its core records (kNone: no core record,
+// kMixed: several roots); also flattens: each core record gets its root
+// written back, so no separate flatten pass runs before (no unions run
+// concurrently, so a chain read by another cell stays valid).  One thread
+// per cell walks its records; a cell of more than kBigCell records goes to a
+// list handled by big_cell_root_kernel, one block per cell (a serial walk of
+// a ~1e4-record C4 city-centre cell took 44 ms).
+constexpr uint32_t kBigCell = 256;
+
+__device__ __forceinline__ uint32_t root_merge(uint32_t a, uint32_t b) {
+    return a == kNone ? b : (b == kNone ? a : (a == b ? a : kMixed));
+}
+
+__device__ __forceinline__ uint32_t core_root(uint32_t* __restrict__ par, uint32_t r) {
+    const uint32_t p0 = par[r];
+    if (p0 == kNone) return kNone;   // not core
+    uint32_t p = p0;
+    while (true) {
+        const uint32_t q = par[p];
+        if (q == p) break;
+        p = q;
+    }
+    if (p != p0) par[r] = p;
+    return p;
+}
+
 __global__ __launch_bounds__(kBlock) void cell_root_kernel(const uint32_t* __restrict__ cstart,
                                                            const uint32_t* __restrict__ ncells,
                                                            uint32_t* __restrict__ par,
-                                                           uint32_t* __restrict__ croot) {
-    // also flattens: each core record (all lie in one cell) gets its root
-    // written back, so no separate flatten pass runs before (no unions run
-    // concurrently, so a chain read by another cell stays valid)
+                                                           uint32_t* __restrict__ croot,
+                                                           uint32_t* __restrict__ big,
+                                                           uint32_t* __restrict__ nbig) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= *ncells) return;
-    const uint32_t e = cstart[c + 1];
-    uint32_t v = kNone;
-    for (uint32_t r = cstart[c]; r < e; ++r) {
-        const uint32_t p0 = par[r];
-        if (p0 == kNone) continue;   // not core
-        uint32_t p = p0;
-        while (true) {
-            const uint32_t q = par[p];
-            if (q == p) break;
-            p = q;
-        }
-        if (p != p0) par[r] = p;
-        v = v == kNone ? p : (p != v ? kMixed : v);
+    const uint32_t s = cstart[c], e = cstart[c + 1];
+    if (e - s > kBigCell) {
+        big[atomicAdd(nbig, 1u)] = c;
+        return;
     }
+    uint32_t v = kNone;
+    for (uint32_t r = s; r < e; ++r) v = root_merge(v, core_root(par, r));
     croot[c] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void big_cell_root_kernel(const uint32_t* __restrict__ cstart,
+                                                               const uint32_t* __restrict__ big,
+                                                               const uint32_t* __restrict__ nbig,
+                                                               uint32_t* __restrict__ par,
+                                                               uint32_t* __restrict__ croot) {
+    __shared__ uint32_t part[kBlock / 64];
+    const uint32_t nb = *nbig;
+    for (uint32_t i = blockIdx.x; i < nb; i += gridDim.x) {
+        const uint32_t c = big[i];
+        const uint32_t e = cstart[c + 1];
+        uint32_t v = kNone;
+        for (uint32_t r = cstart[c] + threadIdx.x; r < e; r += kBlock) v = root_merge(v, core_root(par, r));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v = root_merge(v, (uint32_t)__shfl_xor((int)v, o, 64));
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t w = kNone;
+#pragma unroll
+            for (int k = 0; k < kBlock / 64; ++k) w = root_merge(w, part[k]);
+            croot[c] = w;
+        }
+        __syncthreads();
+    }
 }
 
 // Per directory word (64 consecutive cell keys of a row): the common root of
@@ -1637,6 +1684,18 @@ struct EvTimer {
 inline unsigned blocks(uint64_t n) { return n ? (unsigned)((n + kBlock - 1) / kBlock) : 1u; }
 inline int xsub_of(const Ctx& ctx) { return ctx.xsub < 1 ? 1 : ctx.xsub; }
 
+// Cell roots (link mode 3, border fast path); also flattens the core records.
+void cell_roots(Ctx& ctx, hipStream_t s, uint32_t R, const uint32_t* cstart, const uint32_t* dncells,
+                uint32_t* par, uint32_t* croot) {
+    uint32_t* big = ctx.arena.get<uint32_t>("big_cells", R / (kBigCell + 1) + 1);
+    uint32_t* nbig = ctx.arena.get<uint32_t>("big_count", 4);
+    PD_HIP(hipMemsetAsync(nbig, 0, sizeof(uint32_t), s));
+    hipLaunchKernelGGL(cell_root_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, cstart, dncells, par,
+                       croot, big, nbig);
+    hipLaunchKernelGGL(big_cell_root_kernel, dim3(1024), dim3(kBlock), 0, s, cstart, big, nbig, par,
+                       croot);
+}
+
 // Launch helpers for the three neighbour sweeps: bit k of `variant`
 // (PD_OPT_SWEEP_VARIANT) selects the batched lane kernel for sweep k (0
 // count, 1 link, 2 border) instead of the row-by-row one.
@@ -1848,8 +1907,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
                            R, C, eps, eps2, slo, shi,
                            ctx.centre_window ? (uint32_t)ctx.centre_window : 0xFFFFFFFFu, par);
         uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
-        hipLaunchKernelGGL(cell_root_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, cstart, dncells,
-                           par, croot);
+        cell_roots(ctx, s, R, cstart, dncells, par, croot);
         uint32_t* wroot = ctx.arena.get<uint32_t>("word_root", W);
         hipLaunchKernelGGL(word_root_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, W, croot,
                            wroot);
@@ -1904,8 +1962,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     uint32_t* wroot_final = nullptr;
     if (R && (ctx.variant & 4) && ctx.border_roots) {
         uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
-        hipLaunchKernelGGL(cell_root_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, cstart, dncells,
-                           par, croot);
+        cell_roots(ctx, s, R, cstart, dncells, par, croot);
         wroot_final = ctx.arena.get<uint32_t>("word_root", W);
         hipLaunchKernelGGL(word_root_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, W, croot,
                            wroot_final);

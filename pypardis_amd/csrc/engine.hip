@@ -1159,6 +1159,7 @@ __global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs
 // core-core edge lies in one cell or two neighbouring cells, so every edge is
 // either proven connected or tested: the same guarantee as link_kernel.
 constexpr uint32_t kMixed = 0xFFFFFFFEu;
+constexpr uint32_t kCentreSettle = 16;   // centre-row hits already under our root before stopping
 
 template <typename T, int D, int M>
 __global__ __launch_bounds__(kBlock) void centre_link_kernel(const T* __restrict__ Xs, uint32_t R,
@@ -1184,6 +1185,7 @@ __global__ __launch_bounds__(kBlock) void centre_link_kernel(const T* __restrict
     // uncapped sweep is quadratic in the occupancy (C4 city centres)
     const uint32_t cap = window > 0xFFFFFFFFu - j ? 0xFFFFFFFFu : j + window;
     const uint32_t end = ok ? (e0 < cap ? e0 : cap) : 0u;
+    uint32_t settled = 0;
     for (; j + 4 <= end; j += 4) {
         T b0[D], b1[D], b2[D], b3[D];
         load_raw<T, D>(Xs, j, b0);
@@ -1192,10 +1194,15 @@ __global__ __launch_bounds__(kBlock) void centre_link_kernel(const T* __restrict
         load_raw<T, D>(Xs, j + 3, b3);
         const uint32_t p0 = ld_l1(par + j), p1 = ld_l1(par + j + 1), p2 = ld_l1(par + j + 2),
                        p3 = ld_l1(par + j + 3);
-        if (pr(b0)) lk.edge(j, p0);
-        if (pr(b1)) lk.edge(j + 1, p1);
-        if (pr(b2)) lk.edge(j + 2, p2);
-        if (pr(b3)) lk.edge(j + 3, p3);
+        const bool h0 = pr(b0), h1 = pr(b1), h2 = pr(b2), h3 = pr(b3);
+        // neighbours already under our root: a dense row is joined; stop
+        settled += (h0 && p0 == lk.rr) + (h1 && p1 == lk.rr) + (h2 && p2 == lk.rr) +
+                   (h3 && p3 == lk.rr);
+        if (h0) lk.edge(j, p0);
+        if (h1) lk.edge(j + 1, p1);
+        if (h2) lk.edge(j + 2, p2);
+        if (h3) lk.edge(j + 3, p3);
+        if (settled >= kCentreSettle) return;
     }
     for (; j < end; ++j) {
         T b0[D];

@@ -1117,25 +1117,35 @@ __global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs
                 const uint32_t clen = B > 1 ? pre[B > 1 ? 1 : 0] : tot;   // centre row
                 v0 = vr < clen ? vr : 0u;
             }
-            for (uint32_t v = 0; v < tot; v += 4) {
-                uint32_t j[4];
-                T b[4][D];
+            // the wrap costs two ops per candidate: only waves with a
+            // rotated lane pay it
+            auto sweep = [&](auto ROT) -> bool {
+                for (uint32_t v = 0; v < tot; v += 4) {
+                    uint32_t j[4];
+                    T b[4][D];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    uint32_t w = v0 + v + u;
-                    w = w >= tot ? w - tot : w;
-                    j[u] = v + u < tot ? bpos<B>(w, pre, off) : r;
-                    load_raw<T, D>(Xs, j[u], b[u]);
-                }
+                    for (int u = 0; u < 4; ++u) {
+                        uint32_t w = v + u;
+                        if constexpr (decltype(ROT)::value) {
+                            w += v0;
+                            w = w >= tot ? w - tot : w;
+                        }
+                        j[u] = v + u < tot ? bpos<B>(w, pre, off) : r;
+                        load_raw<T, D>(Xs, j[u], b[u]);
+                    }
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const bool w = (v + u < tot) && pr(b[u]);
-                    cnt += w ? 1u : 0u;
-                    mn = (w && j[u] < mn) ? j[u] : mn;
+                    for (int u = 0; u < 4; ++u) {
+                        const bool h = (v + u < tot) && pr(b[u]);
+                        cnt += h ? 1u : 0u;
+                        mn = (h && j[u] < mn) ? j[u] : mn;
+                    }
+                    if constexpr (ST) n_cand += (tot - v < 4u ? tot - v : 4u);
+                    if (cnt >= stop) return true;
                 }
-                if constexpr (ST) n_cand += (tot - v < 4u ? tot - v : 4u);
-                if (cnt >= stop) return;
-            }
+                return false;
+            };
+            const bool stopped = __any(v0 != 0) ? sweep(std::true_type{}) : sweep(std::false_type{});
+            if (stopped) return;
         }
     });
     core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);

@@ -1,9 +1,11 @@
 """Synthetic workloads named in SURVEY.md §8(d) (configs C0–C4 of BASELINE.json).
 
 All generators are deterministic in ``seed`` and return C-contiguous float32
-(n, d) arrays (C0 is float64, as in the reference's own demo data).  They are
-plain numpy so the CPU oracle, the GPU tests and ``bench.py`` see the same
-points.
+(n, d) arrays (C0 is float64, as in the reference's own demo data).  C0–C3
+are plain numpy so the CPU oracle, the GPU tests and ``bench.py`` see the
+same points; C4 (``gps_skew``, 1B points) is torch, generated on the device
+for the bench and on the CPU for the oracle tests (deterministic per device
+type).
 """
 from __future__ import annotations
 

@@ -54,6 +54,9 @@ def _load():
         lib.oracle_dbscan.argtypes = [P, ctypes.c_int64, ctypes.c_int32, ctypes.c_double,
                                       ctypes.c_int64, ctypes.c_int32, P, P, P]
         lib.oracle_dbscan.restype = ctypes.c_int64
+        lib.oracle_counts_capped.argtypes = [P, ctypes.c_int64, P, ctypes.c_int64, ctypes.c_int32,
+                                             ctypes.c_double, ctypes.c_int32, ctypes.c_int64, P]
+        lib.oracle_counts_capped.restype = ctypes.c_int
         _lib = lib
     return _lib
 
@@ -79,6 +82,18 @@ def counts(X, eps, metric="euclidean"):
     out = np.zeros(len(X), np.int64)
     rc = _load().oracle_counts(X.ctypes.data, len(X), X.shape[1], float(eps),
                                metric_id(metric), out.ctypes.data)
+    assert rc == 0
+    return out
+
+
+def counts_capped(Q, C, eps, cap, metric="euclidean"):
+    """min(#points of C within eps of each query, cap) by brute force (cap <= 0:
+    exact counts).  With C holding every point within eps of the queries (the
+    queries themselves included) this is the count sklearn's core test uses."""
+    Q, C = _as64(Q), _as64(C)
+    out = np.zeros(len(Q), np.int64)
+    rc = _load().oracle_counts_capped(Q.ctypes.data, len(Q), C.ctypes.data, len(C), Q.shape[1],
+                                      float(eps), metric_id(metric), int(cap), out.ctypes.data)
     assert rc == 0
     return out
 

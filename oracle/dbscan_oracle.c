@@ -134,6 +134,27 @@ int oracle_neighbors(const double* X, int64_t n, int32_t d, double eps,
     return rc;
 }
 
+/* Neighbour counts of nq query points against a candidate set (brute force,
+ * same predicate), stopping at `cap` (cap <= 0: no cap).  Used by the
+ * windowed full-size checks where a window is too dense for the sweep: with
+ * the candidates = every point within eps of the queries, out = min(count,
+ * cap) exactly (SK:cluster/_dbscan.py:421-434, the count the core test uses). */
+int oracle_counts_capped(const double* Q, int64_t nq, const double* C, int64_t nc, int32_t d,
+                         double eps, int32_t metric, int64_t cap, int64_t* out) {
+    const double r2 = eps * eps;
+    for (int64_t i = 0; i < nq; ++i) {
+        int64_t c = 0;
+        for (int64_t j = 0; j < nc; ++j) {
+            if (within(Q + i * d, C + j * d, d, eps, r2, metric)) {
+                ++c;
+                if (cap > 0 && c >= cap) break;
+            }
+        }
+        out[i] = c;
+    }
+    return 0;
+}
+
 /* DBSCAN.fit: counts -> core -> dbscan_inner DFS.  labels int64[n],
  * core uint8[n], counts int64[n].  Returns number of clusters (>= 0) or -1. */
 int64_t oracle_dbscan(const double* X, int64_t n, int32_t d, double eps,

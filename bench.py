@@ -258,6 +258,8 @@ def main():
         stages = {k: round(v / args.steps, 3) for k, v in stage_sum.items()
                   if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records")
                   and not k.startswith("s_")}
+        # KD partition + host work around pd_train (wall time, not events)
+        stages["outside_train"] = round(ms_step - stages.get("total", 0.0), 3)
         cpu = None
         if world == 1 and not args.no_cpu:
             try:

@@ -17,6 +17,8 @@
  *   pd_kd_split      R:dbscan/partition.py:66-68    filter(v[axis] >= boundary) relabel
  *                    (also :27-29, the median_search_split filters)
  *   pd_kd_radix_hist R:dbscan/partition.py:23-26    sortBy(v[axis]).collect()[len/2] (rotation)
+ *   pd_kd_pass       R:dbscan/partition.py:66-68 + 86-89 (+ 135-137): one level's split of
+ *                    the previous level fused with this level's moments aggregate
  *   pd_halo_members  R:dbscan/dbscan.py:136-151     _create_neighborhoods filter(contains)
  *   pd_cluster       R:dbscan/dbscan.py:28-30       skc.DBSCAN(**params).fit_predict(x),
  *                                                   core_sample_indices_  (SK:cluster/_dbscan.py:369-446)
@@ -185,6 +187,24 @@ int32_t pd_train(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d
 int32_t pd_kd_moments_dd(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
                          const int32_t* labels, int32_t n_sel, const int32_t* sel_host,
                          double* out_host, void* stream);
+
+/* One fused streaming pass of a KD BFS level (R:dbscan/partition.py:66-68 then
+ * :86-89, and :135-137 on the first level), so a level costs two reads of X
+ * (this pass and pd_kd_counts) instead of three:
+ *   1. labels[i] = split_new_host[s] where labels[i] == split_sel_host[s] and
+ *      v[split_axis_host[s]] >= split_boundary_host[s] (the previous level's
+ *      splits; n_split may be 0);
+ *   2. out_host[s][1 + 4d] = pd_kd_moments_dd of label sel_host[s] over the
+ *      updated labels (n_sel may be 0);
+ *   3. labels_zero != 0 (every label is 0; no split): labels are not read, and
+ *      if lohi_host != NULL also the tight bbox as pd_bbox (n_sel must be 1).
+ * Sums as pd_kd_moments_dd: correctly rounded double-double partials. */
+int32_t pd_kd_pass(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                   int32_t* labels, int32_t labels_zero, int32_t n_split,
+                   const int32_t* split_sel_host, const int32_t* split_axis_host,
+                   const double* split_boundary_host, const int32_t* split_new_host,
+                   int32_t n_sel, const int32_t* sel_host, double* out_host, double* lohi_host,
+                   int64_t* nonfinite_host, void* stream);
 
 /* mask[n] (device, u64): bit r set when some neighbourhood L with
  * part_rank_host[L] == r has an expanded box containing point i;

@@ -40,7 +40,7 @@ EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
            "pd_kd_split", "pd_halo_members", "pd_cluster", "pd_train", "pd_kd_moments_dd",
            "pd_route", "pd_pack", "pd_train_begin", "pd_train_exports", "pd_merge_exports",
            "pd_train_end", "pd_select_roots", "pd_sort_u32", "pd_rank_labels",
-           "pd_kd_radix_hist"]
+           "pd_kd_radix_hist", "pd_kd_pass"]
 
 
 class PardisError(RuntimeError):
@@ -95,6 +95,8 @@ def load():
             "pd_sort_u32": ([P, P, I64, P], I32),
             "pd_rank_labels": ([P, P, I64, P, I64, P, P], I32),
             "pd_kd_radix_hist": ([P, P, I32, I64, I32, P, I32, P, P, P, I32, P, P], I32),
+            "pd_kd_pass": ([P, P, I32, I64, I32, P, I32, I32, P, P, P, P, I32, P, P, P, P, P],
+                           I32),
         }
         for name, (args, res) in sig.items():
             f = getattr(lib, name)
@@ -238,6 +240,51 @@ def kd_split(X, labels, sel, axis, boundary, new, ctx=None):
     _check(load().pd_kd_split(ctx.ptr, X.data_ptr(), dt, X.shape[0], X.shape[1],
                               labels.data_ptr(), len(sel), sel.ctypes.data, axis.ctypes.data,
                               boundary.ctypes.data, new.ctypes.data, _stream(X.device)))
+
+
+def kd_pass(X, labels, split=None, sel=(), labels_zero=False, bbox=False, ctx=None):
+    """One fused KD level pass (pd_kd_pass): apply ``split`` = (sel, axes,
+    boundary, new) of the previous level to ``labels`` in place, then the
+    double-double moment partials (len(sel), 1 + 4d) of the labels ``sel``;
+    with ``bbox`` (first level: labels_zero, one label) also (lo, hi, bad).
+    Returns dd, or (dd, lo, hi, bad)."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    sel = np.ascontiguousarray(sel, np.int32)
+    out = np.zeros((len(sel), 1 + 4 * d), np.float64)
+    ns = 0
+    ss = sa = sb = sn = None
+    if split is not None:
+        ss = np.ascontiguousarray(split[0], np.int32)
+        sa = np.ascontiguousarray(split[1], np.int32)
+        sb = np.ascontiguousarray(split[2], np.float64)
+        sn = np.ascontiguousarray(split[3], np.int32)
+        ns = len(ss)
+    lohi = np.zeros(2 * d, np.float64) if bbox else None
+    bad = np.zeros(1, np.int64)
+    ptr = (lambda a: a.ctypes.data if a is not None else None)
+    _check(load().pd_kd_pass(ctx.ptr, X.data_ptr(), dt, n, d, labels.data_ptr(),
+                             1 if labels_zero else 0, ns, ptr(ss), ptr(sa), ptr(sb), ptr(sn),
+                             len(sel), sel.ctypes.data if len(sel) else None,
+                             out.ctypes.data if len(sel) else None, ptr(lohi), bad.ctypes.data,
+                             _stream(X.device)))
+    if bbox:
+        return out, lohi[:d], lohi[d:], int(bad[0])
+    return out
+
+
+def round_dd(dd):
+    """(S, 1 + 4d) double-double partials of one device -> (S, 3, d) moments
+    {count, sum v, sum v^2}, each rounded once (hi + lo)."""
+    dd = np.asarray(dd, np.float64)
+    S, G = dd.shape
+    d = (G - 1) // 4
+    mom = np.empty((S, 3, d))
+    mom[:, 0, :] = dd[:, :1]
+    mom[:, 1, :] = dd[:, 1:1 + 2 * d:2] + dd[:, 2:2 + 2 * d:2]
+    mom[:, 2, :] = dd[:, 1 + 2 * d::2] + dd[:, 2 + 2 * d::2]
+    return mom
 
 
 def kd_radix_hist(X, labels, sel, axis, prefix, shift, ctx=None):

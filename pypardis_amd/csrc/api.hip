@@ -329,6 +329,30 @@ int32_t pd_kd_moments_dd(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, i
     });
 }
 
+int32_t pd_kd_pass(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                   int32_t* labels, int32_t labels_zero, int32_t n_split, const int32_t* ssel,
+                   const int32_t* saxis, const double* sbound, const int32_t* snew, int32_t n_sel,
+                   const int32_t* sel, double* out, double* lohi, int64_t* bad, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (n_split < 0 || n_sel < 0) throw Error(PD_EINVAL, "bad selection");
+        if (n_split && (!ssel || !saxis || !sbound || !snew)) throw Error(PD_EINVAL, "null split table");
+        if (n_sel && (!sel || !out)) throw Error(PD_EINVAL, "null selection");
+        if (n && !labels) throw Error(PD_EINVAL, "null labels");
+        for (int s = 0; s < n_split; ++s)
+            if (saxis[s] < 0 || saxis[s] >= d || ssel[s] < 0) throw Error(PD_EINVAL, "bad axis/label");
+        if (lohi && (!labels_zero || n_split || n_sel != 1))
+            throw Error(PD_EINVAL, "the bbox is fused into the first level only (one label, no split)");
+        if (n == 0) {
+            if (n_sel) std::memset(out, 0, sizeof(double) * (1 + 4 * d) * n_sel);
+            if (lohi) throw Error(PD_EINVAL, "bbox of an empty set");
+            return;
+        }
+        kd_pass(ctx->c, X, dtype, n, d, labels, labels_zero != 0, n_split, ssel, saxis, sbound, snew,
+                n_sel, sel, out, lohi, bad, (hipStream_t)stream);
+    });
+}
+
 int32_t pd_route(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, int32_t P,
                  const double* ebox, const int32_t* part_rank, int32_t n_ranks, uint64_t* mask,
                  int64_t* counts, void* stream) {

@@ -152,6 +152,14 @@ void kd_split(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
 void kd_radix_hist(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                    int n_sel, const int32_t* sel_host, const int32_t* axis_host,
                    const uint64_t* prefix_host, int shift, int64_t* hist_host, hipStream_t s);
+// One fused streaming pass of a BFS level (kd.hip): apply the splits of the
+// previous level (n_split > 0), then the double-double moment partials of the
+// labels `sel` (out_dd: n_sel x (1 + 4d)), and on the first level (labels all
+// zero, lohi != null) the bbox + non-finite count.
+void kd_pass(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels,
+             bool labels_zero, int n_split, const int32_t* ssel, const int32_t* saxis,
+             const double* sbound, const int32_t* snew, int n_sel, const int32_t* sel,
+             double* out_dd, double* lohi, int64_t* bad, hipStream_t s);
 void kd_moments_dd(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                    int n_sel, const int32_t* sel_host, double* out_host, hipStream_t s);
 void route(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P, const double* ebox_host,

@@ -245,6 +245,379 @@ __global__ void moments_seq_kernel(const T* __restrict__ X, uint64_t n, uint32_t
     if (rem == 0) out[g * G] = cnt;
 }
 
+// ---------------------------------------------------------------- fused level pass
+// One streaming read of X per BFS level does everything the level can do
+// without a host decision: apply the previous level's splits
+// (R:dbscan/partition.py:66-68), then accumulate this level's moments
+// (:86-89) over the new labels, and on the first level the bbox
+// (:135-137).  Each lane takes four consecutive points per step with 16-byte
+// loads (D float4 / 2D double2 per four points) and the four labels as one
+// int4; split results are written back only where a label changed.
+template <typename T, int D, bool VEC>
+__device__ __forceinline__ int load_chunk(const T* __restrict__ X, uint64_t n, uint64_t c,
+                                          T (&v)[4][D]) {
+    const uint64_t i0 = c * 4;
+    const int m = n - i0 >= 4 ? 4 : (int)(n - i0);
+    if (VEC && m == 4) {
+        T t[4 * D];
+        if constexpr (sizeof(T) == 4) {
+            const float4* p = reinterpret_cast<const float4*>(X + i0 * D);
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                const float4 f = p[k];
+                t[4 * k] = f.x;
+                t[4 * k + 1] = f.y;
+                t[4 * k + 2] = f.z;
+                t[4 * k + 3] = f.w;
+            }
+        } else {
+            const double2* p = reinterpret_cast<const double2*>(X + i0 * D);
+#pragma unroll
+            for (int k = 0; k < 2 * D; ++k) {
+                const double2 f = p[k];
+                t[2 * k] = f.x;
+                t[2 * k + 1] = f.y;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int j = 0; j < D; ++j) v[q][j] = t[q * D + j];
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int j = 0; j < D; ++j) v[q][j] = q < m ? X[(i0 + q) * D + j] : T(0);
+    }
+    return m;
+}
+
+template <bool VEC>
+__device__ __forceinline__ void load_labels4(const int32_t* __restrict__ L, uint64_t c, int m,
+                                             int (&lab)[4]) {
+    if (VEC && m == 4) {
+        const int4 v = reinterpret_cast<const int4*>(L)[c];
+        lab[0] = v.x;
+        lab[1] = v.y;
+        lab[2] = v.z;
+        lab[3] = v.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lab[q] = q < m ? L[c * 4 + q] : -1;
+    }
+}
+
+template <bool VEC>
+__device__ __forceinline__ void store_labels4(int32_t* __restrict__ L, uint64_t c, int m,
+                                              const int (&lab)[4]) {
+    if (VEC && m == 4) {
+        reinterpret_cast<int4*>(L)[c] = make_int4(lab[0], lab[1], lab[2], lab[3]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (q < m) L[c * 4 + q] = lab[q];
+    }
+}
+
+template <typename T, int D>
+__device__ __forceinline__ T pick_axis(const T (&v)[D], int ax) {
+    T r = v[0];
+#pragma unroll
+    for (int j = 1; j < D; ++j) r = ax == j ? v[j] : r;
+    return r;
+}
+
+struct SplitTab {
+    const int32_t* slot_of;
+    int ntab;
+    const int32_t* axis;
+    const double* boundary;
+    const int32_t* newlab;
+    int nsplit;
+};
+
+// Label / split tables staged in LDS by the level kernels (larger levels
+// take the one-point-per-lane kernels).
+constexpr int kTabLds = 256;
+
+// NG = labels whose moments this pass accumulates (0: none); LAB: labels are
+// read (false: every point has label 0, the first level); SP: the previous
+// level's splits are applied first; BB: bbox + non-finite count.
+//
+// Moments without per-label masking: a block takes a tile of 4·K·256
+// consecutive points (K four-point chunks per lane), applies the splits,
+// then regroups the tile in LDS by label slot (a counting sort from wave
+// ballots, deterministic) so that every wave accumulates ONE slot: wave w
+// sums slot w % NG, items sub·64 + lane + k·64·(4 / NG).  The double-double
+// work per point is then that of one label, whatever NG is.
+// Block partials: NG x [count, (sum hi, lo) x D, (sumsq hi, lo) x D], then
+// the bbox [lo x D, hi x D, bad].
+template <typename T, int D, bool LAB, bool SP, int NG, bool BB>
+__global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X, uint64_t n,
+                                                         int32_t* __restrict__ labels, SplitTab sp,
+                                                         int4 sel, double* __restrict__ part) {
+    constexpr int K = (sizeof(T) * D <= 16) ? 2 : 1;
+    constexpr int TP = 4 * K * kBlock;   // points per tile
+    constexpr int NW = kBlock / 64;
+    constexpr int NGa = NG > 0 ? NG : 1;
+    static_assert(NW == 4 && (NG == 0 || NG == 1 || NG == 2 || NG == 4), "wave/slot mapping");
+    __shared__ T s_val[NG > 0 ? TP * D : 1];
+    __shared__ int s_wcnt[NW][NGa];
+    __shared__ int s_slot[SP ? kTabLds : 1], s_ax[SP ? kTabLds : 1], s_nl[SP ? kTabLds : 1];
+    __shared__ double s_bd[SP ? kTabLds : 1];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    if constexpr (SP) {
+        for (int k = tid; k < sp.ntab; k += kBlock) s_slot[k] = sp.slot_of[k];
+        for (int k = tid; k < sp.nsplit; k += kBlock) {
+            s_ax[k] = sp.axis[k];
+            s_bd[k] = sp.boundary[k];
+            s_nl[k] = sp.newlab[k];
+        }
+        __syncthreads();
+    }
+    const int sl[4] = {sel.x, sel.y, sel.z, sel.w};
+    const int wslot = w % NGa, sub = w / NGa, nsub = NW / NGa;
+    double cnt = 0;
+    DD s[D], q2[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) s[j] = q2[j] = DD{0.0, 0.0};
+    double lo[D], hi[D], bad = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        lo[j] = INFINITY;
+        hi[j] = -INFINITY;
+    }
+    const uint64_t nch = (n + 3) / 4;
+    const uint64_t ntile = (n + TP - 1) / TP;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+        T v[K][4][D];
+        int slot[K][4];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t ch = t * (TP / 4) + (uint64_t)k * kBlock + tid;
+            int m = 0;
+            if (ch < nch) {
+                m = load_chunk<T, D, true>(X, n, ch, v[k]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int j = 0; j < D; ++j) v[k][q][j] = T(0);
+            }
+            int lab[4] = {0, 0, 0, 0};
+            if constexpr (LAB) {
+                if (m) load_labels4<true>(labels, ch, m, lab);
+            }
+            if constexpr (SP) {
+                bool changed = false;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int L = lab[q];
+                    if (q >= m || L < 0 || L >= sp.ntab) continue;
+                    const int a = s_slot[L];
+                    if (a < 0) continue;
+                    const double x = (double)pick_axis<T, D>(v[k][q], s_ax[a]);
+                    if (x >= s_bd[a]) {
+                        lab[q] = s_nl[a];
+                        changed = true;
+                    }
+                }
+                if (changed) store_labels4<true>(labels, ch, m, lab);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                int g = -1;
+#pragma unroll
+                for (int h = NGa - 1; h >= 0; --h) g = (NG > 0 && lab[q] == sl[h]) ? h : g;
+                slot[k][q] = q < m ? g : -1;
+            }
+            if constexpr (BB) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (q >= m) continue;
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        const double x = (double)v[k][q][j];
+                        if (!isfinite(x)) bad += 1;
+                        lo[j] = fmin(lo[j], x);
+                        hi[j] = fmax(hi[j], x);
+                    }
+                }
+            }
+        }
+        if constexpr (NG > 0) {
+            // counting sort of the tile by slot: wave tallies, then positions
+            int wc[NGa];
+#pragma unroll
+            for (int g = 0; g < NGa; ++g) wc[g] = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int g = 0; g < NGa; ++g) wc[g] += __popcll(__ballot(slot[k][q] == g));
+            if (lane == 0)
+#pragma unroll
+                for (int g = 0; g < NGa; ++g) s_wcnt[w][g] = wc[g];
+            __syncthreads();
+            int run[NGa], seg[NGa];
+            int acc = 0;
+#pragma unroll
+            for (int g = 0; g < NGa; ++g) {
+                seg[g] = acc;
+                int before = 0;
+#pragma unroll
+                for (int u = 0; u < NW; ++u) {
+                    before += u < w ? s_wcnt[u][g] : 0;
+                    acc += s_wcnt[u][g];
+                }
+                run[g] = seg[g] + before;
+            }
+            const int total = s_wcnt[0][wslot] + s_wcnt[1][wslot] + s_wcnt[2][wslot] +
+                              s_wcnt[3][wslot];
+            const int start = seg[wslot];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                    for (int g = 0; g < NGa; ++g) {
+                        const unsigned long long b = __ballot(slot[k][q] == g);
+                        if (slot[k][q] == g) {
+                            const int pos = run[g] + __popcll(b & lt);
+#pragma unroll
+                            for (int j = 0; j < D; ++j) s_val[pos * D + j] = v[k][q][j];
+                        }
+                        run[g] += __popcll(b);
+                    }
+                }
+            __syncthreads();
+            for (int i = sub * 64 + lane; i < total; i += nsub * 64) {
+                const T* p = s_val + (size_t)(start + i) * D;
+                cnt += 1.0;
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    const T x = p[j];
+                    const T xx = x * x;   // squared in the input precision (numpy)
+                    dd_acc(s[j], (double)x);
+                    dd_acc(q2[j], (double)xx);
+                }
+            }
+            __syncthreads();
+        }
+    }
+    constexpr int G = 1 + 4 * D;
+    constexpr int WM = NG * G;
+    constexpr int WB = BB ? 2 * D + 1 : 0;
+    constexpr int W = WM + WB;
+    __shared__ double sm[NW][G + WB];
+    if constexpr (NG > 0) {
+        const double x = wave_sum(cnt);
+        if (lane == 0) sm[w][0] = x;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const DD a = wave_dd(s[j]);
+            const DD b = wave_dd(q2[j]);
+            if (lane == 0) {
+                sm[w][1 + 2 * j] = a.hi;
+                sm[w][2 + 2 * j] = a.lo;
+                sm[w][1 + 2 * D + 2 * j] = b.hi;
+                sm[w][2 + 2 * D + 2 * j] = b.lo;
+            }
+        }
+    }
+    if constexpr (BB) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const double a = wave_min(lo[j]), b = wave_max(hi[j]);
+            if (lane == 0) {
+                sm[w][G + j] = a;
+                sm[w][G + D + j] = b;
+            }
+        }
+        const double bb = wave_sum(bad);
+        if (lane == 0) sm[w][G + 2 * D] = bb;
+    }
+    if constexpr (W > 0) {
+        __syncthreads();
+        double* out = part + (uint64_t)blockIdx.x * W;
+        // moments: slot g = waves g, g + NG, ... merged in that order
+        for (int k = tid; k < W; k += kBlock) {
+            if (k < WM) {
+                const int g = k / G, r = k % G;
+                if (r == 0) {
+                    double a = 0;
+                    for (int u = g; u < NW; u += NGa) a += sm[u][0];
+                    out[k] = a;
+                } else if ((r - 1) % 2 == 0) {
+                    DD a{0.0, 0.0};
+                    for (int u = g; u < NW; u += NGa) a = dd_add(a, DD{sm[u][r], sm[u][r + 1]});
+                    out[k] = a.hi;
+                    out[k + 1] = a.lo;
+                }
+            } else {
+                const int b = k - WM;
+                double a = sm[0][G + b];
+                for (int u = 1; u < NW; ++u)
+                    a = b < D ? fmin(a, sm[u][G + b])
+                              : (b < 2 * D ? fmax(a, sm[u][G + b]) : a + sm[u][G + b]);
+                out[k] = a;
+            }
+        }
+    }
+}
+
+// Deterministic finish of kd_pass_kernel's block partials: per quantity,
+// lane t folds blocks t, t + 256, ... in order, then a fixed-shape tree over
+// the lanes (dd sums / counts / min / max).  out[W] as one block's layout.
+__global__ __launch_bounds__(kBlock) void kd_finish_kernel(const double* __restrict__ part, int nb,
+                                                           int WM, int G, int D, int W,
+                                                           double* __restrict__ out) {
+    __shared__ double sh[kBlock], sl[kBlock];
+    for (int k = 0; k < W; ++k) {
+        const bool mom = k < WM;
+        const int r = mom ? k % G : 0;
+        if (mom && r != 0 && (r - 1) % 2 == 1) continue;   // lo word: handled with its hi
+        const bool is_dd = mom && r != 0;
+        const int b = mom ? -1 : k - WM;   // bbox: 0..D-1 min, D..2D-1 max, 2D bad
+        DD acc{0.0, 0.0};
+        double x = mom || b == 2 * D ? 0.0 : (b < D ? INFINITY : -INFINITY);
+        for (int i = threadIdx.x; i < nb; i += kBlock) {
+            const double* p = part + (uint64_t)i * W;
+            if (is_dd)
+                acc = dd_add(acc, DD{p[k], p[k + 1]});
+            else if (mom || b == 2 * D)
+                x += p[k];
+            else
+                x = b < D ? fmin(x, p[k]) : fmax(x, p[k]);
+        }
+        sh[threadIdx.x] = is_dd ? acc.hi : x;
+        sl[threadIdx.x] = acc.lo;
+        __syncthreads();
+        for (int o = kBlock / 2; o > 0; o >>= 1) {
+            if (threadIdx.x < o) {
+                const int t = threadIdx.x;
+                if (is_dd) {
+                    const DD a = dd_add(DD{sh[t], sl[t]}, DD{sh[t + o], sl[t + o]});
+                    sh[t] = a.hi;
+                    sl[t] = a.lo;
+                } else if (mom || b == 2 * D) {
+                    sh[t] += sh[t + o];
+                } else {
+                    sh[t] = b < D ? fmin(sh[t], sh[t + o]) : fmax(sh[t], sh[t + o]);
+                }
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            out[k] = sh[0];
+            if (is_dd) out[k + 1] = sl[0];
+        }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------- counts
 // counts[slot][i] = #points of the slot's label with v[axis] < bounds[slot][i].
 // mono (every slot's bounds non-decreasing, as mean + (i-3)*0.3*std is for
@@ -280,6 +653,57 @@ __global__ __launch_bounds__(kBlock) void counts_kernel(
             for (int b = 0; b < 7; ++b)
                 if (v < bounds[sl * 7 + b]) atomicAdd(&mine[sl * 8 + b], 1u);
             atomicAdd(&mine[sl * 8 + 7], 1u);
+        }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < n_sel * 8; k += kBlock) {
+        unsigned int v = 0;
+        for (int q = 0; q < rep; ++q) v += lcnt[q * n_sel * 8 + k];
+        if (v) atomicAdd(&out[k], (unsigned long long)v);
+    }
+}
+
+// d <= 4: four points per lane per step (16-byte loads), the label tables
+// and bounds staged in LDS (n_label_tab, n_sel <= kTabLds).
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void counts4_kernel(
+    const T* __restrict__ X, uint64_t n, const int32_t* __restrict__ labels,
+    const int32_t* __restrict__ slot_of, int n_label_tab, const int32_t* __restrict__ axis,
+    const double* __restrict__ bounds, int n_sel, int mono, int rep,
+    unsigned long long* __restrict__ out) {
+    extern __shared__ unsigned int lcnt[];   // rep * n_sel * 8
+    __shared__ int s_slot[kTabLds], s_ax[kTabLds];
+    __shared__ double s_bd[kTabLds * 7];
+    for (int k = threadIdx.x; k < rep * n_sel * 8; k += kBlock) lcnt[k] = 0;
+    for (int k = threadIdx.x; k < n_label_tab; k += kBlock) s_slot[k] = slot_of[k];
+    for (int k = threadIdx.x; k < n_sel; k += kBlock) s_ax[k] = axis[k];
+    for (int k = threadIdx.x; k < n_sel * 7; k += kBlock) s_bd[k] = bounds[k];
+    __syncthreads();
+    unsigned int* mine = lcnt + (threadIdx.x & (rep - 1)) * n_sel * 8;
+    const uint64_t nch = (n + 3) / 4;
+    for (uint64_t ch = (uint64_t)blockIdx.x * kBlock + threadIdx.x; ch < nch;
+         ch += (uint64_t)gridDim.x * kBlock) {
+        T v[4][D];
+        const int m = load_chunk<T, D, true>(X, n, ch, v);
+        int lab[4];
+        load_labels4<true>(labels, ch, m, lab);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (q >= m || lab[q] < 0 || lab[q] >= n_label_tab) continue;
+            const int sl = s_slot[lab[q]];
+            if (sl < 0) continue;
+            const double x = (double)pick_axis<T, D>(v[q], s_ax[sl]);
+            const double* b = s_bd + sl * 7;
+            if (mono) {
+                int cc = 0;
+#pragma unroll
+                for (int i = 0; i < 7; ++i) cc += x < b[i] ? 1 : 0;
+                atomicAdd(&mine[sl * 8 + cc], 1u);
+            } else {
+                for (int i = 0; i < 7; ++i)
+                    if (x < b[i]) atomicAdd(&mine[sl * 8 + i], 1u);
+                atomicAdd(&mine[sl * 8 + 7], 1u);
+            }
         }
     }
     __syncthreads();
@@ -552,6 +976,144 @@ void moments_impl(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const in
 }
 }  // namespace
 
+namespace {
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// The fused four-point kernels need d <= 4 and 16-byte aligned X and labels
+// (torch allocations are); anything else takes the one-point-per-lane kernels.
+inline bool vec_ok(int d, const void* X, const void* labels) {
+    return d <= kMaxDim && aligned16(X) && (!labels || aligned16(labels));
+}
+
+// ... and LDS-sized label tables: labels < kTabLds, <= kTabLds slots.
+inline bool tabs_ok(int n_sel, const int32_t* sel) {
+    if (n_sel > kTabLds) return false;
+    for (int k = 0; k < n_sel; ++k)
+        if (sel[k] >= kTabLds) return false;
+    return true;
+}
+
+template <typename F>
+void dispatch_ng(int ng, F&& f) {
+    switch (ng) {
+        case 0: f(std::integral_constant<int, 0>{}); break;
+        case 1: f(std::integral_constant<int, 1>{}); break;
+        case 2: f(std::integral_constant<int, 2>{}); break;
+        default: f(std::integral_constant<int, 4>{}); break;
+    }
+}
+
+// One launch of kd_pass_kernel + its deterministic finish; returns the
+// finished quantities (NG x G moments, then the bbox) in `res` (host).
+template <typename T, int D, bool LAB, bool SP, int NG, bool BB>
+void run_pass(Ctx& ctx, const T* X, int64_t n, int32_t* labels, const SplitTab& sp, int4 sel,
+              std::vector<double>& res, hipStream_t s) {
+    constexpr int G = 1 + 4 * D, WM = NG * G, W = WM + (BB ? 2 * D + 1 : 0);
+    constexpr int TP = 4 * kBlock * ((sizeof(T) * D <= 16) ? 2 : 1);   // kd_pass_kernel tile
+    // one wave of resident blocks: a second, partial round would leave most
+    // CUs idle at the end (LDS limits residency to a few blocks per CU)
+    static int resident = 0;
+    if (!resident) {
+        int per_cu = 0, dev = 0, cus = 0;
+        PD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(&kd_pass_kernel<T, D, LAB, SP, NG, BB>), kBlock, 0));
+        PD_HIP(hipGetDevice(&dev));
+        PD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        resident = std::max(1, per_cu) * std::max(1, cus);
+    }
+    const int nb = (int)std::min<int64_t>(resident, std::max<int64_t>(1, (n + TP - 1) / TP));
+    double* part = ctx.arena.get<double>("pass_part", (size_t)nb * (W > 0 ? W : 1));
+    hipLaunchKernelGGL((kd_pass_kernel<T, D, LAB, SP, NG, BB>), dim3(nb), dim3(kBlock), 0, s,
+                       X, (uint64_t)n, labels, sp, sel, part);
+    PD_HIP(hipGetLastError());
+    res.assign(W, 0.0);
+    if constexpr (W > 0) {
+        double* fin = ctx.arena.get<double>("pass_fin", W);
+        hipLaunchKernelGGL(kd_finish_kernel, dim3(1), dim3(kBlock), 0, s, part, nb, WM, G, D, W,
+                           fin);
+        PD_HIP(hipGetLastError());
+        double* h = (double*)pinned(ctx, sizeof(double) * W);
+        PD_HIP(hipMemcpyAsync(h, fin, sizeof(double) * W, hipMemcpyDeviceToHost, s));
+        sync(s);
+        std::memcpy(res.data(), h, sizeof(double) * W);
+    }
+}
+}  // namespace
+
+void kd_pass(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels,
+             bool labels_zero, int n_split, const int32_t* ssel, const int32_t* saxis,
+             const double* sbound, const int32_t* snew, int n_sel, const int32_t* sel,
+             double* out_dd, double* lohi, int64_t* bad, hipStream_t s) {
+    const bool lab_first = labels_zero && n_split == 0;
+    if (n_sel == 0 && !lohi) {
+        if (n_split) kd_split(ctx, X, dtype, n, d, labels, n_split, ssel, saxis, sbound, snew, s);
+        return;
+    }
+    if (!vec_ok(d, X, labels) || ctx.seq_moments || !tabs_ok(n_split, ssel)) {
+        // generic passes (any d, unaligned inputs)
+        if (n_split) kd_split(ctx, X, dtype, n, d, labels, n_split, ssel, saxis, sbound, snew, s);
+        if (n_sel) moments_impl(ctx, X, dtype, n, d, labels, n_sel, sel, out_dd, true, s);
+        if (lohi) bbox(ctx, X, dtype, n, d, lohi, bad, s);
+        return;
+    }
+    SplitTab st{nullptr, 0, nullptr, nullptr, nullptr, 0};
+    if (n_split) {
+        LabelTables t = upload_tables(ctx, n_split, ssel, saxis, sbound, 1, snew, s);
+        st = SplitTab{t.slot_of, t.ntab, t.axis, t.dbl, t.newlab, n_split};
+    }
+    const int Gd = 1 + 4 * d;
+    dispatch_t(dtype, [&](auto tp) {
+        using T = std::remove_pointer_t<decltype(tp)>;
+        dispatch_d(d, [&](auto Dc) {
+            constexpr int D = decltype(Dc)::value;
+            constexpr int G = 1 + 4 * D;
+            std::vector<double> res;
+            // the first launch: splits, the first group of labels, the bbox
+            const int ng0 = std::min(n_sel, kGroup);
+            int4 sl = make_int4(-2, -2, -2, -2);
+            for (int g = 0; g < ng0; ++g) (&sl.x)[g] = sel[g];
+            auto take = [&](int g0, int ng) {
+                for (int g = 0; g < ng; ++g) std::memcpy(out_dd + (size_t)(g0 + g) * Gd,
+                                                         res.data() + (size_t)g * G,
+                                                         sizeof(double) * G);
+            };
+            if (lohi) {
+                if (!lab_first) throw Error(-1, "kd_pass: bbox only on the first level");
+                run_pass<T, D, false, false, 1, true>(ctx, (const T*)X, n, labels, st, sl, res, s);
+                take(0, 1);
+                for (int j = 0; j < 2 * D; ++j) lohi[j] = res[G + j];
+                if (bad) *bad = (int64_t)res[G + 2 * D];
+                if (n_sel > 1) throw Error(-1, "kd_pass: one label on the first level");
+                return;
+            }
+            dispatch_ng(ng0, [&](auto NGc) {
+                constexpr int NG = decltype(NGc)::value;
+                if (lab_first)
+                    run_pass<T, D, false, false, NG, false>(ctx, (const T*)X, n, labels, st, sl,
+                                                            res, s);
+                else if (n_split)
+                    run_pass<T, D, true, true, NG, false>(ctx, (const T*)X, n, labels, st, sl,
+                                                          res, s);
+                else
+                    run_pass<T, D, true, false, NG, false>(ctx, (const T*)X, n, labels, st, sl,
+                                                           res, s);
+            });
+            take(0, ng0);
+            for (int g0 = kGroup; g0 < n_sel; g0 += kGroup) {
+                const int ng = std::min(n_sel - g0, kGroup);
+                sl = make_int4(-2, -2, -2, -2);
+                for (int g = 0; g < ng; ++g) (&sl.x)[g] = sel[g0 + g];
+                dispatch_ng(ng, [&](auto NGc) {
+                    constexpr int NG = decltype(NGc)::value;
+                    run_pass<T, D, true, false, NG, false>(ctx, (const T*)X, n, labels, st, sl,
+                                                           res, s);
+                });
+                take(g0, ng);
+            }
+        });
+    });
+}
+
 void kd_moments(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                 int n_sel, const int32_t* sel, double* out, hipStream_t s) {
     moments_impl(ctx, X, dtype, n, d, labels, n_sel, sel, out, false, s);
@@ -585,6 +1147,19 @@ void kd_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32
     if ((size_t)n_sel * 8 * sizeof(unsigned int) > 60 * 1024)
         throw Error(-5, "too many splits in one KD level (> 1920)");
     const unsigned nb = grid_for(n, 2048);
+    if (vec_ok(d, X, labels) && tabs_ok(n_sel, sel)) {
+        dispatch_t(dtype, [&](auto tp) {
+            using T = std::remove_pointer_t<decltype(tp)>;
+            dispatch_d(d, [&](auto Dc) {
+                constexpr int D = decltype(Dc)::value;
+                const unsigned nb4 = grid_for((n + 3) / 4, 2048);
+                hipLaunchKernelGGL((counts4_kernel<T, D>), dim3(nb4), dim3(kBlock),
+                                   sizeof(unsigned int) * rep * n_sel * 8, s, (const T*)X,
+                                   (uint64_t)n, labels, t.slot_of, t.ntab, t.axis, t.dbl, n_sel,
+                                   mono ? 1 : 0, rep, dcnt);
+            });
+        });
+    } else
     dispatch_t(dtype, [&](auto tp) {
         using T = std::remove_pointer_t<decltype(tp)>;
         hipLaunchKernelGGL((counts_kernel<T>), dim3(nb), dim3(kBlock),
@@ -619,6 +1194,20 @@ void kd_split(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
               const int32_t* newlab, hipStream_t s) {
     if (n_sel <= 0) return;
     LabelTables t = upload_tables(ctx, n_sel, sel, axis, boundary, 1, newlab, s);
+    if (vec_ok(d, X, labels) && tabs_ok(n_sel, sel)) {
+        const SplitTab st{t.slot_of, t.ntab, t.axis, t.dbl, t.newlab, n_sel};
+        dispatch_t(dtype, [&](auto tp) {
+            using T = std::remove_pointer_t<decltype(tp)>;
+            dispatch_d(d, [&](auto Dc) {
+                constexpr int D = decltype(Dc)::value;
+                std::vector<double> res;
+                run_pass<T, D, true, true, 0, false>(ctx, (const T*)X, n, labels, st,
+                                                     make_int4(-2, -2, -2, -2), res, s);
+            });
+        });
+        sync(s);
+        return;
+    }
     const unsigned nb = grid_for(n, 4096);
     dispatch_t(dtype, [&](auto tp) {
         using T = std::remove_pointer_t<decltype(tp)>;

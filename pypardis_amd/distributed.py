@@ -68,6 +68,10 @@ class NativeOps(object):
     def moments_dd(self, X, labels, sel):
         return _native.kd_moments_dd(X, labels, sel, ctx=self.ctx)
 
+    def level_pass(self, X, labels, split, sel, labels_zero=False, bbox=False):
+        return _native.kd_pass(X, labels, split=split, sel=sel, labels_zero=labels_zero,
+                               bbox=bbox, ctx=self.ctx)
+
     def counts(self, X, labels, sel, axes, bounds):
         return _native.kd_counts(X, labels, sel, axes, bounds, ctx=self.ctx)
 
@@ -260,8 +264,15 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     if n_total >= 0xFFFFFFFF:
         raise ValueError("the sharded train addresses points with 32-bit global ids")
 
-    # ---- bbox (R:dbscan/partition.py:135-137)
-    if n:
+    # ---- bbox (R:dbscan/partition.py:135-137), fused into the first
+    # level's moments pass for min_var
+    kdlab = ops.zeros(n, torch.int32)
+    levels = _split_schedule(P)
+    fused = split_method == 'min_var'
+    first = None
+    if n and fused and levels:
+        first, lo, hi, bad = ops.level_pass(X, kdlab, None, [0], True, True)
+    elif n:
         lo, hi, bad = ops.bbox(X)
     else:
         lo, hi, bad = np.full(d, np.inf), np.full(d, -np.inf), 0
@@ -274,12 +285,14 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     data_box = np.concatenate([-ext[:d], ext[d:]])
     box = BoundingBox(k=d).union(BoundingBox(data_box[:d], data_box[d:]))
 
-    # ---- KD partition (R:dbscan/partition.py:139-183)
-    kdlab = ops.zeros(n, torch.int32)
+    # ---- KD partition (R:dbscan/partition.py:139-183): per level one fused
+    # pass (the previous level's split + this level's moments) and one counts
+    # pass; the last split runs alone
     boxes = {0: box}
     splits = []
     fp32 = X.dtype == torch.float32
-    for depth, level in enumerate(_split_schedule(P)):
+    pending = None
+    for depth, level in enumerate(levels):
         sel = [c for c, _ in level]
         new = [nl for _, nl in level]
         if split_method == 'rotation':
@@ -297,15 +310,21 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
                 ops.split(X, kdlab, sel, axes, med, new)
             apply_rotation_level(boxes, splits, level, axes, med, less, tot)
             continue
-        part = ops.moments_dd(X, kdlab, sel) if n else np.zeros((len(sel), 1 + 4 * d))
+        if not n:
+            part = np.zeros((len(sel), 1 + 4 * d))
+        elif depth == 0 and first is not None:
+            part = first
+        else:
+            part = ops.level_pass(X, kdlab, pending, sel)
         mom = dd_combine(comm.all_gather_np(part))
         axes, means, vars_, bounds = level_axes(mom)
         cnt = ops.counts(X, kdlab, sel, axes, bounds) if n else np.zeros((len(sel), 8), np.int64)
         cnt = comm.all_reduce(cnt.astype(np.int64), dist.ReduceOp.SUM)
         boundary, cand = level_boundaries(cnt, bounds)
-        if n:
-            ops.split(X, kdlab, sel, axes, boundary, new)
+        pending = (sel, axes, boundary, new)
         apply_level(boxes, splits, level, axes, means, vars_, cnt, cand, boundary)
+    if pending is not None and n:
+        ops.split(X, kdlab, *pending)
     ebox = np.stack([boxes[L].expand(2 * eps).as_array() for L in sorted(boxes)])
     lap("kd")
 

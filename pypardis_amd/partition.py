@@ -277,22 +277,51 @@ class KDPartitioner(object):
             # astronomically large in high dimension; it would never finish
             raise ValueError(f"max_partitions={self.max_partitions} (> 65536; the default is "
                              "4**k): pass max_partitions explicitly")
-        lo, hi, bad = _native.bbox(X)
+        self.labels = torch.zeros(self.points.n, dtype=torch.int32, device=X.device)
+        levels = _split_schedule(self.max_partitions)
+        first = None
+        if levels and self._fused():
+            # the bbox rides on the first level's moments pass (one read of X)
+            first, lo, hi, bad = _native.kd_pass(X, self.labels, sel=[0], labels_zero=True,
+                                                 bbox=True)
+        else:
+            lo, hi, bad = _native.bbox(X)
         if bad:
             raise ValueError("Input contains NaN or infinity.")
         self.data_box = (lo, hi)     # tight box: the engine clips its grids to it
         box = BoundingBox(k=self.k).union(BoundingBox(lo, hi))
-        self.labels = torch.zeros(self.points.n, dtype=torch.int32, device=X.device)
         self.splits = []
-        self._create_partitions(box)
+        self._create_partitions(box, levels, first)
         self.partitions = {L: PartitionView(self.points, self.labels, L)
                            for L in sorted(self.bounding_boxes)}
         self.result = _Union(self.partitions)
 
-    def _create_partitions(self, box):
+    def _fused(self):
+        return self.split_method == 'min_var' and self.sums == 'exact'
+
+    def _create_partitions(self, box, levels, first=None):
         X, labels = self.points.X, self.labels
         self.bounding_boxes = {0: box}
-        for depth, level in enumerate(_split_schedule(self.max_partitions)):
+        if self._fused():
+            # per level two streaming passes: pd_kd_pass (the previous
+            # level's split + this level's moments) and pd_kd_counts; the
+            # last level's split runs alone
+            pending = None
+            for depth, level in enumerate(levels):
+                sel = [c for c, _ in level]
+                new = [nl for _, nl in level]
+                dd = first if depth == 0 and first is not None else \
+                    _native.kd_pass(X, labels, split=pending, sel=sel)
+                axes, means, vars_, bounds = level_axes(_native.round_dd(dd))
+                cnt = _native.kd_counts(X, labels, sel, axes, bounds)
+                boundary, cand = level_boundaries(cnt, bounds)
+                pending = (sel, axes, boundary, new)
+                apply_level(self.bounding_boxes, self.splits, level, axes, means, vars_, cnt,
+                            cand, boundary)
+            if pending is not None:
+                _native.kd_split(X, labels, *pending)
+            return
+        for depth, level in enumerate(levels):
             sel = [c for c, _ in level]
             new = [nl for _, nl in level]
             if self.split_method == 'rotation':

@@ -52,6 +52,16 @@ class OracleOps(object):
                     out[s, base + 2 * j + 1] = lo
         return out
 
+    def level_pass(self, X, labels, split, sel, labels_zero=False, bbox=False):
+        """pd_kd_pass restated: the previous level's split, then moments_dd
+        (and the bbox on the first level)."""
+        if split is not None:
+            self.split(X, labels, *split)
+        dd = self.moments_dd(X, labels, sel)
+        if bbox:
+            return (dd,) + tuple(self.bbox(X))
+        return dd
+
     def counts(self, X, labels, sel, axes, bounds):
         x = X.numpy().astype(np.float64)
         lab = labels.numpy()

@@ -17,6 +17,7 @@ constexpr uint32_t kDupBit = 0x40000000u;     // point lies in >= 2 neighbourhoo
 constexpr uint32_t kIdMask = 0x3FFFFFFFu;     // => n < 2^30 points per device
 constexpr int kMaxDim = 4;                    // grid path; d > 4 is the tile path
 constexpr int kMaxParts = 64;                 // one bit per neighbourhood in the halo mask
+constexpr int kMaxLdsParts = 64;              // neighbourhood grids staged in LDS up to this
 
 struct Error : std::runtime_error {
     int code;
@@ -50,7 +51,9 @@ struct PartGrid {
     int64_t nc[kMaxDim];    // cells per axis (0 => empty neighbourhood)
     uint64_t base;          // first key of this neighbourhood
     double elo[kMaxDim];    // expanded box (halo membership test), inclusive
-    double ehi[kMaxDim];
+    double ehi[kMaxDim];    // (empty neighbourhood: +inf / -inf, a box nothing is in)
+    float flo[kMaxDim];     // the same test for fp32 coordinates in fp32: the smallest
+    float fhi[kMaxDim];     // float >= elo, the largest float <= ehi (exact equivalence)
 };
 
 // XCD-aware block remap (cdna_hip_programming.md T1, bijective form): blocks

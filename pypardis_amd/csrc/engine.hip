@@ -39,6 +39,8 @@
 #include <vector>
 
 #include "internal.hpp"
+#include "scan.hpp"
+#include "stream.hpp"
 #include "uf.hpp"
 
 namespace pd {
@@ -271,13 +273,21 @@ __device__ __forceinline__ uint64_t lin_of(const int64_t (&c)[D], const PartGrid
     return k;
 }
 
-template <int D>
-__device__ __forceinline__ bool in_box(const double (&v)[D], const PartGrid& g) {
-    bool in = g.nc[0] > 0;
+// Box test in the input precision: for fp32 coordinates v, (double)v >= elo
+// iff v >= flo (flo = the smallest float >= elo), likewise for ehi / fhi.
+template <typename T, int D>
+__device__ __forceinline__ bool in_box_t(const T (&v)[D], const PartGrid& g) {
+    bool in = true;
 #pragma unroll
-    for (int j = 0; j < D; ++j) in &= (g.elo[j] <= v[j]) & (g.ehi[j] >= v[j]);
+    for (int j = 0; j < D; ++j) {
+        if constexpr (std::is_same<T, float>::value)
+            in &= (g.flo[j] <= v[j]) & (g.fhi[j] >= v[j]);
+        else
+            in &= (g.elo[j] <= v[j]) & (g.ehi[j] >= v[j]);
+    }
     return in;
 }
+
 
 // Directory word (16 B, one load): occupancy bits of 64 consecutive cell
 // keys + the number of occupied cells before them.
@@ -465,39 +475,174 @@ __device__ __forceinline__ int part_of_wave(const uint32_t* __restrict__ ps, int
 }
 
 // ------------------------------------------------------------------ kernels
+// Halo records (R:dbscan/dbscan.py:136-151) in two ordered passes over the
+// points: halo_tile_kernel counts each tile's records (a tile = one block's
+// 4·256 points), the host scans the tile counts (rocPRIM), and
+// halo_write_kernel recomputes the memberships and writes the (cell key,
+// point id | owner bit | duplicate bit) records at tile offset + wave
+// offset.  No per-point count array, no inter-block waiting (the dispatch
+// order is undefined: cdna_hip_programming.md Guideline 16).
+// Lane l of wave w takes points base + 256 w + 64 q + l (q = 0..3): every
+// load and every record store of one step q is contiguous across the wave.
+// The membership of each point is a bit mask over the neighbourhoods (P <=
+// 64; MASK = false recomputes instead), built branch-free in the input
+// precision with one wave-uniform grid load per neighbourhood.
+template <typename T, int D, bool MASK>
+__device__ __forceinline__ void halo_points(const T* __restrict__ X, uint64_t n,
+                                            const PartGrid* __restrict__ parts, int P,
+                                            uint64_t (&idx)[4], T (&v)[4][D],
+                                            unsigned long long (&m)[4], uint32_t (&cnt)[4]) {
+    const uint64_t base = (uint64_t)blockIdx.x * (4 * kBlock) + (threadIdx.x >> 6) * 256 +
+                          (threadIdx.x & 63);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        idx[q] = base + 64 * q;
+        m[q] = 0;
+        cnt[q] = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) v[q][j] = idx[q] < n ? X[idx[q] * D + j] : T(NAN);
+    }
+    for (int L = 0; L < P; ++L) {
+        const PartGrid& g = parts[L];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool in = in_box_t<T, D>(v[q], g);
+            cnt[q] += in ? 1u : 0u;
+            if constexpr (MASK) m[q] |= (unsigned long long)in << L;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t block_sum_u32(uint32_t v) {
+    __shared__ uint32_t ws[kBlock / 64];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    uint32_t t = 0;
+#pragma unroll
+    for (int u = 0; u < kBlock / 64; ++u) t += ws[u];
+    return t;
+}
+
 template <typename T, int D>
-__global__ __launch_bounds__(kBlock) void halo_count_kernel(const T* __restrict__ X, uint64_t n,
-                                                            const PartGrid* __restrict__ parts,
-                                                            int P, uint32_t* __restrict__ cnt) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    double v[D];
-    load_d<T, D>(X, i, v);
-    uint32_t c = 0;
-    for (int L = 0; L < P; ++L) c += in_box<D>(v, parts[L]) ? 1u : 0u;
-    cnt[i] = c;
+__global__ __launch_bounds__(kBlock) void halo_tile_kernel(const T* __restrict__ X, uint64_t n,
+                                                           const PartGrid* __restrict__ parts,
+                                                           int P, uint32_t* __restrict__ tile_cnt) {
+    uint64_t idx[4];
+    T v[4][D];
+    unsigned long long m[4];
+    uint32_t cnt[4];
+    halo_points<T, D, false>(X, n, parts, P, idx, v, m, cnt);
+    const uint32_t t = block_sum_u32(cnt[0] + cnt[1] + cnt[2] + cnt[3]);
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = t;
 }
 
 template <typename T, int D, typename K>
-__global__ __launch_bounds__(kBlock) void records_kernel(
-    const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
-    const int32_t* __restrict__ owner, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ hcnt, K* __restrict__ keys, uint32_t* __restrict__ vals) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
+__device__ __forceinline__ void halo_record(const T (&tv)[D], const PartGrid& g, K& key) {
     double v[D];
-    load_d<T, D>(X, i, v);
-    const int own = owner ? owner[i] : 0;
-    const uint32_t dup = hcnt[i] >= 2 ? kDupBit : 0u;
-    uint64_t o = off[i];
-    for (int L = 0; L < P; ++L) {
-        const PartGrid& g = parts[L];
-        if (!in_box<D>(v, g)) continue;
-        int64_t c[D];
-        cell_of<D>(v, g, c);
-        keys[o] = (K)(g.base + lin_of<D>(c, g));
-        vals[o] = (uint32_t)i | dup | (L == own ? kOwnerBit : 0u);
-        ++o;
+#pragma unroll
+    for (int j = 0; j < D; ++j) v[j] = (double)tv[j];
+    int64_t c[D];
+    cell_of<D>(v, g, c);
+    key = (K)(g.base + lin_of<D>(c, g));
+}
+
+// The grid fields a record key needs, per neighbourhood, staged in LDS: the
+// lanes of a wave key their points in different neighbourhoods, and per-lane
+// global loads of the grids cost more than the arithmetic.
+template <int D>
+struct KeyGrid {
+    double lo[D], inv[D];
+    int64_t nc[D];
+    uint64_t base;
+};
+
+template <typename T, int D, typename K>
+__device__ __forceinline__ K key_of(const T (&tv)[D], const KeyGrid<D>& g) {
+    uint64_t k = 0;
+#pragma unroll
+    for (int j = D - 1; j >= 0; --j) {
+        int64_t q = (int64_t)floor(((double)tv[j] - g.lo[j]) * g.inv[j]);
+        q = q < 0 ? 0 : q;
+        q = q >= g.nc[j] ? g.nc[j] - 1 : q;
+        k = k * (uint64_t)g.nc[j] + (uint64_t)q;
+    }
+    return (K)(g.base + k);
+}
+
+// Records of a tile in (wave, step, lane, neighbourhood) order:
+// deterministic.  Each point's first record (its lowest neighbourhood) is
+// computed for all lanes at once and stored after the loop, so one step's
+// stores are contiguous; the extra records of the few halo duplicates follow.
+template <typename T, int D, typename K, bool MASK>
+__global__ __launch_bounds__(kBlock) void halo_write_kernel(
+    const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
+    const int32_t* __restrict__ owner, const uint64_t* __restrict__ tile_off, K* __restrict__ keys,
+    uint32_t* __restrict__ vals) {
+    uint64_t idx[4];
+    T v[4][D];
+    unsigned long long m[4];
+    uint32_t cnt[4];
+    halo_points<T, D, MASK>(X, n, parts, P, idx, v, m, cnt);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t ex[4], wtot = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t x = cnt[q];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+            if (lane >= o) x += y;
+        }
+        ex[q] = wtot + x - cnt[q];
+        wtot += (uint32_t)__shfl((int)x, 63, 64);
+    }
+    __shared__ uint32_t ws[kBlock / 64];
+    __shared__ KeyGrid<D> kg[MASK ? 64 : 1];
+    if (lane == 0) ws[w] = wtot;
+    if constexpr (MASK) {
+        for (int L = threadIdx.x; L < P; L += kBlock) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                kg[L].lo[j] = parts[L].lo[j];
+                kg[L].inv[j] = parts[L].inv[j];
+                kg[L].nc[j] = parts[L].nc[j];
+            }
+            kg[L].base = parts[L].base;
+        }
+    }
+    __syncthreads();
+    uint64_t wbase = tile_off[blockIdx.x];
+#pragma unroll
+    for (int u = 0; u < kBlock / 64; ++u) wbase += u < w ? ws[u] : 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (!cnt[q]) continue;
+        const int own = owner ? owner[idx[q]] : 0;   // P == 1: neighbourhood 0
+        const uint32_t tag = (uint32_t)idx[q] | (cnt[q] >= 2 ? kDupBit : 0u);
+        uint64_t o = wbase + ex[q];
+        if constexpr (MASK) {
+            unsigned long long mm = m[q];
+            do {
+                const int L = __ffsll(mm) - 1;
+                mm &= mm - 1;
+                const K key = key_of<T, D, K>(v[q], kg[L]);
+                keys[o] = key;
+                vals[o] = tag | (own == L ? kOwnerBit : 0u);
+                ++o;
+            } while (mm);
+        } else {
+            for (int L = 0; L < P; ++L) {
+                const PartGrid& g = parts[L];
+                if (!in_box_t<T, D>(v[q], g)) continue;
+                K key;
+                halo_record<T, D, K>(v[q], g, key);
+                keys[o] = key;
+                vals[o] = tag | (own == L ? kOwnerBit : 0u);
+                ++o;
+            }
+        }
     }
 }
 
@@ -535,23 +680,75 @@ __global__ void part_start_kernel(const K* __restrict__ keys, uint64_t R,
     ps[L] = (uint32_t)lo;
 }
 
-// Cell starts: flag[r] = 1 where a new key begins, and the key's occupancy
-// bit in its directory word.  Keys are sorted, so the lanes of one word are
-// contiguous: a segmented OR-scan across the wave (Hillis-Steele, equal words
-// at distance o imply equal words in between) leaves each word's bits in its
-// last lane, which adds them with one atomicOr (the bits of different lanes
-// are distinct, and a word can continue into the neighbouring waves).
+// Cell starts, two ordered passes over the sorted keys (four records per
+// lane): a record whose key differs from its predecessor's starts a cell;
+// cell_tile_kernel counts each tile's starts, the host scans the counts, and
+// cell_write_kernel numbers the cells (tile offset + block scan), so
+// cstart[cell] = record.
 template <typename K>
-__global__ __launch_bounds__(kBlock) void run_flag_kernel(const K* __restrict__ keys, uint64_t R,
-                                                          uint32_t* __restrict__ flag,
+__device__ __forceinline__ uint32_t cell_starts4(const K* __restrict__ keys, uint64_t R,
+                                                 uint64_t r0, uint32_t (&st)[4]) {
+    uint32_t c = 0;
+    uint64_t prev = r0 > 0 && r0 < R ? (uint64_t)keys[r0 - 1] : ~0ull;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t r = r0 + q;
+        st[q] = 0;
+        if (r < R) {
+            const uint64_t k = (uint64_t)keys[r];
+            st[q] = (r == 0 || k != prev) ? 1u : 0u;
+            prev = k;
+        }
+        c += st[q];
+    }
+    return c;
+}
+
+template <typename K>
+__global__ __launch_bounds__(kBlock) void cell_tile_kernel(const K* __restrict__ keys, uint64_t R,
+                                                           uint32_t* __restrict__ tile_cnt) {
+    uint32_t st[4];
+    const uint64_t r0 = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    const uint32_t t = block_sum_u32(cell_starts4<K>(keys, R, r0, st));
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = t;
+}
+
+template <typename K>
+__global__ __launch_bounds__(kBlock) void cell_write_kernel(const K* __restrict__ keys, uint64_t R,
+                                                            const uint64_t* __restrict__ tile_off,
+                                                            uint32_t* __restrict__ cstart,
+                                                            uint32_t* __restrict__ ncells) {
+    uint32_t st[4];
+    const uint64_t r0 = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    uint32_t btot;
+    const uint32_t c = cell_starts4<K>(keys, R, r0, st);
+    uint32_t cid = (uint32_t)tile_off[blockIdx.x] + block_excl_scan(c, btot);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (st[q]) cstart[cid] = (uint32_t)(r0 + q);
+        cid += st[q];
+        if (r0 + q == R - 1) {
+            cstart[cid] = (uint32_t)R;
+            *ncells = cid;
+        }
+    }
+}
+
+// Directory occupancy bits, one lane per cell: the cells are sorted, so the
+// lanes of one directory word are contiguous and a segmented OR-scan across
+// the wave (Hillis-Steele; equal words at distance o imply equal words in
+// between) leaves each word's bits in its last lane, which adds them with
+// one atomicOr (a word can continue into the neighbouring waves).
+template <typename K>
+__global__ __launch_bounds__(kBlock) void dir_bits_kernel(const K* __restrict__ keys,
+                                                          const uint32_t* __restrict__ cstart,
+                                                          const uint32_t* __restrict__ ncells,
                                                           uint4* __restrict__ dir) {
-    const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const bool in = r < R;
-    const uint64_t k = in ? (uint64_t)keys[r] : ~0ull;
-    const bool start = in && ((r == 0) || ((uint64_t)keys[r - 1] != k));
-    if (in) flag[r] = start ? 1u : 0u;
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    const bool in = c < *ncells;
+    const uint64_t k = in ? (uint64_t)keys[cstart[c]] : ~0ull;
     const uint64_t word = k >> 6;
-    unsigned long long v = start ? (1ull << (k & 63)) : 0ull;
+    unsigned long long v = in ? (1ull << (k & 63)) : 0ull;
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -561,34 +758,44 @@ __global__ __launch_bounds__(kBlock) void run_flag_kernel(const K* __restrict__ 
     }
     const uint64_t wn = (uint64_t)__shfl_down((long long)word, 1, 64);
     const bool last = lane == 63 || wn != word;
-    if (in && last && v) atomicOr(reinterpret_cast<unsigned long long*>(dir + word), v);
+    if (in && last) atomicOr(reinterpret_cast<unsigned long long*>(dir + word), v);
 }
 
-struct DirPopc {
-    __device__ uint32_t operator()(const uint4& w) const {
-        return (uint32_t)__popc(w.x) + (uint32_t)__popc(w.y);
+// Directory ranks dir[w].z = occupied cells in words < w: per-tile popcount
+// sums, a host-side scan of the tile sums, then the block-scan write (four
+// words per lane).
+__device__ __forceinline__ uint32_t dir_popc4(const uint4* __restrict__ dir, uint64_t W,
+                                              uint64_t w0, uint32_t (&pc)[4]) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        pc[q] = 0;
+        if (w0 + q < W) {
+            const uint4 d = dir[w0 + q];
+            pc[q] = (uint32_t)__popc(d.x) + (uint32_t)__popc(d.y);
+        }
+        t += pc[q];
     }
-};
-
-__global__ __launch_bounds__(kBlock) void dir_pack_kernel(uint4* __restrict__ dir,
-                                                          const uint32_t* __restrict__ rank,
-                                                          uint64_t W) {
-    const uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (w < W) dir[w].z = rank[w];
+    return t;
 }
 
-__global__ __launch_bounds__(kBlock) void cell_start_kernel(const uint32_t* __restrict__ flag,
-                                                            const uint32_t* __restrict__ cid,
-                                                            uint64_t R,
-                                                            uint32_t* __restrict__ cstart,
-                                                            uint32_t* __restrict__ ncells) {
-    const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R) return;
-    if (flag[r]) cstart[cid[r]] = (uint32_t)r;
-    if (r == R - 1) {
-        const uint32_t nc = cid[r] + flag[r];
-        cstart[nc] = (uint32_t)R;
-        *ncells = nc;
+__global__ __launch_bounds__(kBlock) void dir_tile_kernel(const uint4* __restrict__ dir, uint64_t W,
+                                                          uint32_t* __restrict__ tile_cnt) {
+    uint32_t pc[4];
+    const uint32_t t =
+        block_sum_u32(dir_popc4(dir, W, ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4, pc));
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(kBlock) void dir_write_kernel(uint4* __restrict__ dir, uint64_t W,
+                                                           const uint64_t* __restrict__ tile_off) {
+    uint32_t pc[4], btot;
+    const uint64_t w0 = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    uint32_t z = (uint32_t)tile_off[blockIdx.x] + block_excl_scan(dir_popc4(dir, W, w0, pc), btot);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (w0 + q < W) dir[w0 + q].z = z;
+        z += pc[q];
     }
 }
 
@@ -1673,11 +1880,6 @@ __global__ __launch_bounds__(kBlock) void label_kernel(const uint32_t* __restric
     if (i == n - 1) *ncl = (int64_t)rnk[i] + flag[i];
 }
 
-__global__ void total_kernel(const uint64_t* __restrict__ off, const uint32_t* __restrict__ cnt,
-                             uint64_t n, uint64_t* __restrict__ tot) {
-    *tot = n ? off[n - 1] + cnt[n - 1] : 0;
-}
-
 // ------------------------------------------------------------------ driver
 struct EvTimer {
     Ctx& ctx;
@@ -1699,6 +1901,24 @@ struct EvTimer {
 };
 
 inline unsigned blocks(uint64_t n) { return n ? (unsigned)((n + kBlock - 1) / kBlock) : 1u; }
+
+// Exclusive scan of `tiles` per-tile counts into u64 offsets (off[tiles] =
+// total); with `read_total` the total is copied back (syncs) and returned.
+uint64_t tile_offsets(Ctx& ctx, uint32_t* cnt, unsigned tiles, uint64_t* off, hipStream_t s,
+                      bool read_total) {
+    PD_HIP(hipMemsetAsync(cnt + tiles, 0, sizeof(uint32_t), s));
+    size_t tb = 0;
+    PD_HIP(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint64_t)0, (size_t)tiles + 1,
+                                   rocprim::plus<uint64_t>(), s));
+    void* tmp = ctx.arena.get<char>("tile_scan_tmp", tb);
+    PD_HIP(rocprim::exclusive_scan(tmp, tb, cnt, off, (uint64_t)0, (size_t)tiles + 1,
+                                   rocprim::plus<uint64_t>(), s));
+    if (!read_total) return 0;
+    uint64_t* h = (uint64_t*)pinned(ctx, sizeof(uint64_t));
+    PD_HIP(hipMemcpyAsync(h, off + tiles, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    sync(s);
+    return *h;
+}
 inline int xsub_of(const Ctx& ctx) { return ctx.xsub < 1 ? 1 : ctx.xsub; }
 
 // Cell roots (link mode 3, border fast path); also flattens the core records.
@@ -1790,35 +2010,26 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     }
     const T* X = (const T*)a.X;
 
-    // ---- halo records (R:dbscan/dbscan.py:136-151)
-    uint32_t* hcnt = ctx.arena.get<uint32_t>("hcnt", n);
-    uint64_t* hoff = ctx.arena.get<uint64_t>("hoff", n);
-    uint64_t* dtot = ctx.arena.get<uint64_t>("tot", 4);
-    hipLaunchKernelGGL((halo_count_kernel<T, D>), dim3(blocks(n)), dim3(kBlock), 0, s, X, n, parts,
-                       P, hcnt);
-    {
-        size_t tb = 0;
-        PD_HIP(rocprim::exclusive_scan(nullptr, tb, hcnt, hoff, (uint64_t)0, (size_t)n,
-                                       rocprim::plus<uint64_t>(), s));
-        void* tmp = ctx.arena.get<char>("scan_tmp", tb);
-        PD_HIP(rocprim::exclusive_scan(tmp, tb, hcnt, hoff, (uint64_t)0, (size_t)n,
-                                       rocprim::plus<uint64_t>(), s));
-    }
-    hipLaunchKernelGGL(total_kernel, dim3(1), dim3(1), 0, s, hoff, hcnt, n, dtot);
-    uint64_t* htot = (uint64_t*)pinned(ctx, sizeof(uint64_t));
-    PD_HIP(hipMemcpyAsync(htot, dtot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    sync(s);
-    const uint64_t R64 = *htot;
+    // ---- halo records (R:dbscan/dbscan.py:136-151): tile counts, scan, write
+    const unsigned htiles = (unsigned)std::max<uint64_t>(1, (n + 4 * kBlock - 1) / (4 * kBlock));
+    uint32_t* tcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)htiles + 1);
+    uint64_t* toff = ctx.arena.get<uint64_t>("tile_off", (size_t)htiles + 1);
+    hipLaunchKernelGGL((halo_tile_kernel<T, D>), dim3(htiles), dim3(kBlock), 0, s, X, n, parts, P,
+                       tcnt);
+    const uint64_t R64 = tile_offsets(ctx, tcnt, htiles, toff, s, true);
     if (R64 >= 0xFFFFFFFEull) throw Error(-5, "more than 2^32-2 halo records on one device");
     const uint32_t R = (uint32_t)R64;
     ctx.t.records = R;
-
     K* keys = ctx.arena.get<K>("keys", R);
-    K* keys2 = ctx.arena.get<K>("keys2", R);
     uint32_t* vals = ctx.arena.get<uint32_t>("vals", R);
+    K* keys2 = ctx.arena.get<K>("keys2", R);
     uint32_t* vals2 = ctx.arena.get<uint32_t>("vals2", R);
-    hipLaunchKernelGGL((records_kernel<T, D, K>), dim3(blocks(n)), dim3(kBlock), 0, s, X, n, parts,
-                       P, a.owner, hoff, hcnt, keys, vals);
+    if (P <= 64)
+        hipLaunchKernelGGL((halo_write_kernel<T, D, K, true>), dim3(htiles), dim3(kBlock), 0, s, X,
+                           n, parts, P, a.owner, toff, keys, vals);
+    else
+        hipLaunchKernelGGL((halo_write_kernel<T, D, K, false>), dim3(htiles), dim3(kBlock), 0, s,
+                           X, n, parts, P, a.owner, toff, keys, vals);
     PD_HIP(hipGetLastError());
     tm.mark();   // 1
 
@@ -1845,35 +2056,31 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
                        (uint64_t)R, parts, P, part_start);
     const uint64_t W = (Gtot >> 6) + 2;
     uint4* dir = ctx.arena.get<uint4>("dir", W);
-    uint32_t* rank = ctx.arena.get<uint32_t>("dir_rank", W);
     PD_HIP(hipMemsetAsync(dir, 0, sizeof(uint4) * W, s));
-    uint32_t* flag = ctx.arena.get<uint32_t>("flag", R);
-    uint32_t* cid = ctx.arena.get<uint32_t>("cid", R);
     uint32_t* cstart = ctx.arena.get<uint32_t>("cstart", (size_t)R + 1);
     uint32_t* dncells = ctx.arena.get<uint32_t>("ncells", 4);
     if (R) {
-        hipLaunchKernelGGL((run_flag_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s, keys,
-                           (uint64_t)R, flag, dir);
-        size_t tb = 0;
-        PD_HIP(rocprim::exclusive_scan(nullptr, tb, flag, cid, 0u, (size_t)R,
-                                       rocprim::plus<uint32_t>(), s));
-        void* tmp = ctx.arena.get<char>("scan_tmp", tb);
-        PD_HIP(rocprim::exclusive_scan(tmp, tb, flag, cid, 0u, (size_t)R,
-                                       rocprim::plus<uint32_t>(), s));
-        hipLaunchKernelGGL(cell_start_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, flag, cid,
-                           (uint64_t)R, cstart, dncells);
+        const unsigned ctiles = (unsigned)((R + 4 * kBlock - 1) / (4 * kBlock));
+        uint32_t* ccnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)ctiles + 1);
+        uint64_t* coff = ctx.arena.get<uint64_t>("tile_off", (size_t)ctiles + 1);
+        hipLaunchKernelGGL((cell_tile_kernel<K>), dim3(ctiles), dim3(kBlock), 0, s, keys,
+                           (uint64_t)R, ccnt);
+        tile_offsets(ctx, ccnt, ctiles, coff, s, false);
+        hipLaunchKernelGGL((cell_write_kernel<K>), dim3(ctiles), dim3(kBlock), 0, s, keys,
+                           (uint64_t)R, coff, cstart, dncells);
+        hipLaunchKernelGGL((dir_bits_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s, keys, cstart,
+                           dncells, dir);
     } else {
         PD_HIP(hipMemsetAsync(cstart, 0, sizeof(uint32_t), s));
+        PD_HIP(hipMemsetAsync(dncells, 0, sizeof(uint32_t), s));
     }
     {
-        rocprim::transform_iterator<const uint4*, DirPopc, uint32_t> pit(dir, DirPopc());
-        size_t tb = 0;
-        PD_HIP(rocprim::exclusive_scan(nullptr, tb, pit, rank, 0u, (size_t)W,
-                                       rocprim::plus<uint32_t>(), s));
-        void* tmp = ctx.arena.get<char>("scan_tmp", tb);
-        PD_HIP(rocprim::exclusive_scan(tmp, tb, pit, rank, 0u, (size_t)W,
-                                       rocprim::plus<uint32_t>(), s));
-        hipLaunchKernelGGL(dir_pack_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, rank, W);
+        const unsigned wtiles = (unsigned)std::max<uint64_t>(1, (W + 4 * kBlock - 1) / (4 * kBlock));
+        uint32_t* wcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)wtiles + 1);
+        uint64_t* woff = ctx.arena.get<uint64_t>("tile_off", (size_t)wtiles + 1);
+        hipLaunchKernelGGL(dir_tile_kernel, dim3(wtiles), dim3(kBlock), 0, s, dir, W, wcnt);
+        tile_offsets(ctx, wcnt, wtiles, woff, s, false);
+        hipLaunchKernelGGL(dir_write_kernel, dim3(wtiles), dim3(kBlock), 0, s, dir, W, woff);
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 4
@@ -2302,8 +2509,19 @@ void train(Ctx& ctx, TrainArgs& a) {
                 cells *= (long double)g.nc[j];
             }
         }
+        for (int j = 0; j < d; ++j) {
+            float fl = (float)g.elo[j], fh = (float)g.ehi[j];
+            if ((double)fl < g.elo[j]) fl = std::nextafter(fl, INFINITY);
+            if ((double)fh > g.ehi[j]) fh = std::nextafter(fh, -INFINITY);
+            g.flo[j] = fl;
+            g.fhi[j] = fh;
+        }
         if (empty) {
-            for (int j = 0; j < d; ++j) g.nc[j] = 0;
+            for (int j = 0; j < d; ++j) {
+                g.nc[j] = 0;
+                g.elo[j] = g.flo[j] = INFINITY;   // a box no point is in
+                g.ehi[j] = g.fhi[j] = -INFINITY;
+            }
             continue;
         }
         if (cells > 4.0e18L) throw Error(-5, "grid too large (sum of cells > 4e18)");

@@ -30,6 +30,6 @@ if [ "${PROF:-1}" = "1" ]; then
       > gpurun_out/prof_iter.log 2>&1 || { tail -5 gpurun_out/prof_iter.log; exit 1; }
   f=$(ls gpurun_out/prof_iter/*/it_kernel_stats.csv 2>/dev/null | head -1)
   [ -z "$f" ] && f=$(find gpurun_out/prof_iter -name "*kernel_stats.csv" | head -1)
-  python tools/kstats.py "$f" | head -40
+  python tools/kstats.py "$f" 45
 fi
 echo "iter ok"

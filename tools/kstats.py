@@ -21,7 +21,8 @@ def short(name):
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
-for r in rows:
+lim = int(sys.argv[2]) if len(sys.argv) > 2 else len(rows)
+for r in rows[:lim]:
     print("%-48s %5s %10.1f %9.3f" % (short(r["Name"])[:48], r["Calls"],
                                       float(r["AverageNs"]) / 1e3,
                                       float(r["TotalDurationNs"]) / 1e6))

@@ -117,6 +117,21 @@ __device__ __forceinline__ void wave_atomic_min(uint32_t* base, bool valid, uint
     }
 }
 
+// Append val to list where pred holds, one atomic per wave: a wave's entries
+// land contiguously (in lane order), so lists keep the spatial locality of
+// the records that produced them.  Every lane of the wave must call this.
+__device__ __forceinline__ void wave_append(uint32_t* __restrict__ list, uint32_t* __restrict__ count,
+                                            bool pred, uint32_t val) {
+    const unsigned long long b = __ballot(pred);
+    if (!b) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll(b) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(b));
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    if (pred) list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = val;
+}
+
 template <typename T, int D>
 __device__ __forceinline__ void load_d(const T* __restrict__ X, uint64_t i, double (&v)[D]) {
 #pragma unroll
@@ -646,16 +661,23 @@ __global__ __launch_bounds__(kBlock) void halo_write_kernel(
     }
 }
 
+// Coordinates into key order (padded rows); also lists the records of halo
+// points that live in several neighbourhoods (the merge only touches those).
 template <typename T, int D>
 __global__ __launch_bounds__(kBlock) void gather_kernel(const T* __restrict__ X, uint64_t R,
                                                         const uint32_t* __restrict__ vals,
-                                                        T* __restrict__ Xs) {
+                                                        T* __restrict__ Xs,
+                                                        uint32_t* __restrict__ dup_list,
+                                                        uint32_t* __restrict__ dup_count) {
     const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R) return;
-    const uint64_t i = vals[r] & kIdMask;
-    constexpr int S = Stride<D>::v;
+    const uint32_t v = r < R ? vals[r] : 0u;
+    if (r < R) {
+        const uint64_t i = v & kIdMask;
+        constexpr int S = Stride<D>::v;
 #pragma unroll
-    for (int j = 0; j < S; ++j) Xs[r * S + j] = j < D ? X[i * D + j] : T(0);
+        for (int j = 0; j < S; ++j) Xs[r * S + j] = j < D ? X[i * D + j] : T(0);
+    }
+    wave_append(dup_list, dup_count, r < R && (v & kDupBit), (uint32_t)r);
 }
 
 template <typename K>
@@ -977,28 +999,85 @@ __global__ __launch_bounds__(kBlock) void jump_kernel(uint32_t R, const uint8_t*
     par[r] = par[par[r]];   // chains hold core records only
 }
 
-// A point's copies in several neighbourhoods: link every core copy to one
-// representative (the smallest record), gluing the neighbourhoods' clusters.
-__global__ __launch_bounds__(kBlock) void rep_kernel(const uint32_t* __restrict__ vals, uint32_t R,
-                                                     const uint8_t* __restrict__ core,
+// A point's copies in several neighbourhoods (the dup list): link every core
+// copy to one representative (the smallest record), gluing the
+// neighbourhoods' clusters.
+__global__ __launch_bounds__(kBlock) void rep_kernel(const uint32_t* __restrict__ list,
+                                                     const uint32_t* __restrict__ count,
+                                                     const uint32_t* __restrict__ vals,
+                                                     const uint32_t* __restrict__ par,
                                                      uint32_t* __restrict__ rep) {
-    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R || !(core[r] & 1)) return;
-    const uint32_t v = vals[r];
-    if (v & kDupBit) atomicMin(rep + (v & kIdMask), r);
+    const uint32_t nl = *count;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nl; i += gridDim.x * kBlock) {
+        const uint32_t r = list[i];
+        if (par[r] != kNone) atomicMin(rep + (vals[r] & kIdMask), r);
+    }
 }
 
-__global__ __launch_bounds__(kBlock) void merge_kernel(const uint32_t* __restrict__ vals,
-                                                       uint32_t R,
-                                                       const uint8_t* __restrict__ core,
+__global__ __launch_bounds__(kBlock) void merge_kernel(const uint32_t* __restrict__ list,
+                                                       const uint32_t* __restrict__ count,
+                                                       const uint32_t* __restrict__ vals,
                                                        const uint32_t* __restrict__ rep,
                                                        uint32_t* __restrict__ par) {
-    const uint32_t r = rec_index();
-    if (r >= R || !(core[r] & 1)) return;
-    const uint32_t v = vals[r];
-    if (!(v & kDupBit)) return;
-    const uint32_t q = rep[v & kIdMask];
-    if (q != r) uf_unite(par, r, q);
+    const uint32_t nl = *count;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nl; i += gridDim.x * kBlock) {
+        const uint32_t r = list[i];
+        if (ld_rlx(par + r) == kNone) continue;   // not core (par is the core flag)
+        const uint32_t q = rep[vals[r] & kIdMask];
+        if (q != r) uf_unite(par, r, q);
+    }
+}
+
+// Roots: every core record's parent becomes its root (flatten), each root
+// gets the smallest (global) point id of its component (wave-aggregated
+// atomicMin), and the roots are listed (one entry per component of this
+// device) with the count of core records.
+__global__ __launch_bounds__(kBlock) void roots_kernel(uint32_t R, const uint32_t* __restrict__ vals,
+                                                       const uint32_t* __restrict__ gid,
+                                                       uint32_t* __restrict__ par,
+                                                       uint32_t* __restrict__ gmin,
+                                                       uint32_t* __restrict__ root_list,
+                                                       uint32_t* __restrict__ counts, int stats) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t x0 = r < R ? par[r] : kNone;
+    const bool core = x0 != kNone;
+    uint32_t root = 0;
+    if (core) {
+        uint32_t x = x0;
+        while (true) {
+            const uint32_t p = par[x];
+            if (p == x) break;
+            x = p;
+        }
+        if (x != x0) par[r] = x;
+        root = x;
+    }
+    uint32_t pt = core ? (vals[r] & kIdMask) : kNone;
+    if (core && gid) pt = gid[pt];
+    wave_atomic_min(gmin, core, root, pt);
+    // roots are rare (one per component): a wave-aggregated append is cheap
+    if (root_list) wave_append(root_list, counts, core && root == r, r);
+    if (stats) {   // core records (sweep statistics): one atomic per block
+        const uint32_t c = block_sum_u32(core ? 1u : 0u);
+        if (threadIdx.x == 0 && c) atomicAdd(counts + 1, c);
+    }
+}
+
+// Single device: each component's key becomes its label — the rank of its
+// smallest core point id among all components (sklearn's numbering), from
+// the sorted (key, root) pairs.
+__global__ __launch_bounds__(kBlock) void root_keys_kernel(const uint32_t* __restrict__ root_list,
+                                                           uint32_t C,
+                                                           const uint32_t* __restrict__ gmin,
+                                                           uint32_t* __restrict__ keys) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < C) keys[i] = gmin[root_list[i]];
+}
+
+__global__ __launch_bounds__(kBlock) void root_rank_kernel(const uint32_t* __restrict__ roots_sorted,
+                                                           uint32_t C, uint32_t* __restrict__ gmin) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < C) gmin[roots_sorted[i]] = i;
 }
 
 __global__ __launch_bounds__(kBlock) void flatten_kernel(uint32_t R,
@@ -1019,22 +1098,6 @@ __global__ __launch_bounds__(kBlock) void flatten_kernel(uint32_t R,
         x = p;
     }
     if (x != x0) par[r] = x;
-}
-
-// Component key = smallest (global) id of its core points.  gid maps local
-// point ids to global ids on a sharded train (null: identity).
-__global__ __launch_bounds__(kBlock) void gmin_kernel(const uint32_t* __restrict__ vals,
-                                                      uint32_t R,
-                                                      const uint8_t* __restrict__ core,
-                                                      const uint32_t* __restrict__ par,
-                                                      const uint32_t* __restrict__ gid,
-                                                      uint32_t* __restrict__ gmin) {
-    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    const bool ok = r < R && (core[r] & 1);
-    const uint32_t root = ok ? par[r] : 0u;
-    uint32_t pt = ok ? (vals[r] & kIdMask) : kNone;
-    if (ok && gid) pt = gid[pt];
-    wave_atomic_min(gmin, ok, root, pt);
 }
 
 // Sharded train, phase A exports: (global id, local component key) of every
@@ -1088,29 +1151,40 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
                                                        int core_bit,
                                                        uint32_t* __restrict__ key_out,
                                                        uint8_t* __restrict__ core_out,
-                                                       uint32_t* __restrict__ cnt_out) {
+                                                       uint32_t* __restrict__ cnt_out,
+                                                       uint32_t* __restrict__ tile_cnt) {
     const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R) return;
-    const uint32_t v = vals[r];
-    if (!(v & kOwnerBit)) return;
-    const uint32_t pt = v & kIdMask;
-    const uint8_t fl = core[r];
-    if (core_out && !core_bit) core_out[pt] = fl & 1;
-    if (cnt_out) cnt_out[pt] = cnt_rec[r];
-    if (fl & 1) key_out[pt] = gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u);
+    const uint32_t v = r < R ? vals[r] : 0u;
+    const bool own = r < R && (v & kOwnerBit);
+    const uint8_t fl = own ? core[r] : 0;
+    if (own) {
+        const uint32_t pt = v & kIdMask;
+        if (core_out && !core_bit) core_out[pt] = fl & 1;
+        if (cnt_out) cnt_out[pt] = cnt_rec[r];
+        if (fl & 1) key_out[pt] = gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u);
+    }
+    // border candidates (owner record, not core, has a neighbour) per tile;
+    // border_list_kernel lists them in order after a scan of the counts
+    const uint32_t c = block_sum_u32(own && (fl & 3) == 2 ? 1u : 0u);
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(kBlock) void border_list_kernel(uint32_t R,
+                                                             const uint32_t* __restrict__ vals,
+                                                             const uint8_t* __restrict__ core,
+                                                             const uint64_t* __restrict__ tile_off,
+                                                             uint32_t* __restrict__ blist) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    const bool cand = r < R && (vals[r] & kOwnerBit) && (core[r] & 3) == 2;
+    uint32_t btot;
+    const uint32_t off = block_excl_scan(cand ? 1u : 0u, btot);
+    if (btot == 0) return;
+    if (cand) blist[tile_off[blockIdx.x] + off] = r;
 }
 
 struct IsCore {
     const uint8_t* core;
     __device__ bool operator()(uint32_t r) const { return core[r] & 1; }
-};
-
-struct IsBorderCandidate {   // owner record, not core, has a neighbour
-    const uint8_t* core;
-    const uint32_t* vals;
-    __device__ bool operator()(uint32_t r) const {
-        return (core[r] & 3) == 2 && (vals[r] & kOwnerBit);
-    }
 };
 
 // Border records (compacted list): smallest cluster key among the core
@@ -1852,6 +1926,18 @@ __global__ __launch_bounds__(kBlock) void border2_kernel(
     key_out[vals[r] & kIdMask] = best;
 }
 
+// Single device: key_out holds each point's label (rank; kNone = noise) with
+// the core flag in bit 30 — split it into labels and the core mask.
+__global__ __launch_bounds__(kBlock) void final_label_kernel(const uint32_t* __restrict__ key,
+                                                             uint64_t n, int32_t* __restrict__ labels,
+                                                             uint8_t* __restrict__ core_out) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = key[i];
+    labels[i] = k == kNone ? -1 : (int32_t)(k & ~kKeyCoreBit);
+    if (core_out) core_out[i] = (k != kNone && (k & kKeyCoreBit)) ? 1 : 0;
+}
+
 // Keys may carry kKeyCoreBit (owner_kernel core_bit mode): strip it.
 __device__ __forceinline__ uint32_t key_id(uint32_t k, int core_bit) {
     return (core_bit && k != kNone) ? (k & ~kKeyCoreBit) : k;
@@ -2046,8 +2132,11 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     }
     tm.mark();   // 2
     T* Xs = ctx.arena.get<T>("Xs", (size_t)R * Stride<D>::v);
+    uint32_t* dup_list = ctx.arena.get<uint32_t>("dup_list", R);
+    uint32_t* lcount = ctx.arena.get<uint32_t>("list_counts", 8);   // dup, roots, core, border
+    PD_HIP(hipMemsetAsync(lcount, 0, sizeof(uint32_t) * 8, s));
     hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X, (uint64_t)R,
-                       vals, Xs);
+                       vals, Xs, dup_list, lcount);
     tm.mark();   // 3
 
     // ---- cell directory
@@ -2166,20 +2255,46 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     PD_HIP(hipGetLastError());
     tm.mark();   // 6
     if (P > 1 && R) {
+        // the merge touches only the records of points in several neighbourhoods
         uint32_t* rep = ctx.arena.get<uint32_t>("rep", n);
         PD_HIP(hipMemsetAsync(rep, 0xFF, sizeof(uint32_t) * n, s));
-        hipLaunchKernelGGL(rep_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, vals, R, core, rep);
-        hipLaunchKernelGGL(merge_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, vals, R, core, rep,
+        const unsigned gb = std::min(blocks(R), 2048u);
+        hipLaunchKernelGGL(rep_kernel, dim3(gb), dim3(kBlock), 0, s, dup_list, lcount, vals, par,
+                           rep);
+        hipLaunchKernelGGL(merge_kernel, dim3(gb), dim3(kBlock), 0, s, dup_list, lcount, vals, rep,
                            par);
     }
     tm.mark();   // 7
     uint32_t* gmin = ctx.arena.get<uint32_t>("gmin", R);
+    uint32_t n_roots = 0;
     if (R) {
-        hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
+        // single device: the components are listed so that their keys can be
+        // ranked here (labels); sharded: keys stay global ids (merge first)
+        uint32_t* root_list = a.phase == 0 ? ctx.arena.get<uint32_t>("root_list", R) : nullptr;
         PD_HIP(hipMemsetAsync(gmin, 0xFF, sizeof(uint32_t) * R, s));
-        hipLaunchKernelGGL(gmin_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, vals, R, core, par,
-                           a.gid, gmin);
+        hipLaunchKernelGGL(roots_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, vals, a.gid, par,
+                           gmin, root_list, lcount + 1, ctx.sweep_stats ? 1 : 0);
+        uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t) * 4);
+        PD_HIP(hipMemcpyAsync(h, lcount + 1, sizeof(uint32_t) * 2, hipMemcpyDeviceToHost, s));
+        sync(s);
+        n_roots = a.phase == 0 ? h[0] : 0;
+        if (ctx.sweep_stats) ctx.t.core_records = h[1];
+        if (n_roots) {
+            uint32_t* rk = ctx.arena.get<uint32_t>("root_keys", n_roots);
+            uint32_t* rk2 = ctx.arena.get<uint32_t>("root_keys2", n_roots);
+            uint32_t* rl2 = ctx.arena.get<uint32_t>("root_list2", n_roots);
+            hipLaunchKernelGGL(root_keys_kernel, dim3(blocks(n_roots)), dim3(kBlock), 0, s,
+                               root_list, n_roots, gmin, rk);
+            rocprim::double_buffer<uint32_t> kb(rk, rk2), vb(root_list, rl2);
+            size_t tb = 0;
+            PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)n_roots, 0u, 32u, s));
+            void* tmp = ctx.arena.get<char>("root_sort_tmp", tb);
+            PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)n_roots, 0u, 32u, s));
+            hipLaunchKernelGGL(root_rank_kernel, dim3(blocks(n_roots)), dim3(kBlock), 0, s,
+                               vb.current(), n_roots, gmin);
+        }
     }
+    ctx.st.n_roots = n_roots;
     // final cell / word roots for the border sweep's single-root fast path
     // (PD_OPT_BORDER_ROOTS; off by default: on C2 the extra root passes and
     // the 9-row word checks cost more than the sweep they save)
@@ -2263,13 +2378,17 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     const int core_bit = a.phase == 2 ? 0 : 1;
     PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
     if (a.core && !core_bit) PD_HIP(hipMemsetAsync(a.core, 0, n, s));
-    if (R)
-    {
-        hipLaunchKernelGGL(owner_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, vals, core, par,
-                           gmin, st.cnt_rec, core_bit, key_out, a.core, a.counts);
-        uint32_t* blist = nullptr;
-        const uint32_t NB =
-            select_records(ctx, "border_list", R, IsBorderCandidate{core, vals}, &blist, s);
+    if (R) {
+        uint32_t* blist = ctx.arena.get<uint32_t>("border_list", R);
+        const unsigned tiles = blocks(R);
+        uint32_t* tcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)tiles + 1);
+        uint64_t* toff = ctx.arena.get<uint64_t>("tile_off", (size_t)tiles + 1);
+        hipLaunchKernelGGL(owner_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core, par, gmin,
+                           st.cnt_rec, core_bit, key_out, a.core, a.counts, tcnt);
+        const uint32_t NB = (uint32_t)tile_offsets(ctx, tcnt, tiles, toff, s, true);
+        if (NB)
+            hipLaunchKernelGGL(border_list_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core,
+                               toff, blist);
         if (NB)
             launch_border<T, D, M>(ctx.variant, s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par,
                                    gmin, st.wroot, key_out);
@@ -2280,10 +2399,13 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         tm.mark();
         return;
     }
-
-    rank_labels_async(ctx, key_out, n, a.labels, s, core_bit, a.core);
+    // single device: key_out already holds ranks (root_rank_kernel)
+    if (n)
+        hipLaunchKernelGGL(final_label_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key_out, n,
+                           a.labels, a.core);
+    PD_HIP(hipGetLastError());
     tm.mark();   // 10
-    a.n_clusters = rank_labels_count(ctx, s);
+    a.n_clusters = st.n_roots;
 }
 
 // Host-side bookkeeping after phase A (and B): cell count, stage times.

@@ -64,6 +64,7 @@ struct PhaseState {
     float slo = -1.0f, shi = 0.0f;
     uint32_t ncells = 0;
     uint32_t n_exports = 0;
+    uint32_t n_roots = 0;        // components on this device (single device: clusters)
     void* Xs = nullptr;
     void* parts = nullptr;
     uint32_t* part_start = nullptr;

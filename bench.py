@@ -59,6 +59,7 @@ def parse():
                     help="PD_OPT_SWEEP_VARIANT override (bit 0 count, 1 link, 2 border)")
     ap.add_argument("--count-rotate", type=int, default=None,
                     help="PD_OPT_COUNT_ROTATE override (0 = count sweeps always start at the row)")
+    ap.add_argument("--jump-rounds", type=int, default=None, help="PD_OPT_JUMP_ROUNDS override")
     ap.add_argument("--centre-window", type=int, default=None,
                     help="PD_OPT_CENTRE_WINDOW override (link mode 3 centre-row union)")
     ap.add_argument("--rehearse", action="store_true",
@@ -162,6 +163,8 @@ def main():
         ctx.set_option(_native.PD_OPT_COUNT_ROTATE, args.count_rotate)
     if args.link_mode is not None:
         ctx.set_option(_native.PD_OPT_LINK_MODE, args.link_mode)
+    if args.jump_rounds is not None:
+        ctx.set_option(_native.PD_OPT_JUMP_ROUNDS, args.jump_rounds)
     if world > 1:
         from pypardis_amd.distributed import NativeOps, train_sharded
         lo, hi = rank * n // world, (rank + 1) * n // world

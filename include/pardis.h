@@ -58,12 +58,16 @@ enum pd_option {
                                       the reference's single-slice aggregate (slow; for
                                       bit-identical split boundaries).  Default: correctly
                                       rounded, order-independent double-double sums. */
-    PD_OPT_LINK_MODE = 4,  /* union strategy (tuning; labels identical): 3 (default) union
-                              sweep over each core record's own row only, then one pass over
-                              neighbouring cells that tests record pairs only where the
-                              cells' roots differ; 0 initial forest from the count pass's
-                              smallest neighbour + pointer jumping, then a lock-free union
-                              sweep over all core-core edges; 2 that sweep alone */
+    PD_OPT_LINK_MODE = 4,  /* union strategy (tuning; labels identical).  5 (default): forest
+                              from the count pass's two smallest neighbours, a union over the
+                              PD_OPT_CENTRE_WINDOW records after each record (staged in LDS
+                              per wave), then one pass over neighbouring cells that tests
+                              record pairs only where the cells' roots differ (cells whose
+                              rows hold one root are screened out first); 3: the same with a
+                              union over each core record's own row instead of the window;
+                              4: no window union; 0: initial forest + pointer jumping, then a
+                              lock-free union sweep over all core-core edges; 2 that sweep
+                              alone */
     PD_OPT_JUMP_ROUNDS = 5, /* pointer-jumping rounds for link mode 0 (default 4) */
     PD_OPT_XSUB = 6,        /* sub-cells per eps along axis 0 (default 2): finer rows follow
                                the eps-ball's chord more tightly, at 1/xsub the directory
@@ -89,9 +93,11 @@ enum pd_option {
                                 record (r & ~255) when that lies in the query's own row, and
                                 wraps (dense cells: spreads the row-start hot spot; same
                                 counts, same labels); default 1024, 0 = never */,
-    PD_OPT_CENTRE_WINDOW = 13 /* link mode 3: forward candidates each core record tests in the
-                                centre-row union (a heuristic: the cell verify proves or tests
-                                every edge, so labels are the same); default 64, 0 = all */
+    PD_OPT_CENTRE_WINDOW = 13 /* link mode 5: records after each record tested by the window
+                                union (16, 32 or 64; default 16); mode 3: forward candidates
+                                each core record tests in the centre-row union (0 = all).  A
+                                heuristic either way: the cell verify proves or tests every
+                                edge, so labels are the same */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -12,23 +12,57 @@ the GPU box: no JVM, and the reference never travels):
      with the reference's default algorithm='auto' (kd_tree for d <= 15,
      brute GEMM above) — the reference's arithmetic engine
      (R:dbscan/dbscan.py:28-29) — one task per neighbourhood in a process
-     pool, as Spark ``local[*]`` runs ``mapPartitions``; BLAS held to one
-     thread per task, so ``workers`` is the core count used
+     pool over every host core, as Spark ``local[*]`` runs ``mapPartitions``
+     (one task per KD partition, so at most max_partitions cores are busy);
+     BLAS held to one thread per task
   4. merge: local clusters linked through points core in two neighbourhoods;
      a point takes its owner neighbourhood's label (R:dbscan/dbscan.py:153-165
      intent).
 
-Only bench.py's ``cpu_baseline`` leg calls this.
+bench.py runs this module as a child process (``python -m oracle.cpu_ref``),
+never forked from its GPU-initialised process:
+
+  python -m oracle.cpu_ref --config C2 --n 1000000 [--global-jobs]
+
+prints one JSON object: rate, seconds, host cores and CPU model, and (with
+--global-jobs) the rate of one global sklearn DBSCAN with n_jobs = cores, the
+fastest CPU path for the same answer.
 """
 from __future__ import annotations
 
+import argparse
+import json
 import multiprocessing as mp
 import os
+import sys
 import time
 
 import numpy as np
 
 from . import halo, kd_partition
+
+
+def host_info():
+    """Cores this process may use (affinity, capped by OMP_NUM_THREADS when
+    set — a GPU box grants a share of a larger machine), nproc and the CPU
+    model string."""
+    nproc = os.cpu_count() or 1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = nproc
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        avail = min(avail, int(omp))
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return dict(nproc=nproc, cores=max(1, avail), model=model)
 
 
 def _sk_task(args):
@@ -53,9 +87,9 @@ def run(X, eps, min_samples, max_partitions, metric="euclidean", workers=None):
     kd = kd_partition(X, max_partitions)
     _, _, members = halo(X, kd["box_lo"], kd["box_hi"], eps)
     P = len(members)
-    workers = workers or min(P, 16, os.cpu_count() or 1)
+    workers = workers or host_info()["cores"]
     tasks = [(X[m].astype(np.float64), eps, min_samples, metric) for m in members]
-    if workers > 1:
+    if workers > 1 and P > 1:
         with mp.get_context("fork").Pool(workers) as pool:
             local = pool.map(_sk_task, tasks, chunksize=1)
     else:
@@ -91,4 +125,40 @@ def run(X, eps, min_samples, max_partitions, metric="euclidean", workers=None):
         rank = np.empty(nn, np.int64)
         rank[used[np.argsort(first[used])]] = np.arange(len(used))
         labels[ok] = rank[labels[ok]]
-    return labels, time.perf_counter() - t0, workers
+    return labels, time.perf_counter() - t0, min(workers, P)
+
+
+def global_sklearn(X, eps, min_samples, metric="euclidean", jobs=None):
+    """One global sklearn DBSCAN (kd_tree / auto) with n_jobs threads: the
+    fastest CPU path for the same labels.  Returns seconds."""
+    from sklearn.cluster import DBSCAN
+    t0 = time.perf_counter()
+    DBSCAN(eps=eps, min_samples=min_samples, metric=metric, algorithm="auto",
+           n_jobs=jobs or host_info()["cores"]).fit(np.asarray(X, np.float64))
+    return time.perf_counter() - t0
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--n", type=int, required=True)
+    ap.add_argument("--global-jobs", action="store_true")
+    args = ap.parse_args(argv)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from pypardis_amd import synth
+    from . import build
+    build()
+    X, cfg = synth.make_config(args.config, n=args.n)
+    P = cfg.get("max_partitions") or 1
+    info = host_info()
+    _, secs, busy = run(X, cfg["eps"], cfg["min_samples"], P)
+    out = dict(n=args.n, seconds=secs, value=args.n / secs, max_partitions=P,
+               workers=info["cores"], busy_max=busy, **info)
+    if args.global_jobs:
+        g = global_sklearn(X, cfg["eps"], cfg["min_samples"])
+        out.update(global_seconds=g, global_value=args.n / g)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

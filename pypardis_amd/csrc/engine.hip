@@ -881,13 +881,16 @@ done:
     // bit0: core; bit1: has a neighbour besides itself (else it is noise and
     // the border pass skips it)
     core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
-    mn_out[r] = mn;
+    reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, kNone);
     if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
     if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
 }
 
 // Initial forest.  parent doubles as the core flag: kNone marks a non-core
 // record, so an edge test costs one load.
+// The count pass keeps the two smallest neighbours it saw (mn2[r]): the
+// parent is the smaller of them that is core and below r — two candidates
+// leave about half the trees of one (tools/init_forest_study.py).
 __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t R, const uint8_t* __restrict__ core,
                                                       const uint32_t* __restrict__ mn,
                                                       int use_mn, uint32_t* __restrict__ par) {
@@ -897,8 +900,11 @@ __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t R, const uint8_t*
     if (core[r] & 1) {
         p = r;
         if (use_mn) {
-            const uint32_t m = mn[r];
-            if (m < r && (core[m] & 1)) p = m;
+            const uint2 m = reinterpret_cast<const uint2*>(mn)[r];
+            if (m.x < r && (core[m.x] & 1))
+                p = m.x;
+            else if (m.y < r && (core[m.y] & 1))
+                p = m.y;
         }
     }
     par[r] = p;
@@ -1375,7 +1381,7 @@ __global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs
     load_rec<T, D>(Xs, r, a);
     const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
     const uint32_t stop = full ? 0xFFFFFFFFu : ms;
-    uint32_t cnt = 0, mn = r, n_cand = 0;
+    uint32_t cnt = 0, mn = kNone, mn2 = kNone, n_cand = 0;
     with_part(C.part_start, C.P, r, [&](int L, auto U) {
         const QueryCell<D> Q = decltype(U)::value ? query_cell_u<D>(C.parts + L, a)
                                                   : query_cell<D>(C.parts + L, a);
@@ -1418,7 +1424,9 @@ __global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs
                     for (int u = 0; u < 4; ++u) {
                         const bool h = (v + u < tot) && pr(b[u]);
                         cnt += h ? 1u : 0u;
-                        mn = (h && j[u] < mn) ? j[u] : mn;
+                        const uint32_t jj = h ? j[u] : kNone;
+                        mn2 = min(mn2, max(mn, jj));   // the two smallest hits
+                        mn = min(mn, jj);
                     }
                     if constexpr (ST) n_cand += (tot - v < 4u ? tot - v : 4u);
                     if (cnt >= stop) return true;
@@ -1430,7 +1438,7 @@ __global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs
         }
     });
     core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
-    mn_out[r] = mn;
+    reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, mn2);
     if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
     if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
 }
@@ -1500,6 +1508,75 @@ __global__ __launch_bounds__(kBlock) void centre_link_kernel(const T* __restrict
         load_raw<T, D>(Xs, j, b0);
         const uint32_t p0 = ld_l1(par + j);
         if (pr(b0)) lk.edge(j, p0);
+    }
+}
+
+// Link mode 5: the union over record windows.  A wave stages its 64
+// records plus the W after them (coordinates and parents of the smallest-
+// neighbour forest, flattened) in LDS once; each core lane then tests the W
+// records that follow it in key order — its own cell and row first, the
+// next rows after — and unions the core ones within eps whose root differs.
+// No per-record row lookup, no global candidate loads: the same role as the
+// centre-row union of mode 3 (a heuristic; the cell verify proves or tests
+// every core-core edge, so the labels are the same) at a fraction of the
+// fixed cost per record.
+template <typename T, int D, int M, int W, bool ST>
+__global__ __launch_bounds__(kBlock) void window_link_kernel(const T* __restrict__ Xs, uint32_t R,
+                                                             double eps, double eps2, float lo,
+                                                             float hi, uint32_t* __restrict__ par,
+                                                             unsigned long long* __restrict__ stats) {
+    constexpr int E = 64 + W;
+    __shared__ T sx[kBlock / 64][E][D];
+    __shared__ uint32_t sp[kBlock / 64][E];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t b = xcd_block(blockIdx.x, gridDim.x) * kBlock + w * 64;
+    for (int e = lane; e < E; e += 64) {
+        const uint32_t j = b + e;
+        T v[D];
+        uint32_t p = kNone;
+        if (j < R) {
+            load_raw<T, D>(Xs, j, v);
+            p = ld_l1(par + j);
+        } else {
+#pragma unroll
+            for (int k = 0; k < D; ++k) v[k] = T(0);
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) sx[w][e][k] = v[k];
+        sp[w][e] = p;
+    }
+    __syncthreads();
+    const uint32_t r = b + lane;
+    const uint32_t p0 = r < R ? sp[w][lane] : kNone;
+    if (p0 == kNone) return;   // not core
+    Pred<T, D, M> pr;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        pr.ar[k] = sx[w][lane][k];
+        pr.a[k] = (double)pr.ar[k];
+    }
+    pr.eps = eps;
+    pr.eps2 = eps2;
+    pr.lo = lo;
+    pr.hi = hi;
+    Linker<ST> lk{par, p0, {}};
+#pragma unroll 4
+    for (int k = 1; k <= W; ++k) {
+        const uint32_t pj = sp[w][lane + k];
+        if (pj == kNone || pj == lk.rr || r + k >= R) continue;   // non-core / same tree
+        T bj[D];
+#pragma unroll
+        for (int q = 0; q < D; ++q) bj[q] = sx[w][lane + k][q];
+        if constexpr (ST) ++lk.st.cand;
+        if (pr(bj)) lk.edge(r + k, pj);
+    }
+    if constexpr (ST) {
+        atomicAdd(stats + 1, (unsigned long long)lk.st.cand);
+        atomicAdd(stats + 2, (unsigned long long)lk.st.hit);
+        atomicAdd(stats + 3, (unsigned long long)lk.st.core);
+        atomicAdd(stats + 4, (unsigned long long)lk.st.same);
+        atomicAdd(stats + 5, (unsigned long long)lk.st.find_same);
+        atomicAdd(stats + 6, (unsigned long long)lk.st.unions);
     }
 }
 
@@ -1634,41 +1711,21 @@ __device__ __noinline__ void pair_block(const T* __restrict__ Xs, uint32_t s0, u
     }
 }
 
-template <typename T, int D, int M, typename K>
-__global__ __launch_bounds__(kBlock) void cell_verify_kernel(
-    const T* __restrict__ Xs, const K* __restrict__ keys, const uint32_t* __restrict__ ncells,
-    const uint32_t* __restrict__ croot, const uint32_t* __restrict__ wroot, Cells C, int xsub,
-    double eps, double eps2, float lo, float hi, uint32_t* __restrict__ par,
-    uint2* __restrict__ plist, uint32_t pcap, uint32_t* __restrict__ pcount,
-    unsigned long long* __restrict__ stats) {
+// The forward rows of cell c (its own row from the cell on, and the rows
+// after it: key order is lexicographic from the last axis; row q's offsets
+// o_j = digit j-1 of q in base 3, minus 1): their key ranges [k0, k1).
+template <int D, typename K>
+struct ForwardRows {
+    static constexpr int NF = (NRows<D>::v + 1) / 2;
+    uint64_t k0[NF], k1[NF];
+    bool ok[NF];
+};
+
+template <int D, typename K>
+__device__ __forceinline__ void forward_rows(const K* __restrict__ keys, const Cells& C, uint32_t s0,
+                                             int xsub, ForwardRows<D, K>& fr) {
     constexpr int NR = NRows<D>::v;
-    constexpr uint32_t kBuf = 1024;
-    // cell pairs whose roots differ go to a list, resolved by pair_kernel, so
-    // the rare record-level work does not stall this kernel's waves: staged
-    // per block in LDS, one global reservation per block (overflow of the
-    // block buffer or of the list: resolved in place)
-    __shared__ uint2 lbuf[kBuf];
-    __shared__ uint32_t lcnt, lbase;
-    if (threadIdx.x == 0) lcnt = 0;
-    __syncthreads();
-    const uint32_t c = xcd_block(blockIdx.x, gridDim.x) * kBlock + threadIdx.x;
-    const uint32_t rc = c < *ncells ? croot[c] : kNone;
-    uint32_t pairs = 0;
-    if (rc != kNone) {
-    const uint32_t s0 = C.cstart[c], e0 = C.cstart[c + 1];
-    auto defer = [&](uint32_t c2) {
-        ++pairs;
-        const uint32_t slot = atomicAdd(&lcnt, 1u);
-        if (slot < kBuf) {
-            lbuf[slot] = make_uint2(c, c2);
-        } else {
-            const bool same = c2 == c;
-            const bool uni = !same && rc != kMixed && croot[c2] != kMixed;
-            pair_block<T, D, M>(Xs, s0, e0, same ? s0 : C.cstart[c2], same ? e0 : C.cstart[c2 + 1],
-                                same, uni, eps, eps2, lo, hi, par);
-        }
-    };
-    if (rc == kMixed) defer(c);
+    constexpr int NF = ForwardRows<D, K>::NF;
     // the cell's grid coordinates (wave-uniform neighbourhood in the common case)
     const int L = part_of_wave(C.part_start, C.P, s0);
     const PartGrid* gp = C.parts + L;
@@ -1698,12 +1755,6 @@ __global__ __launch_bounds__(kBlock) void cell_verify_kernel(
         }
         lin = qt;
     }
-    // forward rows (key order is lexicographic from the last axis; row q's
-    // offsets o_j = digit j-1 of q in base 3, minus 1): their key ranges, and
-    // a first look at their directory-word roots, all issued together
-    constexpr int NF = (NR + 1) / 2;   // the own row and the rows after it
-    uint64_t k0[NF], k1[NF];
-    bool okr[NF];
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
         const int q = NR / 2 + f;   // rows NR/2 .. NR-1 are the own row and those after
@@ -1722,24 +1773,112 @@ __global__ __launch_bounds__(kBlock) void cell_verify_kernel(
 #pragma unroll
         for (int j = D - 1; j >= 0; --j)
             kk = kk * (uint64_t)nc[j] + (uint64_t)(j == 0 ? x0 : cc[j] + o[j]);
-        k0[f] = okq ? kk + base : 0;
-        k1[f] = okq ? kk + base + (uint64_t)(x1 - x0) + 1 : 1;
-        okr[f] = okq;
+        fr.k0[f] = okq ? kk + base : 0;
+        fr.k1[f] = okq ? kk + base + (uint64_t)(x1 - x0) + 1 : 1;
+        fr.ok[f] = okq;
     }
+}
+
+// Cell verify, first pass: which cells need record-level work at all.  A
+// cell with one root R (not mixed) whose forward rows' directory words hold
+// no root but R is settled; the others are flagged (flag byte per cell, and
+// per-tile counts for the ordered work list).
+template <int D, typename K>
+__global__ __launch_bounds__(kBlock) void verify_screen_kernel(
+    const K* __restrict__ keys, const uint32_t* __restrict__ ncells,
+    const uint32_t* __restrict__ croot, const uint32_t* __restrict__ wroot, Cells C, int xsub,
+    uint8_t* __restrict__ flags, uint32_t* __restrict__ tile_cnt) {
+    constexpr int NF = ForwardRows<D, K>::NF;
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t nc = *ncells;
+    const uint32_t rc = c < nc ? croot[c] : kNone;
+    bool work = rc == kMixed;
+    if (rc != kNone && rc != kMixed) {
+        ForwardRows<D, K> fr;
+        forward_rows<D, K>(keys, C, C.cstart[c], xsub, fr);
+        uint32_t wa[NF], wb[NF];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+            wa[f] = wroot[fr.k0[f] >> 6];
+            wb[f] = wroot[(fr.k1[f] - 1) >> 6];
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+            work |= fr.ok[f] && !((wa[f] == kNone || wa[f] == rc) && (wb[f] == kNone || wb[f] == rc));
+    }
+    if (c < nc) flags[c] = work ? 1 : 0;
+    const uint32_t t = block_sum_u32(work ? 1u : 0u);
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = t;
+}
+
+// Ordered list of the indices i < n with flags[i] set (tile offsets from a
+// scan of the per-tile counts).
+__global__ __launch_bounds__(kBlock) void flag_list_kernel(const uint8_t* __restrict__ flags,
+                                                           const uint32_t* __restrict__ n_dev,
+                                                           const uint64_t* __restrict__ tile_off,
+                                                           uint32_t* __restrict__ list) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const bool f = i < *n_dev && flags[i];
+    uint32_t btot;
+    const uint32_t off = block_excl_scan(f ? 1u : 0u, btot);
+    if (f) list[tile_off[blockIdx.x] + off] = i;
+}
+
+// Cell verify, second pass, over the flagged cells only: per forward row
+// whose words hold another root, the neighbouring cells whose root differs
+// are deferred as cell pairs.
+template <typename T, int D, int M, typename K>
+__global__ __launch_bounds__(kBlock) void cell_verify_kernel(
+    const T* __restrict__ Xs, const K* __restrict__ keys, const uint32_t* __restrict__ clist,
+    uint32_t nlist, const uint32_t* __restrict__ croot, const uint32_t* __restrict__ wroot,
+    Cells C, int xsub, double eps, double eps2, float lo, float hi, uint32_t* __restrict__ par,
+    uint2* __restrict__ plist, uint32_t pcap, uint32_t* __restrict__ pcount,
+    unsigned long long* __restrict__ stats) {
+    constexpr int NF = ForwardRows<D, K>::NF;
+    constexpr uint32_t kBuf = 1024;
+    // cell pairs whose roots differ go to a list, resolved by pair_kernel, so
+    // the rare record-level work does not stall this kernel's waves: staged
+    // per block in LDS, one global reservation per block (overflow of the
+    // block buffer or of the list: resolved in place)
+    __shared__ uint2 lbuf[kBuf];
+    __shared__ uint32_t lcnt, lbase;
+    if (threadIdx.x == 0) lcnt = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t c = i < nlist ? clist[i] : 0u;
+    const uint32_t rc = i < nlist ? croot[c] : kNone;
+    uint32_t pairs = 0;
+    if (rc != kNone) {
+    const uint32_t s0 = C.cstart[c], e0 = C.cstart[c + 1];
+    auto defer = [&](uint32_t c2) {
+        ++pairs;
+        const uint32_t slot = atomicAdd(&lcnt, 1u);
+        if (slot < kBuf) {
+            lbuf[slot] = make_uint2(c, c2);
+        } else {
+            const bool same = c2 == c;
+            const bool uni = !same && rc != kMixed && croot[c2] != kMixed;
+            pair_block<T, D, M>(Xs, s0, e0, same ? s0 : C.cstart[c2], same ? e0 : C.cstart[c2 + 1],
+                                same, uni, eps, eps2, lo, hi, par);
+        }
+    };
+    if (rc == kMixed) defer(c);
+    ForwardRows<D, K> fr;
+    forward_rows<D, K>(keys, C, s0, xsub, fr);
     uint32_t wa[NF], wb[NF];
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-        wa[f] = wroot[k0[f] >> 6];
-        wb[f] = wroot[(k1[f] - 1) >> 6];
+        wa[f] = wroot[fr.k0[f] >> 6];
+        wb[f] = wroot[(fr.k1[f] - 1) >> 6];
     }
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-        if (!okr[f]) continue;
+        if (!fr.ok[f]) continue;
         // the row's words hold no root but ours: nothing to test
         if (rc != kMixed && (wa[f] == kNone || wa[f] == rc) && (wb[f] == kNone || wb[f] == rc))
             continue;
-        const uint32_t i0 = dir_rank(C.dir[k0[f] >> 6], k0[f]);
-        const uint32_t i1 = dir_rank(C.dir[k1[f] >> 6], k1[f]);
+        const uint32_t i0 = dir_rank(C.dir[fr.k0[f] >> 6], fr.k0[f]);
+        const uint32_t i1 = dir_rank(C.dir[fr.k1[f] >> 6], fr.k1[f]);
         for (uint32_t c2 = i0 > c + 1 ? i0 : c + 1; c2 < i1; ++c2) {
             const uint32_t r2 = croot[c2];
             if (r2 == kNone || (r2 == rc && rc != kMixed)) continue;
@@ -2186,7 +2325,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         }
     }
     uint8_t* core = ctx.arena.get<uint8_t>("core", R);
-    uint32_t* mn = ctx.arena.get<uint32_t>("minnbr", R);
+    uint32_t* mn = ctx.arena.get<uint32_t>("minnbr", 2 * (size_t)R);   // two smallest (uint2)
     uint32_t* cnt_rec = a.counts ? ctx.arena.get<uint32_t>("cnt_rec", R) : nullptr;
     unsigned long long* sst = nullptr;
     if (ctx.sweep_stats) {
@@ -2212,13 +2351,32 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     tm.mark();   // 5
 
     uint32_t* par = ctx.arena.get<uint32_t>("parent", R);
-    if (R && mode == 3) {
+    if (R && (mode == 3 || mode == 4 || mode == 5)) {
         // forest from the count pass's smallest neighbour (links across rows)
         hipLaunchKernelGGL(init_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, mn, 1, par);
         hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
-        hipLaunchKernelGGL((centre_link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs,
-                           R, C, eps, eps2, slo, shi,
-                           ctx.centre_window ? (uint32_t)ctx.centre_window : 0xFFFFFFFFu, par);
+        if (mode == 3) {
+            hipLaunchKernelGGL((centre_link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                               Xs, R, C, eps, eps2, slo, shi,
+                               ctx.centre_window ? (uint32_t)ctx.centre_window : 0xFFFFFFFFu, par);
+        } else if (mode == 5) {
+            const int cw = ctx.centre_window;
+            auto go = [&](auto Wc) {
+                constexpr int Wv = decltype(Wc)::value;
+                if (sst)
+                    hipLaunchKernelGGL((window_link_kernel<T, D, M, Wv, true>), dim3(blocks(R)),
+                                       dim3(kBlock), 0, s, Xs, R, eps, eps2, slo, shi, par, sst);
+                else
+                    hipLaunchKernelGGL((window_link_kernel<T, D, M, Wv, false>), dim3(blocks(R)),
+                                       dim3(kBlock), 0, s, Xs, R, eps, eps2, slo, shi, par, sst);
+            };
+            if (cw <= 16)
+                go(std::integral_constant<int, 16>{});
+            else if (cw <= 32)
+                go(std::integral_constant<int, 32>{});
+            else
+                go(std::integral_constant<int, 64>{});
+        }
         uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
         cell_roots(ctx, s, R, cstart, dncells, par, croot);
         uint32_t* wroot = ctx.arena.get<uint32_t>("word_root", W);
@@ -2228,9 +2386,22 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         uint2* plist = ctx.arena.get<uint2>("pair_list", pcap);
         uint32_t* pcount = ctx.arena.get<uint32_t>("pair_count", 4);
         PD_HIP(hipMemsetAsync(pcount, 0, sizeof(uint32_t), s));
-        hipLaunchKernelGGL((cell_verify_kernel<T, D, M, K>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                           Xs, keys, dncells, croot, wroot, C, xsub_of(ctx), eps, eps2, slo, shi,
-                           par, plist, pcap, pcount, sst);
+        // verify: screen every cell, then work on the flagged ones only
+        const unsigned vtiles = blocks(R);
+        uint8_t* vflag = ctx.arena.get<uint8_t>("verify_flags", R);
+        uint32_t* vlist = ctx.arena.get<uint32_t>("verify_list", R);
+        uint32_t* vcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)vtiles + 1);
+        uint64_t* voff = ctx.arena.get<uint64_t>("tile_off", (size_t)vtiles + 1);
+        hipLaunchKernelGGL((verify_screen_kernel<D, K>), dim3(vtiles), dim3(kBlock), 0, s, keys,
+                           dncells, croot, wroot, C, xsub_of(ctx), vflag, vcnt);
+        const uint32_t NV = (uint32_t)tile_offsets(ctx, vcnt, vtiles, voff, s, true);
+        if (NV) {
+            hipLaunchKernelGGL(flag_list_kernel, dim3(vtiles), dim3(kBlock), 0, s, vflag, dncells,
+                               voff, vlist);
+            hipLaunchKernelGGL((cell_verify_kernel<T, D, M, K>), dim3(blocks(NV)), dim3(kBlock), 0,
+                               s, Xs, keys, vlist, NV, croot, wroot, C, xsub_of(ctx), eps, eps2,
+                               slo, shi, par, plist, pcap, pcount, sst);
+        }
         hipLaunchKernelGGL((pair_kernel<T, D, M>), dim3(std::min(blocks(pcap), 4096u)), dim3(kBlock), 0, s, Xs, plist,
                            pcount, pcap, cstart, croot, eps, eps2, slo, shi, par);
     } else if (R) {

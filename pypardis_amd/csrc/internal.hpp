@@ -87,10 +87,12 @@ struct Ctx {
     bool timing = false;
     bool full_counts = false;    // debug: count every neighbour (no early exit)
     bool seq_moments = false;    // reference-order (sequential) KD moment sums
-    int link_mode = 3;           // 3 samples + cell verify; 0 init forest + jumps + union sweep; 2 union sweep only
+    int link_mode = 5;           // 5 window union + cell verify; 3 centre-row union + cell verify;
+                                 // 4 cell verify alone; 0 init forest + jumps + union sweep; 2 union sweep only
     int jump_rounds = 4;
     int xsub = 2;                // axis-0 sub-cells per eps
-    int centre_window = 64;     // link mode 3: forward candidates per centre-row union (0: all)
+    int centre_window = 16;     // link mode 5: records after each record tested (16/32/64);
+                                 // mode 3: forward candidates per centre-row union (0: all)
     int count_rotate = 1024;     // count sweep: lists longer than this start near the query (0: off)
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes

@@ -229,7 +229,7 @@ def test_train_matches_oracle(native, case):
 
 
 @pytest.mark.parametrize("variant,link_mode,border_roots",
-                         [(0, 3, 0), (7, 3, 1), (5, 0, 0), (7, 2, 0)])
+                         [(0, 5, 0), (7, 3, 1), (5, 0, 0), (7, 2, 0), (5, 4, 0), (5, 3, 0)])
 def test_sweep_variants_exact(native, variant, link_mode, border_roots):
     """PD_OPT_SWEEP_VARIANT x PD_OPT_LINK_MODE: the row-by-row and the
     batched sweep kernels, and the sampled-union + cell-verify link (3) or the
@@ -592,15 +592,19 @@ def test_c4_skew_vs_oracle(native, case):
     # rotated count starts on every long list / never; centre-row union
     # window of 1 candidate / unbounded
     ctx = native.context()
-    for opt, val, default in ((native.PD_OPT_COUNT_ROTATE, 16, 1024),
-                              (native.PD_OPT_COUNT_ROTATE, 0, 1024),
-                              (native.PD_OPT_CENTRE_WINDOW, 1, 64),
-                              (native.PD_OPT_CENTRE_WINDOW, 0, 64)):
-        ctx.set_option(opt, val)
+    for opts in (((native.PD_OPT_COUNT_ROTATE, 16, 1024),),
+                 ((native.PD_OPT_COUNT_ROTATE, 0, 1024),),
+                 ((native.PD_OPT_CENTRE_WINDOW, 64, 16),),
+                 ((native.PD_OPT_LINK_MODE, 3, 5), (native.PD_OPT_CENTRE_WINDOW, 1, 16)),
+                 ((native.PD_OPT_LINK_MODE, 3, 5), (native.PD_OPT_CENTRE_WINDOW, 0, 16))):
+        for opt, val, _ in opts:
+            ctx.set_option(opt, val)
         try:
             m = DBSCAN(eps=eps, min_samples=ms, max_partitions=8).train(Xd)
         finally:
-            ctx.set_option(opt, default)
+            for opt, _, default in opts:
+                ctx.set_option(opt, default)
+        opt, val = opts[-1][0], opts[-1][1]
         assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), want), (opt, val)
         assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_w), (opt, val)
 

@@ -8,22 +8,32 @@
            partition (3 BFS levels of GPU passes), 2·eps halo, per-neighbourhood
            DBSCAN, merge, global labels (labels stay in HBM).
 
-  python bench.py [--gpus N --steps K --warmup W] [--points N] [--no-cpu]
+  python bench.py [--gpus N --steps K --warmup W] [--config C2|C1|C3|C4]
+                  [--points N] [--no-cpu] [--no-host]
 
-For N > 1 (torch.distributed.run, one rank per GPU, RCCL) the same 100M
-points are split by index over the ranks and the step is the sharded train
-(pypardis_amd/distributed.py: KD levels with all-reduced moments/counts,
-routing + all-to-all-v of the halo records, per-GPU clustering of its
-max_partitions/N neighbourhoods, all-gather label merge, global ranks):
-strong scaling, value = total points / max-over-ranks time.
+For N > 1 (torch.distributed.run, one rank per GPU, RCCL) the same points are
+split by index over the ranks and the step is the sharded train (KD levels
+with all-reduced moments/counts, routing + all-to-all-v of the halo records,
+per-GPU clustering of its neighbourhoods, all-gather label merge, global
+ranks): strong scaling, value = total points / max-over-ranks time.
 
-Roofline object: the neighbour-count kernel (count2_kernel in engine.hip, or
-count_kernel with --sweep-variant bit 0 clear).
-achieved = B_nc / t, B_nc = records * (3^d*4d + 4d + 4) + (cells + 1) * 4 bytes
-(340 B per record in 3-D), t = the kernel's HIP-event time on
-its own stream, averaged over the timed steps.  traffic = FETCH_SIZE*2 +
-WRITE_SIZE per launch from profiles/*pmc*.json when present (gfx950 FETCH_SIZE
-reads half the bytes of wide streaming loads: MI355X_MICROARCH.md §HBM).
+Roofline object — the neighbour-count kernel (count2_kernel, engine.hip):
+  frac / achieved: the algorithmic MODEL of SURVEY.md §8(d), B_nc = records *
+      (3^d*4d + 4d + 4) + (cells + 1) * 4 bytes, over the kernel's HIP-event
+      time on its own stream.  It charges every candidate cell's coordinates
+      once per record with no cache reuse: a work model, not a DRAM reading;
+  traffic / hbm_frac / l2_hit: MEASURED, from the newest PMC summary of the
+      same kernel and config (profiles/rNN_vMM_pmc[_cK]_summary.json, made by
+      tools/pmc_run.sh): traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per
+      launch (gfx950 FETCH_SIZE counts half the bytes of wide reads:
+      MI355X_MICROARCH.md §HBM), hbm_frac = traffic / kernel time / 8 TB/s;
+  limiter: candidate tests per record and per second (the kernel's work unit).
+stage_roofline gives the link stage the same measured accounting.
+
+Other legs (single process): cpu_baseline — the reference's algorithm on the
+host cores, in a child process started before the GPU is touched
+(python -m oracle.cpu_ref); host_input — the same train from host numpy (H2D
+inside the step) and from a list of (key, vector) records.
 """
 from __future__ import annotations
 
@@ -31,6 +41,8 @@ import argparse
 import glob
 import json
 import os
+import re
+import subprocess
 import sys
 import time
 
@@ -41,6 +53,10 @@ sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md; no sparsity)
+BASELINE_METRIC = "points clustered/sec (whole node), 100M 3-D pts, 1/2/4/8 GPUs; % HBM roofline"
+LINK_KERNELS = ("init_kernel", "flatten_kernel", "window_link_kernel", "centre_link_kernel",
+                "link_kernel", "link2_kernel", "cell_root_kernel", "word_root_kernel",
+                "verify_screen_kernel", "flag_list_kernel", "cell_verify_kernel", "pair_kernel")
 
 
 def parse():
@@ -51,8 +67,9 @@ def parse():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--points", type=int, default=None, help="override point count")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-input legs")
     ap.add_argument("--cpu-n", type=int, default=None,
-                    help="CPU baseline sample size (default 1M points; 20k for d > 15)")
+                    help="CPU baseline sample size (default 1M; 10M for C4; 20k for d > 15)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--link-mode", type=int, default=None, help="PD_OPT_LINK_MODE override")
     ap.add_argument("--sweep-variant", type=int, default=None,
@@ -61,15 +78,17 @@ def parse():
                     help="PD_OPT_COUNT_ROTATE override (0 = count sweeps always start at the row)")
     ap.add_argument("--jump-rounds", type=int, default=None, help="PD_OPT_JUMP_ROUNDS override")
     ap.add_argument("--centre-window", type=int, default=None,
-                    help="PD_OPT_CENTRE_WINDOW override (link mode 3 centre-row union)")
+                    help="PD_OPT_CENTRE_WINDOW override (link window length)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
     return ap.parse_args()
 
 
-def default_cpu_n(d):
-    return 20_000 if d > 15 else 1_000_000
+def default_cpu_n(cfg_name, d):
+    if d > 15:
+        return 20_000
+    return 10_000_000 if cfg_name == "C4" else 1_000_000
 
 
 def b_nc(records, cells, d):
@@ -77,63 +96,230 @@ def b_nc(records, cells, d):
     return records * per + (cells + 1) * 4, per
 
 
-def load_pmc(kernel="count_kernel", config="C2"):
-    """Per-launch HBM bytes of `kernel` from the newest PMC summary of the same
-    config that has it (profiles/rNN_vMM_pmc[_cK]_summary.json; no _cK tag =
-    C2; newest = highest (round, version))."""
-    import re
+def _order(f):
+    m = re.search(r"r(\d+)_v(\d+)", os.path.basename(f))
+    return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
 
-    def order(f):
-        m = re.search(r"r(\d+)_v(\d+)", os.path.basename(f))
-        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
 
+def load_pmc(config="C2"):
+    """Newest PMC summary of `config` (profiles/rNN_vMM_pmc[_cK]_summary.json;
+    no _cK tag = C2; newest = highest (round, version)): (dict, file name)."""
     def tag(f):
         m = re.search(r"pmc_(c\d)_", os.path.basename(f))
         return m.group(1).upper() if m else "C2"
 
-    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*pmc*.json")), key=order,
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*pmc*summary*.json")), key=_order,
                     reverse=True):
         if tag(f) != config:
             continue
         try:
-            k = json.load(open(f)).get(kernel)
+            return json.load(open(f)), os.path.basename(f)
         except Exception:
             continue
-        if k and "hbm_bytes_per_launch" in k:
-            return dict(bytes_per_launch=k["hbm_bytes_per_launch"], source=os.path.basename(f))
-    return None
+    return None, None
 
 
-def cpu_baseline(cfg_name, n_sample, n_full):
-    import oracle
-    from oracle import cpu_ref
-    from pypardis_amd import synth
-    X, cfg = synth.make_config(cfg_name, n=n_sample)
-    oracle.build()
-    labels, secs, workers = cpu_ref.run(X, cfg["eps"], cfg["min_samples"],
-                                        cfg.get("max_partitions") or 1)
-    out = {"value": n_sample / secs, "unit": "points/s", "cores": workers, "kind": "port",
-           "seconds": secs,
-           "sample": (f"{cfg_name} {'sample of the same distribution (NOT density-preserving: ' if cfg_name == 'C4' else 'density-preserving slice'}"
-                      f"{'sparser than the full set, so the CPU rate is optimistic)' if cfg_name == 'C4' else ''}, {n_sample} pts, "
-                      f"max_partitions={cfg.get('max_partitions')}: numpy KD + halo, "
-                      f"sklearn 1.7.2 DBSCAN (algorithm='auto') per neighbourhood in a "
-                      f"{workers}-process pool, 1 BLAS thread each (Spark local[*] emulation), "
-                      "owner-rule merge")}
-    if X.shape[1] > 15:   # brute force: O(n^2) work, the rate falls as 1/n
+def pmc_fields(k):
+    """Measured per-launch HBM bytes and L2 hit rate from one kernel's counters."""
+    out = {}
+    if "FETCH_SIZE" in k or "WRITE_SIZE" in k:
+        out["hbm_bytes"] = (2 * k.get("FETCH_SIZE", 0.0) + k.get("WRITE_SIZE", 0.0)) * 1024
+    h, m = k.get("TCC_HIT_sum"), k.get("TCC_MISS_sum")
+    if h is not None and m is not None and h + m > 0:
+        out["l2_hit"] = h / (h + m)
+    return out
+
+
+def calibration():
+    fs = sorted(glob.glob(os.path.join(HERE, "profiles", "*cpu_calibration*.json")), key=_order)
+    if not fs:
+        return None
+    try:
+        c = json.load(open(fs[-1]))
+    except Exception:
+        return None
+    c["source"] = os.path.basename(fs[-1])
+    return c
+
+
+def cpu_baseline(cfg_name, n_sample, n_full, d):
+    """The reference's algorithm on the host cores (oracle/cpu_ref.py), in a
+    child process started before this process touches the GPU."""
+    cmd = [sys.executable, "-m", "oracle.cpu_ref", "--config", cfg_name, "--n", str(n_sample)]
+    if d <= 15:
+        cmd.append("--global-jobs")
+    r = subprocess.run(cmd, cwd=HERE, capture_output=True, text=True, timeout=1800)
+    if r.returncode != 0:
+        return {"value": None, "error": (r.stderr or r.stdout)[-2000:]}
+    c = json.loads(r.stdout.strip().splitlines()[-1])
+    if cfg_name == "C4":
+        desc = ("sample of the same distribution at 1% of the full size; its cities are "
+                "100x sparser, so neighbour lists are 100x shorter than at 1B: the rate is "
+                "an optimistic extrapolation to the full set")
+    else:
+        desc = "density-preserving slice"
+    out = {"value": c["value"], "unit": "points/s", "cores": c["workers"], "kind": "port",
+           "seconds": c["seconds"], "nproc": c["nproc"], "cpu_model": c["model"],
+           "sample": (f"{cfg_name} {desc}, {n_sample} pts, max_partitions={c['max_partitions']}: "
+                      f"numpy KD + halo, sklearn DBSCAN (algorithm='auto') per neighbourhood in "
+                      f"a {c['workers']}-process pool (Spark local[*] runs one task per KD "
+                      f"partition, so at most {c['busy_max']} are busy), 1 BLAS thread each, "
+                      f"owner-rule merge; host: {c['nproc']} CPUs visible ({c['model']}), "
+                      f"{c['workers']} usable")}
+    if "global_value" in c:
+        out["global_sklearn_value"] = c["global_value"]
+        out["global_sklearn_note"] = (f"one global sklearn DBSCAN, n_jobs={c['workers']}: the "
+                                      "fastest CPU path to the same labels (not the reference's "
+                                      "partitioned pipeline)")
+    cal = calibration()
+    if cal:
+        out["calibration"] = {k: cal[k] for k in ("n", "reference_seconds",
+                                                  "cpu_ref_seconds_1_worker",
+                                                  "ratio_reference_over_cpu_ref", "source")}
+        out["sample"] += (f"; calibration ({cal['n']} pts, one process each, build container): "
+                          f"the reference itself {cal['reference_seconds']:.1f} s, this port "
+                          f"{cal['cpu_ref_seconds_1_worker']:.1f} s")
+    if d > 15:   # brute force: O(n^2) work, the rate falls as 1/n
         out["extrapolated_full_value"] = out["value"] * n_sample / n_full
         out["sample"] += f"; brute O(n^2): at the full {n_full} pts x{n_sample / n_full:.3g}"
+    elif cfg_name == "C4":
+        out["extrapolated"] = True
+    return out
+
+
+def grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages):
+    alg_bytes, per = b_nc(rec, cells, d)
+    achieved = alg_bytes / (t_cnt * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "frac_kind": "model: algorithmic B_nc, every candidate cell read once per record",
+            "traffic": None, "kernel": "count2_kernel", "kernel_ms": t_cnt,
+            "bytes_per_record": per, "records": rec, "cells": cells,
+            "algorithmic_bytes": alg_bytes, "pmc_source": pmc_src}
+    k = (pmc or {}).get("count2_kernel")
+    if k:
+        f = pmc_fields(k)
+        if "hbm_bytes" in f:
+            roof["traffic"] = f["hbm_bytes"]
+            roof["hbm_frac"] = f["hbm_bytes"] / (t_cnt * 1e-3) / (HBM_PEAK_GBS * 1e9)
+        if "l2_hit" in f:
+            roof["l2_hit"] = f["l2_hit"]
+    if sweep and sweep.get("s_count_cand") and rec:
+        cand = sweep["s_count_cand"]
+        roof["limiter"] = {
+            "kind": "issue/latency of the candidate tests (gathers served by L2), not DRAM "
+                    "bandwidth: compare hbm_frac with frac",
+            "candidate_tests": cand, "candidate_tests_per_record": cand / rec,
+            "candidate_tests_per_s": cand / (t_cnt * 1e-3),
+            "records_per_s": rec / (t_cnt * 1e-3)}
+    stage = None
+    if pmc and stages.get("link"):
+        kb = {}
+        for name in LINK_KERNELS:
+            if name in pmc:
+                f = pmc_fields(pmc[name])
+                if "hbm_bytes" in f:
+                    kb[name] = f["hbm_bytes"]
+        if kb:
+            tot = sum(kb.values())
+            stage = {"stage": "link", "ms": stages["link"], "hbm_bytes": tot,
+                     "achieved_gbs": tot / (stages["link"] * 1e-3) / 1e9,
+                     "hbm_frac": tot / (stages["link"] * 1e-3) / (HBM_PEAK_GBS * 1e9),
+                     "kernels_hbm_bytes": kb,
+                     "bound": "latency of dependent union-find gathers and atomics",
+                     "pmc_source": pmc_src}
+    return roof, stage
+
+
+def dense_roofline(n, d, t_cnt, cells, pmc, pmc_src):
+    # dense tiles (dense.hip): the count pass's Gram tiles, 2 d flops per pair
+    # over the 64 x 64 wave tiles it computes (the engine reports them in
+    # cells_n; the projection window prunes the rest of the n^2 pairs); the
+    # MFMA executes 3 split-bf16 products with d padded to 16 ks
+    ks = 1 if d <= 16 else 2 if d <= 32 else 4 if d <= 64 else 8
+    n_pad = -(-n // 64) * 64
+    tiles = cells if cells > 0 else (n_pad // 64) ** 2
+    alg = 2.0 * d * 64 * 64 * tiles
+    exe = 3 * 2.0 * 64 * 64 * 16 * ks * tiles
+    achieved = alg / (t_cnt * 1e-3) / 1e12
+    roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS,
+            "frac_kind": "algorithmic: 2 d flops per computed pair", "traffic": None,
+            "kernel": "tile_kernel (count pass)", "kernel_ms": t_cnt,
+            "algorithmic_flops": alg, "mfma_executed_flops": exe,
+            "wave_tiles": tiles, "tiles_all_pairs": (n_pad // 64) ** 2,
+            "tile_fraction": tiles / (n_pad // 64) ** 2,
+            "mfma_executed_tflops": exe / (t_cnt * 1e-3) / 1e12,
+            "mfma_utilisation": exe / (t_cnt * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+            "pmc_source": pmc_src}
+    k = (pmc or {}).get("tile_kernel_m0")
+    if k:
+        f = pmc_fields(k)
+        roof["traffic"] = f.get("hbm_bytes")
+        if "hbm_bytes" in f:
+            roof["hbm_frac"] = f["hbm_bytes"] / (t_cnt * 1e-3) / (HBM_PEAK_GBS * 1e9)
+        if "l2_hit" in f:
+            roof["l2_hit"] = f["l2_hit"]
+    return roof
+
+
+def host_legs(DBSCAN, eps, ms, P, Xh):
+    """The same train from host memory: a numpy array (H2D inside the step),
+    and a list of (key, vector) records — the reference's RDD element form
+    (R:dbscan/dbscan.py:104-109) — with the ingest (as_points) timed apart."""
+    import torch
+    from pypardis_amd._data import as_points
+    out = {}
+    DBSCAN(eps=eps, min_samples=ms, max_partitions=P).train(Xh)   # warm
+    torch.cuda.synchronize()
+    reps = 2
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        DBSCAN(eps=eps, min_samples=ms, max_partitions=P).train(Xh)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    out["numpy"] = {"points": len(Xh), "ms_per_step": 1e3 * t, "value": len(Xh) / t,
+                    "note": "DBSCAN.train(numpy array): H2D copy of the points inside the step"}
+    nr = min(len(Xh), 1_000_000)
+    recs = list(zip(range(nr), Xh[:nr]))
+    t0 = time.perf_counter()
+    pts = as_points(recs)
+    torch.cuda.synchronize()
+    t_in = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    DBSCAN(eps=eps, min_samples=ms, max_partitions=P).train(pts)
+    torch.cuda.synchronize()
+    t_tr = time.perf_counter() - t0
+    out["records"] = {"records": nr, "ingest_s": t_in, "ingest_records_per_s": nr / t_in,
+                      "train_s": t_tr, "value": nr / (t_in + t_tr),
+                      "note": "list of (int key, ndarray) records: vectorised unzip + stack + "
+                              "H2D (ingest), then train"}
     return out
 
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    from pypardis_amd import synth
+    cfgd = synth.CONFIGS[args.config]
+    n_cfg = args.points or cfgd["n"]
+    d_cfg = cfgd["d"]
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        # before the GPU is initialised, so the child inherits no HIP state
+        try:
+            cpu = cpu_baseline(args.config,
+                               min(args.cpu_n or default_cpu_n(args.config, d_cfg), n_cfg),
+                               n_cfg, d_cfg)
+        except Exception as e:   # report, never fake
+            cpu = {"value": None, "error": repr(e)}
+
+    import torch
+    import torch.distributed as dist
+
     if args.rehearse:
         local_rank = 0
     if world > 1:
@@ -146,7 +332,7 @@ def main():
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
 
-    from pypardis_amd import DBSCAN, _native, synth
+    from pypardis_amd import DBSCAN, _native
 
     # C4 (1B points) is generated on the device: a host-side build of 1B
     # points would dominate the run; the other configs are numpy
@@ -155,16 +341,14 @@ def main():
     n, d = X.shape
     eps, ms, P = cfg["eps"], cfg["min_samples"], cfg.get("max_partitions") or 1
     ctx = _native.context(local_rank)
-    if args.sweep_variant is not None:
-        ctx.set_option(_native.PD_OPT_SWEEP_VARIANT, args.sweep_variant)
-    if args.centre_window is not None:
-        ctx.set_option(_native.PD_OPT_CENTRE_WINDOW, args.centre_window)
-    if args.count_rotate is not None:
-        ctx.set_option(_native.PD_OPT_COUNT_ROTATE, args.count_rotate)
-    if args.link_mode is not None:
-        ctx.set_option(_native.PD_OPT_LINK_MODE, args.link_mode)
-    if args.jump_rounds is not None:
-        ctx.set_option(_native.PD_OPT_JUMP_ROUNDS, args.jump_rounds)
+    for opt, val in ((_native.PD_OPT_SWEEP_VARIANT, args.sweep_variant),
+                     (_native.PD_OPT_CENTRE_WINDOW, args.centre_window),
+                     (_native.PD_OPT_COUNT_ROTATE, args.count_rotate),
+                     (_native.PD_OPT_LINK_MODE, args.link_mode),
+                     (_native.PD_OPT_JUMP_ROUNDS, args.jump_rounds)):
+        if val is not None:
+            ctx.set_option(opt, val)
+    Xh = None
     if world > 1:
         from pypardis_amd.distributed import NativeOps, train_sharded
         lo, hi = rank * n // world, (rank + 1) * n // world
@@ -176,6 +360,7 @@ def main():
             return train_sharded(Xd, eps, ms, max_partitions=max(P, world), ops=ops)
     else:
         Xd = X if torch.is_tensor(X) else torch.from_numpy(X).to(dev)
+        Xh = None if torch.is_tensor(X) else X
 
         def step():
             return DBSCAN(eps=eps, min_samples=ms, max_partitions=P).train(Xd)
@@ -219,58 +404,36 @@ def main():
     ms_step = 1e3 * el / args.steps
     value = n * args.steps / el
     ncl = m.n_clusters if world > 1 else m.n_clusters_
+    shard_stats = m.stats if world > 1 else None
+    del m
+
+    host = None
+    if world == 1 and not args.no_host and d <= 4:
+        host = host_legs(DBSCAN, eps, ms, P, Xh if Xh is not None else Xd.cpu().numpy())
 
     if rank == 0:
         t_cnt = float(np.mean(count_ms))
-        if d <= 4:
-            alg_bytes, per = b_nc(rec, cells, d)
-            achieved = alg_bytes / (t_cnt * 1e-3) / 1e9
-            variant = args.sweep_variant if args.sweep_variant is not None \
-                else _native.SWEEP_VARIANT_DEFAULT
-            kname = "count2_kernel" if variant & 1 else "count_kernel"
-            pmc = load_pmc(kname, args.config)
-            roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS,
-                    "traffic": pmc["bytes_per_launch"] if pmc else None, "kernel": kname,
-                    "kernel_ms": t_cnt, "bytes_per_record": per, "records": rec,
-                    "cells": cells, "algorithmic_bytes": alg_bytes}
-            dtype = "f64"
-        else:
-            # dense tiles (dense.hip): the count pass's Gram tiles, 2 d flops
-            # per pair over the 64 x 64 wave tiles it computes (the engine
-            # reports them in cells_n; the projection window prunes the rest
-            # of the n^2 pairs); the MFMA executes 3 split-bf16 products
-            # with d padded to 16 ks
-            ks = 1 if d <= 16 else 2 if d <= 32 else 4 if d <= 64 else 8
-            n_pad = -(-n // 64) * 64
-            tiles = cells if cells > 0 else (n_pad // 64) ** 2
-            alg = 2.0 * d * 64 * 64 * tiles
-            exe = 3 * 2.0 * 64 * 64 * 16 * ks * tiles
-            achieved = alg / (t_cnt * 1e-3) / 1e12
-            pmc = load_pmc("tile_kernel_m0", args.config)   # the count-pass launch
-            roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS,
-                    "traffic": pmc["bytes_per_launch"] if pmc else None,
-                    "kernel": "tile_kernel (count pass)", "kernel_ms": t_cnt,
-                    "algorithmic_flops": alg, "mfma_executed_flops": exe,
-                    "wave_tiles": tiles, "tiles_all_pairs": (n_pad // 64) ** 2,
-                    "tile_fraction": tiles / (n_pad // 64) ** 2,
-                    "mfma_executed_tflops": exe / (t_cnt * 1e-3) / 1e12,
-                    "mfma_utilisation": exe / (t_cnt * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS}
-            dtype = "bf16x3 (split bf16 MFMA, fp32 accumulate) + f64 recheck"
         stages = {k: round(v / args.steps, 3) for k, v in stage_sum.items()
                   if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records")
                   and not k.startswith("s_")}
         # KD partition + host work around pd_train (wall time, not events)
         stages["outside_train"] = round(ms_step - stages.get("total", 0.0), 3)
-        cpu = None
-        if world == 1 and not args.no_cpu:
-            try:
-                cpu = cpu_baseline(args.config, min(args.cpu_n or default_cpu_n(d), n), n)
-            except Exception as e:   # report, never fake
-                cpu = {"value": None, "error": repr(e)}
+        pmc, pmc_src = load_pmc(args.config)
+        stage_roof = None
+        if d <= 4:
+            roof, stage_roof = grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages)
+            dtype = f"{'f32' if Xd.dtype == torch.float32 else 'f64'} coords, f64 predicate"
+        else:
+            roof = dense_roofline(n, d, t_cnt, cells, pmc, pmc_src)
+            dtype = "bf16x3 (split bf16 MFMA, fp32 accumulate) + f64 recheck"
+        if args.config == "C2" and n == cfgd["n"]:
+            metric = BASELINE_METRIC
+        else:
+            metric = (f"points clustered/sec (whole node), {n} {d}-D pts ({args.config}); "
+                      f"% {'HBM' if d <= 4 else 'MFMA'} roofline")
+        kind = {"C4": "gps_skew"}.get(args.config, "blobs_noise" if d <= 4 else "embeddings")
         out = {
-            "metric": "points clustered/sec (whole node), 100M 3-D pts, 1/2/4/8 GPUs; % HBM roofline",
+            "metric": metric,
             "value": value,
             "unit": "points/s",
             "n_gpus": world,
@@ -282,17 +445,19 @@ def main():
             "vs_baseline": None,
             "dtype": dtype,
             "data": "synthetic",
-            "config": {"workload": f"{args.config}: "
-                                   f"{'gps_skew' if args.config == 'C4' else 'blobs_noise' if d <= 4 else 'embeddings'} "
-                                   f"n={n} d={d} eps={eps} min_samples={ms} max_partitions={P}",
+            "config": {"workload": f"{args.config}: {kind} n={n} d={d} eps={eps} "
+                                   f"min_samples={ms} max_partitions={P}",
                        "n_points": n, "d": d, "eps": eps, "min_samples": ms,
-                       "max_partitions": P, "input": "fp32 device-resident",
+                       "max_partitions": P,
+                       "input": f"{str(Xd.dtype).replace('torch.', '')} device-resident",
                        "parallelism": f"kd-sharded{world}" if world > 1 else "single"},
             "roofline": roof,
+            "stage_roofline": stage_roof,
             "cpu_baseline": cpu,
+            "host_input": host,
             "stages_ms": stages,
             "n_clusters": ncl,
-            "shard_stats": m.stats if world > 1 else None,
+            "shard_stats": shard_stats,
             "sweep_stats": sweep,
         }
         line = json.dumps(out)

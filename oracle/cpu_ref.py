@@ -111,16 +111,20 @@ def run(X, eps, min_samples, max_partitions, metric="euclidean", workers=None):
     g = coo_matrix((np.ones(int(same.sum())), (nodes[:-1][same], nodes[1:][same])), shape=(nn, nn))
     _, comp = connected_components(g, directed=False)
     labels = np.full(n, -1, np.int64)
+    is_core = np.zeros(n, bool)
     owner = kd["owner"]
-    for L, (lab, _) in enumerate(local):
+    for L, (lab, core) in enumerate(local):
         mem = members[L]
         own = (owner[mem] == L) & (lab >= 0)
         labels[mem[own]] = comp[base[L] + lab[own]]
-    # number components by their smallest member, as sklearn would
+        is_core[mem[owner[mem] == L]] = core[owner[mem] == L]
+    # number components by their smallest core point, as sklearn would
+    # (border points keep the cluster their neighbourhood's sklearn gave them)
     ok = labels >= 0
     if ok.any():
         first = np.full(nn, n, np.int64)
-        np.minimum.at(first, labels[ok], np.nonzero(ok)[0])
+        okc = ok & is_core
+        np.minimum.at(first, labels[okc], np.nonzero(okc)[0])
         used = np.unique(labels[ok])
         rank = np.empty(nn, np.int64)
         rank[used[np.argsort(first[used])]] = np.arange(len(used))

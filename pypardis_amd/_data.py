@@ -76,25 +76,46 @@ def _keys(keys):
     return a
 
 
+def _is_keys_and_matrix(data):
+    """A ``(keys, X)`` pair: X is an array/tensor of points (ndim 1 or 2) and
+    keys a sequence of scalars of the same length.  A tuple of two (key,
+    vector) records is not one: its second element is a record, not a
+    matrix."""
+    if not (isinstance(data, tuple) and len(data) == 2):
+        return False
+    keys, X = data
+    if not isinstance(X, (np.ndarray, torch.Tensor)) or X.ndim not in (1, 2):
+        return False
+    try:
+        return len(keys) == len(X) and all(np.isscalar(k) for k in keys[:8])
+    except TypeError:
+        return False
+
+
 def as_points(data, device=None):
     if isinstance(data, PointSet):
         return data
     dev = _device(device)
     if isinstance(data, (torch.Tensor, np.ndarray)):
         return PointSet(_to_tensor(data, dev))
-    if isinstance(data, tuple) and len(data) == 2 and not np.isscalar(data[0]) \
-            and hasattr(data[0], "__len__") and hasattr(data[1], "__len__") \
-            and len(data[0]) == len(data[1]) and len(data[0]) != 2:
+    if _is_keys_and_matrix(data):
         keys, X = data
         return PointSet(_to_tensor(X, dev), _keys(keys))
-    recs = data.collect() if hasattr(data, "collect") else list(data)
+    recs = data.collect() if hasattr(data, "collect") else data
+    if not isinstance(recs, (list, tuple)):
+        recs = list(recs)
     if not recs:
         raise ValueError("no points")
-    keys = [k for k, _ in recs]
-    vecs = [np.asarray(v) for _, v in recs]
-    dt = np.result_type(*[v.dtype for v in vecs[:64]])
-    X = np.stack(vecs).astype(dt if dt in (np.float32, np.float64) else np.float64)
+    # vectorised unzip of the (key, vector) records
+    keys, vecs = zip(*recs)
+    X = np.asarray(vecs)
+    if X.dtype == object or X.ndim not in (1, 2):
+        X = np.stack([np.asarray(v) for v in vecs])
+    # float32 stays float32 only if every vector is float32 (np.asarray of
+    # a mixed list already promotes); anything else becomes float64
+    if X.dtype not in (np.float32, np.float64):
+        X = X.astype(np.float64)
     k = _keys(keys)
-    if k.dtype == np.int64 and np.array_equal(k, np.arange(len(k))):
+    if k.dtype == np.int64 and len(k) and k[0] == 0 and np.array_equal(k, np.arange(len(k))):
         k = None
     return PointSet(_to_tensor(X, dev), k)

@@ -125,6 +125,41 @@ def test_as_points_forms_cpu():
     assert p.keys[1] == 2
 
 
+def test_as_points_edge_forms_cpu():
+    X = np.arange(6, dtype=np.float32).reshape(3, 2)
+    # a tuple of exactly two (key, vector) records is records, not (keys, X)
+    p = as_points(((7, X[0]), (9, X[1])), device="cpu")
+    assert list(p.keys) == [7, 9] and p.n == 2 and p.d == 2
+    # (keys, X) with two points
+    p = as_points((np.array([4, 5]), X[:2]), device="cpu")
+    assert list(p.keys) == [4, 5] and torch.equal(p.X, torch.from_numpy(X[:2]))
+    # dtype from every vector: one float64 vector after many float32 ones
+    recs = [(i, X[i % 3]) for i in range(100)] + [(100, np.array([0.1, 0.2]))]
+    p = as_points(recs, device="cpu")
+    assert p.X.dtype == torch.float64 and float(p.X[100, 0]) == 0.1
+    # integer vectors become float64; 1-D input is one axis
+    assert as_points([(0, [1, 2]), (1, [3, 4])], device="cpu").X.dtype == torch.float64
+    assert as_points(np.arange(5.0), device="cpu").d == 1
+    with pytest.raises(ValueError):
+        as_points([], device="cpu")
+
+
+def test_map_cluster_id():
+    """R:dbscan/dbscan.py:37-53: first label of the group, '*' stripped; noise
+    or unmapped labels give -1; a broadcast wrapper or a plain dict."""
+    from pypardis_amd import map_cluster_id
+
+    class Broadcast:
+        def __init__(self, v):
+            self.value = v
+
+    fwd = {"0:0": 3, "1:2": 3, "2:1": 5}
+    assert map_cluster_id((10, ["0:0*", "1:2"]), Broadcast(fwd)) == (10, 3)
+    assert map_cluster_id((11, ["2:1"]), fwd) == (11, 5)
+    assert map_cluster_id((12, ["1:-1*", "0:0"]), fwd) == (12, -1)
+    assert map_cluster_id((13, iter(["4:7"])), fwd) == (13, -1)
+
+
 def test_c4_generator():
     """C4 GPS-like skew: deterministic in the seed, float32, inside the
     lon/lat box, 5% uniform noise, heavy Zipf skew (the densest eps-cell of

@@ -11,11 +11,13 @@
   python bench.py [--gpus N --steps K --warmup W] [--config C2|C1|C3|C4]
                   [--points N] [--no-cpu] [--no-host]
 
-For N > 1 (torch.distributed.run, one rank per GPU, RCCL) the same points are
-split by index over the ranks and the step is the sharded train (KD levels
-with all-reduced moments/counts, routing + all-to-all-v of the halo records,
-per-GPU clustering of its neighbourhoods, all-gather label merge, global
-ranks): strong scaling, value = total points / max-over-ranks time.
+For N > 1 (torch.distributed.run, one rank per GPU) the same points are split
+by index over the ranks and each rank calls DBSCAN(...).train(its slice) in
+the process group: the sharded train over RCCL through libpardis's pd_comm_*
+(KD levels with all-reduced moments/counts, routing + all-to-all-v of the halo
+records, per-GPU clustering of its neighbourhoods, all-gather of the merge
+exports, global ranks, labels returned to the ranks holding the points):
+strong scaling, value = total points / max-over-ranks time.
 
 Roofline object — the neighbour-count kernel (count2_kernel, engine.hip):
   frac / achieved: the algorithmic MODEL of SURVEY.md §8(d), B_nc = records *
@@ -349,22 +351,17 @@ def main():
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None
-    if world > 1:
-        from pypardis_amd.distributed import NativeOps, train_sharded
+    if world > 1:   # this rank's slice; DBSCAN.train in the process group shards
         lo, hi = rank * n // world, (rank + 1) * n // world
         Xd = X[lo:hi].clone() if torch.is_tensor(X) else \
             torch.from_numpy(np.ascontiguousarray(X[lo:hi])).to(dev)
-        ops = NativeOps(dev)
-
-        def step():
-            return train_sharded(Xd, eps, ms, max_partitions=max(P, world), ops=ops)
     else:
         Xd = X if torch.is_tensor(X) else torch.from_numpy(X).to(dev)
         Xh = None if torch.is_tensor(X) else X
-
-        def step():
-            return DBSCAN(eps=eps, min_samples=ms, max_partitions=P).train(Xd)
     del X
+
+    def step():
+        return DBSCAN(eps=eps, min_samples=ms, max_partitions=max(P, world)).train(Xd)
 
     for _ in range(args.warmup):
         m = step()
@@ -403,8 +400,8 @@ def main():
                  if k.startswith("s_") or k in ("records", "core_records")}
     ms_step = 1e3 * el / args.steps
     value = n * args.steps / el
-    ncl = m.n_clusters if world > 1 else m.n_clusters_
-    shard_stats = m.stats if world > 1 else None
+    ncl = m.n_clusters_
+    shard_stats = m.shard.stats if m.shard is not None else None
     del m
 
     host = None

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 1
+#define PD_ABI_VERSION 2
 
 enum pd_status {
     PD_OK = 0,
@@ -243,17 +243,20 @@ int32_t pd_train_begin(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int
 int32_t pd_train_exports(pd_ctx* ctx, uint32_t* gid, uint32_t* key, int64_t capacity,
                          void* stream);
 
-/* Union of all devices' exports over the id space [0, n_space):
- * parent[n_space] (device) receives each id's global key (its component's
- * smallest id; identity for ids in no export). */
-int32_t pd_merge_exports(pd_ctx* ctx, uint32_t n_space, const uint32_t* gid,
-                         const uint32_t* key, int64_t m, uint32_t* parent, void* stream);
+/* Union of all devices' exports (gid[m], key[m]: every device's
+ * pd_train_exports, gathered): ids[u] = the distinct ids the pairs name,
+ * ascending; keys[u] = each one's global key (its component's smallest id).
+ * Capacity of ids / keys: 2 m.  *u_host = u.  O(m log m): the id space is
+ * never materialised.  Replaces the driver-side ClusterAggregator
+ * (R:dbscan/dbscan.py:153-161, R:dbscan/aggregator.py:9-73). */
+int32_t pd_merge_exports(pd_ctx* ctx, const uint32_t* gid, const uint32_t* key, int64_t m,
+                         uint32_t* ids, uint32_t* keys, int64_t* u_host, void* stream);
 
-/* Phase B: keymap (device, nullable) from pd_merge_exports; keys[n] = global
- * cluster key of each owned point (0xFFFFFFFF = noise or not owned here),
- * core[n] (nullable) = owned core point. */
-int32_t pd_train_end(pd_ctx* ctx, int64_t n, const uint32_t* keymap, uint32_t* keys,
-                     uint8_t* core, void* stream);
+/* Phase B: (map_ids, map_keys, n_map) from pd_merge_exports (n_map may be 0);
+ * keys[n] = global cluster key of each owned point (0xFFFFFFFF = noise or not
+ * owned here), core[n] (nullable) = owned core point. */
+int32_t pd_train_end(pd_ctx* ctx, int64_t n, const uint32_t* map_ids, const uint32_t* map_keys,
+                     int64_t n_map, uint32_t* keys, uint8_t* core, void* stream);
 
 /* roots (device, capacity n) = global ids of owned points that are their
  * cluster's key, i.e. one id per cluster over all devices; *m_host = count. */
@@ -264,9 +267,62 @@ int32_t pd_select_roots(pd_ctx* ctx, const uint32_t* keys, const uint32_t* gid, 
 int32_t pd_sort_u32(pd_ctx* ctx, uint32_t* data, int64_t n, void* stream);
 
 /* labels[i] = rank of keys[i] among the sorted roots (all devices' roots),
- * -1 for 0xFFFFFFFF — sklearn's numbering, as pd_train's labels. */
+ * -1 for 0xFFFFFFFF — sklearn's numbering, as pd_train's labels.  A key that
+ * is not among the roots (roots not gathered from every device) is an error:
+ * PD_EINVAL.  Synchronises the stream. */
 int32_t pd_rank_labels(pd_ctx* ctx, const uint32_t* keys, int64_t n, const uint32_t* roots,
                        int64_t n_roots, int32_t* labels, void* stream);
+
+/* Results back to the devices that hold the points (R:dbscan/dbscan.py:162-164
+ * result RDD): the owned records (owner[i] >= 0) of this device packed as
+ * out[2 m] = (gid, (label + 1) | core << 31) pairs in ascending gid, and
+ * counts_host[r] = how many fall in [gid_offsets_host[r],
+ * gid_offsets_host[r + 1]) (device r's input slice).  The gids must ascend
+ * (the pd_pack / all-to-all order); *m_host = m. */
+int32_t pd_owned_results(pd_ctx* ctx, int64_t n, const int32_t* owner, const uint32_t* gid,
+                         const int32_t* labels, const uint8_t* core, int32_t n_ranks,
+                         const int64_t* gid_offsets_host, uint32_t* out, int64_t capacity,
+                         int64_t* counts_host, int64_t* m_host, void* stream);
+
+/* labels[gid - gid_base] / core[...] (nullable) from m received pairs of
+ * pd_owned_results; m must equal n and every point must receive exactly one
+ * result (PD_EINVAL otherwise). */
+int32_t pd_scatter_results(pd_ctx* ctx, const uint32_t* pairs, int64_t m, uint32_t gid_base,
+                           int64_t n, int32_t* labels, uint8_t* core, void* stream);
+
+/* ---- RCCL collectives of the sharded train (one rank per device).  They
+ * replace Spark's data movement: partitionBy shuffle (R:dbscan/dbscan.py:
+ * 114-118) -> pd_comm_all_to_all_v; collect / broadcast of the cluster-id map
+ * (R:dbscan/dbscan.py:153-161) -> pd_comm_all_gather_v; the KD aggregates
+ * (R:dbscan/partition.py:60-63,86-89,135-137) -> pd_comm_all_reduce.  Buffers
+ * are device pointers, counts are elements; calls are stream-ordered. */
+typedef struct pd_comm pd_comm;
+#define PD_COMM_ID_BYTES 128
+enum pd_elem { PD_E_U8 = 0, PD_E_I32 = 1, PD_E_U32 = 2, PD_E_I64 = 3, PD_E_U64 = 4,
+               PD_E_F32 = 5, PD_E_F64 = 6 };
+enum pd_reduce { PD_R_SUM = 0, PD_R_MAX = 1, PD_R_MIN = 2 };
+
+/* ncclGetUniqueId: rank 0 creates the id, the caller hands the
+ * PD_COMM_ID_BYTES bytes to every rank (any host channel). */
+int32_t pd_comm_unique_id(uint8_t* id_host);
+/* ncclCommInitRank on the context's device (collective over n_ranks). */
+int32_t pd_comm_init(pd_ctx* ctx, int32_t n_ranks, int32_t rank, const uint8_t* id_host,
+                     pd_comm** out);
+/* One process driving n devices: out_host[i] = rank i on devices_host[i]
+ * (ncclCommInitAll). */
+int32_t pd_comm_init_all(int32_t n, const int32_t* devices_host, pd_comm** out_host);
+int32_t pd_comm_destroy(pd_comm* comm);
+int32_t pd_comm_all_reduce(pd_comm* comm, const void* send, void* recv, int64_t count,
+                           int32_t elem, int32_t op, void* stream);
+/* recv = concatenation over ranks r of counts_host[r] elements. */
+int32_t pd_comm_all_gather_v(pd_comm* comm, const void* send, void* recv,
+                             const int64_t* counts_host, int32_t elem, void* stream);
+/* send grouped by destination rank, recv grouped by source rank. */
+int32_t pd_comm_all_to_all_v(pd_comm* comm, const void* send, const int64_t* send_counts_host,
+                             void* recv, const int64_t* recv_counts_host, int32_t elem,
+                             void* stream);
+int32_t pd_comm_broadcast(pd_comm* comm, void* buf, int64_t count, int32_t elem, int32_t root,
+                          void* stream);
 
 #ifdef __cplusplus
 }

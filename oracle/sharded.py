@@ -70,9 +70,12 @@ def phase_b(state, keymap=None):
     n = state["n"]
     X = state["X"]
     gmin = state["gmin"].copy()
-    if keymap is not None:
-        ok = gmin < len(keymap)
-        gmin[ok] = np.asarray(keymap)[gmin[ok]]
+    if keymap is not None:   # (ids ascending, their global keys)
+        ids, keys = (np.asarray(a, np.int64) for a in keymap)
+        if len(ids):
+            pos = np.minimum(np.searchsorted(ids, gmin), len(ids) - 1)
+            hit = ids[pos] == gmin
+            gmin[hit] = keys[pos[hit]]
     nroot, node_base, owner = state["nroot"], state["node_base"], state["owner"]
     key = np.full(n, -1, np.int64)
     is_core = np.zeros(n, np.uint8)
@@ -96,10 +99,14 @@ def phase_b(state, keymap=None):
     return key, is_core
 
 
-def merge(n_space, gid, key):
-    """Global key of every id: union of the exported (id, key) pairs, each
-    component's root its smallest id (pd_merge_exports)."""
-    uf = _UF(int(n_space))
-    for a, b in zip(np.asarray(gid).tolist(), np.asarray(key).tolist()):
+def merge(gid, key):
+    """Union of the exported (id, key) pairs over the ids they name
+    (pd_merge_exports): (ids ascending, global key of each = its component's
+    smallest id)."""
+    gid = np.asarray(gid, np.int64)
+    key = np.asarray(key, np.int64)
+    ids = np.unique(np.concatenate([gid, key]))
+    uf = _UF(len(ids))
+    for a, b in zip(np.searchsorted(ids, gid).tolist(), np.searchsorted(ids, key).tolist()):
         uf.union(int(a), int(b))
-    return np.array([uf.find(v) for v in range(int(n_space))], np.int64)
+    return ids, ids[np.array([uf.find(v) for v in range(len(ids))], np.int64)]

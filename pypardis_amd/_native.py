@@ -40,7 +40,10 @@ EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
            "pd_kd_split", "pd_halo_members", "pd_cluster", "pd_train", "pd_kd_moments_dd",
            "pd_route", "pd_pack", "pd_train_begin", "pd_train_exports", "pd_merge_exports",
            "pd_train_end", "pd_select_roots", "pd_sort_u32", "pd_rank_labels",
-           "pd_kd_radix_hist", "pd_kd_pass"]
+           "pd_kd_radix_hist", "pd_kd_pass", "pd_owned_results", "pd_scatter_results",
+           "pd_comm_unique_id", "pd_comm_init", "pd_comm_init_all", "pd_comm_destroy",
+           "pd_comm_all_reduce", "pd_comm_all_gather_v", "pd_comm_all_to_all_v",
+           "pd_comm_broadcast"]
 
 
 class PardisError(RuntimeError):
@@ -89,14 +92,24 @@ def load():
                         I32),
             "pd_train_begin": ([P, P, I32, I64, I32, D, I32, I32, I32, P, P, P, P, P, P, P], I32),
             "pd_train_exports": ([P, P, P, I64, P], I32),
-            "pd_merge_exports": ([P, U32, P, P, I64, P, P], I32),
-            "pd_train_end": ([P, I64, P, P, P, P], I32),
+            "pd_merge_exports": ([P, P, P, I64, P, P, P, P], I32),
+            "pd_train_end": ([P, I64, P, P, I64, P, P, P], I32),
             "pd_select_roots": ([P, P, P, I64, P, P, P], I32),
             "pd_sort_u32": ([P, P, I64, P], I32),
             "pd_rank_labels": ([P, P, I64, P, I64, P, P], I32),
             "pd_kd_radix_hist": ([P, P, I32, I64, I32, P, I32, P, P, P, I32, P, P], I32),
             "pd_kd_pass": ([P, P, I32, I64, I32, P, I32, I32, P, P, P, P, I32, P, P, P, P, P],
                            I32),
+            "pd_owned_results": ([P, I64, P, P, P, P, I32, P, P, I64, P, P, P], I32),
+            "pd_scatter_results": ([P, P, I64, U32, I64, P, P, P], I32),
+            "pd_comm_unique_id": ([P], I32),
+            "pd_comm_init": ([P, I32, I32, P, ctypes.POINTER(P)], I32),
+            "pd_comm_init_all": ([I32, P, P], I32),
+            "pd_comm_destroy": ([P], I32),
+            "pd_comm_all_reduce": ([P, P, P, I64, I32, I32, P], I32),
+            "pd_comm_all_gather_v": ([P, P, P, P, I32, P], I32),
+            "pd_comm_all_to_all_v": ([P, P, P, P, P, I32, P], I32),
+            "pd_comm_broadcast": ([P, P, I64, I32, I32, P], I32),
         }
         for name, (args, res) in sig.items():
             f = getattr(lib, name)
@@ -443,25 +456,32 @@ def train_exports(m, device, ctx=None):
     return gid[:m], key[:m]
 
 
-def merge_exports(n_space, gid, key, ctx=None):
-    """Global key of every id in [0, n_space) (int32 device tensor)."""
+def merge_exports(gid, key, ctx=None):
+    """Union of all devices' exports: (ids, keys) int32 device tensors — the
+    distinct ids named, ascending (u32 order), and each one's global key."""
     device = gid.device
     ctx = ctx or context(device.index)
-    parent = torch.empty(max(n_space, 1), dtype=torch.int32, device=device)
     m = gid.shape[0]
-    _check(load().pd_merge_exports(ctx.ptr, int(n_space), gid.data_ptr() if m else None,
-                                   key.data_ptr() if m else None, m, parent.data_ptr(),
-                                   _stream(device)))
-    return parent[:n_space]
+    ids = torch.empty(max(2 * m, 1), dtype=torch.int32, device=device)
+    keys = torch.empty(max(2 * m, 1), dtype=torch.int32, device=device)
+    u = np.zeros(1, np.int64)
+    _check(load().pd_merge_exports(ctx.ptr, gid.data_ptr() if m else None,
+                                   key.data_ptr() if m else None, m, ids.data_ptr(),
+                                   keys.data_ptr(), u.ctypes.data, _stream(device)))
+    return ids[:int(u[0])], keys[:int(u[0])]
 
 
 def train_end(n, keymap, device, ctx=None):
-    """Phase B: (keys int32[n], core uint8[n]) device tensors (owned points)."""
+    """Phase B: (keys int32[n], core uint8[n]) device tensors (owned points).
+    keymap: (ids, keys) from merge_exports, or None."""
     ctx = ctx or context(device)
     keys = torch.empty(max(n, 1), dtype=torch.int32, device=device)
     core = torch.empty(max(n, 1), dtype=torch.uint8, device=device)
-    _check(load().pd_train_end(ctx.ptr, n, keymap.data_ptr() if keymap is not None else None,
-                               keys.data_ptr(), core.data_ptr(), _stream(device)))
+    ids, mk = keymap if keymap is not None else (None, None)
+    nm = 0 if ids is None else ids.shape[0]
+    _check(load().pd_train_end(ctx.ptr, n, ids.data_ptr() if nm else None,
+                               mk.data_ptr() if nm else None, nm, keys.data_ptr(),
+                               core.data_ptr(), _stream(device)))
     return keys[:n], core[:n]
 
 
@@ -494,3 +514,125 @@ def rank_labels(keys, roots, ctx=None):
                                  roots.data_ptr() if nr else None, nr, labels.data_ptr(),
                                  _stream(device)))
     return labels[:n]
+
+
+def owned_results(owner, gid, labels, core, gid_offsets, ctx=None):
+    """(pairs int32[m, 2] device, counts int64[W] host): the owned records as
+    (gid, (label + 1) | core << 31), grouped by the device holding the point."""
+    device = gid.device
+    ctx = ctx or context(device.index)
+    n = gid.shape[0]
+    off = np.ascontiguousarray(gid_offsets, np.int64)
+    W = len(off) - 1
+    out = torch.empty((max(n, 1), 2), dtype=torch.int32, device=device)
+    counts = np.zeros(W, np.int64)
+    m = np.zeros(1, np.int64)
+    ptr = (lambda t: t.data_ptr() if t is not None and n else None)
+    _check(load().pd_owned_results(ctx.ptr, n, ptr(owner), ptr(gid), ptr(labels), ptr(core), W,
+                                   off.ctypes.data, out.data_ptr(), n, counts.ctypes.data,
+                                   m.ctypes.data, _stream(device)))
+    return out[:int(m[0])], counts
+
+
+def scatter_results(pairs, gid_base, n, device, ctx=None):
+    """(labels int32[n], core uint8[n]) of this device's input points."""
+    ctx = ctx or context(device.index)
+    labels = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    core = torch.empty(max(n, 1), dtype=torch.uint8, device=device)
+    m = pairs.shape[0]
+    _check(load().pd_scatter_results(ctx.ptr, pairs.data_ptr() if m else None, m, int(gid_base),
+                                     n, labels.data_ptr(), core.data_ptr(), _stream(device)))
+    return labels[:n], core[:n]
+
+
+# ------------------------------------------------------------------ RCCL
+PD_COMM_ID_BYTES = 128
+PD_R_SUM, PD_R_MAX, PD_R_MIN = 0, 1, 2
+_ELEM = {torch.uint8: 0, torch.bool: 0, torch.int32: 1, torch.int64: 3, torch.float32: 5,
+         torch.float64: 6}
+
+
+def comm_unique_id():
+    buf = (ctypes.c_uint8 * PD_COMM_ID_BYTES)()
+    _check(load().pd_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+    return bytes(buf)
+
+
+class Comm:
+    """One rank of an RCCL communicator (pd_comm_*).  Device tensors in and
+    out, on this rank's device and the current stream."""
+
+    def __init__(self, ptr, device, n_ranks, rank):
+        self.ptr = ptr
+        self.device = torch.device("cuda", int(device))
+        self.world = int(n_ranks)
+        self.rank = int(rank)
+
+    @classmethod
+    def init(cls, n_ranks, rank, uid, device):
+        ctx = context(device)
+        buf = (ctypes.c_uint8 * PD_COMM_ID_BYTES).from_buffer_copy(uid)
+        ptr = ctypes.c_void_p()
+        _check(load().pd_comm_init(ctx.ptr, int(n_ranks), int(rank),
+                                   ctypes.cast(buf, ctypes.c_void_p), ctypes.byref(ptr)))
+        return cls(ptr, device, n_ranks, rank)
+
+    @classmethod
+    def init_all(cls, devices):
+        devs = np.ascontiguousarray(devices, np.int32)
+        ptrs = (ctypes.c_void_p * len(devs))()
+        require_gpu()
+        _check(load().pd_comm_init_all(len(devs), devs.ctypes.data,
+                                       ctypes.cast(ptrs, ctypes.c_void_p)))
+        return [cls(ctypes.c_void_p(ptrs[i]), int(devs[i]), len(devs), i)
+                for i in range(len(devs))]
+
+    def destroy(self):
+        if self.ptr:
+            load().pd_comm_destroy(self.ptr)
+            self.ptr = None
+
+    def _elem(self, t):
+        if t.dtype not in _ELEM:
+            raise TypeError(f"no RCCL element type for {t.dtype}")
+        if not t.is_cuda or not t.is_contiguous():
+            raise ValueError("RCCL buffers must be contiguous device tensors")
+        return _ELEM[t.dtype]
+
+    def all_reduce(self, t, op=PD_R_SUM):
+        """In place."""
+        _check(load().pd_comm_all_reduce(self.ptr, t.data_ptr(), t.data_ptr(), t.numel(),
+                                         self._elem(t), int(op), _stream(self.device)))
+        return t
+
+    def all_gather_v(self, t, counts):
+        """Concatenation over ranks of counts[r] rows of t's row shape."""
+        row = int(np.prod(t.shape[1:])) if t.dim() > 1 else 1
+        c = np.ascontiguousarray(np.asarray(counts, np.int64) * row)
+        out = torch.empty((int(np.sum(counts)),) + tuple(t.shape[1:]), dtype=t.dtype,
+                          device=self.device)
+        if out.numel() == 0:
+            return out
+        _check(load().pd_comm_all_gather_v(self.ptr, t.data_ptr() if t.numel() else None,
+                                           out.data_ptr(), c.ctypes.data, self._elem(out),
+                                           _stream(self.device)))
+        return out
+
+    def all_to_all_v(self, send, send_counts, recv_counts):
+        """send rows grouped by destination; returns rows grouped by source."""
+        row = int(np.prod(send.shape[1:])) if send.dim() > 1 else 1
+        sc = np.ascontiguousarray(np.asarray(send_counts, np.int64) * row)
+        rc = np.ascontiguousarray(np.asarray(recv_counts, np.int64) * row)
+        out = torch.empty((int(np.sum(recv_counts)),) + tuple(send.shape[1:]), dtype=send.dtype,
+                          device=self.device)
+        _check(load().pd_comm_all_to_all_v(self.ptr, send.data_ptr() if send.numel() else None,
+                                           sc.ctypes.data,
+                                           out.data_ptr() if out.numel() else None,
+                                           rc.ctypes.data, self._elem(send),
+                                           _stream(self.device)))
+        return out
+
+    def broadcast(self, t, root=0):
+        _check(load().pd_comm_broadcast(self.ptr, t.data_ptr(), t.numel(), self._elem(t),
+                                        int(root), _stream(self.device)))
+        return t

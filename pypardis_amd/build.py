@@ -68,7 +68,10 @@ def build(force=False, verbose=True):
         raise RuntimeError("libpardis build failed:\n" + "\n".join(errs))
     objs = [o for o, _ in results]
     if force or _mtime(LIB) < max(_mtime(o) for o in objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+        # librccl.so.1 (pd_comm_*): under torch the process already holds
+        # torch's RCCL (same soname), so one RCCL serves both
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
+               "-L/opt/rocm/lib", "-lrccl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")

@@ -67,6 +67,31 @@ static void check_common(pd_ctx* ctx, const void* X, int64_t n, int32_t d) {
 
 }  // namespace pd
 
+struct pd_comm {
+    pd::Comm* c;
+};
+
+namespace pd {
+template <typename F>
+static int32_t comm_guard(pd_comm* comm, F&& f) {
+    try {
+        if (!comm || !comm->c) throw Error(PD_EINVAL, "null communicator");
+        PD_HIP(hipSetDevice(comm_device(comm->c)));
+        f();
+        return PD_OK;
+    } catch (const Error& e) {
+        g_err = e.what();
+        return e.code;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return PD_EINVAL;
+    } catch (...) {
+        g_err = "unknown error";
+        return PD_EINVAL;
+    }
+}
+}  // namespace pd
+
 using namespace pd;
 
 extern "C" {
@@ -420,23 +445,26 @@ int32_t pd_train_exports(pd_ctx* ctx, uint32_t* gid, uint32_t* key, int64_t capa
     });
 }
 
-int32_t pd_merge_exports(pd_ctx* ctx, uint32_t n_space, const uint32_t* gid, const uint32_t* key,
-                         int64_t m, uint32_t* parent, void* stream) {
+int32_t pd_merge_exports(pd_ctx* ctx, const uint32_t* gid, const uint32_t* key, int64_t m,
+                         uint32_t* ids, uint32_t* keys, int64_t* u, void* stream) {
     return guard(ctx, [&] {
-        if (!ctx) throw Error(PD_EINVAL, "null context");
-        if (m < 0 || (m && (!gid || !key)) || (n_space && !parent))
-            throw Error(PD_EINVAL, "null argument");
-        merge_exports(ctx->c, n_space, gid, key, m, parent, (hipStream_t)stream);
+        if (!ctx || !u) throw Error(PD_EINVAL, "null argument");
+        if (m < 0 || (m && (!gid || !key || !ids || !keys))) throw Error(PD_EINVAL, "null argument");
+        *u = merge_exports(ctx->c, gid, key, m, ids, keys, (hipStream_t)stream);
     });
 }
 
-int32_t pd_train_end(pd_ctx* ctx, int64_t n, const uint32_t* keymap, uint32_t* keys, uint8_t* core,
-                     void* stream) {
+int32_t pd_train_end(pd_ctx* ctx, int64_t n, const uint32_t* map_ids, const uint32_t* map_keys,
+                     int64_t n_map, uint32_t* keys, uint8_t* core, void* stream) {
     return guard(ctx, [&] {
         if (!ctx) throw Error(PD_EINVAL, "null context");
+        if (n_map < 0 || n_map > (int64_t)0xFFFFFFFE || (n_map && (!map_ids || !map_keys)))
+            throw Error(PD_EINVAL, "bad key map");
         TrainArgs a;
         a.n = n;
-        a.keymap = keymap;
+        a.map_ids = map_ids;
+        a.map_keys = map_keys;
+        a.n_map = n_map;
         a.keys_out = keys;
         a.core = core;
         a.phase = 2;
@@ -466,6 +494,93 @@ int32_t pd_rank_labels(pd_ctx* ctx, const uint32_t* keys, int64_t n, const uint3
         if (!ctx || n < 0 || n_roots < 0 || (n && (!keys || !labels)) || (n_roots && !roots))
             throw Error(PD_EINVAL, "bad argument");
         rank_labels(ctx->c, keys, n, roots, n_roots, labels, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_owned_results(pd_ctx* ctx, int64_t n, const int32_t* owner, const uint32_t* gid,
+                         const int32_t* labels, const uint8_t* core, int32_t n_ranks,
+                         const int64_t* gid_offsets, uint32_t* out, int64_t capacity,
+                         int64_t* counts, int64_t* m, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || !gid_offsets || !counts || !m || n < 0) throw Error(PD_EINVAL, "bad argument");
+        if (n && (!owner || !gid || !labels)) throw Error(PD_EINVAL, "null argument");
+        if (capacity > 0 && !out) throw Error(PD_EINVAL, "null output buffer");
+        *m = owned_results(ctx->c, n, owner, gid, labels, core, n_ranks, gid_offsets, out, capacity,
+                           counts, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_scatter_results(pd_ctx* ctx, const uint32_t* pairs, int64_t m, uint32_t gid_base,
+                           int64_t n, int32_t* labels, uint8_t* core, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || m < 0 || n < 0 || (m && !pairs) || (n && !labels))
+            throw Error(PD_EINVAL, "bad argument");
+        scatter_results(ctx->c, pairs, m, gid_base, n, labels, core, (hipStream_t)stream);
+    });
+}
+
+// ---------------------------------------------------------------- RCCL
+
+int32_t pd_comm_unique_id(uint8_t* id) {
+    return guard(nullptr, [&] {
+        if (!id) throw Error(PD_EINVAL, "null id");
+        comm_unique_id(id);
+    });
+}
+
+int32_t pd_comm_init(pd_ctx* ctx, int32_t n_ranks, int32_t rank, const uint8_t* id, pd_comm** out) {
+    return guard(ctx, [&] {
+        if (!ctx || !id || !out) throw Error(PD_EINVAL, "null argument");
+        pd::Comm* c = comm_init(ctx->c.device, n_ranks, rank, id);
+        *out = new pd_comm{c};
+    });
+}
+
+int32_t pd_comm_init_all(int32_t n, const int32_t* devices, pd_comm** out) {
+    return guard(nullptr, [&] {
+        if (n < 1 || !devices || !out) throw Error(PD_EINVAL, "bad argument");
+        std::vector<pd::Comm*> cs(n, nullptr);
+        comm_init_all(n, devices, cs.data());
+        for (int i = 0; i < n; ++i) out[i] = new pd_comm{cs[i]};
+    });
+}
+
+int32_t pd_comm_destroy(pd_comm* comm) {
+    if (!comm) return PD_OK;
+    comm_destroy(comm->c);
+    delete comm;
+    return PD_OK;
+}
+
+int32_t pd_comm_all_reduce(pd_comm* comm, const void* send, void* recv, int64_t count, int32_t elem,
+                           int32_t op, void* stream) {
+    return comm_guard(comm, [&] {
+        if (count < 0 || (count && (!send || !recv))) throw Error(PD_EINVAL, "bad buffer");
+        comm_all_reduce(comm->c, send, recv, count, elem, op, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_comm_all_gather_v(pd_comm* comm, const void* send, void* recv, const int64_t* counts,
+                             int32_t elem, void* stream) {
+    return comm_guard(comm, [&] {
+        if (!counts) throw Error(PD_EINVAL, "null counts");
+        comm_all_gather_v(comm->c, send, recv, counts, elem, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_comm_all_to_all_v(pd_comm* comm, const void* send, const int64_t* send_counts,
+                             void* recv, const int64_t* recv_counts, int32_t elem, void* stream) {
+    return comm_guard(comm, [&] {
+        if (!send_counts || !recv_counts) throw Error(PD_EINVAL, "null counts");
+        comm_all_to_all_v(comm->c, send, send_counts, recv, recv_counts, elem, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_comm_broadcast(pd_comm* comm, void* buf, int64_t count, int32_t elem, int32_t root,
+                          void* stream) {
+    return comm_guard(comm, [&] {
+        if (count < 0 || (count && !buf)) throw Error(PD_EINVAL, "bad buffer");
+        comm_broadcast(comm->c, buf, count, elem, root, (hipStream_t)stream);
     });
 }
 

@@ -1133,14 +1133,25 @@ __global__ __launch_bounds__(kBlock) void export_kernel(uint32_t NL,
     out_key[i] = gmin[par[r]];
 }
 
-// Phase B: replace each local component's key by its global key.
+// Phase B: replace each local component's key by its global key (ids in no
+// export keep their own: the component never left this device).
 __global__ __launch_bounds__(kBlock) void remap_kernel(uint32_t R, const uint8_t* __restrict__ core,
                                                        const uint32_t* __restrict__ par,
-                                                       const uint32_t* __restrict__ keymap,
-                                                       uint32_t* __restrict__ gmin) {
+                                                       const uint32_t* __restrict__ map_ids,
+                                                       const uint32_t* __restrict__ map_keys,
+                                                       uint32_t n_map, uint32_t* __restrict__ gmin) {
     const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
     if (r >= R || !(core[r] & 1) || par[r] != r) return;
-    gmin[r] = keymap[gmin[r]];
+    const uint32_t k = gmin[r];
+    uint32_t lo = 0, hi = n_map;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (map_ids[mid] < k)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    if (lo < n_map && map_ids[lo] == k) gmin[r] = map_keys[lo];
 }
 
 // Owner records: publish core flag / count, and the cluster key of core
@@ -2540,9 +2551,9 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     const float slo = st.slo, shi = st.shi;
     if (a.phase == 2) {
         tm.mark();   // 0
-        if (a.keymap && R)
+        if (a.n_map > 0 && R)
             hipLaunchKernelGGL(remap_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par,
-                               a.keymap, gmin);
+                               a.map_ids, a.map_keys, (uint32_t)a.n_map, gmin);
     }
     uint32_t* key_out = a.phase == 2 ? a.keys_out : ctx.arena.get<uint32_t>("key_out", n);
     // single device: core flags travel in the keys (ids < 2^30); sharded: global ids

@@ -126,7 +126,11 @@ struct TrainArgs {
     int phase = 0;
     const uint32_t* gid = nullptr;    // device, global id per local point (null: identity)
     const uint8_t* xr = nullptr;      // device, point also lives on another device
-    const uint32_t* keymap = nullptr; // device, global parent over the id space (phase 2)
+    // device, phase 2: the merged exports (pd_merge_exports): ascending
+    // distinct ids and each one's global key
+    const uint32_t* map_ids = nullptr;
+    const uint32_t* map_keys = nullptr;
+    int64_t n_map = 0;
     uint32_t* keys_out = nullptr;     // device out, n: cluster key per owned point (phase 2)
     int64_t n_exports = 0;            // out (phase 1)
 };
@@ -173,13 +177,34 @@ int64_t pack(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const uint64_
              const int32_t* local_index_host, uint32_t gid_base, void* coords_out,
              uint32_t* gid_out, int32_t* owner_out, uint8_t* xr_out, int64_t cap, hipStream_t s);
 void train_exports(Ctx& ctx, uint32_t* gid_out, uint32_t* key_out, int64_t cap, hipStream_t s);
-void merge_exports(Ctx& ctx, uint32_t n_space, const uint32_t* gid, const uint32_t* key, int64_t m,
-                   uint32_t* parent, hipStream_t s);
+int64_t merge_exports(Ctx& ctx, const uint32_t* gid, const uint32_t* key, int64_t m,
+                      uint32_t* ids_out, uint32_t* keys_out, hipStream_t s);
 int64_t select_roots(Ctx& ctx, const uint32_t* keys, const uint32_t* gid, int64_t n, uint32_t* out,
                      hipStream_t s);
 void sort_u32(Ctx& ctx, uint32_t* data, int64_t n, hipStream_t s);
 void rank_labels(Ctx& ctx, const uint32_t* keys, int64_t n, const uint32_t* roots, int64_t nr,
                  int32_t* labels, hipStream_t s);
+int64_t owned_results(Ctx& ctx, int64_t n, const int32_t* owner, const uint32_t* gid,
+                      const int32_t* labels, const uint8_t* core, int n_ranks,
+                      const int64_t* gid_offsets_host, uint32_t* out, int64_t cap,
+                      int64_t* counts_host, hipStream_t s);
+void scatter_results(Ctx& ctx, const uint32_t* pairs, int64_t m, uint32_t gid_base, int64_t n,
+                     int32_t* labels, uint8_t* core, hipStream_t s);
+
+// RCCL communicator (comm.hip): one rank of a device group
+struct Comm;
+Comm* comm_init(int device, int n_ranks, int rank, const uint8_t* id);
+void comm_init_all(int n, const int32_t* devices, Comm** out);
+void comm_destroy(Comm* c);
+void comm_unique_id(uint8_t* id);
+int comm_device(const Comm* c);
+void comm_all_reduce(Comm* c, const void* send, void* recv, int64_t count, int elem, int op,
+                     hipStream_t s);
+void comm_all_gather_v(Comm* c, const void* send, void* recv, const int64_t* counts, int elem,
+                       hipStream_t s);
+void comm_all_to_all_v(Comm* c, const void* send, const int64_t* send_counts, void* recv,
+                       const int64_t* recv_counts, int elem, hipStream_t s);
+void comm_broadcast(Comm* c, void* buf, int64_t count, int elem, int root, hipStream_t s);
 void halo_members(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P,
                   const double* ebox_host, int64_t* counts_host, int64_t* members_dev,
                   int64_t members_cap, hipStream_t s);

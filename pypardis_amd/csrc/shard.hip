@@ -111,8 +111,9 @@ __global__ __launch_bounds__(kBlock) void iota_kernel(uint32_t* __restrict__ p, 
     if (i < n) p[i] = i;
 }
 
-// Union-find over the global id space, smaller root wins (the component's
-// root is then its smallest id = its smallest core point).
+// Union-find over the compacted export ids (index into the ascending id
+// list), smaller root wins, so a component's root is its smallest id = its
+// smallest core point.
 __device__ __forceinline__ uint32_t find_root(uint32_t* par, uint32_t x) {
     uint32_t p = __hip_atomic_load(par + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while (p != x) {
@@ -122,20 +123,27 @@ __device__ __forceinline__ uint32_t find_root(uint32_t* par, uint32_t x) {
     return x;
 }
 
+__device__ __forceinline__ uint32_t lower_bound(const uint32_t* a, uint32_t n, uint32_t v) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < v)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
 __global__ __launch_bounds__(kBlock) void unite_kernel(const uint32_t* __restrict__ ga,
                                                        const uint32_t* __restrict__ gb, int64_t m,
-                                                       uint32_t n_space,
-                                                       uint32_t* __restrict__ par,
-                                                       uint32_t* __restrict__ bad) {
+                                                       const uint32_t* __restrict__ ids,
+                                                       uint32_t u, uint32_t* __restrict__ par) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= m) return;
-    uint32_t a = ga[i], b = gb[i];
-    if (a >= n_space || b >= n_space) {
-        atomicOr(bad, 1u);
-        return;
-    }
-    a = find_root(par, a);
-    b = find_root(par, b);
+    // both ids are in the list (it is the set of all of them)
+    uint32_t a = find_root(par, lower_bound(ids, u, ga[i]));
+    uint32_t b = find_root(par, lower_bound(ids, u, gb[i]));
     while (a != b) {
         if (a > b) {
             const uint32_t t = a;
@@ -151,21 +159,28 @@ __global__ __launch_bounds__(kBlock) void unite_kernel(const uint32_t* __restric
     }
 }
 
-__global__ __launch_bounds__(kBlock) void flatten_all_kernel(uint32_t* __restrict__ par,
-                                                             uint32_t n) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    uint32_t x = par[i];
-    if (x == i) return;
+// keys_out[j] = id of the root of ids[j]'s component (after every union).
+__global__ __launch_bounds__(kBlock) void map_keys_kernel(const uint32_t* __restrict__ par,
+                                                          const uint32_t* __restrict__ ids,
+                                                          uint32_t u,
+                                                          uint32_t* __restrict__ keys_out) {
+    const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= u) return;
+    uint32_t x = par[j];
     while (true) {
         const uint32_t p = par[x];
         if (p == x) break;
         x = p;
     }
-    par[i] = x;
+    keys_out[j] = ids[x];
 }
 
-struct IsRoot {   // owned core point whose key is its own global id
+// Owned core point whose key is its own global id.  One per cluster over all
+// devices: a cluster's key is the global id of its smallest core point, and
+// pd_train_end writes keys for owned records only (a point is owned by exactly
+// one device: the one holding its KD partition; halo copies keep kNone), so
+// the smallest core point passes this test on exactly one device.
+struct IsRoot {
     const uint32_t* keys;
     const uint32_t* gid;
     __device__ bool operator()(uint32_t i) const {
@@ -182,7 +197,8 @@ __global__ __launch_bounds__(kBlock) void map_gid_kernel(uint32_t* __restrict__ 
 
 __global__ __launch_bounds__(kBlock) void rank_kernel(const uint32_t* __restrict__ keys, uint64_t n,
                                                       const uint32_t* __restrict__ roots,
-                                                      uint32_t nr, int32_t* __restrict__ labels) {
+                                                      uint32_t nr, int32_t* __restrict__ labels,
+                                                      uint32_t* __restrict__ bad) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = keys[i];
@@ -190,15 +206,76 @@ __global__ __launch_bounds__(kBlock) void rank_kernel(const uint32_t* __restrict
         labels[i] = -1;
         return;
     }
-    uint32_t lo = 0, hi = nr;   // first root >= k
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (roots[mid] < k)
-            lo = mid + 1;
-        else
-            hi = mid;
+    const uint32_t lo = lower_bound(roots, nr, k);
+    if (lo < nr && roots[lo] == k) {
+        labels[i] = (int32_t)lo;
+    } else {   // a key with no root: the exports / roots were not gathered from every device
+        labels[i] = -2;
+        atomicOr(bad, 1u);
     }
-    labels[i] = (lo < nr && roots[lo] == k) ? (int32_t)lo : -2;   // -2: key without a root
+}
+
+// Owned records of a sharded train packed for the return to the devices that
+// hold the points: (global id, (label + 1) | core << 31), in the input order
+// (ascending global id); per destination device r (ids in
+// [gid_off[r], gid_off[r + 1])) a count.  Ids must ascend (pd_pack order), so
+// each destination's block is contiguous; `bad` flags a descent.
+__global__ __launch_bounds__(kBlock) void owned_pack_kernel(
+    const uint32_t* __restrict__ list, uint32_t m, const uint32_t* __restrict__ gid,
+    const int32_t* __restrict__ labels, const uint8_t* __restrict__ core,
+    const int64_t* __restrict__ gid_off, int n_ranks, uint32_t* __restrict__ out,
+    unsigned long long* __restrict__ counts, uint32_t* __restrict__ bad) {
+    __shared__ unsigned int sc[kMaxRanks];
+    for (int k = threadIdx.x; k < n_ranks; k += kBlock) sc[k] = 0;
+    __syncthreads();
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k < m) {
+        const uint32_t i = list[k];
+        const uint32_t g = gid[i];
+        if (k && gid[list[k - 1]] >= g) atomicOr(bad, 1u);
+        int r = 0;
+        while (r + 1 < n_ranks && (int64_t)g >= gid_off[r + 1]) ++r;
+        if ((int64_t)g < gid_off[0] || (int64_t)g >= gid_off[n_ranks]) atomicOr(bad, 2u);
+        atomicAdd(&sc[r], 1u);
+        out[2 * (size_t)k] = g;
+        out[2 * (size_t)k + 1] = (uint32_t)(labels[i] + 1) | (core && core[i] ? 0x80000000u : 0u);
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < n_ranks; q += kBlock)
+        if (sc[q]) atomicAdd(counts + q, (unsigned long long)sc[q]);
+}
+
+struct IsOwned {
+    const int32_t* owner;
+    __device__ bool operator()(uint32_t i) const { return owner[i] >= 0; }
+};
+
+constexpr int32_t kUnset = (int32_t)0x80000000;
+
+__global__ __launch_bounds__(kBlock) void fill_i32_kernel(int32_t* __restrict__ p, uint64_t n,
+                                                          int32_t v) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void scatter_results_kernel(
+    const uint32_t* __restrict__ pairs, uint64_t m, uint32_t gid_base, uint64_t n,
+    int32_t* __restrict__ labels, uint8_t* __restrict__ core, uint32_t* __restrict__ bad) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= m) return;
+    const uint32_t g = pairs[2 * k], v = pairs[2 * k + 1];
+    if (g < gid_base || (uint64_t)(g - gid_base) >= n) {
+        atomicOr(bad, 1u);
+        return;
+    }
+    labels[g - gid_base] = (int32_t)(v & 0x7FFFFFFFu) - 1;
+    if (core) core[g - gid_base] = (uint8_t)(v >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void unset_check_kernel(const int32_t* __restrict__ labels,
+                                                             uint64_t n, uint32_t* __restrict__ bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n && labels[i] == kUnset) atomicOr(bad, 2u);
 }
 
 }  // namespace
@@ -289,25 +366,39 @@ void train_exports(Ctx& ctx, uint32_t* gid_out, uint32_t* key_out, int64_t cap, 
                           hipMemcpyDeviceToDevice, s));
 }
 
-void merge_exports(Ctx& ctx, uint32_t n_space, const uint32_t* gid, const uint32_t* key, int64_t m,
-                   uint32_t* parent, hipStream_t s) {
-    if (n_space == 0xFFFFFFFFu) throw Error(-5, "id space must be < 2^32 - 1");
-    if (n_space)
-        hipLaunchKernelGGL(iota_kernel, dim3(blocks(n_space)), dim3(kBlock), 0, s, parent, n_space);
-    uint32_t* dbad = ctx.arena.get<uint32_t>("merge_bad", 4);
-    PD_HIP(hipMemsetAsync(dbad, 0, sizeof(uint32_t), s));
-    if (m > 0) {
-        hipLaunchKernelGGL(unite_kernel, dim3(blocks((uint64_t)m)), dim3(kBlock), 0, s, gid, key, m,
-                           n_space, parent, dbad);
-    }
-    if (n_space)
-        hipLaunchKernelGGL(flatten_all_kernel, dim3(blocks(n_space)), dim3(kBlock), 0, s, parent,
-                           n_space);
-    PD_HIP(hipGetLastError());
-    uint32_t* hb = (uint32_t*)pinned(ctx, sizeof(uint32_t));
-    PD_HIP(hipMemcpyAsync(hb, dbad, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+// O(exports): the union of the pairs runs over the distinct ids they name
+// (sorted, unique), not over the whole id space.
+int64_t merge_exports(Ctx& ctx, const uint32_t* gid, const uint32_t* key, int64_t m,
+                      uint32_t* ids_out, uint32_t* keys_out, hipStream_t s) {
+    if (m <= 0) return 0;
+    if (m > (int64_t)0x7FFFFFFF) throw Error(-5, "too many exports");
+    const size_t m2 = 2 * (size_t)m;
+    uint32_t* buf = ctx.arena.get<uint32_t>("mx_buf", m2);
+    uint32_t* alt = ctx.arena.get<uint32_t>("mx_alt", m2);
+    PD_HIP(hipMemcpyAsync(buf, gid, sizeof(uint32_t) * m, hipMemcpyDeviceToDevice, s));
+    PD_HIP(hipMemcpyAsync(buf + m, key, sizeof(uint32_t) * m, hipMemcpyDeviceToDevice, s));
+    rocprim::double_buffer<uint32_t> kb(buf, alt);
+    size_t tb = 0;
+    PD_HIP(rocprim::radix_sort_keys(nullptr, tb, kb, m2, 0u, 32u, s));
+    void* tmp = ctx.arena.get<char>("mx_tmp", tb);
+    PD_HIP(rocprim::radix_sort_keys(tmp, tb, kb, m2, 0u, 32u, s));
+    uint32_t* du = ctx.arena.get<uint32_t>("mx_count", 4);
+    tb = 0;
+    PD_HIP(rocprim::unique(nullptr, tb, kb.current(), ids_out, du, m2, rocprim::equal_to<uint32_t>(), s));
+    tmp = ctx.arena.get<char>("mx_tmp2", tb);
+    PD_HIP(rocprim::unique(tmp, tb, kb.current(), ids_out, du, m2, rocprim::equal_to<uint32_t>(), s));
+    uint32_t* hu = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+    PD_HIP(hipMemcpyAsync(hu, du, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     sync(s);
-    if (*hb) throw Error(-1, "merge_exports: id outside the id space");
+    const uint32_t u = *hu;
+    uint32_t* par = ctx.arena.get<uint32_t>("mx_par", u);
+    hipLaunchKernelGGL(iota_kernel, dim3(blocks(u)), dim3(kBlock), 0, s, par, u);
+    hipLaunchKernelGGL(unite_kernel, dim3(blocks((uint64_t)m)), dim3(kBlock), 0, s, gid, key, m,
+                       ids_out, u, par);
+    hipLaunchKernelGGL(map_keys_kernel, dim3(blocks(u)), dim3(kBlock), 0, s, par, ids_out, u,
+                       keys_out);
+    PD_HIP(hipGetLastError());
+    return (int64_t)u;
 }
 
 int64_t select_roots(Ctx& ctx, const uint32_t* keys, const uint32_t* gid, int64_t n, uint32_t* out,
@@ -349,12 +440,88 @@ void sort_u32(Ctx& ctx, uint32_t* data, int64_t n, hipStream_t s) {
 
 void rank_labels(Ctx& ctx, const uint32_t* keys, int64_t n, const uint32_t* roots, int64_t nr,
                  int32_t* labels, hipStream_t s) {
-    (void)ctx;
     if (nr > (int64_t)0x7FFFFFFF) throw Error(-5, "too many clusters");
-    if (n)
-        hipLaunchKernelGGL(rank_kernel, dim3(blocks((uint64_t)n)), dim3(kBlock), 0, s, keys,
-                           (uint64_t)n, roots, (uint32_t)nr, labels);
+    if (!n) return;
+    uint32_t* dbad = ctx.arena.get<uint32_t>("rank_bad", 4);
+    PD_HIP(hipMemsetAsync(dbad, 0, sizeof(uint32_t), s));
+    hipLaunchKernelGGL(rank_kernel, dim3(blocks((uint64_t)n)), dim3(kBlock), 0, s, keys,
+                       (uint64_t)n, roots, (uint32_t)nr, labels, dbad);
     PD_HIP(hipGetLastError());
+    uint32_t* hb = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+    PD_HIP(hipMemcpyAsync(hb, dbad, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    sync(s);
+    if (*hb) throw Error(-1, "rank_labels: a cluster key has no root among the roots given "
+                             "(roots must be gathered from every device)");
+}
+
+int64_t owned_results(Ctx& ctx, int64_t n, const int32_t* owner, const uint32_t* gid,
+                      const int32_t* labels, const uint8_t* core, int n_ranks,
+                      const int64_t* gid_off_host, uint32_t* out, int64_t cap,
+                      int64_t* counts_host, hipStream_t s) {
+    if (n_ranks < 1 || n_ranks > kMaxRanks) throw Error(-1, "n_ranks must be in [1, 64]");
+    if (n > (int64_t)kIdMask) throw Error(-5, "n must be < 2^30 points per device");
+    for (int r = 0; r < n_ranks; ++r)
+        if (gid_off_host[r + 1] < gid_off_host[r]) throw Error(-1, "gid offsets must ascend");
+    int64_t* doff = ctx.arena.get<int64_t>("own_off", kMaxRanks + 1);
+    int64_t* hoff = (int64_t*)pinned(ctx, sizeof(int64_t) * (kMaxRanks + 1));
+    std::memcpy(hoff, gid_off_host, sizeof(int64_t) * (n_ranks + 1));
+    PD_HIP(hipMemcpyAsync(doff, hoff, sizeof(int64_t) * (n_ranks + 1), hipMemcpyHostToDevice, s));
+    uint32_t* list = ctx.arena.get<uint32_t>("own_list", n + 1);
+    uint32_t* dcount = ctx.arena.get<uint32_t>("own_count", 4);
+    PD_HIP(hipMemsetAsync(dcount, 0, sizeof(uint32_t), s));
+    if (n) {
+        rocprim::counting_iterator<uint32_t> it(0u);
+        size_t tb = 0;
+        IsOwned pred{owner};
+        PD_HIP(rocprim::select(nullptr, tb, it, list, dcount, (size_t)n, pred, s));
+        void* tmp = ctx.arena.get<char>("own_tmp", tb);
+        PD_HIP(rocprim::select(tmp, tb, it, list, dcount, (size_t)n, pred, s));
+    }
+    // one pinned block: m, bad, counts (the offsets were copied already)
+    PD_HIP(hipStreamSynchronize(s));
+    uint32_t* hm = (uint32_t*)pinned(ctx, 16 + sizeof(unsigned long long) * kMaxRanks);
+    PD_HIP(hipMemcpyAsync(hm, dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    sync(s);
+    const uint32_t m = hm[0];
+    if ((int64_t)m > cap) throw Error(-1, "owned_results: output buffer too small");
+    unsigned long long* dc = ctx.arena.get<unsigned long long>("own_cnt", kMaxRanks);
+    uint32_t* dbad = ctx.arena.get<uint32_t>("own_bad", 4);
+    PD_HIP(hipMemsetAsync(dc, 0, sizeof(unsigned long long) * kMaxRanks, s));
+    PD_HIP(hipMemsetAsync(dbad, 0, sizeof(uint32_t), s));
+    if (m)
+        hipLaunchKernelGGL(owned_pack_kernel, dim3(blocks(m)), dim3(kBlock), 0, s, list, m, gid,
+                           labels, core, doff, n_ranks, out, dc, dbad);
+    PD_HIP(hipGetLastError());
+    unsigned long long* hc = (unsigned long long*)((char*)hm + 16);
+    PD_HIP(hipMemcpyAsync(hm + 1, dbad, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    PD_HIP(hipMemcpyAsync(hc, dc, sizeof(unsigned long long) * n_ranks, hipMemcpyDeviceToHost, s));
+    sync(s);
+    if (hm[1] & 1) throw Error(-1, "owned_results: global ids do not ascend");
+    if (hm[1] & 2) throw Error(-1, "owned_results: global id outside the offsets");
+    for (int r = 0; r < n_ranks; ++r) counts_host[r] = (int64_t)hc[r];
+    return (int64_t)m;
+}
+
+void scatter_results(Ctx& ctx, const uint32_t* pairs, int64_t m, uint32_t gid_base, int64_t n,
+                     int32_t* labels, uint8_t* core, hipStream_t s) {
+    if (m != n) throw Error(-1, "scatter_results: " + std::to_string(m) + " results for " +
+                                    std::to_string(n) + " points");
+    if (!n) return;
+    uint32_t* dbad = ctx.arena.get<uint32_t>("scat_bad", 4);
+    PD_HIP(hipMemsetAsync(dbad, 0, sizeof(uint32_t), s));
+    hipLaunchKernelGGL(fill_i32_kernel, dim3(blocks((uint64_t)n)), dim3(kBlock), 0, s, labels,
+                       (uint64_t)n, kUnset);
+    hipLaunchKernelGGL(scatter_results_kernel, dim3(blocks((uint64_t)m)), dim3(kBlock), 0, s,
+                       pairs, (uint64_t)m, gid_base, (uint64_t)n, labels, core, dbad);
+    hipLaunchKernelGGL(unset_check_kernel, dim3(blocks((uint64_t)n)), dim3(kBlock), 0, s, labels,
+                       (uint64_t)n, dbad);
+    PD_HIP(hipGetLastError());
+    uint32_t* hb = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+    PD_HIP(hipMemcpyAsync(hb, dbad, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    sync(s);
+    if (*hb & 1) throw Error(-1, "scatter_results: global id outside this device's points");
+    if (*hb & 2) throw Error(-1, "scatter_results: a point received no result (each point must "
+                                 "be owned by exactly one device)");
 }
 
 }  // namespace pd

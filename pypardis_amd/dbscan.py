@@ -134,6 +134,39 @@ class _Assignments(object):
         return self.points.n
 
 
+class _ShardedAssignments(object):
+    """``DBSCAN.result`` of a sharded train: this rank holds the (key, label)
+    pairs of its input slice, like one partition of the reference's result
+    RDD.  ``collect()`` / ``count()`` are collectives (every rank calls them)
+    and return the whole, sorted by key (R:dbscan/dbscan.py:162-164)."""
+
+    def __init__(self, points, labels, gid_base, n_total, group):
+        self.points = points
+        self.labels = labels
+        self.gid_base = gid_base
+        self.n_total = n_total
+        self.group = group
+
+    def local(self):
+        lab = self.labels.cpu().numpy().astype(np.int64)
+        if self.points.keys is None:
+            return self.gid_base + np.arange(self.points.n, dtype=np.int64), lab
+        return self.points.keys, lab
+
+    def collect(self):
+        import torch.distributed as dist
+        keys, lab = self.local()
+        parts = [None] * dist.get_world_size(self.group)
+        dist.all_gather_object(parts, (keys, lab), group=self.group)
+        keys = np.concatenate([p[0] for p in parts])
+        lab = np.concatenate([p[1] for p in parts])
+        order = np.argsort(keys, kind="stable")
+        return list(zip(keys[order].tolist(), lab[order].tolist()))
+
+    def count(self):
+        return self.n_total
+
+
 class DBSCAN(object):
     """
     :eps: nearest neighbor radius
@@ -148,15 +181,40 @@ class DBSCAN(object):
     :cluster_dict: kept for API parity; the reference never assigns it
 
     MI355X additions: ``labels_`` (device int32, input order),
-    ``core_sample_mask_`` (device uint8), ``n_clusters_``; ``kd_sums`` selects
-    the KD moment summation (see KDPartitioner) — it changes the boxes only,
-    never the labels.
+    ``core_sample_mask_`` (device uint8), ``n_clusters_``.
+
+    ``kd_sums``: KD moment summation.  'exact' (default): correctly rounded,
+    order-independent double-double sums — the same boxes on one device or
+    many; 'sequential': the reference's left-to-right fold, bit-identical to
+    its boxes (on C0 a split the reference decides by round-off differs
+    otherwise), single device only.  Never changes the labels.
+
+    Multi-GPU (the reference's fan-out over executors, R:dbscan/dbscan.py:
+    104-126):
+      * inside an initialised torch.distributed process group of more than
+        one rank (one process per GPU, e.g. torchrun), ``train(slice)``
+        clusters the union of every rank's slice; each rank passes its own
+        slice and gets ``labels_`` / ``core_sample_mask_`` for it (input
+        order), the global ``n_clusters_``, the same ``bounding_boxes`` /
+        ``expanded_boxes``, ``neighbors`` over its slice, and a ``result``
+        whose ``collect()`` (a collective) returns every (key, label).  Keys
+        of array input are global indices (rank offset + row).  Collectives
+        run on RCCL through libpardis (pd_comm_*) for an "nccl" group;
+      * ``n_gpus=N > 1`` without a process group: this process drives GPUs
+        0..N-1 itself (one thread per device, pd_comm_init_all), the input
+        split by index;
+      * ``n_gpus=1``: one device even inside a process group.
+    ``group``: the process group to use (default: the world group).
+    ``device``: where the points go (default: the current CUDA device).
     """
 
     def __init__(self, eps=0.5, min_samples=5, metric=euclidean, max_partitions=None,
-                 kd_sums='exact'):
+                 kd_sums='exact', n_gpus=None, device=None, group=None):
         self.eps = eps
         self.kd_sums = kd_sums
+        self.n_gpus = n_gpus
+        self.device = device
+        self.group = group
         self.min_samples = int(min_samples)
         self.metric = metric
         self.max_partitions = max_partitions
@@ -170,6 +228,20 @@ class DBSCAN(object):
         self.core_sample_mask_ = None
         self.n_clusters_ = None
         self.partitioner = None
+        self.shard = None
+
+    def _process_group(self):
+        if self.group is not None:
+            return self.group
+        if self.n_gpus == 1:
+            return None
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            if self.n_gpus not in (None, dist.get_world_size()):
+                raise ValueError(f"n_gpus={self.n_gpus} inside a process group of "
+                                 f"{dist.get_world_size()} ranks")
+            return dist.group.WORLD
+        return None
 
     def train(self, data):
         """
@@ -181,7 +253,12 @@ class DBSCAN(object):
         if self.min_samples < 1:
             raise ValueError("min_samples must be >= 1")
         metric = _native.metric_code(self.metric)
-        points = as_points(data)
+        group = self._process_group()
+        if group is not None:
+            return self._train_group(data, group, metric)
+        if self.n_gpus is not None and int(self.n_gpus) > 1:
+            return self._train_devices(data, metric)
+        points = as_points(data, self.device)
         parts = KDPartitioner(points, self.max_partitions, sums=self.kd_sums)
         self.partitioner = parts
         self.data = points
@@ -199,6 +276,61 @@ class DBSCAN(object):
         self.n_clusters_ = ncl
         self.result = _Assignments(points, labels)
         return self
+
+    # ------------------------------------------------------------ multi-GPU
+    def _sharded_checks(self, points):
+        if points.d > 4:
+            raise NotImplementedError("the multi-GPU train is built for d <= 4; the dense "
+                                      "high-dimensional path runs on one device (n_gpus=1)")
+        if self.kd_sums != 'exact':
+            raise ValueError("kd_sums='sequential' is single-device (the fold order of one "
+                             "slice); the multi-GPU train uses the exact sums")
+        P = self.max_partitions if self.max_partitions is not None else 4 ** points.d
+        return int(P)
+
+    def _set_sharded(self, points, labels, core, res, result):
+        self.data = points
+        self.labels_ = labels
+        self.core_sample_mask_ = core
+        self.n_clusters_ = res.n_clusters
+        self.bounding_boxes = res.bounding_boxes
+        self.expanded_boxes = {L: box.expand(2 * self.eps)
+                               for L, box in sorted(res.bounding_boxes.items())}
+        self.neighbors = _Neighborhoods(points, self.expanded_boxes)
+        self.result = result
+        self.shard = res
+        return self
+
+    def _train_group(self, data, group, metric):
+        from . import distributed
+        points = as_points(data, self.device)
+        P = self._sharded_checks(points)
+        res = distributed.train_sharded(points.X, self.eps, self.min_samples, metric=metric,
+                                        max_partitions=P, group=group)
+        result = _ShardedAssignments(points, res.local_labels, res.gid_base, res.n_total, group)
+        return self._set_sharded(points, res.local_labels, res.local_core, res, result)
+
+    def _train_devices(self, data, metric):
+        from . import distributed
+        W = int(self.n_gpus)
+        _native.require_gpu()
+        if torch.cuda.device_count() < W:
+            raise ValueError(f"n_gpus={W} but {torch.cuda.device_count()} GPU(s) are visible")
+        points = as_points(data, self.device)
+        P = self._sharded_checks(points)
+        n = points.n
+        cuts = [r * n // W for r in range(W + 1)]
+        slices = [points.X[cuts[r]:cuts[r + 1]].to(torch.device("cuda", r)).contiguous()
+                  for r in range(W)]
+        torch.cuda.synchronize(points.X.device)
+        comms = distributed.device_comms(range(W))
+        ops = [distributed.NativeOps(torch.device("cuda", r)) for r in range(W)]
+        res = distributed.train_threads(slices, self.eps, self.min_samples, comms, ops,
+                                        metric=metric, max_partitions=P)
+        dev = points.X.device
+        labels = torch.cat([r.local_labels.to(dev) for r in res])
+        core = torch.cat([r.local_core.to(dev) for r in res])
+        return self._set_sharded(points, labels, core, res[0], _Assignments(points, labels))
 
     def assignments(self):
         """

@@ -97,8 +97,8 @@ class NativeOps(object):
     def exports(self, m):
         return _native.train_exports(m, self.device, ctx=self.ctx)
 
-    def merge(self, n_space, gid, key):
-        return _native.merge_exports(n_space, gid, key, ctx=self.ctx)
+    def merge(self, gid, key):
+        return _native.merge_exports(gid, key, ctx=self.ctx)
 
     def train_end(self, n, keymap):
         return _native.train_end(n, keymap, self.device, ctx=self.ctx)
@@ -111,6 +111,12 @@ class NativeOps(object):
 
     def rank_labels(self, keys, roots):
         return _native.rank_labels(keys, roots, ctx=self.ctx)
+
+    def owned_results(self, owner, gid, labels, core, gid_offsets):
+        return _native.owned_results(owner, gid, labels, core, gid_offsets, ctx=self.ctx)
+
+    def scatter_results(self, pairs, gid_base, n):
+        return _native.scatter_results(pairs, gid_base, n, self.device, ctx=self.ctx)
 
     def timings(self):
         return self.ctx.timings()
@@ -161,8 +167,9 @@ def partition_ranks(P, world):
     return part_rank, local_index
 
 
-class _Comm(object):
-    """torch.distributed on the right device for the backend."""
+class _TorchComm(object):
+    """Collectives through a torch.distributed process group (gloo on the
+    host: the CPU tests; any backend without device buffers)."""
 
     def __init__(self, group, device):
         self.group = group
@@ -176,7 +183,8 @@ class _Comm(object):
 
     def all_reduce(self, arr, op):
         t = torch.as_tensor(np.ascontiguousarray(arr)).to(self.device)
-        dist.all_reduce(t, op=op, group=self.group)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM,
+                        group=self.group)
         return t.cpu().numpy()
 
     def all_gather_np(self, arr):
@@ -186,23 +194,86 @@ class _Comm(object):
         return np.stack([o.cpu().numpy() for o in outs])
 
     def all_gather_var(self, t):
-        """Concatenate 1-D tensors of different lengths from every rank."""
+        """Concatenate tensors of different lengths (dim 0) from every rank."""
         sizes = self.all_gather_np(np.array([t.shape[0]], np.int64))[:, 0]
         mx = max(int(sizes.max()), 1)
-        buf = torch.zeros(mx, dtype=t.dtype, device=self.device)
+        buf = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=self.device)
         buf[:t.shape[0]] = self.to(t)
         outs = [torch.empty_like(buf) for _ in range(self.world)]
         dist.all_gather(outs, buf, group=self.group)
         return torch.cat([o[:int(s)] for o, s in zip(outs, sizes)])
 
-    def all_to_all_v(self, send, send_counts, recv_counts, width=1):
-        """send (sum(send_counts) * width) elements grouped by destination."""
-        recv = torch.empty(int(sum(recv_counts)) * width, dtype=send.dtype, device=self.device)
+    def all_to_all_v(self, send, send_counts, recv_counts):
+        """Rows of `send` grouped by destination -> rows grouped by source."""
+        row = tuple(send.shape[1:])
+        w = int(np.prod(row)) if row else 1
+        recv = torch.empty(int(sum(recv_counts)) * w, dtype=send.dtype, device=self.device)
         dist.all_to_all_single(recv, self.to(send.reshape(-1)),
-                               output_split_sizes=[int(c) * width for c in recv_counts],
-                               input_split_sizes=[int(c) * width for c in send_counts],
+                               output_split_sizes=[int(c) * w for c in recv_counts],
+                               input_split_sizes=[int(c) * w for c in send_counts],
                                group=self.group)
-        return recv
+        return recv.reshape((-1,) + row)
+
+
+class RcclComm(object):
+    """Collectives through libpardis's RCCL communicator (pd_comm_*): device
+    buffers on this rank's GPU, grouped point-to-point sends for the
+    variable-size exchanges.  torch.distributed only hands the 128-byte
+    RCCL id from rank 0 to the others."""
+
+    def __init__(self, comm):
+        self.comm = comm
+        self.world = comm.world
+        self.rank = comm.rank
+        self.device = comm.device
+
+    @classmethod
+    def from_group(cls, group, device):
+        device = torch.device(device)
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = _native.comm_unique_id() if rank == 0 else bytes(_native.PD_COMM_ID_BYTES)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        if dist.get_backend(group) == "nccl":
+            t = t.to(device)
+        dist.broadcast(t, dist.get_global_rank(group, 0) if group is not None else 0,
+                       group=group)
+        return cls(_native.Comm.init(world, rank, bytes(t.cpu().tolist()), device.index))
+
+    def to(self, t):
+        return t.to(self.device)
+
+    def all_reduce(self, arr, op):
+        t = torch.as_tensor(np.ascontiguousarray(arr)).to(self.device)
+        self.comm.all_reduce(t, _native.PD_R_MAX if op == "max" else _native.PD_R_SUM)
+        return t.cpu().numpy()
+
+    def all_gather_np(self, arr):
+        a = np.ascontiguousarray(arr)
+        t = torch.as_tensor(a.reshape(1, -1) if a.ndim == 0 else a[None]).to(self.device)
+        out = self.comm.all_gather_v(t, [1] * self.world)
+        return out.cpu().numpy()
+
+    def all_gather_var(self, t):
+        sizes = self.all_gather_np(np.array([t.shape[0]], np.int64))[:, 0]
+        return self.comm.all_gather_v(self.to(t).contiguous(), sizes)
+
+    def all_to_all_v(self, send, send_counts, recv_counts):
+        return self.comm.all_to_all_v(self.to(send).contiguous(), send_counts, recv_counts)
+
+
+_rccl_cache = {}
+
+
+def make_comm(group, device):
+    """RCCL (pd_comm) for an "nccl" group on GPU ranks, torch.distributed
+    otherwise.  The RCCL communicator is built once per (group, device)."""
+    device = torch.device(device)
+    if dist.get_backend(group) == "nccl" and device.type == "cuda":
+        key = (id(group), device.index)
+        if key not in _rccl_cache:
+            _rccl_cache[key] = RcclComm.from_group(group, device)
+        return _rccl_cache[key]
+    return _TorchComm(group, device)
 
 
 class ShardedResult(object):
@@ -211,28 +282,31 @@ class ShardedResult(object):
     :gid: global ids of the points this rank owns (ascending)
     :labels: their DBSCAN labels (sklearn numbering over all points, -1 noise)
     :core: their core flags
+    :local_labels, local_core: labels / core flags of this rank's INPUT
+        points in input order (returned by the owners; None when
+        ``return_local`` was off)
+    :gid_base: global id of this rank's first input point
+    :n_total: points over all ranks
     :n_clusters: number of clusters over all points
-    :splits, boxes: the KD trace and boxes (identical on every rank)
+    :splits: the KD trace (identical on every rank)
+    :bounding_boxes: label -> BoundingBox of each KD partition
+    :boxes: (P, 2, d) expanded boxes
     """
 
-    def __init__(self, gid, labels, core, n_clusters, splits, boxes, stats):
-        self.gid = gid
-        self.labels = labels
-        self.core = core
-        self.n_clusters = n_clusters
-        self.splits = splits
-        self.boxes = boxes
-        self.stats = stats
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
 
 
 def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitions=None,
-                  group=None, ops=None, split_method='min_var'):
+                  group=None, ops=None, split_method='min_var', comm=None, return_local=True):
     """Sharded DBSCAN train over the ranks of ``group`` (default: world).
 
     X: this rank's (n_i, d) slice (float32/float64, on this rank's GPU for
     NativeOps); the global id of row j is sum(n_0 .. n_{i-1}) + j.
     ``max_partitions`` defaults to the world size (one KD partition per GPU).
     ``split_method``: 'min_var' (default) or 'rotation' (KDPartitioner's).
+    ``comm``: a collective layer (make_comm(group, device) by default: RCCL
+    through libpardis for an "nccl" group, torch.distributed otherwise).
     """
     if split_method not in ('min_var', 'rotation'):
         split_method = 'min_var'   # the reference's fallback (R:dbscan/partition.py:129-130)
@@ -240,7 +314,7 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
         raise NotImplementedError("the sharded train is built for d <= 4 (the dense "
                                   "high-dimensional path runs on one device)")
     ops = ops or NativeOps(X.device)
-    comm = _Comm(group, getattr(ops, "device", X.device))
+    comm = comm or make_comm(group, getattr(ops, "device", X.device))
     W, rank = comm.world, comm.rank
     n, d = X.shape
     P = int(max_partitions) if max_partitions is not None else W
@@ -259,8 +333,9 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
 
     # ---- global ids
     sizes = comm.all_gather_np(np.array([n], np.int64))[:, 0]
-    gid_base = int(sizes[:rank].sum())
-    n_total = int(sizes.sum())
+    gid_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    gid_base = int(gid_off[rank])
+    n_total = int(gid_off[-1])
     if n_total >= 0xFFFFFFFF:
         raise ValueError("the sharded train addresses points with 32-bit global ids")
 
@@ -276,13 +351,15 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
         lo, hi, bad = ops.bbox(X)
     else:
         lo, hi, bad = np.full(d, np.inf), np.full(d, -np.inf), 0
-    ext = comm.all_reduce(np.concatenate([-np.asarray(lo), np.asarray(hi)]), dist.ReduceOp.MAX)
-    nbad = comm.all_reduce(np.array([bad], np.int64), dist.ReduceOp.SUM)[0]
+    # one all-reduce (max) of (-lo, hi, non-finite count): any count > 0 fails
+    ext = comm.all_reduce(np.concatenate([-np.asarray(lo, np.float64),
+                                          np.asarray(hi, np.float64), [float(bad)]]), "max")
+    nbad = ext[2 * d]
     if nbad:
         raise ValueError("Input contains NaN or infinity.")
     if n_total == 0:
         raise ValueError("no points on any rank")
-    data_box = np.concatenate([-ext[:d], ext[d:]])
+    data_box = np.concatenate([-ext[:d], ext[d:2 * d]])
     box = BoundingBox(k=d).union(BoundingBox(data_box[:d], data_box[d:]))
 
     # ---- KD partition (R:dbscan/partition.py:139-183): per level one fused
@@ -303,7 +380,7 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
             def hist(prefix, shift):
                 h = ops.radix_hist(X, kdlab, sel, axes, prefix, shift) if n else \
                     np.zeros((len(sel), 256), np.int64)
-                return comm.all_reduce(np.asarray(h, np.int64), dist.ReduceOp.SUM)
+                return comm.all_reduce(np.asarray(h, np.int64), "sum")
 
             med, less, tot = level_medians(hist, len(sel), fp32)
             if n:
@@ -319,7 +396,7 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
         mom = dd_combine(comm.all_gather_np(part))
         axes, means, vars_, bounds = level_axes(mom)
         cnt = ops.counts(X, kdlab, sel, axes, bounds) if n else np.zeros((len(sel), 8), np.int64)
-        cnt = comm.all_reduce(cnt.astype(np.int64), dist.ReduceOp.SUM)
+        cnt = comm.all_reduce(cnt.astype(np.int64), "sum")
         boundary, cand = level_boundaries(cnt, bounds)
         pending = (sel, axes, boundary, new)
         apply_level(boxes, splits, level, axes, means, vars_, cnt, cand, boundary)
@@ -349,10 +426,9 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
             if m != c:
                 raise RuntimeError(f"pack: {m} points for rank {dest}, route said {c}")
         off += c
-    recv_counts = comm.all_to_all_v(torch.as_tensor(send_counts, dtype=torch.int64),
-                                    np.ones(W, np.int64), np.ones(W, np.int64)).cpu().numpy()
+    recv_counts = comm.all_gather_np(send_counts.astype(np.int64))[:, rank].astype(np.int64)
     dev = getattr(ops, "device", X.device)
-    Xr = comm.all_to_all_v(s_coords, send_counts, recv_counts, d).to(dev).reshape(-1, d)
+    Xr = comm.all_to_all_v(s_coords, send_counts, recv_counts).to(dev).reshape(-1, d)
     gid = comm.all_to_all_v(s_gid, send_counts, recv_counts).to(dev)
     owner = comm.all_to_all_v(s_owner, send_counts, recv_counts).to(dev)
     xr = comm.all_to_all_v(s_xr, send_counts, recv_counts).to(dev)
@@ -373,10 +449,11 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     stats["exports"] = int(e_gid.shape[0])
     lap("phase_a")
 
-    # ---- global key merge (R:dbscan/dbscan.py:153-165)
-    all_gid = comm.all_gather_var(e_gid).to(dev)
-    all_key = comm.all_gather_var(e_key).to(dev)
-    keymap = ops.merge(n_total, all_gid, all_key) if all_gid.shape[0] else None
+    # ---- global key merge (R:dbscan/dbscan.py:153-165): one gather of the
+    # (id, key) pairs, then the same O(exports) union on every rank
+    ex = comm.all_gather_var(torch.stack([e_gid, e_key], 1)).to(dev)
+    keymap = ops.merge(ex[:, 0].contiguous(), ex[:, 1].contiguous()) if ex.shape[0] else None
+    stats["exports_total"] = int(ex.shape[0])
     lap("merge")
 
     # ---- phase B, labels
@@ -385,10 +462,66 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     else:
         keys, core = ops.empty(0, torch.int32), ops.empty(0, torch.uint8)
     roots = ops.select_roots(keys, gid) if nr else ops.empty(0, torch.int32)
-    all_roots = comm.all_gather_var(roots).to(dev)
+    all_roots = comm.all_gather_var(roots).to(dev).contiguous()
     ops.sort(all_roots)
     labels = ops.rank_labels(keys, all_roots) if nr else ops.empty(0, torch.int32)
     own = owner >= 0
     lap("phase_b")
-    return ShardedResult(gid[own], labels[own], core[own], int(all_roots.shape[0]), splits,
-                         ebox, stats)
+
+    # ---- results back to the ranks that hold the points, in input order
+    # (the reference's result RDD, R:dbscan/dbscan.py:162-164)
+    loc_labels = loc_core = None
+    if return_local:
+        pairs, back = ops.owned_results(owner, gid, labels, core, gid_off)
+        got = comm.all_gather_np(back.astype(np.int64))[:, rank].astype(np.int64)
+        pairs_in = comm.all_to_all_v(pairs, back, got).to(dev)
+        loc_labels, loc_core = ops.scatter_results(pairs_in, gid_base, n)
+        lap("results")
+    return ShardedResult(gid=gid[own], labels=labels[own], core=core[own],
+                         local_labels=loc_labels, local_core=loc_core, gid_base=gid_base,
+                         n_total=n_total, n_clusters=int(all_roots.shape[0]), splits=splits,
+                         bounding_boxes=boxes, boxes=ebox, stats=stats)
+
+
+def train_threads(slices, eps, min_samples, comms, ops, metric=_native.PD_EUCLIDEAN,
+                  max_partitions=None, split_method='min_var'):
+    """One process driving several devices: rank r = thread r runs
+    ``train_sharded`` on slices[r] with comms[r] (e.g. RcclComm over
+    pd_comm_init_all) and ops[r].  Returns the per-rank results in rank order;
+    the first rank error is raised (after every thread has finished)."""
+    import threading
+
+    W = len(slices)
+    out, errs = [None] * W, [None] * W
+
+    def body(r):
+        try:
+            dev = getattr(ops[r], "device", None)
+            if dev is not None and torch.device(dev).type == "cuda":
+                torch.cuda.set_device(torch.device(dev))
+            out[r] = train_sharded(slices[r], eps, min_samples, metric=metric,
+                                   max_partitions=max_partitions, ops=ops[r], comm=comms[r],
+                                   split_method=split_method)
+        except BaseException as e:   # noqa: B902 - re-raised below
+            errs[r] = e
+
+    ts = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(W)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
+    return out
+
+
+_device_comms = {}
+
+
+def device_comms(devices):
+    """RCCL communicators of one process over `devices` (cached)."""
+    key = tuple(int(d) for d in devices)
+    if key not in _device_comms:
+        _device_comms[key] = [RcclComm(c) for c in _native.Comm.init_all(list(key))]
+    return _device_comms[key]

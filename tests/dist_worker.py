@@ -20,7 +20,7 @@ def cut_points(n, world):
 
 
 def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native,
-             split_method='min_var'):
+             split_method='min_var', api=False, keyed=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -39,19 +39,47 @@ def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native,
             sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
             from sharded_ops import OracleOps
             ops = OracleOps()
-        res = train_sharded(Xi, eps, min_samples, metric=metric, max_partitions=P, ops=ops,
-                            split_method=split_method)
+        extra = {}
+        if api:
+            # the reference API: dbscan.DBSCAN(...).train(this rank's slice)
+            # inside the process group; CPU runs swap the device stages for
+            # the oracle stand-in (the orchestration is the product's)
+            import dbscan
+            from pypardis_amd import distributed
+            if not native:
+                distributed.NativeOps = lambda device: ops
+            data = Xi
+            if keyed:   # (key, vector) records with string keys
+                data = [("k%06d" % (cuts[rank] + j), v) for j, v in enumerate(Xi.cpu().numpy())]
+            model = dbscan.DBSCAN(eps=eps, min_samples=min_samples,
+                                  metric=["euclidean", "cityblock"][metric], max_partitions=P,
+                                  device=None if native else "cpu")
+            model.train(data)
+            res = model.shard
+            pairs = model.assignments()
+            extra = dict(n_clusters_=np.int64(model.n_clusters_),
+                         boxes_api=np.array([model.bounding_boxes[L].as_array()
+                                             for L in sorted(model.bounding_boxes)]),
+                         assign_keys=np.array([str(k) for k, _ in pairs]),
+                         assign_labels=np.array([v for _, v in pairs], np.int64),
+                         count=np.int64(model.result.count()))
+            loc = model.labels_.cpu().numpy(), model.core_sample_mask_.cpu().numpy()
+        else:
+            res = train_sharded(Xi, eps, min_samples, metric=metric, max_partitions=P, ops=ops,
+                                split_method=split_method)
+            loc = res.local_labels.cpu().numpy(), res.local_core.cpu().numpy()
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), gid=res.gid.cpu().numpy(),
                  labels=res.labels.cpu().numpy(), core=res.core.cpu().numpy(),
                  ncl=np.int64(res.n_clusters), splits=np.array(res.splits, np.float64),
                  ebox=res.boxes, exports=np.int64(res.stats["exports"]),
-                 received=np.int64(res.stats["received"]))
+                 received=np.int64(res.stats["received"]), loc_labels=loc[0], loc_core=loc[1],
+                 lo=np.int64(cuts[rank]), **extra)
     finally:
         dist.destroy_process_group()
 
 
 def run_world(world, X, eps, min_samples, metric, P, out_dir, native=False, timeout=600,
-              split_method='min_var'):
+              split_method='min_var', api=False, keyed=False):
     """Spawn `world` ranks; return the assembled (labels, core, n_clusters,
     splits) over all points."""
     import socket
@@ -64,7 +92,7 @@ def run_world(world, X, eps, min_samples, metric, P, out_dir, native=False, time
     ctx = mp.get_context("spawn")
     procs = [ctx.Process(target=run_rank,
                          args=(r, world, port, X, eps, min_samples, metric, P, out_dir, native,
-                               split_method))
+                               split_method, api, keyed))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -82,8 +110,15 @@ def run_world(world, X, eps, min_samples, metric, P, out_dir, native=False, time
     core = np.zeros(n, np.uint8)
     seen = np.zeros(n, np.int64)
     ncl, splits, exports, received = set(), [], 0, 0
+    loc_labels = np.full(n, -3, np.int64)
+    loc_core = np.zeros(n, np.uint8)
+    ranks = []
     for r in range(world):
         z = np.load(os.path.join(out_dir, f"r{r}.npz"))
+        ranks.append(dict(z))
+        lo = int(z["lo"])
+        loc_labels[lo:lo + len(z["loc_labels"])] = z["loc_labels"]
+        loc_core[lo:lo + len(z["loc_core"])] = z["loc_core"]
         g = z["gid"].astype(np.int64)
         labels[g] = z["labels"]
         core[g] = z["core"]
@@ -93,4 +128,45 @@ def run_world(world, X, eps, min_samples, metric, P, out_dir, native=False, time
         exports += int(z["exports"])
         received += int(z["received"])
     return dict(labels=labels, core=core, seen=seen, ncl=ncl, splits=splits, exports=exports,
-                received=received)
+                received=received, loc_labels=loc_labels, loc_core=loc_core, ranks=ranks)
+
+
+def _rccl_rank(port, X, eps, min_samples, P, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    import dbscan
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        m = dbscan.DBSCAN(eps=eps, min_samples=min_samples, max_partitions=P,
+                          group=dist.group.WORLD).train(torch.from_numpy(X).cuda())
+        from pypardis_amd import distributed
+        assert any(isinstance(c, distributed.RcclComm) for c in distributed._rccl_cache.values())
+        np.savez(os.path.join(out_dir, "rccl.npz"), labels=m.labels_.cpu().numpy(),
+                 ncl=np.int64(m.n_clusters_))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_rccl_world1(X, eps, min_samples, P, out_dir, timeout=300):
+    """One rank in an "nccl" process group (spawned), DBSCAN through RCCL."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = mp.get_context("spawn").Process(target=_rccl_rank,
+                                        args=(port, X, eps, min_samples, P, out_dir))
+    p.start()
+    p.join(timeout)
+    if p.is_alive():
+        p.kill()
+        p.join()
+    if p.exitcode != 0:
+        raise RuntimeError(f"rank exit code {p.exitcode}")
+    z = np.load(os.path.join(out_dir, "rccl.npz"))
+    return dict(labels=z["labels"], n_clusters=int(z["ncl"]))

@@ -125,11 +125,14 @@ class OracleOps(object):
         g, k = self.exp
         return (torch.from_numpy(g.astype(np.int32)), torch.from_numpy(k.astype(np.int32)))
 
-    def merge(self, n_space, gid, key):
-        return torch.from_numpy(osh.merge(n_space, gid.numpy(), key.numpy()).astype(np.int32))
+    def merge(self, gid, key):
+        ids, keys = osh.merge(gid.numpy().view(np.uint32), key.numpy().view(np.uint32))
+        return (torch.from_numpy(ids.astype(np.uint32).view(np.int32)),
+                torch.from_numpy(keys.astype(np.uint32).view(np.int32)))
 
     def train_end(self, n, keymap):
-        keys, core = osh.phase_b(self.state, None if keymap is None else keymap.numpy())
+        km = None if keymap is None else tuple(t.numpy().view(np.uint32) for t in keymap)
+        keys, core = osh.phase_b(self.state, km)
         return torch.from_numpy(keys.astype(np.int32)), torch.from_numpy(core)
 
     def select_roots(self, keys, gid):
@@ -141,7 +144,33 @@ class OracleOps(object):
         return data
 
     def rank_labels(self, keys, roots):
-        k = keys.numpy().astype(np.int64)
-        r = roots.numpy().astype(np.int64)
-        lab = np.where(k >= 0, np.searchsorted(r, k), -1)
-        return torch.from_numpy(lab.astype(np.int32))
+        k = keys.numpy().view(np.uint32).astype(np.int64)
+        r = roots.numpy().view(np.uint32).astype(np.int64)
+        m = k != 0xFFFFFFFF
+        pos = np.searchsorted(r, k[m])
+        if m.any() and (len(r) == 0 or (r[np.minimum(pos, len(r) - 1)] != k[m]).any()):
+            raise RuntimeError("rank_labels: a cluster key has no root")   # pd_rank_labels
+        lab = np.full(len(k), -1, np.int32)
+        lab[m] = pos
+        return torch.from_numpy(lab)
+
+    def owned_results(self, owner, gid, labels, core, gid_offsets):
+        """pd_owned_results restated: (gid, (label + 1) | core << 31) of the
+        owned records, ascending gid, and the count per holding rank."""
+        own = owner.numpy() >= 0
+        g = gid.numpy().view(np.uint32)[own].astype(np.int64)
+        assert (np.diff(g) > 0).all()
+        v = (labels.numpy()[own].astype(np.int64) + 1) | (core.numpy()[own].astype(np.int64) << 31)
+        pairs = np.stack([g, v], 1).astype(np.uint32).view(np.int32)
+        counts = np.diff(np.searchsorted(g, np.asarray(gid_offsets, np.int64)))
+        return torch.from_numpy(np.ascontiguousarray(pairs)), counts.astype(np.int64)
+
+    def scatter_results(self, pairs, gid_base, n):
+        p = pairs.numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
+        idx = p[:, 0] - gid_base
+        assert len(p) == n and (np.sort(idx) == np.arange(n)).all()
+        labels = np.empty(n, np.int32)
+        core = np.empty(n, np.uint8)
+        labels[idx] = (p[:, 1] & 0x7FFFFFFF) - 1
+        core[idx] = p[:, 1] >> 31
+        return torch.from_numpy(labels), torch.from_numpy(core)

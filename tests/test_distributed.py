@@ -31,6 +31,9 @@ def test_sharded_labels_equal_sklearn(tmp_path, name, world, P):
     np.testing.assert_array_equal(out["core"], g["sk_core"].astype(np.uint8))
     assert out["ncl"] == {int(g["sk_labels"].max()) + 1}
     assert out["received"] >= len(X)   # halo copies travel to both sides
+    # labels returned to the ranks holding the points, in input order
+    np.testing.assert_array_equal(out["loc_labels"], g["sk_labels"])
+    np.testing.assert_array_equal(out["loc_core"], g["sk_core"].astype(np.uint8))
     if name in ("b2d_20k", "b3d_20k", "lattice_900"):
         assert out["exports"] > 0      # the cross-rank merge is exercised
     kd = oracle.kd_partition(X, P, sums="exact")
@@ -96,3 +99,50 @@ def test_sharded_c4_skew(tmp_path):
     np.testing.assert_array_equal(out["core"], core.astype(np.uint8))
     assert out["ncl"] == {nc}
     assert out["received"] >= len(X)
+
+
+@pytest.mark.parametrize("name,world,P,keyed", [("b2d_20k", 2, 8, False), ("c0", 3, 4, True),
+                                                 ("c0_p5_cityblock", 2, 5, False)])
+def test_reference_api_in_process_group(tmp_path, name, world, P, keyed):
+    """dbscan.DBSCAN(...).train(slice) inside a gloo process group runs the
+    sharded train: every rank gets its slice's labels in input order, the
+    global n_clusters_, identical bounding boxes (those of one process), and
+    assignments() returns every (key, label) sorted by key."""
+    g = load_golden(name)
+    metric = str(g["metric"]) if "metric" in g else "euclidean"
+    X = g["X"]
+    mcode = 1 if metric in ("cityblock", "manhattan") else 0
+    out = run_world(world, X, float(g["eps"]), int(g["min_samples"]), mcode, P, str(tmp_path),
+                    api=True, keyed=keyed)
+    np.testing.assert_array_equal(out["loc_labels"], g["sk_labels"])
+    np.testing.assert_array_equal(out["loc_core"], g["sk_core"].astype(np.uint8))
+    kd = oracle.kd_partition(X, P, sums="exact")
+    want_keys = np.array([("k%06d" % i) if keyed else str(i) for i in range(len(X))])
+    order = np.arange(len(X))   # key order = input order (numeric / zero-padded keys)
+    for z in out["ranks"]:
+        assert int(z["n_clusters_"]) == int(g["sk_labels"].max()) + 1
+        np.testing.assert_array_equal(z["boxes_api"][:, 0], kd["box_lo"])
+        np.testing.assert_array_equal(z["boxes_api"][:, 1], kd["box_hi"])
+        np.testing.assert_array_equal(z["assign_keys"], want_keys[order])
+        np.testing.assert_array_equal(z["assign_labels"], g["sk_labels"][order])
+        assert int(z["count"]) == len(X)
+
+
+def test_train_threads_local_comm():
+    """One process, several ranks as threads (the n_gpus > 1 path without a
+    process group): distributed.train_threads with an in-process collective
+    layer and the oracle stand-in gives sklearn's labels on every slice."""
+    from local_comm import local_comms
+    from pypardis_amd.distributed import train_threads
+    from sharded_ops import OracleOps
+    import torch
+    g = load_golden("b3d_20k")
+    X = g["X"]
+    W = 3
+    cuts = [r * len(X) // W for r in range(W + 1)]
+    slices = [torch.from_numpy(np.ascontiguousarray(X[cuts[r]:cuts[r + 1]])) for r in range(W)]
+    res = train_threads(slices, float(g["eps"]), int(g["min_samples"]), local_comms(W),
+                        [OracleOps() for _ in range(W)], max_partitions=4)
+    labels = np.concatenate([r.local_labels.numpy() for r in res])
+    np.testing.assert_array_equal(labels, g["sk_labels"])
+    assert {r.n_clusters for r in res} == {int(g["sk_labels"].max()) + 1}

@@ -420,13 +420,17 @@ def test_sharded_stage_primitives(native):
         np.testing.assert_array_equal(out[2].cpu().numpy(), np.where(pr[kl] == dest, li[kl], -1))
         many = np.array([bin(v).count("1") > 1 for v in want[idx]])
         np.testing.assert_array_equal(out[3].cpu().numpy().astype(bool), many)
-    # merge: random pairs over an id space
-    n_space = 20_000
-    ga = rng.integers(0, n_space, 5000)
-    gb = rng.integers(0, n_space, 5000)
-    km = native.merge_exports(n_space, torch.from_numpy(ga.astype(np.int32)).cuda(),
-                              torch.from_numpy(gb.astype(np.int32)).cuda())
-    np.testing.assert_array_equal(km.cpu().numpy(), osh.merge(n_space, ga, gb))
+    # merge: random pairs over a sparse id space (ids up to 2^32 - 2)
+    pool = rng.choice(0xFFFFFFFE, 8000, replace=False)
+    ga = pool[rng.integers(0, len(pool), 5000)]
+    gb = pool[rng.integers(0, len(pool), 5000)]
+    as_i32 = (lambda a: torch.from_numpy(a.astype(np.uint32).view(np.int32)).cuda())
+    ids, mk = native.merge_exports(as_i32(ga), as_i32(gb))
+    wids, wkeys = osh.merge(ga, gb)
+    np.testing.assert_array_equal(ids.cpu().numpy().view(np.uint32), wids)
+    np.testing.assert_array_equal(mk.cpu().numpy().view(np.uint32), wkeys)
+    e = native.merge_exports(as_i32(ga[:0]), as_i32(gb[:0]))
+    assert e[0].shape[0] == 0
     # roots / sort / ranks
     gid = np.sort(rng.choice(1 << 30, 30_000, replace=False)).astype(np.int64)
     keys = np.where(rng.random(len(gid)) < 0.3, -1, gid[rng.integers(0, len(gid), len(gid))])
@@ -438,10 +442,44 @@ def test_sharded_stage_primitives(native):
     shuf = torch.from_numpy(rng.permutation(roots).astype(np.int32)).cuda()
     native.sort_u32(shuf)
     np.testing.assert_array_equal(shuf.cpu().numpy(), np.sort(roots))
-    labs = native.rank_labels(kd_, shuf).cpu().numpy()
-    ok = (keys >= 0) & np.isin(keys, roots)
-    np.testing.assert_array_equal(labs[ok], np.searchsorted(roots, keys[ok]))
-    assert (labs[keys < 0] == -1).all() and (labs[(keys >= 0) & ~ok] == -2).all()
+    ok = (keys < 0) | np.isin(keys, roots)
+    kd_ok = torch.from_numpy(np.where(ok, keys, -1).astype(np.int32)).cuda()
+    labs = native.rank_labels(kd_ok, shuf).cpu().numpy()
+    m = (keys >= 0) & ok
+    np.testing.assert_array_equal(labs[m], np.searchsorted(roots, keys[m]))
+    assert (labs[~m] == -1).all()
+    # a key with no root (roots not gathered from every device) is an error
+    with pytest.raises(native.PardisError, match="no root"):
+        native.rank_labels(kd_, shuf)
+    # results back to the holders: owned records, grouped by holding rank
+    n = 40_000
+    owner = torch.from_numpy(np.where(rng.random(n) < 0.6, 0, -1).astype(np.int32)).cuda()
+    g2 = np.sort(rng.choice(100_000, n, replace=False)).astype(np.int64)
+    lab2 = rng.integers(-1, 1000, n).astype(np.int32)
+    core2 = (rng.random(n) < 0.5).astype(np.uint8)
+    offs = np.array([0, 30_000, 70_000, 100_000], np.int64)
+    pairs, cnt = native.owned_results(owner, torch.from_numpy(g2.astype(np.int32)).cuda(),
+                                      torch.from_numpy(lab2).cuda(),
+                                      torch.from_numpy(core2).cuda(), offs)
+    own = owner.cpu().numpy() >= 0
+    p = pairs.cpu().numpy().view(np.uint32).astype(np.int64)
+    np.testing.assert_array_equal(p[:, 0], g2[own])
+    np.testing.assert_array_equal((p[:, 1] & 0x7FFFFFFF) - 1, lab2[own])
+    np.testing.assert_array_equal(p[:, 1] >> 31, core2[own])
+    assert cnt.tolist() == np.diff(np.searchsorted(g2[own], offs)).tolist()
+    # scatter: a full permutation of one holder's slice
+    base, nloc = 1000, 5000
+    perm = rng.permutation(nloc)
+    lab3 = rng.integers(-1, 50, nloc).astype(np.int64)
+    pr3 = np.stack([perm + base, ((lab3[perm] + 1) | (perm % 2) << 31)], 1)
+    pt = torch.from_numpy(pr3.astype(np.uint32).view(np.int32)).cuda()
+    l3, c3 = native.scatter_results(pt, base, nloc, torch.device("cuda", 0))
+    np.testing.assert_array_equal(l3.cpu().numpy(), lab3)
+    np.testing.assert_array_equal(c3.cpu().numpy(), np.arange(nloc) % 2)
+    with pytest.raises(native.PardisError, match="no result"):
+        dup = pt.clone()
+        dup[1] = dup[0]
+        native.scatter_results(dup, base, nloc, torch.device("cuda", 0))
 
 
 SHARDED = [("b3d_20k", 2, 8), ("c0", 3, 4), ("c0_p5_cityblock", 2, 5), ("dup_1d", 2, 3)]
@@ -459,6 +497,64 @@ def test_sharded_native_equals_sklearn(native, tmp_path, name, world, P):
     assert (out["seen"] == 1).all()
     np.testing.assert_array_equal(out["labels"], g["sk_labels"])
     np.testing.assert_array_equal(out["core"], g["sk_core"].astype(np.uint8))
+    np.testing.assert_array_equal(out["loc_labels"], g["sk_labels"])
+    np.testing.assert_array_equal(out["loc_core"], g["sk_core"].astype(np.uint8))
+
+
+@pytest.mark.parametrize("name,world,P,keyed", [("b3d_20k", 2, 8, False), ("c0", 3, 4, True)])
+def test_reference_api_process_group_native(native, tmp_path, name, world, P, keyed):
+    """dbscan.DBSCAN(...).train(slice) in a gloo process group, every device
+    stage native on cuda:0: input-order labels on every rank, the global
+    cluster count, and assignments() over all ranks."""
+    from dist_worker import run_world
+    g = load_golden(name)
+    X = g["X"]
+    out = run_world(world, X, float(g["eps"]), int(g["min_samples"]), 0, P, str(tmp_path),
+                    native=True, api=True, keyed=keyed)
+    np.testing.assert_array_equal(out["loc_labels"], g["sk_labels"])
+    np.testing.assert_array_equal(out["loc_core"], g["sk_core"].astype(np.uint8))
+    for z in out["ranks"]:
+        assert int(z["n_clusters_"]) == int(g["sk_labels"].max()) + 1
+        np.testing.assert_array_equal(z["assign_labels"], g["sk_labels"])
+        assert int(z["count"]) == len(X)
+
+
+def test_rccl_comm_single_rank(native):
+    """pd_comm_* through RCCL on one device (a 1-rank communicator: this box
+    has one GPU): the collectives' data movement, then the whole sharded
+    train on RcclComm (threaded runner, pd_comm_init_all) against pd_cluster."""
+    from pypardis_amd import distributed, synth
+    comm = distributed.device_comms([0])[0]
+    t = torch.arange(10, dtype=torch.float64, device="cuda")
+    assert comm.all_reduce(t.cpu().numpy(), "max").tolist() == list(range(10))
+    v = torch.arange(7, dtype=torch.int32, device="cuda")
+    assert comm.all_gather_var(v).cpu().tolist() == list(range(7))
+    w = torch.arange(12, dtype=torch.int64, device="cuda").reshape(6, 2)
+    np.testing.assert_array_equal(comm.all_to_all_v(w, [6], [6]).cpu().numpy(),
+                                  w.cpu().numpy())
+    np.testing.assert_array_equal(comm.all_gather_np(np.array([3, 4])), [[3, 4]])
+    X, cfg = synth.make_config("C2", n=300_000)
+    Xd = _dev(X)
+    lab1, core1, _, nc1 = native.cluster(Xd, cfg["eps"], cfg["min_samples"])
+    res = distributed.train_threads([Xd], cfg["eps"], cfg["min_samples"], [comm],
+                                    [distributed.NativeOps(torch.device("cuda", 0))],
+                                    max_partitions=8)
+    assert res[0].n_clusters == nc1
+    np.testing.assert_array_equal(res[0].local_labels.cpu().numpy(), lab1.cpu().numpy())
+    np.testing.assert_array_equal(res[0].local_core.cpu().numpy(), core1.cpu().numpy())
+
+
+def test_rccl_process_group_single_rank(native, tmp_path):
+    """A 1-rank "nccl" process group: the RCCL id is handed over through
+    torch.distributed and DBSCAN(...).train runs the sharded path on
+    pd_comm (forced with group=)."""
+    from dist_worker import run_rccl_world1
+    from pypardis_amd import synth
+    X, cfg = synth.make_config("C2", n=200_000)
+    lab1, _, _, nc1 = native.cluster(_dev(X), cfg["eps"], cfg["min_samples"])
+    got = run_rccl_world1(X, cfg["eps"], cfg["min_samples"], 8, str(tmp_path))
+    assert got["n_clusters"] == nc1
+    np.testing.assert_array_equal(got["labels"], lab1.cpu().numpy())
 
 
 def test_sharded_native_large(native, tmp_path):
@@ -472,6 +568,7 @@ def test_sharded_native_large(native, tmp_path):
     assert (out["seen"] == 1).all()
     assert out["ncl"] == {nc1}
     assert out["exports"] > 0
+    np.testing.assert_array_equal(out["loc_labels"], lab1.cpu().numpy().astype(np.int64))
     np.testing.assert_array_equal(out["labels"], lab1.cpu().numpy().astype(np.int64))
     np.testing.assert_array_equal(out["core"], core1.cpu().numpy())
 

@@ -13,6 +13,8 @@ either); anything else becomes float64.
 """
 from __future__ import annotations
 
+from operator import itemgetter
+
 import numpy as np
 import torch
 
@@ -106,11 +108,21 @@ def as_points(data, device=None):
         recs = list(recs)
     if not recs:
         raise ValueError("no points")
-    # vectorised unzip of the (key, vector) records
-    keys, vecs = zip(*recs)
-    X = np.asarray(vecs)
-    if X.dtype == object or X.ndim not in (1, 2):
-        X = np.stack([np.asarray(v) for v in vecs])
+    # unzip of the (key, vector) records: itemgetter maps (an order of
+    # magnitude faster than zip(*recs)), one concatenate for equal-length
+    # vectors
+    keys = list(map(itemgetter(0), recs))
+    vecs = list(map(itemgetter(1), recs))
+    X = None
+    if np.ndim(vecs[0]) == 1 and len(set(map(len, vecs))) == 1:
+        try:
+            X = np.concatenate(vecs).reshape(len(vecs), -1)
+        except (ValueError, TypeError):
+            X = None
+    if X is None:
+        X = np.asarray(vecs)
+        if X.dtype == object or X.ndim not in (1, 2):
+            X = np.stack([np.asarray(v) for v in vecs])
     # float32 stays float32 only if every vector is float32 (np.asarray of
     # a mixed list already promotes); anything else becomes float64
     if X.dtype not in (np.float32, np.float64):

@@ -58,13 +58,16 @@ enum pd_option {
                                       the reference's single-slice aggregate (slow; for
                                       bit-identical split boundaries).  Default: correctly
                                       rounded, order-independent double-double sums. */
-    PD_OPT_LINK_MODE = 4,  /* union strategy (tuning; labels identical).  5 (default): forest
-                              from the count pass's two smallest neighbours, a union over the
-                              PD_OPT_CENTRE_WINDOW records after each record (staged in LDS
-                              per wave), then one pass over neighbouring cells that tests
-                              record pairs only where the cells' roots differ (cells whose
-                              rows hold one root are screened out first); 3: the same with a
-                              union over each core record's own row instead of the window;
+    PD_OPT_LINK_MODE = 4,  /* union strategy (tuning; labels identical).  6 (default): forest
+                              from the count pass's two smallest neighbours; a union over the
+                              PD_OPT_CENTRE_WINDOW records after each record, staged per wave
+                              in LDS with each record's root (the flatten), its edges reduced
+                              in an LDS forest so that one global union runs per pair of trees
+                              the window joins; then one pass over neighbouring cells that
+                              tests record pairs only where the cells' roots differ (cells
+                              whose rows hold one root are screened out first); 5: the same
+                              with a separate flatten and a global find per window edge; 3:
+                              a union over each core record's own row instead of the window;
                               4: no window union; 0: initial forest + pointer jumping, then a
                               lock-free union sweep over all core-core edges; 2 that sweep
                               alone */
@@ -93,7 +96,7 @@ enum pd_option {
                                 record (r & ~255) when that lies in the query's own row, and
                                 wraps (dense cells: spreads the row-start hot spot; same
                                 counts, same labels); default 1024, 0 = never */,
-    PD_OPT_CENTRE_WINDOW = 13 /* link mode 5: records after each record tested by the window
+    PD_OPT_CENTRE_WINDOW = 13 /* link modes 5/6: records after each record tested by the window
                                 union (16, 32 or 64; default 16); mode 3: forward candidates
                                 each core record tests in the centre-row union (0 = all).  A
                                 heuristic either way: the cell verify proves or tests every

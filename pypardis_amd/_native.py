@@ -28,7 +28,7 @@ PD_OPT_DENSE_PRUNE = 11
 PD_OPT_COUNT_ROTATE = 12
 PD_OPT_CENTRE_WINDOW = 13
 SWEEP_VARIANT_DEFAULT = 5
-LINK_MODE_DEFAULT = 5
+LINK_MODE_DEFAULT = 6
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
                 "s_count_cand", "s_link_cand", "s_link_hit", "s_link_core", "s_link_same",

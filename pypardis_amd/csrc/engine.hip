@@ -1591,6 +1591,135 @@ __global__ __launch_bounds__(kBlock) void window_link_kernel(const T* __restrict
     }
 }
 
+// Root of x without path writes (L1 reads: a stale parent is still an
+// ancestor, so the walk ends at a root of some moment).
+__device__ __forceinline__ uint32_t root_l1(const uint32_t* par, uint32_t x) {
+    uint32_t p = ld_l1(par + x);
+    while (p != x) {
+        x = p;
+        p = ld_l1(par + x);
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint32_t lds_find(const uint32_t* lp, uint32_t x) {
+    uint32_t p = lp[x];
+    while (p != x) {
+        x = p;
+        p = lp[x];
+    }
+    return x;
+}
+
+// Union in an LDS forest (smaller index wins; CAS on the larger root).
+__device__ __forceinline__ void lds_union(uint32_t* lp, uint32_t a, uint32_t b) {
+    while (true) {
+        a = lds_find(lp, a);
+        b = lds_find(lp, b);
+        if (a == b) return;
+        if (a > b) {
+            const uint32_t t = a;
+            a = b;
+            b = t;
+        }
+        if (atomicCAS(lp + b, b, a) == b) return;
+    }
+}
+
+// Link mode 6: the window union of mode 5 with the flatten fused into the
+// staging and the edges reduced in LDS first.  A wave stages its 64 records
+// and the W after them with each one's current root (own records get it
+// written back: the flatten), each core lane tests the W records after it
+// and unions the core ones within eps of another tree in an LDS forest over
+// the window's slots; then each slot whose tree differs from its LDS
+// component's representative unites the two trees in the global forest —
+// one global union per pair of trees the window joins (the wave's edges
+// between the same two trees cost one), instead of a find per edge.
+template <typename T, int D, int M, int W, bool ST>
+__global__ __launch_bounds__(kBlock) void window_uf_kernel(const T* __restrict__ Xs, uint32_t R,
+                                                           double eps, double eps2, float lo,
+                                                           float hi, uint32_t* __restrict__ par,
+                                                           unsigned long long* __restrict__ stats) {
+    constexpr int E = 64 + W;
+    static_assert(E <= 128, "two slots per lane");
+    __shared__ T sx[kBlock / 64][E][D];
+    __shared__ uint32_t sp[kBlock / 64][E];
+    __shared__ uint32_t lp[kBlock / 64][E];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t b = xcd_block(blockIdx.x, gridDim.x) * kBlock + w * 64;
+    for (int e = lane; e < E; e += 64) {
+        const uint32_t j = b + e;
+        T v[D];
+        uint32_t p = kNone;
+        if (j < R) {
+            load_raw<T, D>(Xs, j, v);
+            p = ld_l1(par + j);
+            if (p != kNone && p != j) {
+                const uint32_t root = root_l1(par, p);
+                if (e < 64 && root != p) st_rlx(par + j, root);   // the flatten
+                p = root;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < D; ++k) v[k] = T(0);
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) sx[w][e][k] = v[k];
+        sp[w][e] = p;
+        lp[w][e] = (uint32_t)e;
+    }
+    __syncthreads();
+    const uint32_t r = b + lane;
+    const uint32_t p0 = r < R ? sp[w][lane] : kNone;
+    LinkStats st;
+    if (p0 != kNone) {
+        Pred<T, D, M> pr;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            pr.ar[k] = sx[w][lane][k];
+            pr.a[k] = (double)pr.ar[k];
+        }
+        pr.eps = eps;
+        pr.eps2 = eps2;
+        pr.lo = lo;
+        pr.hi = hi;
+#pragma unroll 4
+        for (int k = 1; k <= W; ++k) {
+            const uint32_t pj = sp[w][lane + k];
+            if (pj == kNone || pj == p0 || r + k >= R) continue;   // non-core / same tree
+            T bj[D];
+#pragma unroll
+            for (int q = 0; q < D; ++q) bj[q] = sx[w][lane + k][q];
+            if constexpr (ST) ++st.cand;
+            if (pr(bj)) {
+                if constexpr (ST) ++st.hit;
+                lds_union(lp[w], (uint32_t)lane, (uint32_t)(lane + k));
+            }
+        }
+    }
+    __syncthreads();
+    for (int e = lane; e < E; e += 64) {
+        const uint32_t pe = sp[w][e];
+        if (pe == kNone) continue;
+        const uint32_t lr = lds_find(lp[w], (uint32_t)e);
+        const uint32_t pl = sp[w][lr];
+        if (pl == pe) continue;
+        // the slot before carries the same pair of trees: its lane unites them
+        if (e > 0 && sp[w][e - 1] == pe && lds_find(lp[w], (uint32_t)(e - 1)) == lr) continue;
+        if constexpr (ST) ++st.unions;
+        uf_link_roots(par, uf_find_l1(par, pl), uf_find_l1(par, pe));
+    }
+    if constexpr (ST) {   // one atomic per block and counter
+        const uint32_t c = block_sum_u32(st.cand), h = block_sum_u32(st.hit),
+                       u = block_sum_u32(st.unions);
+        if (threadIdx.x == 0) {
+            atomicAdd(stats + 1, (unsigned long long)c);
+            atomicAdd(stats + 2, (unsigned long long)h);
+            atomicAdd(stats + 6, (unsigned long long)u);
+        }
+    }
+}
+
 // Per cell, the common root of its core records (kNone: no core record,
 // kMixed: several roots); also flattens: each core record gets its root
 // written back, so no separate flatten pass runs before (no unions run
@@ -1656,6 +1785,82 @@ __global__ __launch_bounds__(kBlock) void big_cell_root_kernel(const uint32_t* _
 #pragma unroll
             for (int k = 0; k < kBlock / 64; ++k) w = root_merge(w, part[k]);
             croot[c] = w;
+        }
+        __syncthreads();
+    }
+}
+
+// wroot[w] = root_merge(wroot[w], v) atomically (monotone: kNone -> a root
+// -> kMixed).
+__device__ __forceinline__ void word_merge(uint32_t* wroot, uint64_t w, uint32_t v) {
+    if (v == kNone) return;
+    uint32_t cur = ld_rlx(wroot + w);
+    while (true) {
+        const uint32_t want = root_merge(cur, v);
+        if (want == cur) return;
+        const uint32_t prev = atomicCAS(wroot + w, cur, want);
+        if (prev == cur) return;
+        cur = prev;
+    }
+}
+
+// cell_root_kernel with the word roots fused in: the cells of a wave are
+// consecutive in key order, so lanes of one directory word (key >> 6) merge
+// their cell roots by a segmented shuffle scan and the segment's last lane
+// merges the result into the word atomically (a word can span two waves).
+// wroot must start at kNone.
+template <typename K>
+__global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
+    const uint32_t* __restrict__ cstart, const uint32_t* __restrict__ ncells,
+    const K* __restrict__ keys, uint32_t* __restrict__ par, uint32_t* __restrict__ croot,
+    uint32_t* __restrict__ wroot, uint32_t* __restrict__ big, uint32_t* __restrict__ nbig) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const uint32_t nc = *ncells;
+    uint32_t v = kNone;
+    uint64_t word = ~0ull;
+    if (c < nc) {
+        const uint32_t s = cstart[c], e = cstart[c + 1];
+        word = (uint64_t)keys[s] >> 6;
+        if (e - s > kBigCell) {
+            big[atomicAdd(nbig, 1u)] = c;   // its root joins the word in big_cell_word_root
+        } else {
+            for (uint32_t r = s; r < e; ++r) v = root_merge(v, core_root(par, r));
+            croot[c] = v;
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t nv = (uint32_t)__shfl_up((int)v, o, 64);
+        const uint64_t nw = (uint64_t)__shfl_up((long long)word, o, 64);
+        if (lane >= o && nw == word) v = root_merge(v, nv);
+    }
+    const uint64_t next = (uint64_t)__shfl_down((long long)word, 1, 64);
+    if (c < nc && (lane == 63 || next != word)) word_merge(wroot, word, v);
+}
+
+template <typename K>
+__global__ __launch_bounds__(kBlock) void big_cell_word_root_kernel(
+    const uint32_t* __restrict__ cstart, const K* __restrict__ keys,
+    const uint32_t* __restrict__ big, const uint32_t* __restrict__ nbig,
+    uint32_t* __restrict__ par, uint32_t* __restrict__ croot, uint32_t* __restrict__ wroot) {
+    __shared__ uint32_t part[kBlock / 64];
+    const uint32_t nb = *nbig;
+    for (uint32_t i = blockIdx.x; i < nb; i += gridDim.x) {
+        const uint32_t c = big[i];
+        const uint32_t e = cstart[c + 1];
+        uint32_t v = kNone;
+        for (uint32_t r = cstart[c] + threadIdx.x; r < e; r += kBlock) v = root_merge(v, core_root(par, r));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v = root_merge(v, (uint32_t)__shfl_xor((int)v, o, 64));
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t w = kNone;
+#pragma unroll
+            for (int k = 0; k < kBlock / 64; ++k) w = root_merge(w, part[k]);
+            croot[c] = w;
+            word_merge(wroot, (uint64_t)keys[cstart[c]] >> 6, w);
         }
         __syncthreads();
     }
@@ -2362,11 +2567,29 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     tm.mark();   // 5
 
     uint32_t* par = ctx.arena.get<uint32_t>("parent", R);
-    if (R && (mode == 3 || mode == 4 || mode == 5)) {
+    if (R && (mode == 3 || mode == 4 || mode == 5 || mode == 6)) {
         // forest from the count pass's smallest neighbour (links across rows)
         hipLaunchKernelGGL(init_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, mn, 1, par);
-        hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
-        if (mode == 3) {
+        if (mode != 6)
+            hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
+        if (mode == 6) {
+            const int cw = ctx.centre_window;
+            auto go = [&](auto Wc) {
+                constexpr int Wv = decltype(Wc)::value;
+                if (sst)
+                    hipLaunchKernelGGL((window_uf_kernel<T, D, M, Wv, true>), dim3(blocks(R)),
+                                       dim3(kBlock), 0, s, Xs, R, eps, eps2, slo, shi, par, sst);
+                else
+                    hipLaunchKernelGGL((window_uf_kernel<T, D, M, Wv, false>), dim3(blocks(R)),
+                                       dim3(kBlock), 0, s, Xs, R, eps, eps2, slo, shi, par, sst);
+            };
+            if (cw <= 16)
+                go(std::integral_constant<int, 16>{});
+            else if (cw <= 32)
+                go(std::integral_constant<int, 32>{});
+            else
+                go(std::integral_constant<int, 64>{});
+        } else if (mode == 3) {
             hipLaunchKernelGGL((centre_link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s,
                                Xs, R, C, eps, eps2, slo, shi,
                                ctx.centre_window ? (uint32_t)ctx.centre_window : 0xFFFFFFFFu, par);
@@ -2389,10 +2612,21 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
                 go(std::integral_constant<int, 64>{});
         }
         uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
-        cell_roots(ctx, s, R, cstart, dncells, par, croot);
         uint32_t* wroot = ctx.arena.get<uint32_t>("word_root", W);
-        hipLaunchKernelGGL(word_root_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, W, croot,
-                           wroot);
+        if (mode == 6) {   // cell and word roots in one pass
+            uint32_t* big = ctx.arena.get<uint32_t>("big_cells", R / (kBigCell + 1) + 1);
+            uint32_t* nbig = ctx.arena.get<uint32_t>("big_count", 4);
+            PD_HIP(hipMemsetAsync(nbig, 0, sizeof(uint32_t), s));
+            PD_HIP(hipMemsetAsync(wroot, 0xFF, sizeof(uint32_t) * W, s));
+            hipLaunchKernelGGL((cell_word_root_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                               cstart, dncells, keys, par, croot, wroot, big, nbig);
+            hipLaunchKernelGGL((big_cell_word_root_kernel<K>), dim3(1024), dim3(kBlock), 0, s,
+                               cstart, keys, big, nbig, par, croot, wroot);
+        } else {
+            cell_roots(ctx, s, R, cstart, dncells, par, croot);
+            hipLaunchKernelGGL(word_root_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, W, croot,
+                               wroot);
+        }
         const uint32_t pcap = (uint32_t)std::min<uint64_t>(R, 64ull << 20);
         uint2* plist = ctx.arena.get<uint2>("pair_list", pcap);
         uint32_t* pcount = ctx.arena.get<uint32_t>("pair_count", 4);

@@ -87,7 +87,8 @@ struct Ctx {
     bool timing = false;
     bool full_counts = false;    // debug: count every neighbour (no early exit)
     bool seq_moments = false;    // reference-order (sequential) KD moment sums
-    int link_mode = 5;           // 5 window union + cell verify; 3 centre-row union + cell verify;
+    int link_mode = 6;           // 6 LDS-reduced window union + cell verify; 5 window union + cell verify;
+                                 // 3 centre-row union + cell verify;
                                  // 4 cell verify alone; 0 init forest + jumps + union sweep; 2 union sweep only
     int jump_rounds = 4;
     int xsub = 2;                // axis-0 sub-cells per eps

@@ -229,7 +229,8 @@ def test_train_matches_oracle(native, case):
 
 
 @pytest.mark.parametrize("variant,link_mode,border_roots",
-                         [(0, 5, 0), (7, 3, 1), (5, 0, 0), (7, 2, 0), (5, 4, 0), (5, 3, 0)])
+                         [(0, 5, 0), (7, 3, 1), (5, 0, 0), (7, 2, 0), (5, 4, 0), (5, 3, 0),
+                          (5, 6, 0), (0, 6, 0)])
 def test_sweep_variants_exact(native, variant, link_mode, border_roots):
     """PD_OPT_SWEEP_VARIANT x PD_OPT_LINK_MODE: the row-by-row and the
     batched sweep kernels, and the sampled-union + cell-verify link (3) or the
@@ -693,7 +694,9 @@ def test_c4_skew_vs_oracle(native, case):
                  ((native.PD_OPT_COUNT_ROTATE, 0, 1024),),
                  ((native.PD_OPT_CENTRE_WINDOW, 64, 16),),
                  ((native.PD_OPT_LINK_MODE, 3, 5), (native.PD_OPT_CENTRE_WINDOW, 1, 16)),
-                 ((native.PD_OPT_LINK_MODE, 3, 5), (native.PD_OPT_CENTRE_WINDOW, 0, 16))):
+                 ((native.PD_OPT_LINK_MODE, 3, 5), (native.PD_OPT_CENTRE_WINDOW, 0, 16)),
+                 ((native.PD_OPT_LINK_MODE, 6, 5),),
+                 ((native.PD_OPT_LINK_MODE, 6, 5), (native.PD_OPT_CENTRE_WINDOW, 64, 16))):
         for opt, val, _ in opts:
             ctx.set_option(opt, val)
         try:

@@ -14,7 +14,7 @@ if [ -n "${TESTS:-}" ]; then
   rc=$?; tail -4 gpurun_out/pytest_iter.log
   [ $rc -eq 0 ] || { grep -E "Error|assert" gpurun_out/pytest_iter.log | head -20; exit $rc; }
 fi
-timeout -k 10 300 python -u bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu ${BENCH_ARGS:-} \
+timeout -k 10 300 python -u bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu --no-host ${BENCH_ARGS:-} \
     --json-out gpurun_out/bench_iter.json > gpurun_out/bench_iter.log 2>&1 \
     || { tail -20 gpurun_out/bench_iter.log; exit 1; }
 python - <<'EOF'
@@ -26,7 +26,7 @@ print("kd", b.get("kd_ms"))
 EOF
 if [ "${PROF:-1}" = "1" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_iter \
-      -o it -- python bench.py --steps 3 --warmup 1 --no-cpu ${BENCH_ARGS:-} \
+      -o it -- python bench.py --steps 3 --warmup 1 --no-cpu --no-host ${BENCH_ARGS:-} \
       > gpurun_out/prof_iter.log 2>&1 || { tail -5 gpurun_out/prof_iter.log; exit 1; }
   f=$(ls gpurun_out/prof_iter/*/it_kernel_stats.csv 2>/dev/null | head -1)
   [ -z "$f" ] && f=$(find gpurun_out/prof_iter -name "*kernel_stats.csv" | head -1)

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 IFS='|' read -ra SETS <<< "$SWEEP"
 for a in "${SETS[@]}"; do
-  timeout -k 10 300 python -u bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu ${BENCH_ARGS:-} $a \
+  timeout -k 10 300 python -u bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu --no-host ${BENCH_ARGS:-} $a \
       --json-out gpurun_out/sweep.json > gpurun_out/sweep.log 2>&1 || { tail -5 gpurun_out/sweep.log; exit 1; }
   python -c "
 import json; b=json.load(open('gpurun_out/sweep.json'))

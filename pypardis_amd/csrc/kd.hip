@@ -266,6 +266,9 @@ struct SplitTab {
 // Label / split tables staged in LDS by the level kernels (larger levels
 // take the one-point-per-lane kernels).
 constexpr int kTabLds = 256;
+// kd_pass_kernel: up to this many labels are summed per lane without the
+// LDS regroup
+constexpr int kDirectMax = 1;
 
 // NG = labels whose moments this pass accumulates (0: none); LAB: labels are
 // read (false: every point has label 0, the first level); SP: the previous
@@ -288,7 +291,7 @@ __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X
     constexpr int NW = kBlock / 64;
     constexpr int NGa = NG > 0 ? NG : 1;
     static_assert(NW == 4 && (NG == 0 || NG == 1 || NG == 2 || NG == 4), "wave/slot mapping");
-    __shared__ T s_val[NG > 0 ? TP * D : 1];
+    __shared__ T s_val[(NG > kDirectMax) ? TP * D : 1];
     __shared__ int s_wcnt[NW][NGa];
     __shared__ int s_slot[SP ? kTabLds : 1], s_ax[SP ? kTabLds : 1], s_nl[SP ? kTabLds : 1];
     __shared__ double s_bd[SP ? kTabLds : 1];
@@ -308,6 +311,16 @@ __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X
     DD s[D], q2[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) s[j] = q2[j] = DD{0.0, 0.0};
+    constexpr bool kDirect = NG >= 1 && NG <= kDirectMax;
+    constexpr int ND = kDirect ? NG : 1;
+    double dc[ND];
+    DD ds[ND][D], dq[ND][D];
+#pragma unroll
+    for (int g = 0; g < ND; ++g) {
+        dc[g] = 0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) ds[g][j] = dq[g][j] = DD{0.0, 0.0};
+    }
     double lo[D], hi[D], bad = 0;
 #pragma unroll
     for (int j = 0; j < D; ++j) {
@@ -373,7 +386,28 @@ __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X
                 }
             }
         }
-        if constexpr (NG > 0) {
+        if constexpr (NG >= 1 && NG <= kDirectMax) {
+            // few labels: every lane sums its own points into one accumulator
+            // per label (adding 0.0 to the others' is exact), no regroup
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                    for (int g = 0; g < NG; ++g) {
+                        const bool on = slot[k][q] == g;
+                        if (NG == 1 && !on) continue;
+                        dc[g] += on ? 1.0 : 0.0;
+#pragma unroll
+                        for (int j = 0; j < D; ++j) {
+                            const T x = on ? v[k][q][j] : T(0);
+                            const T xx = x * x;   // squared in the input precision (numpy)
+                            dd_acc(ds[g][j], (double)x);
+                            dd_acc(dq[g][j], (double)xx);
+                        }
+                    }
+                }
+        } else if constexpr (NG > 0) {
             // counting sort of the tile by slot: wave tallies, then positions
             int wc[NGa];
 #pragma unroll
@@ -438,6 +472,41 @@ __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X
     constexpr int WM = NG * G;
     constexpr int WB = BB ? 2 * D + 1 : 0;
     constexpr int W = WM + WB;
+    if constexpr (kDirect) {
+        // every wave holds all NG slots: fold them into the regroup layout
+        // (slot g in wave g's row) through LDS, waves in order
+        __shared__ double sd[NW][NG][G];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const double x = wave_sum(dc[g]);
+            if (lane == 0) sd[w][g][0] = x;
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const DD a = wave_dd(ds[g][j]);
+                const DD b = wave_dd(dq[g][j]);
+                if (lane == 0) {
+                    sd[w][g][1 + 2 * j] = a.hi;
+                    sd[w][g][2 + 2 * j] = a.lo;
+                    sd[w][g][1 + 2 * D + 2 * j] = b.hi;
+                    sd[w][g][2 + 2 * D + 2 * j] = b.lo;
+                }
+            }
+        }
+        __syncthreads();
+        if (w < NG) {   // wave g carries slot g (the others stay empty)
+            const int g = w;
+            if (lane == 0) {
+                for (int u = 0; u < NW; ++u) {
+                    cnt += sd[u][g][0];
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        s[j] = dd_add(s[j], DD{sd[u][g][1 + 2 * j], sd[u][g][2 + 2 * j]});
+                        q2[j] = dd_add(q2[j], DD{sd[u][g][1 + 2 * D + 2 * j], sd[u][g][2 + 2 * D + 2 * j]});
+                    }
+                }
+            }
+        }
+    }
     __shared__ double sm[NW][G + WB];
     if constexpr (NG > 0) {
         const double x = wave_sum(cnt);
@@ -639,6 +708,70 @@ __global__ __launch_bounds__(kBlock) void counts4_kernel(
         for (int q = 0; q < rep; ++q) v += lcnt[q * n_sel * 8 + k];
         if (v) atomicAdd(&out[k], (unsigned long long)v);
     }
+}
+
+// n_sel <= 4 (NS slots): per-lane register counters instead of LDS atomics
+// (a wave's lanes mostly hit the same few bins, so shared counters
+// serialise): c[s][i] = #points of slot s with v[axis] < bound i, c[s][7] =
+// #points of slot s; one wave reduction and one LDS atomic per counter and
+// wave at the end.  Labels < kTabLds.
+template <typename T, int D, int NS>
+__global__ __launch_bounds__(kBlock) void counts_reg_kernel(
+    const T* __restrict__ X, uint64_t n, const int32_t* __restrict__ labels,
+    const int32_t* __restrict__ slot_of, int n_label_tab, const int32_t* __restrict__ axis,
+    const double* __restrict__ bounds, int n_sel, unsigned long long* __restrict__ out) {
+    __shared__ int s_slot[kTabLds];
+    __shared__ unsigned int s_cnt[NS * 8];
+    for (int k = threadIdx.x; k < n_label_tab; k += kBlock) s_slot[k] = slot_of[k];
+    for (int k = threadIdx.x; k < NS * 8; k += kBlock) s_cnt[k] = 0;
+    int ax[NS];
+    double b[NS][7];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        ax[q] = q < n_sel ? axis[q] : 0;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) b[q][i] = q < n_sel ? bounds[q * 7 + i] : 0.0;
+    }
+    __syncthreads();
+    uint32_t c[NS][8];
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c[q][i] = 0;
+    const uint64_t nch = (n + 3) / 4;
+    for (uint64_t ch = (uint64_t)blockIdx.x * kBlock + threadIdx.x; ch < nch;
+         ch += (uint64_t)gridDim.x * kBlock) {
+        T v[4][D];
+        const int m = load_chunk<T, D, true>(X, n, ch, v);
+        int lab[4];
+        load_labels4<true>(labels, ch, m, lab);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const int L = lab[p];
+            const int sl = (p < m && L >= 0 && L < n_label_tab) ? s_slot[L] : -1;
+#pragma unroll
+            for (int q = 0; q < NS; ++q) {
+                if (sl != q) continue;
+                const double x = (double)pick_axis<T, D>(v[p], ax[q]);
+                ++c[q][7];
+#pragma unroll
+                for (int i = 0; i < 7; ++i) c[q][i] += x < b[q][i] ? 1u : 0u;
+            }
+        }
+    }
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            uint32_t t = c[q][i];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) t += (uint32_t)__shfl_xor((int)t, o, 64);
+            if (lane == 0 && t) atomicAdd(&s_cnt[q * 8 + i], t);
+        }
+    __syncthreads();
+    for (int k = threadIdx.x; k < n_sel * 8 && k < NS * 8; k += kBlock)
+        if (s_cnt[k]) atomicAdd(&out[k], (unsigned long long)s_cnt[k]);
 }
 
 // ---------------------------------------------------------------- split
@@ -1074,7 +1207,29 @@ void kd_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32
     if ((size_t)n_sel * 8 * sizeof(unsigned int) > 60 * 1024)
         throw Error(-5, "too many splits in one KD level (> 1920)");
     const unsigned nb = grid_for(n, 2048);
-    if (vec_ok(d, X, labels) && tabs_ok(n_sel, sel)) {
+    if (n_sel <= 4 && vec_ok(d, X, labels) && tabs_ok(n_sel, sel)) {
+        // direct less-than counts in registers
+        dispatch_t(dtype, [&](auto tp) {
+            using T = std::remove_pointer_t<decltype(tp)>;
+            dispatch_d(d, [&](auto Dc) {
+                constexpr int D = decltype(Dc)::value;
+                const unsigned nb4 = grid_for((n + 3) / 4, 2048);
+                auto go = [&](auto NSc) {
+                    constexpr int NS = decltype(NSc)::value;
+                    hipLaunchKernelGGL((counts_reg_kernel<T, D, NS>), dim3(nb4), dim3(kBlock), 0, s,
+                                       (const T*)X, (uint64_t)n, labels, t.slot_of, t.ntab, t.axis,
+                                       t.dbl, n_sel, dcnt);
+                };
+                if (n_sel == 1)
+                    go(std::integral_constant<int, 1>{});
+                else if (n_sel == 2)
+                    go(std::integral_constant<int, 2>{});
+                else
+                    go(std::integral_constant<int, 4>{});
+            });
+        });
+        mono = false;   // the counters are already n_less / n_total
+    } else if (vec_ok(d, X, labels) && tabs_ok(n_sel, sel)) {
         dispatch_t(dtype, [&](auto tp) {
             using T = std::remove_pointer_t<decltype(tp)>;
             dispatch_d(d, [&](auto Dc) {

@@ -60,7 +60,8 @@ constexpr float kPadNorm = 1.0e30f;       // norm of padding rows: never a neigh
 inline unsigned nblocks(uint64_t n, unsigned per = kBlock) {
     return n ? (unsigned)((n + per - 1) / per) : 1u;
 }
-inline uint32_t pad_rows(uint32_t m) { return (m + kTile - 1) / kTile * kTile; }
+// rows padded to a whole wave's query block (4 x 32 with kCountQT = 4)
+inline uint32_t pad_rows(uint32_t m) { return (m + 2 * kTile - 1) / (2 * kTile) * (2 * kTile); }
 
 // A point set in MFMA fragment layout.
 struct FragSet {
@@ -173,7 +174,9 @@ struct TileArgs {
 };
 
 constexpr int kMaxBand = 256;   // bands (host keeps nband <= this)
-constexpr int kMaxSeg = 1024;   // sub-band segments a block keeps (else one per band)
+constexpr int kMaxSeg = 1024;
+constexpr bool kSubWindow = false;  // count pass: one p3 window per sub-band (measured 109 vs
+                                     // 74 ms on C3: 0.35 vs 0.22 of the tiles)   // sub-band segments a block keeps (else one per band)
 
 // First index in the ascending p[lo, hi) with p[k] >= v (upper: > v).
 __device__ __forceinline__ uint32_t p_bound(const double* __restrict__ p, uint32_t lo, uint32_t hi,
@@ -220,6 +223,8 @@ __device__ __forceinline__ void tile_hit(const TileArgs<T>& A, uint32_t i, uint3
 // block halve the streamed bytes per MFMA but measured slower on C3: 125 vs
 // 110 ms — an 8-wave barrier per tile, one block per CU.)
 constexpr int tile_threads(int) { return 256; }
+constexpr int kCountQT = 2;   // query tiles (of 32) per wave in the count pass (4: one
+                              // wave per SIMD, measured 125 vs 74 ms on C3)
 
 template <int KS>
 struct TileLds {
@@ -228,9 +233,13 @@ struct TileLds {
     float nta[2][kTile];       // -ta_j = -(1+c)|x_j|^2 / 2
 };
 
-template <typename T, int MODE, int KS>
-__global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_eu(KS >= 8 ? 1 : 2))) void tile_kernel(TileArgs<T> A) {
+// QT: 32-query groups per wave (B operand tiles held in registers).  QT = 4
+// doubles the MFMA work per streamed byte (each staged tile feeds 2 x 4 x 3 x
+// KS MFMAs per wave) at one wave per SIMD.
+template <typename T, int MODE, int KS, int QT>
+__global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_eu((KS >= 8 || QT > 2) ? 1 : 2))) void tile_kernel(TileArgs<T> A) {
     constexpr int TB = tile_threads(KS);
+    constexpr int QW = 32 * QT;                  // query rows per wave
     constexpr int NC = 2 * 2 * KS * 64;          // 16-byte chunks per tile (hi + lo)
     constexpr int NCH = (NC + TB - 1) / TB;      // per thread
     __shared__ TileLds<KS> S;
@@ -243,25 +252,25 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
     // C3; handing bands out centre-first measured 91 ms).
     uint32_t lblk;
     if (A.p3) {
-        const uint32_t bpb = A.band / ((TB / 64) * kTile);   // blocks per band
+        const uint32_t bpb = A.band / ((TB / 64) * QW);   // blocks per band
         const uint32_t x = blockIdx.x % 8u, k = blockIdx.x / 8u;
         lblk = (x + 8u * (k / bpb)) * bpb + k % bpb;
     } else {
         lblk = xcd_block(blockIdx.x, gridDim.x);
     }
-    const uint32_t blk_i0 = lblk * (TB / 64) * kTile;
+    const uint32_t blk_i0 = lblk * (TB / 64) * QW;
     if (blk_i0 >= A.I.m) return;   // spare block of the pruned grid (whole block, no barrier yet)
-    const uint32_t i0 = blk_i0 + wave * kTile;
+    const uint32_t i0 = blk_i0 + wave * QW;
     const bool wave_ok = i0 < A.I.m;
     const int col = lane & 31, h = lane >> 5;
     const float nJmax = *A.J.nmax;
-    // the wave's 64 query points: B operand fragments, kept in registers
-    bf16x8 bh[2][KS], bl[2][KS];
-    uint32_t iq[2];
-    float ai[2], bi[2];
-    bool ok[2];
+    // the wave's 32 QT query points: B operand fragments, kept in registers
+    bf16x8 bh[QT][KS], bl[QT][KS];
+    uint32_t iq[QT];
+    float ai[QT], bi[QT];
+    bool ok[QT];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < QT; ++t) {
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const uint64_t o = ((uint64_t)((wave_ok ? i0 : 0) / 32 + t) * KS + s) * 64 + lane;
@@ -274,7 +283,12 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
         ai[t] = ((1.0f + kBandC) * nI - A.elo) * 0.5f;
         bi[t] = ((1.0f - kBandC) * nI - A.ehi) * 0.5f - kBandC * 1.001f * nJmax;
     }
-    uint32_t cnt[2] = {0u, 0u}, best[2] = {kNone, kNone};
+    uint32_t cnt[QT], best[QT];
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+        cnt[t] = 0u;
+        best[t] = kNone;
+    }
 
     // streamed segments [seg_lo, seg_hi) of J rows (tile-aligned starts):
     // all of J, from the diagonal (link), or one per band in the window
@@ -285,11 +299,17 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
     if (A.p3 && blk_i0 < A.I.m) {
         const uint32_t b = blk_i0 / A.band;                 // a block lies in one band
         const uint32_t k = (blk_i0 - b * A.band) / A.sub;   // ... and one sub-band
-        const uint32_t last = min(blk_i0 + (uint32_t)(TB / 64) * kTile, A.I.m) - 1u;
+        const uint32_t last = min(blk_i0 + (uint32_t)(TB / 64) * QW, A.I.m) - 1u;
         const double lo1 = A.bp1[2 * b] - A.win, hi1 = A.bp1[2 * b + 1] + A.win;
         const uint64_t kb = (uint64_t)b * A.nsub + k;
         const double lo2 = A.bp2[2 * kb] - A.win, hi2 = A.bp2[2 * kb + 1] + A.win;
-        const double lo3 = A.p3[blk_i0] - A.win, hi3 = A.p3[last] + A.win;
+        // the sub-band's p3 range (not only this block's rows): the blocks of
+        // a sub-band then stream the same tiles in the same order, so the ones
+        // resident together on an XCD share them in its L2
+        const uint32_t sb0 = b * A.band + k * A.sub;
+        const uint32_t sb1 = min(sb0 + A.sub, min(b * A.band + A.band, A.I.m)) - 1u;
+        const double lo3 = (kSubWindow ? A.p3[sb0] : A.p3[blk_i0]) - A.win;
+        const double hi3 = (kSubWindow ? A.p3[sb1] : A.p3[last]) + A.win;
         // bands are p1-ordered, sub-bands p2-ordered: both ends of their
         // ranges ascend
         uint32_t blo, bhi;
@@ -435,7 +455,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
         const bool far = more && seek(sf, jf);
         if (far) fetch(spare, jf);
         // link: only j > i; tiles wholly below this wave's diagonal are skipped
-        const bool compute = wave_ok && !(MODE == kLink && j0 + kTile <= i0);
+        const bool compute = wave_ok && !(MODE == kLink && j0 + kTile <= i0);   // i0: first query
         if (compute) {
             ++ntiles;
             // C operand: -ta of the tile's rows, element 4q + e = row 32u + 8q + 4h + e
@@ -451,7 +471,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
                     nt[u][4 * q + 2] = v.z;
                     nt[u][4 * q + 3] = v.w;
                 }
-            f32x16 acc[2][2];
+            f32x16 acc[2][QT];
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 bf16x8 ah[2], al[2];
@@ -463,7 +483,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
 #pragma unroll
-                    for (int t = 0; t < 2; ++t) {
+                    for (int t = 0; t < QT; ++t) {
                         acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
                             ah[u], bh[t][s], s == 0 ? nt[u] : acc[u][t], 0, 0, 0);
                         acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bl[t][s],
@@ -473,34 +493,42 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
                     }
             }
             // element e of block q of m-tile u: row j = j0 + 32u + 8q + 4h + e
-            uint64_t band[2] = {0ull, 0ull};
+            uint64_t band[QT];
+#pragma unroll
+            for (int t = 0; t < QT; ++t) band[t] = 0ull;
             bool walk = true;
             if constexpr (MODE == kCount) {
-                uint32_t ci[2] = {0u, 0u}, cm[2] = {0u, 0u};
+                uint32_t ci[QT], cm[QT];
+#pragma unroll
+                for (int t = 0; t < QT; ++t) ci[t] = cm[t] = 0u;
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
 #pragma unroll
                     for (int u = 0; u < 2; ++u)
 #pragma unroll
-                        for (int t = 0; t < 2; ++t) {
+                        for (int t = 0; t < QT; ++t) {
                             ci[t] += acc[u][t][r] >= ai[t] ? 1u : 0u;
                             cm[t] += acc[u][t][r] >= bi[t] ? 1u : 0u;
                         }
-                cnt[0] += ci[0];
-                cnt[1] += ci[1];
-                walk = __any((ci[0] != cm[0]) || (ci[1] != cm[1]));
+                bool differ = false;
+#pragma unroll
+                for (int t = 0; t < QT; ++t) {
+                    cnt[t] += ci[t];
+                    differ |= ci[t] != cm[t];
+                }
+                walk = __any(differ);
                 if (walk) {
                     // fresh compares (keeps the masks above from living across)
 #pragma unroll
                     for (int u = 0; u < 2; ++u)
 #pragma unroll
-                        for (int t = 0; t < 2; ++t) asm volatile("" : "+v"(acc[u][t]));
+                        for (int t = 0; t < QT; ++t) asm volatile("" : "+v"(acc[u][t]));
 #pragma unroll
                     for (int r = 0; r < 16; ++r)
 #pragma unroll
                         for (int u = 0; u < 2; ++u)
 #pragma unroll
-                            for (int t = 0; t < 2; ++t) {
+                            for (int t = 0; t < QT; ++t) {
                                 const float v = acc[u][t][r];
                                 const bool b = v >= bi[t] && !(v >= ai[t]);
                                 band[t] |= b ? (1ull << (16 * u + r)) : 0ull;
@@ -512,7 +540,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
 #pragma unroll
                     for (int u = 0; u < 2; ++u)
 #pragma unroll
-                        for (int t = 0; t < 2; ++t) {
+                        for (int t = 0; t < QT; ++t) {
                             const float v = acc[u][t][r];
                             const int bit = 16 * u + r;
                             band[t] |= v >= bi[t] ? (1ull << bit) : 0ull;   // hits + band
@@ -521,7 +549,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
             }
             // hits (link / border) and band pairs (all modes), lane-divergent
 #pragma unroll
-            for (int t = 0; t < 2 && walk; ++t) {
+            for (int t = 0; t < QT && walk; ++t) {
                 uint32_t m = (uint32_t)band[t];
                 while (m) {
                     const int bit = __builtin_ctz(m);
@@ -558,7 +586,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
     if (A.tiles && lane == 0 && ntiles) atomicAdd(A.tiles, (unsigned long long)ntiles);
     // lanes l and l + 32 hold the same query column
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < QT; ++t) {
         if constexpr (MODE == kCount) {
             cnt[t] += (uint32_t)__shfl_xor((int)cnt[t], 32, 64);
             if (h == 0 && ok[t]) A.cnt[iq[t]] = cnt[t];
@@ -785,13 +813,16 @@ template <typename T, int MODE>
 void run_tiles(const TileArgs<T>& A, const Geometry& G, int metric, hipStream_t s) {
     if (A.I.m == 0 || A.J.m == 0) return;
     if (G.mfma) {
-        const unsigned waves = (A.I.m + kTile - 1) / kTile;
         auto launch = [&](auto ks) {
             constexpr int KS = decltype(ks)::value, TB = tile_threads(KS);
+            // the count pass (the bulk of the MFMA work) takes 4 query tiles per
+            // wave where the registers allow it
+            constexpr int QT = (MODE == kCount && KS <= 4) ? kCountQT : 2;
+            const unsigned waves = (A.I.m + 32 * QT - 1) / (32 * QT);
             // pruned count: 8 x ceil(bands / 8) x blocks per band (tile_kernel)
-            const unsigned grid = A.p3 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (TB / 64 * kTile))
+            const unsigned grid = A.p3 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (TB / 64 * 32 * QT))
                                        : nblocks(waves, TB / 64);
-            hipLaunchKernelGGL((tile_kernel<T, MODE, KS>), dim3(grid), dim3(TB), 0, s, A);
+            hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT>), dim3(grid), dim3(TB), 0, s, A);
         };
         switch (G.KS) {
             case 1: launch(std::integral_constant<int, 1>{}); break;

@@ -21,8 +21,11 @@
 // (SK:neighbors/_binary_tree.pxi.tp:1951-1955, SK:metrics/_dist_metrics.pxd.tp:
 // 39-49): fp64, per-axis difference, squared and summed in axis order with
 // every product and sum rounded separately (__dmul_rn/__dadd_rn: no FMA), then
-// `<= eps*eps`.  Inputs (fp32 or fp64) are widened exactly.  No fp32 shortcut
-// band is needed: the fp64 VALU rate is not the bound here.
+// `<= eps*eps`.  Inputs (fp32 or fp64) are widened exactly.  For fp32 inputs
+// a pair is first screened in fp32 (Pred, PD_OPT_FP32_SCREEN, default on):
+// distances outside a 2^-18 relative band around the threshold are decided
+// there, the rest by the exact fp64 predicate — the answer is identical
+// either way (the band bounds the fp32 rounding error), only cheaper.
 //
 // Labels: components of the core graph get the id of their smallest core
 // point (global index); a border point takes the smallest id among its core

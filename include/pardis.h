@@ -97,10 +97,11 @@ enum pd_option {
                                 wraps (dense cells: spreads the row-start hot spot; same
                                 counts, same labels); default 1024, 0 = never */,
     PD_OPT_CENTRE_WINDOW = 13 /* link modes 5/6: records after each record tested by the window
-                                union (16, 32 or 64; default 16); mode 3: forward candidates
-                                each core record tests in the centre-row union (0 = all).  A
-                                heuristic either way: the cell verify proves or tests every
-                                edge, so labels are the same */
+                                union (2, 4, 8, 16, 32 or 64); mode 3: forward candidates each
+                                core record tests in the centre-row union (0 = all).  Default -1:
+                                mode 6 takes 4 when cells hold <= 4 records on average, else 16
+                                (modes 3/5: 16).  A heuristic either way: the cell verify proves
+                                or tests every edge, so labels are the same */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -156,8 +156,8 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             if (value < 0 || value > 0x7FFFFFFF) throw Error(PD_EINVAL, "count rotate must be >= 0");
             ctx->c.count_rotate = (int)value;
         } else if (option == PD_OPT_CENTRE_WINDOW) {
-            if (value < 0 || value > 0x7FFFFFFF) throw Error(PD_EINVAL, "centre window must be >= 0");
-            ctx->c.centre_window = (int)value;
+            if (value > 0x7FFFFFFF) throw Error(PD_EINVAL, "centre window too large");
+            ctx->c.centre_window = value < 0 ? -1 : (int)value;   // < 0: automatic
         } else if (option == PD_OPT_XSUB) {
             if (value < 1 || value > 16) throw Error(PD_EINVAL, "xsub must be in [1, 16]");
             ctx->c.xsub = (int)value;

@@ -2576,7 +2576,19 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         if (mode != 6)
             hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
         if (mode == 6) {
-            const int cw = ctx.centre_window;
+            // auto window (PD_OPT_CENTRE_WINDOW < 0): sparse cells (a few
+            // records each, C2: 2.3) gain little from the window beyond the
+            // fused flatten, so a short one is cheapest (C2 link 6.59 -> 5.96
+            // ms at 16 -> 4); dense cells (C4 city centres) want the long one
+            // (C4 link 71.5 -> 60.6 ms at 4 -> 16)
+            int cw = ctx.centre_window;
+            if (cw < 0) {
+                uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+                PD_HIP(hipMemcpyAsync(h, dncells, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+                sync(s);
+                const uint32_t nc = *h ? *h : 1u;
+                cw = (uint64_t)R <= 4ull * nc ? 4 : 16;
+            }
             auto go = [&](auto Wc) {
                 constexpr int Wv = decltype(Wc)::value;
                 if (sst)
@@ -2586,7 +2598,13 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
                     hipLaunchKernelGGL((window_uf_kernel<T, D, M, Wv, false>), dim3(blocks(R)),
                                        dim3(kBlock), 0, s, Xs, R, eps, eps2, slo, shi, par, sst);
             };
-            if (cw <= 16)
+            if (cw <= 2)
+                go(std::integral_constant<int, 2>{});
+            else if (cw <= 4)
+                go(std::integral_constant<int, 4>{});
+            else if (cw <= 8)
+                go(std::integral_constant<int, 8>{});
+            else if (cw <= 16)
                 go(std::integral_constant<int, 16>{});
             else if (cw <= 32)
                 go(std::integral_constant<int, 32>{});
@@ -2595,9 +2613,10 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         } else if (mode == 3) {
             hipLaunchKernelGGL((centre_link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s,
                                Xs, R, C, eps, eps2, slo, shi,
-                               ctx.centre_window ? (uint32_t)ctx.centre_window : 0xFFFFFFFFu, par);
+                               ctx.centre_window < 0 ? 16u
+                               : ctx.centre_window ? (uint32_t)ctx.centre_window : 0xFFFFFFFFu, par);
         } else if (mode == 5) {
-            const int cw = ctx.centre_window;
+            const int cw = ctx.centre_window < 0 ? 16 : ctx.centre_window;
             auto go = [&](auto Wc) {
                 constexpr int Wv = decltype(Wc)::value;
                 if (sst)

@@ -92,8 +92,9 @@ struct Ctx {
                                  // 4 cell verify alone; 0 init forest + jumps + union sweep; 2 union sweep only
     int jump_rounds = 4;
     int xsub = 2;                // axis-0 sub-cells per eps
-    int centre_window = 16;     // link mode 5: records after each record tested (16/32/64);
-                                 // mode 3: forward candidates per centre-row union (0: all)
+    int centre_window = -1;      // link modes 5/6: records after each record tested (2..64);
+                                 // mode 3: forward candidates per centre-row union (0: all);
+                                 // < 0 (default): mode 6 picks 4 or 16 by cell occupancy, else 16
     int count_rotate = 1024;     // count sweep: lists longer than this start near the query (0: off)
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes

@@ -690,13 +690,16 @@ def test_c4_skew_vs_oracle(native, case):
     # rotated count starts on every long list / never; centre-row union
     # window of 1 candidate / unbounded
     ctx = native.context()
+    LM, CW = native.LINK_MODE_DEFAULT, -1
     for opts in (((native.PD_OPT_COUNT_ROTATE, 16, 1024),),
                  ((native.PD_OPT_COUNT_ROTATE, 0, 1024),),
-                 ((native.PD_OPT_CENTRE_WINDOW, 64, 16),),
-                 ((native.PD_OPT_LINK_MODE, 3, 5), (native.PD_OPT_CENTRE_WINDOW, 1, 16)),
-                 ((native.PD_OPT_LINK_MODE, 3, 5), (native.PD_OPT_CENTRE_WINDOW, 0, 16)),
-                 ((native.PD_OPT_LINK_MODE, 6, 5),),
-                 ((native.PD_OPT_LINK_MODE, 6, 5), (native.PD_OPT_CENTRE_WINDOW, 64, 16))):
+                 ((native.PD_OPT_CENTRE_WINDOW, 64, CW),),
+                 ((native.PD_OPT_CENTRE_WINDOW, 2, CW),),
+                 ((native.PD_OPT_CENTRE_WINDOW, 4, CW),),
+                 ((native.PD_OPT_LINK_MODE, 3, LM), (native.PD_OPT_CENTRE_WINDOW, 1, CW)),
+                 ((native.PD_OPT_LINK_MODE, 3, LM), (native.PD_OPT_CENTRE_WINDOW, 0, CW)),
+                 ((native.PD_OPT_LINK_MODE, 5, LM),),
+                 ((native.PD_OPT_LINK_MODE, 5, LM), (native.PD_OPT_CENTRE_WINDOW, 64, CW))):
         for opt, val, _ in opts:
             ctx.set_option(opt, val)
         try:

@@ -269,6 +269,9 @@ constexpr int kTabLds = 256;
 // kd_pass_kernel: up to this many labels are summed per lane without the
 // LDS regroup
 constexpr int kDirectMax = 1;
+// more labels: regroup each wave's points by label in its own LDS region
+// (false: one block-wide counting sort per tile, each wave summing one label)
+constexpr bool kWaveRegroup = false;   // measured slower on C2: 0.69 / 1.00 vs 0.61 / 0.82 ms
 
 // NG = labels whose moments this pass accumulates (0: none); LAB: labels are
 // read (false: every point has label 0, the first level); SP: the previous
@@ -312,7 +315,8 @@ __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X
 #pragma unroll
     for (int j = 0; j < D; ++j) s[j] = q2[j] = DD{0.0, 0.0};
     constexpr bool kDirect = NG >= 1 && NG <= kDirectMax;
-    constexpr int ND = kDirect ? NG : 1;
+    constexpr bool kWave = NG > kDirectMax && kWaveRegroup;   // wave-local regroup
+    constexpr int ND = (kDirect || kWave) ? NG : 1;
     double dc[ND];
     DD ds[ND][D], dq[ND][D];
 #pragma unroll
@@ -407,6 +411,64 @@ __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X
                         }
                     }
                 }
+        } else if constexpr (kWave) {
+            // each wave regroups its own 4·K·64 points by slot in its LDS
+            // region (ballot counting sort, no block barrier), then sums each
+            // slot's run into that slot's accumulators: one set of
+            // double-double sums per point, no cross-wave imbalance
+            constexpr int WP = 4 * K * 64;
+            T* wv = s_val + (size_t)w * WP * D;
+            int wc[NG], run[NG];
+#pragma unroll
+            for (int g = 0; g < NG; ++g) wc[g] = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int g = 0; g < NG; ++g) wc[g] += __popcll(__ballot(slot[k][q] == g));
+            int acc0 = 0;
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                run[g] = acc0;
+                acc0 += wc[g];
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int g = 0; g < NG; ++g) {
+                        const unsigned long long b = __ballot(slot[k][q] == g);
+                        if (slot[k][q] == g) {
+                            const int pos = run[g] + __popcll(b & lt);
+#pragma unroll
+                            for (int j = 0; j < D; ++j) wv[pos * D + j] = v[k][q][j];
+                        }
+                        run[g] += __popcll(b);
+                    }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            int start = 0;
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                for (int i = lane; i < wc[g]; i += 64) {
+                    const T* p = wv + (size_t)(start + i) * D;
+                    dc[g] += 1.0;
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        const T x = p[j];
+                        const T xx = x * x;   // squared in the input precision (numpy)
+                        dd_acc(ds[g][j], (double)x);
+                        dd_acc(dq[g][j], (double)xx);
+                    }
+                }
+                start += wc[g];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         } else if constexpr (NG > 0) {
             // counting sort of the tile by slot: wave tallies, then positions
             int wc[NGa];
@@ -472,7 +534,7 @@ __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X
     constexpr int WM = NG * G;
     constexpr int WB = BB ? 2 * D + 1 : 0;
     constexpr int W = WM + WB;
-    if constexpr (kDirect) {
+    if constexpr (kDirect || kWave) {
         // every wave holds all NG slots: fold them into the regroup layout
         // (slot g in wave g's row) through LDS, waves in order
         __shared__ double sd[NW][NG][G];

@@ -154,10 +154,22 @@ def cpu_baseline(cfg_name, n_sample, n_full, d):
     cmd = [sys.executable, "-m", "oracle.cpu_ref", "--config", cfg_name, "--n", str(n_sample)]
     if d <= 15:
         cmd.append("--global-jobs")
-    r = subprocess.run(cmd, cwd=HERE, capture_output=True, text=True, timeout=1800)
-    if r.returncode != 0:
-        return {"value": None, "error": (r.stderr or r.stdout)[-2000:]}
-    c = json.loads(r.stdout.strip().splitlines()[-1])
+    p = subprocess.Popen(cmd, cwd=HERE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    t0 = time.time()
+    while True:   # a heartbeat on stderr while the host cores work
+        try:
+            out, err = p.communicate(timeout=30)
+            break
+        except subprocess.TimeoutExpired:
+            if time.time() - t0 > 1800:
+                p.kill()
+                out, err = p.communicate()
+                return {"value": None, "error": "CPU baseline timed out (1800 s)"}
+            print(f"[bench] CPU baseline running ({time.time() - t0:.0f} s)", file=sys.stderr,
+                  flush=True)
+    if p.returncode != 0:
+        return {"value": None, "error": (err or out)[-2000:]}
+    c = json.loads(out.strip().splitlines()[-1])
     if cfg_name == "C4":
         desc = ("sample of the same distribution at 1% of the full size; its cities are "
                 "100x sparser, so neighbour lists are 100x shorter than at 1B: the rate is "

@@ -294,6 +294,36 @@ int32_t pd_owned_results(pd_ctx* ctx, int64_t n, const int32_t* owner, const uin
 int32_t pd_scatter_results(pd_ctx* ctx, const uint32_t* pairs, int64_t m, uint32_t gid_base,
                            int64_t n, int32_t* labels, uint8_t* core, void* stream);
 
+/* ---- Sharded dense train (d > 4): the reference runs any k through the same
+ * per-partition sklearn fit (R:dbscan/partition.py:131-133, R:dbscan/dbscan.py:
+ * 123-124, SK:cluster/_dbscan.py:410-434); here every rank holds all n points
+ * (an all-gather of the slices) and computes the distance tiles of its share
+ * of the rows: row chunks of 2048 dealt round-robin over the ranks.  Four
+ * stages with one collective between each (the caller's):
+ *   pd_dense_count  -> counts: this rank's rows' neighbour counts (self
+ *                      included), 0 elsewhere        [all-reduce SUM, u32]
+ *   pd_dense_link   <- the summed counts; -> forest: this rank's union-find
+ *                      over the core rows (*n_core)  [all-gather, n_ranks x n_core]
+ *   pd_dense_border <- the gathered forests; -> best: smallest adjacent core
+ *                      key per border candidate, INT32_MAX where none or not
+ *                      this rank's row (*n_border)   [all-reduce MIN, i32]
+ *   pd_dense_finish <- the reduced best; labels / core / counts of all n
+ *                      points, *n_clusters — equal on every rank and to
+ *                      pd_cluster's.
+ * Calls on one context must follow this order; X must stay valid until
+ * pd_dense_finish.  n < 2^31 - 1.  data_box: 2 x d tight bbox (host).
+ * Single rank (rank 0 of 1): the stages chained without collectives equal
+ * pd_cluster.  Buffers are device pointers sized n (counts, forest, best). */
+int32_t pd_dense_count(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, double eps,
+                       int32_t min_samples, int32_t metric, const double* data_box_host,
+                       int32_t rank, int32_t n_ranks, uint32_t* counts, void* stream);
+int32_t pd_dense_link(pd_ctx* ctx, const uint32_t* counts, uint32_t* forest, int64_t* n_core_host,
+                      void* stream);
+int32_t pd_dense_border(pd_ctx* ctx, const uint32_t* forests, int32_t n_forests, int32_t* best,
+                        int64_t* n_border_host, void* stream);
+int32_t pd_dense_finish(pd_ctx* ctx, const int32_t* best, int32_t* labels, uint8_t* core,
+                        uint32_t* counts, int64_t* n_clusters_host, void* stream);
+
 /* ---- RCCL collectives of the sharded train (one rank per device).  They
  * replace Spark's data movement: partitionBy shuffle (R:dbscan/dbscan.py:
  * 114-118) -> pd_comm_all_to_all_v; collect / broadcast of the cluster-id map

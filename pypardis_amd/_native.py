@@ -43,7 +43,8 @@ EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
            "pd_kd_radix_hist", "pd_kd_pass", "pd_owned_results", "pd_scatter_results",
            "pd_comm_unique_id", "pd_comm_init", "pd_comm_init_all", "pd_comm_destroy",
            "pd_comm_all_reduce", "pd_comm_all_gather_v", "pd_comm_all_to_all_v",
-           "pd_comm_broadcast"]
+           "pd_comm_broadcast", "pd_dense_count", "pd_dense_link", "pd_dense_border",
+           "pd_dense_finish"]
 
 
 class PardisError(RuntimeError):
@@ -110,6 +111,10 @@ def load():
             "pd_comm_all_gather_v": ([P, P, P, P, I32, P], I32),
             "pd_comm_all_to_all_v": ([P, P, P, P, P, I32, P], I32),
             "pd_comm_broadcast": ([P, P, I64, I32, I32, P], I32),
+            "pd_dense_count": ([P, P, I32, I64, I32, D, I32, I32, P, I32, I32, P, P], I32),
+            "pd_dense_link": ([P, P, P, P, P], I32),
+            "pd_dense_border": ([P, P, I32, P, P, P], I32),
+            "pd_dense_finish": ([P, P, P, P, P, P, P], I32),
         }
         for name, (args, res) in sig.items():
             f = getattr(lib, name)
@@ -547,6 +552,62 @@ def scatter_results(pairs, gid_base, n, device, ctx=None):
 
 # ------------------------------------------------------------------ RCCL
 PD_COMM_ID_BYTES = 128
+# ------------------------------------------------ sharded dense train (d > 4)
+def dense_count(X, eps, min_samples, metric, data_box, rank, world, ctx=None):
+    """Stage 1 (pd_dense_count): int32[n] counts of this rank's rows, 0 elsewhere.
+    X (all n points) must stay alive until dense_finish."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    dbox = np.ascontiguousarray(data_box, np.float64).reshape(2 * d)
+    counts = torch.empty(max(n, 1), dtype=torch.int32, device=X.device)
+    _check(load().pd_dense_count(ctx.ptr, X.data_ptr() if n else None, dt, n, d, float(eps),
+                                 int(min_samples), int(metric), dbox.ctypes.data, int(rank),
+                                 int(world), counts.data_ptr(), _stream(X.device)))
+    return counts[:n]
+
+
+def dense_link(counts, ctx=None):
+    """Stage 2 (pd_dense_link): this rank's forest over the core rows, int32[n_core]."""
+    device = counts.device
+    ctx = ctx or context(device.index)
+    n = counts.shape[0]
+    forest = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    mc = np.zeros(1, np.int64)
+    _check(load().pd_dense_link(ctx.ptr, counts.contiguous().data_ptr() if n else None,
+                                forest.data_ptr(), mc.ctypes.data, _stream(device)))
+    return forest[:int(mc[0])]
+
+
+def dense_border(forests, n_forests, n, ctx=None):
+    """Stage 3 (pd_dense_border): int32[n_border] smallest adjacent core key per
+    border candidate (INT32_MAX: none, or not this rank's row)."""
+    device = forests.device
+    ctx = ctx or context(device.index)
+    best = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    mb = np.zeros(1, np.int64)
+    f = forests.contiguous()
+    _check(load().pd_dense_border(ctx.ptr, f.data_ptr() if f.numel() else None, int(n_forests),
+                                  best.data_ptr(), mb.ctypes.data, _stream(device)))
+    return best[:int(mb[0])]
+
+
+def dense_finish(best, n, device, want_counts=False, ctx=None):
+    """Stage 4 (pd_dense_finish): (labels int32[n], core uint8[n], counts or
+    None, n_clusters) over all points."""
+    ctx = ctx or context(device)
+    labels = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    core = torch.empty(max(n, 1), dtype=torch.uint8, device=device)
+    counts = torch.empty(max(n, 1), dtype=torch.int32, device=device) if want_counts else None
+    ncl = np.zeros(1, np.int64)
+    b = best.contiguous()
+    _check(load().pd_dense_finish(ctx.ptr, b.data_ptr() if b.numel() else None,
+                                  labels.data_ptr(), core.data_ptr(),
+                                  counts.data_ptr() if counts is not None else None,
+                                  ncl.ctypes.data, _stream(device)))
+    return labels[:n], core[:n], (counts[:n] if counts is not None else None), int(ncl[0])
+
+
 PD_R_SUM, PD_R_MAX, PD_R_MIN = 0, 1, 2
 _ELEM = {torch.uint8: 0, torch.bool: 0, torch.int32: 1, torch.int64: 3, torch.float32: 5,
          torch.float64: 6}

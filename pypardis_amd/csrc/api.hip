@@ -519,6 +519,61 @@ int32_t pd_scatter_results(pd_ctx* ctx, const uint32_t* pairs, int64_t m, uint32
     });
 }
 
+// ---------------------------------------------------------------- sharded dense train
+
+int32_t pd_dense_count(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, double eps,
+                       int32_t min_samples, int32_t metric, const double* data_box, int32_t rank,
+                       int32_t n_ranks, uint32_t* counts, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (d <= kMaxDim) throw Error(PD_EINVAL, "pd_dense_* is the d > 4 path (pd_train for d <= 4)");
+        if (!data_box) throw Error(PD_EINVAL, "null data_box");
+        if (n > 0 && !counts) throw Error(PD_EINVAL, "null counts");
+        if (n_ranks < 1 || rank < 0 || rank >= n_ranks) throw Error(PD_EINVAL, "bad rank / n_ranks");
+        TrainArgs a;
+        a.X = X;
+        a.dtype = dtype;
+        a.n = n;
+        a.d = d;
+        a.eps = eps;
+        a.min_samples = min_samples;
+        a.metric = metric;
+        a.data_box = data_box;
+        a.stream = (hipStream_t)stream;
+        dense_count(ctx->c, a, rank, n_ranks, counts);
+    });
+}
+
+int32_t pd_dense_link(pd_ctx* ctx, const uint32_t* counts, uint32_t* forest, int64_t* n_core,
+                      void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || !n_core) throw Error(PD_EINVAL, "null argument");
+        if (ctx->c.dn.n && (!counts || !forest)) throw Error(PD_EINVAL, "null buffer");
+        *n_core = dense_link(ctx->c, counts, forest, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_dense_border(pd_ctx* ctx, const uint32_t* forests, int32_t n_forests, int32_t* best,
+                        int64_t* n_border, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || !n_border || n_forests < 0) throw Error(PD_EINVAL, "bad argument");
+        if (ctx->c.dn.n && !best) throw Error(PD_EINVAL, "null best");
+        if (n_forests && ctx->c.dn.n_core && !forests) throw Error(PD_EINVAL, "null forests");
+        *n_border = dense_border(ctx->c, forests, n_forests, best, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_dense_finish(pd_ctx* ctx, const int32_t* best, int32_t* labels, uint8_t* core,
+                        uint32_t* counts, int64_t* n_clusters, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx) throw Error(PD_EINVAL, "null context");
+        if (ctx->c.dn.n && !labels) throw Error(PD_EINVAL, "null labels");
+        if (ctx->c.dn.n_border && !best) throw Error(PD_EINVAL, "null best");
+        const int64_t ncl = dense_finish(ctx->c, best, labels, core, counts, (hipStream_t)stream);
+        if (n_clusters) *n_clusters = ncl;
+    });
+}
+
 // ---------------------------------------------------------------- RCCL
 
 int32_t pd_comm_unique_id(uint8_t* id) {

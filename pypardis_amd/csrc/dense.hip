@@ -171,7 +171,19 @@ struct TileArgs {
     uint32_t whole_bands;       // 1: one run per band (the overflow path), for tests
     double win;
     unsigned long long* tiles;  // wave tiles computed (null: not counted)
+    // sharded train: this device computes the I rows of the chunks
+    // (kShardChunk rows each) c with c % shard_world == shard_rank
+    uint32_t shard_rank, shard_world;
 };
+
+// Rows per shard chunk: a multiple of every block's query rows (256) and of
+// the pruned count's sub-band (2048), so a block lies in one chunk and the
+// chunks dealt round-robin give every rank a slice of every band (balanced
+// windows, and one sub-band per band per XCD at 8 ranks).
+constexpr uint32_t kShardChunk = 2048;
+__device__ __forceinline__ bool not_my_rows(uint32_t row0, uint32_t rank, uint32_t world) {
+    return world > 1 && (row0 / kShardChunk) % world != rank;
+}
 
 constexpr int kMaxBand = 256;   // bands (host keeps nband <= this)
 constexpr int kMaxSeg = 1024;
@@ -259,7 +271,9 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
         lblk = xcd_block(blockIdx.x, gridDim.x);
     }
     const uint32_t blk_i0 = lblk * (TB / 64) * QW;
-    if (blk_i0 >= A.I.m) return;   // spare block of the pruned grid (whole block, no barrier yet)
+    // spare block of the pruned grid, or another rank's rows (whole block, no
+    // barrier yet)
+    if (blk_i0 >= A.I.m || not_my_rows(blk_i0, A.shard_rank, A.shard_world)) return;
     const uint32_t i0 = blk_i0 + wave * QW;
     const bool wave_ok = i0 < A.I.m;
     const int col = lane & 31, h = lane >> 5;
@@ -602,6 +616,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
 // scale): one lane per query, the streamed point broadcast to the wave.
 template <typename T, int MODE, int M>
 __global__ __launch_bounds__(kBlock) void brute_kernel(TileArgs<T> A) {
+    if (not_my_rows(blockIdx.x * kBlock, A.shard_rank, A.shard_world)) return;
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     const bool ok = i < A.I.m;
     const uint32_t p = ok ? (A.I.idx ? A.I.idx[i] : i) : 0u;
@@ -643,6 +658,30 @@ __global__ __launch_bounds__(kBlock) void scatter_best_kernel(const uint32_t* __
                                                               uint32_t* __restrict__ key_out) {
     const uint32_t b = blockIdx.x * kBlock + threadIdx.x;
     if (b < m) key_out[list[b]] = best[b];
+}
+
+// Sharded link: the union of every rank's forest over the core rows (each
+// forest's edges i -> parent[i] carry its rank's connectivity).
+__global__ __launch_bounds__(kBlock) void merge_forests_kernel(uint32_t* __restrict__ par,
+                                                               const uint32_t* __restrict__ f,
+                                                               uint32_t m, uint64_t total) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= total) return;
+    const uint32_t i = (uint32_t)(t % m), p = f[t];
+    if (p != i && p < m) uf_unite(par, i, p);
+}
+
+// Border keys in the exchange format (int32, none = INT32_MAX: a MIN
+// all-reduce over the ranks picks the smallest adjacent key) and back.
+__global__ __launch_bounds__(kBlock) void best_to_i32_kernel(const uint32_t* __restrict__ b,
+                                                             uint32_t m, int32_t* __restrict__ o) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k < m) o[k] = b[k] == kNone ? INT32_MAX : (int32_t)b[k];
+}
+__global__ __launch_bounds__(kBlock) void best_from_i32_kernel(const int32_t* __restrict__ o,
+                                                               uint32_t m, uint32_t* __restrict__ b) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    if (k < m) b[k] = o[k] == INT32_MAX ? kNone : (uint32_t)o[k];
 }
 
 __global__ __launch_bounds__(kBlock) void outputs_kernel(const uint32_t* __restrict__ cnt,
@@ -857,19 +896,53 @@ struct Ev {
     }
 };
 
+Geometry geometry_of(const DenseState& ds) {
+    Geometry G;
+    G.KS = ds.KS;
+    G.center = ds.center;
+    G.scale = ds.scale;
+    G.elo = ds.elo;
+    G.ehi = ds.ehi;
+    G.mfma = ds.mfma;
+    return G;
+}
+
 template <typename T>
-void run_dense(Ctx& ctx, TrainArgs& a) {
+TileArgs<T> base_args(const DenseState& ds) {
+    TileArgs<T> A{};
+    A.X = (const T*)ds.X;
+    A.d = ds.d;
+    A.eps = ds.eps;
+    A.eps2 = ds.eps * ds.eps;
+    A.elo = ds.elo;
+    A.ehi = ds.ehi;
+    A.shard_rank = (uint32_t)ds.rank;
+    A.shard_world = (uint32_t)ds.world;
+    return A;
+}
+
+// Stage 1: neighbour counts (all x all tiles; this rank's rows when world >
+// 1, every other row's count left 0 so the ranks' arrays sum to the whole).
+template <typename T>
+void count_stage(Ctx& ctx, TrainArgs& a, int rank, int world) {
     hipStream_t s = a.stream;
+    DenseState& ds = ctx.dn;
+    ds = DenseState{};
     const T* X = (const T*)a.X;
     const uint32_t n = (uint32_t)a.n;
     const int d = a.d;
-    const uint32_t ms = (uint32_t)a.min_samples;
-    Ev ev(ctx, s);
-    ev.mark();   // 0
+    ds.X = a.X;
+    ds.dtype = a.dtype;
+    ds.d = d;
+    ds.metric = a.metric;
+    ds.n = n;
+    ds.min_samples = (uint32_t)a.min_samples;
+    ds.eps = a.eps;
+    ds.rank = rank;
+    ds.world = world;
 
     // geometry: centre on the bbox midpoint, scale by a power of two
-    Geometry G;
-    G.KS = d <= 16 ? 1 : d <= 32 ? 2 : d <= 64 ? 4 : 8;
+    ds.KS = d <= 16 ? 1 : d <= 32 ? 2 : d <= 64 ? 4 : 8;
     std::vector<double> hc(d);
     double span = 0.0;
     for (int k = 0; k < d; ++k) {
@@ -879,27 +952,20 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
     }
     int e2 = 0;
     if (span > 0.0) std::frexp(span, &e2);
-    G.scale = std::ldexp(1.0, -e2);   // max |scaled coordinate| in [0.5, 1]
-    const double eps2 = a.eps * a.eps;
-    const double eps2s = eps2 * G.scale * G.scale;
-    G.mfma = a.metric == 0 && d <= 128 && std::isfinite(eps2s) && eps2s > 1e-30 && eps2s < 1e30;
-    if (G.mfma) {
-        G.elo = std::nextafter((float)(eps2s * (1.0 - 1.0 / 1048576.0)), 0.0f);
-        G.ehi = std::nextafter((float)(eps2s * (1.0 + 1.0 / 1048576.0)), INFINITY);
-        G.center = ctx.arena.get<double>("dn_center", d);
+    ds.scale = std::ldexp(1.0, -e2);   // max |scaled coordinate| in [0.5, 1]
+    const double eps2s = a.eps * a.eps * ds.scale * ds.scale;
+    ds.mfma = a.metric == 0 && d <= 128 && std::isfinite(eps2s) && eps2s > 1e-30 && eps2s < 1e30;
+    if (ds.mfma) {
+        ds.elo = std::nextafter((float)(eps2s * (1.0 - 1.0 / 1048576.0)), 0.0f);
+        ds.ehi = std::nextafter((float)(eps2s * (1.0 + 1.0 / 1048576.0)), INFINITY);
+        ds.center = ctx.arena.get<double>("dn_center", d);
         double* h = (double*)pinned(ctx, sizeof(double) * d);
         std::memcpy(h, hc.data(), sizeof(double) * d);
-        PD_HIP(hipMemcpyAsync(G.center, h, sizeof(double) * d, hipMemcpyHostToDevice, s));
+        PD_HIP(hipMemcpyAsync(ds.center, h, sizeof(double) * d, hipMemcpyHostToDevice, s));
     }
-    TileArgs<T> A{};
-    A.X = X;
-    A.d = d;
-    A.eps = a.eps;
-    A.eps2 = eps2;
-    A.elo = G.elo;
-    A.ehi = G.ehi;
+    const Geometry G = geometry_of(ds);
+    TileArgs<T> A = base_args<T>(ds);
 
-    // ---- neighbour counts (all x all)
     uint32_t* cnt = ctx.arena.get<uint32_t>("dn_cnt", n);
     unsigned long long* dtiles = nullptr;
     if (G.mfma && ctx.dense_prune) {
@@ -991,6 +1057,7 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
         PD_HIP(hipGetLastError());
         const FragSet Fs = make_frags<T>(ctx, "dn_all", X, d, sid, n, G, s);
         uint32_t* cs = ctx.arena.get<uint32_t>("dn_cnt_sorted", n);
+        if (world > 1) PD_HIP(hipMemsetAsync(cs, 0, sizeof(uint32_t) * n, s));
         dtiles = ctx.arena.get<unsigned long long>("dn_tiles", 1);
         PD_HIP(hipMemsetAsync(dtiles, 0, sizeof(unsigned long long), s));
         A.I = A.J = Fs;
@@ -1009,67 +1076,124 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
         hipLaunchKernelGGL(scatter_cnt_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, cs, sid, n,
                            cnt);
         PD_HIP(hipGetLastError());
-        A.p3 = nullptr;
-        A.tiles = nullptr;
     } else {
         const FragSet Fall = make_frags<T>(ctx, "dn_all", X, d, nullptr, n, G, s);
+        if (world > 1) PD_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * n, s));
         A.I = A.J = Fall;
         A.cnt = cnt;
         run_tiles<T, kCount>(A, G, a.metric, s);
     }
-    A.cnt = cnt;
-    ev.mark();   // 1
+    ds.cnt = cnt;
+    ds.tiles = dtiles;
+    ds.stage = 1;
+}
 
-    // ---- core-core components
+// Stage 2: core list from the (whole) counts; union-find over the core x
+// core tiles j > i of this rank's rows.
+template <typename T>
+void link_stage(Ctx& ctx, hipStream_t s) {
+    DenseState& ds = ctx.dn;
+    const Geometry G = geometry_of(ds);
     uint32_t* clist = nullptr;
-    const uint32_t mc = select_ids(ctx, "dn_core", n, CntAtLeast{cnt, ms}, &clist, s);
-    uint32_t* par = ctx.arena.get<uint32_t>("dn_par", mc + 1);
-    uint32_t* keyc = ctx.arena.get<uint32_t>("dn_keyc", mc + 1);
-    uint32_t* key_out = ctx.arena.get<uint32_t>("dn_key", n);
-    PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
-    FragSet Fcore{};
+    const uint32_t mc = select_ids(ctx, "dn_core", ds.n, CntAtLeast{ds.cnt, ds.min_samples}, &clist, s);
+    ds.n_core = mc;
+    ds.clist = clist;
+    ds.par = ctx.arena.get<uint32_t>("dn_par", mc + 1);
+    ds.keyc = ctx.arena.get<uint32_t>("dn_keyc", mc + 1);
     if (mc) {
-        hipLaunchKernelGGL(iota_kernel, dim3(nblocks(mc)), dim3(kBlock), 0, s, par, mc);
-        Fcore = make_frags<T>(ctx, "dn_cf", X, d, clist, mc, G, s);
+        hipLaunchKernelGGL(iota_kernel, dim3(nblocks(mc)), dim3(kBlock), 0, s, ds.par, mc);
+        const FragSet Fcore = make_frags<T>(ctx, "dn_cf", (const T*)ds.X, ds.d, clist, mc, G, s);
+        ds.cf[0] = Fcore.hi;
+        ds.cf[1] = Fcore.lo;
+        ds.cf[2] = Fcore.norm;
+        ds.cf[3] = Fcore.nmax;
+        TileArgs<T> A = base_args<T>(ds);
         A.I = A.J = Fcore;
-        A.par = par;
-        run_tiles<T, kLink>(A, G, a.metric, s);
-        hipLaunchKernelGGL(flatten_keys_kernel, dim3(nblocks(mc)), dim3(kBlock), 0, s, par, clist,
-                           mc, keyc, key_out);
-        PD_HIP(hipGetLastError());
+        A.par = ds.par;
+        run_tiles<T, kLink>(A, G, ds.metric, s);
     }
-    ev.mark();   // 2
+    ds.stage = 2;
+}
 
-    // ---- border points: smallest key among the core neighbours
+// Stage 3: components (the union of `n_forests` forests when sharded), keys,
+// border candidates' smallest adjacent core key over this rank's rows.
+template <typename T>
+void border_stage(Ctx& ctx, const uint32_t* forests, int n_forests, hipStream_t s) {
+    DenseState& ds = ctx.dn;
+    const Geometry G = geometry_of(ds);
+    const uint32_t n = ds.n, mc = ds.n_core;
+    ds.key_out = ctx.arena.get<uint32_t>("dn_key", n);
+    PD_HIP(hipMemsetAsync(ds.key_out, 0xFF, sizeof(uint32_t) * n, s));
+    ds.n_border = 0;
     if (mc) {
+        if (forests && n_forests > 0) {
+            const uint64_t total = (uint64_t)mc * (uint64_t)n_forests;
+            hipLaunchKernelGGL(iota_kernel, dim3(nblocks(mc)), dim3(kBlock), 0, s, ds.par, mc);
+            hipLaunchKernelGGL(merge_forests_kernel, dim3(nblocks(total)), dim3(kBlock), 0, s,
+                               ds.par, forests, mc, total);
+        }
+        hipLaunchKernelGGL(flatten_keys_kernel, dim3(nblocks(mc)), dim3(kBlock), 0, s, ds.par,
+                           ds.clist, mc, ds.keyc, ds.key_out);
+        PD_HIP(hipGetLastError());
         uint32_t* blist = nullptr;
-        const uint32_t mb = select_ids(ctx, "dn_border", n, BorderCand{cnt, ms}, &blist, s);
+        const uint32_t mb = select_ids(ctx, "dn_border", n, BorderCand{ds.cnt, ds.min_samples},
+                                       &blist, s);
+        ds.n_border = mb;
+        ds.blist = blist;
         if (mb) {
-            uint32_t* best = ctx.arena.get<uint32_t>("dn_best", mb);
-            A.I = make_frags<T>(ctx, "dn_bf", X, d, blist, mb, G, s);
+            ds.best = ctx.arena.get<uint32_t>("dn_best", mb);
+            if (ds.world > 1) PD_HIP(hipMemsetAsync(ds.best, 0xFF, sizeof(uint32_t) * mb, s));
+            FragSet Fcore;
+            Fcore.hi = (const bf16x8*)ds.cf[0];
+            Fcore.lo = (const bf16x8*)ds.cf[1];
+            Fcore.norm = (const float*)ds.cf[2];
+            Fcore.nmax = (const float*)ds.cf[3];
+            Fcore.idx = ds.clist;
+            Fcore.m = mc;
+            TileArgs<T> A = base_args<T>(ds);
+            A.I = make_frags<T>(ctx, "dn_bf", (const T*)ds.X, ds.d, blist, mb, G, s);
             A.J = Fcore;
-            A.keyJ = keyc;
-            A.best = best;
-            run_tiles<T, kBorder>(A, G, a.metric, s);
-            hipLaunchKernelGGL(scatter_best_kernel, dim3(nblocks(mb)), dim3(kBlock), 0, s, best,
-                               blist, mb, key_out);
-            PD_HIP(hipGetLastError());
+            A.keyJ = ds.keyc;
+            A.best = ds.best;
+            run_tiles<T, kBorder>(A, G, ds.metric, s);
         }
     }
-    ev.mark();   // 3
+    ds.stage = 3;
+}
 
-    // ---- outputs and labels
-    hipLaunchKernelGGL(outputs_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, cnt, (uint64_t)n, ms,
-                       ctx.full_counts ? 1 : 0, a.core, a.counts);
-    rank_labels_async(ctx, key_out, n, a.labels, s);
+// Stage 4: border keys into the key array, core flags / counts, labels.
+void finish_stage(Ctx& ctx, int32_t* labels, uint8_t* core, uint32_t* counts, hipStream_t s) {
+    DenseState& ds = ctx.dn;
+    if (ds.n_border)
+        hipLaunchKernelGGL(scatter_best_kernel, dim3(nblocks(ds.n_border)), dim3(kBlock), 0, s,
+                           ds.best, ds.blist, ds.n_border, ds.key_out);
+    hipLaunchKernelGGL(outputs_kernel, dim3(nblocks(ds.n)), dim3(kBlock), 0, s, ds.cnt,
+                       (uint64_t)ds.n, ds.min_samples, ctx.full_counts ? 1 : 0, core, counts);
+    PD_HIP(hipGetLastError());
+    rank_labels_async(ctx, ds.key_out, ds.n, labels, s);   // count: rank_labels_count
+}
+
+template <typename T>
+void run_dense(Ctx& ctx, TrainArgs& a) {
+    hipStream_t s = a.stream;
+    Ev ev(ctx, s);
+    ev.mark();   // 0
+    count_stage<T>(ctx, a, 0, 1);
+    ev.mark();   // 1
+    link_stage<T>(ctx, s);
+    ev.mark();   // 2 (flatten of the components and the border tiles: border)
+    border_stage<T>(ctx, nullptr, 0, s);
+    ev.mark();   // 3
+    finish_stage(ctx, a.labels, a.core, a.counts, s);
     ev.mark();   // 4
     a.n_clusters = rank_labels_count(ctx, s);
-    ctx.t.records = n;
-    ctx.t.core_records = mc;
+    DenseState& ds = ctx.dn;
+    ctx.t.records = ds.n;
+    ctx.t.core_records = ds.n_core;
     ctx.t.cells_n = 0;   // dense: wave tiles computed by the count pass (timing on)
-    if (dtiles && ctx.timing) {
+    if (ds.tiles && ctx.timing) {
         unsigned long long nt = 0;
-        PD_HIP(hipMemcpy(&nt, dtiles, sizeof(nt), hipMemcpyDeviceToHost));
+        PD_HIP(hipMemcpy(&nt, ds.tiles, sizeof(nt), hipMemcpyDeviceToHost));
         ctx.t.cells_n = (int64_t)nt;
     }
     ctx.t.grid_cells = 0;
@@ -1082,20 +1206,76 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
     }
 }
 
+template <typename F>
+void by_dtype(int dtype, F&& f) {
+    if (dtype == 0)
+        f(float{});
+    else if (dtype == 1)
+        f(double{});
+    else
+        throw Error(-1, "dtype must be 0 (float32) or 1 (float64)");
+}
+
 }  // namespace
 
 void dense_train(Ctx& ctx, TrainArgs& a) {
     if (a.phase != 0)
-        throw Error(-5, "the sharded train is built for d <= 4 only (dense tiles are single-device)");
+        throw Error(-5, "the grid phases (pd_train_begin/end) are d <= 4; d > 4 shards with pd_dense_*");
     if (!a.data_box) throw Error(-1, "dense path needs the data bbox");
     if (a.n >= 0xFFFFFFFFll) throw Error(-5, "dense path: n must be < 2^32 - 1");
     ctx.st.valid = false;
-    if (a.dtype == 0)
-        run_dense<float>(ctx, a);
-    else if (a.dtype == 1)
-        run_dense<double>(ctx, a);
-    else
-        throw Error(-1, "dtype must be 0 (float32) or 1 (float64)");
+    by_dtype(a.dtype, [&](auto t) { run_dense<decltype(t)>(ctx, a); });
+}
+
+void dense_count(Ctx& ctx, TrainArgs& a, int rank, int world, uint32_t* counts_out) {
+    if (!a.data_box) throw Error(-1, "dense path needs the data bbox");
+    if (a.n >= 0x7FFFFFFFll) throw Error(-5, "sharded dense path: n must be < 2^31 - 1");
+    if (world < 1 || rank < 0 || rank >= world) throw Error(-1, "bad rank / world");
+    ctx.st.valid = false;
+    by_dtype(a.dtype, [&](auto t) { count_stage<decltype(t)>(ctx, a, rank, world); });
+    if (a.n)
+        PD_HIP(hipMemcpyAsync(counts_out, ctx.dn.cnt, sizeof(uint32_t) * a.n,
+                              hipMemcpyDeviceToDevice, a.stream));
+}
+
+uint32_t dense_link(Ctx& ctx, const uint32_t* counts, uint32_t* forest_out, hipStream_t s) {
+    DenseState& ds = ctx.dn;
+    if (ds.stage != 1) throw Error(-1, "pd_dense_link: call pd_dense_count first");
+    if (ds.n)
+        PD_HIP(hipMemcpyAsync(ds.cnt, counts, sizeof(uint32_t) * ds.n, hipMemcpyDeviceToDevice, s));
+    by_dtype(ds.dtype, [&](auto t) { link_stage<decltype(t)>(ctx, s); });
+    if (ds.n_core)
+        PD_HIP(hipMemcpyAsync(forest_out, ds.par, sizeof(uint32_t) * ds.n_core,
+                              hipMemcpyDeviceToDevice, s));
+    return ds.n_core;
+}
+
+uint32_t dense_border(Ctx& ctx, const uint32_t* forests, int n_forests, int32_t* best_out,
+                      hipStream_t s) {
+    DenseState& ds = ctx.dn;
+    if (ds.stage != 2) throw Error(-1, "pd_dense_border: call pd_dense_link first");
+    by_dtype(ds.dtype, [&](auto t) { border_stage<decltype(t)>(ctx, forests, n_forests, s); });
+    if (ds.n_border) {
+        hipLaunchKernelGGL(best_to_i32_kernel, dim3(nblocks(ds.n_border)), dim3(kBlock), 0, s,
+                           ds.best, ds.n_border, best_out);
+        PD_HIP(hipGetLastError());
+    }
+    return ds.n_border;
+}
+
+int64_t dense_finish(Ctx& ctx, const int32_t* best, int32_t* labels, uint8_t* core,
+                     uint32_t* counts, hipStream_t s) {
+    DenseState& ds = ctx.dn;
+    if (ds.stage != 3) throw Error(-1, "pd_dense_finish: call pd_dense_border first");
+    if (ds.n_border) {
+        hipLaunchKernelGGL(best_from_i32_kernel, dim3(nblocks(ds.n_border)), dim3(kBlock), 0, s,
+                           best, ds.n_border, ds.best);
+        PD_HIP(hipGetLastError());
+    }
+    finish_stage(ctx, labels, core, counts, s);
+    const int64_t ncl = rank_labels_count(ctx, s);
+    ds.stage = 0;
+    return ncl;
 }
 
 }  // namespace pd

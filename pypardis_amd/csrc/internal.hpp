@@ -80,6 +80,36 @@ struct PhaseState {
     uint32_t* exp_key = nullptr;
 };
 
+// Dense path (d > 4, dense.hip) state carried between its stages: count ->
+// link -> border -> finish.  Single device runs them back to back; the
+// sharded dense train (pd_dense_*) runs each stage on every rank over its
+// share of the tile rows, with a collective between stages.  Pointers are
+// arena buffers (or the caller's X, which must stay alive until finish).
+struct DenseState {
+    int stage = 0;               // last stage run (0 none, 1 count, 2 link, 3 border)
+    const void* X = nullptr;
+    int dtype = 0, d = 0, metric = 0;
+    uint32_t n = 0, min_samples = 1;
+    double eps = 0;
+    int rank = 0, world = 1;     // tile rows of chunk c belong to rank c % world
+    // geometry (scaled bf16 split; see dense.hip)
+    int KS = 1;
+    bool mfma = false;
+    double scale = 1.0;
+    double* center = nullptr;
+    float elo = 0, ehi = 0;
+    uint32_t* cnt = nullptr;     // [n] neighbour counts, input order
+    uint32_t n_core = 0, n_border = 0;
+    uint32_t* clist = nullptr;   // core point ids, ascending
+    uint32_t* par = nullptr;     // union-find over the core rows
+    uint32_t* keyc = nullptr;    // cluster key per core row
+    uint32_t* key_out = nullptr; // [n] cluster key per point
+    uint32_t* blist = nullptr;   // border candidate ids, ascending
+    uint32_t* best = nullptr;    // smallest adjacent core key per border candidate
+    const void* cf[4] = {};      // core fragment set: hi, lo, norm, nmax
+    unsigned long long* tiles = nullptr;
+};
+
 struct Ctx {
     int device = 0;
     Arena arena;
@@ -103,6 +133,7 @@ struct Ctx {
     int variant = 5;             // PD_OPT_SWEEP_VARIANT: batched count + border, row-wise link
     Timings t;
     PhaseState st;
+    DenseState dn;
     hipEvent_t ev[16] = {};
 };
 
@@ -140,6 +171,14 @@ struct TrainArgs {
 void train(Ctx& ctx, TrainArgs& a);
 // d > kMaxDim: dense distance tiles on the matrix cores (dense.hip)
 void dense_train(Ctx& ctx, TrainArgs& a);
+// sharded dense train (dense.hip): every rank holds all n points and runs
+// each stage over its share of the tile rows (pd_dense_* in pardis.h)
+void dense_count(Ctx& ctx, TrainArgs& a, int rank, int world, uint32_t* counts_out);
+uint32_t dense_link(Ctx& ctx, const uint32_t* counts, uint32_t* forest_out, hipStream_t s);
+uint32_t dense_border(Ctx& ctx, const uint32_t* forests, int n_forests, int32_t* best_out,
+                      hipStream_t s);
+int64_t dense_finish(Ctx& ctx, const int32_t* best, int32_t* labels, uint8_t* core,
+                     uint32_t* counts, hipStream_t s);
 // labels from cluster keys (engine.hip): async, then the cluster count (syncs)
 // core_bit: keys carry the core flag in bit 30 (stripped; written to
 // core_from_key when not null)

@@ -279,9 +279,6 @@ class DBSCAN(object):
 
     # ------------------------------------------------------------ multi-GPU
     def _sharded_checks(self, points):
-        if points.d > 4:
-            raise NotImplementedError("the multi-GPU train is built for d <= 4; the dense "
-                                      "high-dimensional path runs on one device (n_gpus=1)")
         if self.kd_sums != 'exact':
             raise ValueError("kd_sums='sequential' is single-device (the fold order of one "
                              "slice); the multi-GPU train uses the exact sums")

@@ -28,6 +28,10 @@ holds a slice of the points in its GPU's HBM and the same steps are:
 Result: each rank returns the global ids and labels of the points it owns
 (every point is owned by exactly one rank: the one holding its KD partition).
 
+d > 4 (the dense tile path) shares steps 1-2 (the KD boxes of the API) and
+then all-gathers the slices: the distance tiles need every point on every
+GPU, and each rank computes its share of the tile rows (``_train_dense``).
+
 The device work goes through an ``ops`` object (``NativeOps``: libpardis on
 this rank's GPU).  Collectives run on ``comm_device``: the GPU under RCCL
 ("nccl"), the host under gloo.
@@ -118,6 +122,21 @@ class NativeOps(object):
     def scatter_results(self, pairs, gid_base, n):
         return _native.scatter_results(pairs, gid_base, n, self.device, ctx=self.ctx)
 
+    # -- dense (d > 4) stages
+    def dense_count(self, X, eps, min_samples, metric, data_box, rank, world):
+        return _native.dense_count(X, eps, min_samples, metric, data_box, rank, world,
+                                   ctx=self.ctx)
+
+    def dense_link(self, counts):
+        return _native.dense_link(counts, ctx=self.ctx)
+
+    def dense_border(self, forests, n_forests, n):
+        return _native.dense_border(forests, n_forests, n, ctx=self.ctx)
+
+    def dense_finish(self, best, n):
+        labels, core, _, ncl = _native.dense_finish(best, n, self.device, ctx=self.ctx)
+        return labels, core, ncl
+
     def timings(self):
         return self.ctx.timings()
 
@@ -167,6 +186,9 @@ def partition_ranks(P, world):
     return part_rank, local_index
 
 
+_TORCH_OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
+
+
 class _TorchComm(object):
     """Collectives through a torch.distributed process group (gloo on the
     host: the CPU tests; any backend without device buffers)."""
@@ -186,6 +208,13 @@ class _TorchComm(object):
         dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM,
                         group=self.group)
         return t.cpu().numpy()
+
+    def all_reduce_t(self, t, op):
+        """Element-wise reduction ("sum", "min", "max") of a tensor over the
+        ranks; returns the result on the collective's device."""
+        r = self.to(t).contiguous().clone()
+        dist.all_reduce(r, op=_TORCH_OPS[op], group=self.group)
+        return r
 
     def all_gather_np(self, arr):
         t = torch.as_tensor(np.ascontiguousarray(arr)).to(self.device)
@@ -246,6 +275,12 @@ class RcclComm(object):
         t = torch.as_tensor(np.ascontiguousarray(arr)).to(self.device)
         self.comm.all_reduce(t, _native.PD_R_MAX if op == "max" else _native.PD_R_SUM)
         return t.cpu().numpy()
+
+    def all_reduce_t(self, t, op):
+        r = self.to(t).contiguous().clone()
+        code = {"sum": _native.PD_R_SUM, "min": _native.PD_R_MIN, "max": _native.PD_R_MAX}[op]
+        self.comm.all_reduce(r, code)
+        return r
 
     def all_gather_np(self, arr):
         a = np.ascontiguousarray(arr)
@@ -310,9 +345,8 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     """
     if split_method not in ('min_var', 'rotation'):
         split_method = 'min_var'   # the reference's fallback (R:dbscan/partition.py:129-130)
-    if X.dim() != 2 or X.shape[1] > 4:
-        raise NotImplementedError("the sharded train is built for d <= 4 (the dense "
-                                  "high-dimensional path runs on one device)")
+    if X.dim() != 2:
+        raise ValueError("X must be an (n, d) tensor")
     ops = ops or NativeOps(X.device)
     comm = comm or make_comm(group, getattr(ops, "device", X.device))
     W, rank = comm.world, comm.rank
@@ -400,10 +434,14 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
         boundary, cand = level_boundaries(cnt, bounds)
         pending = (sel, axes, boundary, new)
         apply_level(boxes, splits, level, axes, means, vars_, cnt, cand, boundary)
-    if pending is not None and n:
+    dense = d > 4
+    if pending is not None and n and not dense:
         ops.split(X, kdlab, *pending)
     ebox = np.stack([boxes[L].expand(2 * eps).as_array() for L in sorted(boxes)])
     lap("kd")
+    if dense:
+        return _train_dense(X, eps, min_samples, metric, comm, ops, gid_off, data_box,
+                            dict(splits=splits, bounding_boxes=boxes, boxes=ebox), stats, lap)
 
     # ---- route + exchange (R:dbscan/dbscan.py:114-118,136-151)
     part_rank, local_index = partition_ranks(P, W)
@@ -481,6 +519,39 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
                          local_labels=loc_labels, local_core=loc_core, gid_base=gid_base,
                          n_total=n_total, n_clusters=int(all_roots.shape[0]), splits=splits,
                          bounding_boxes=boxes, boxes=ebox, stats=stats)
+
+
+def _train_dense(X, eps, min_samples, metric, comm, ops, gid_off, data_box, kd, stats, lap):
+    """d > 4 (the dense MFMA tile path, dense.hip): the tiles need every point,
+    so the slices are all-gathered (1M x 64-D fp32 is 256 MB per GPU) and each
+    rank computes its share of the tile rows (row chunks dealt round-robin,
+    pd_dense_*).  Four stages, one collective between each: counts (sum),
+    core forests (gather), border keys (min).  Every rank ends with the labels
+    of all points — sklearn's over the union — and returns its slice's."""
+    W, rank = comm.world, comm.rank
+    n = X.shape[0]
+    n_total = int(gid_off[-1])
+    dev = getattr(ops, "device", X.device)
+    Xf = comm.all_gather_var(X.contiguous()).to(dev).contiguous()
+    stats["received"] = int(Xf.shape[0])
+    lap("exchange")
+    cnt = ops.dense_count(Xf, eps, min_samples, metric, data_box, rank, W)
+    cnt = comm.all_reduce_t(cnt, "sum").to(dev)
+    lap("count")
+    forest = ops.dense_link(cnt)
+    forests = comm.all_gather_var(forest).to(dev)
+    stats["exports"] = int(forest.shape[0])
+    lap("link")
+    best = ops.dense_border(forests, W, n_total)
+    best = comm.all_reduce_t(best, "min").to(dev)
+    labels, core, ncl = ops.dense_finish(best, n_total)
+    lap("border")
+    lo = int(gid_off[rank])
+    loc_labels, loc_core = labels[lo:lo + n], core[lo:lo + n]
+    gid = torch.arange(lo, lo + n, dtype=torch.int32, device=dev)
+    return ShardedResult(gid=gid, labels=loc_labels, core=loc_core, local_labels=loc_labels,
+                         local_core=loc_core, gid_base=lo, n_total=n_total, n_clusters=ncl,
+                         stats=stats, **kd)
 
 
 def train_threads(slices, eps, min_samples, comms, ops, metric=_native.PD_EUCLIDEAN,

@@ -165,6 +165,75 @@ class OracleOps(object):
         counts = np.diff(np.searchsorted(g, np.asarray(gid_offsets, np.int64)))
         return torch.from_numpy(np.ascontiguousarray(pairs)), counts.astype(np.int64)
 
+    # -- dense (d > 4) stages: pd_dense_* restated.  This rank's rows are the
+    # 2048-row chunks c with c % world == rank (the stand-in deals input rows;
+    # the device deals its pruned row order — any split sums to the same).
+    def dense_count(self, X, eps, min_samples, metric, data_box, rank, world):
+        m = "euclidean" if metric == 0 else "cityblock"
+        off, nbr = oracle.neighbors(X.numpy(), eps, m)
+        n = len(off) - 1
+        mine = (np.arange(n) // 2048) % world == rank
+        self.dn = dict(off=off, nbr=nbr, ms=min_samples, n=n, rank=rank, world=world)
+        return torch.from_numpy((np.diff(off) * mine).astype(np.int32))
+
+    def dense_link(self, counts):
+        dn = self.dn
+        core = counts.numpy() >= dn["ms"]
+        clist = np.nonzero(core)[0]
+        row = np.full(dn["n"], -1, np.int64)
+        row[clist] = np.arange(len(clist))
+        cmine = self._core_share(len(clist))
+        uf = oracle._UF(len(clist))
+        off, nbr = dn["off"], dn["nbr"]
+        for a in np.nonzero(cmine)[0]:
+            p = clist[a]
+            for q in nbr[off[p]:off[p + 1]]:
+                b = row[q]
+                if b > a:
+                    uf.union(a, b)
+        dn.update(clist=clist, row=row, counts=counts.numpy().copy())
+        return torch.from_numpy(np.array([uf.find(a) for a in range(len(clist))], np.int32))
+
+    def _core_share(self, m):
+        r, w = self.dn["rank"], self.dn["world"]
+        return (np.arange(m) // 2048) % w == r
+
+    def dense_border(self, forests, n_forests, n):
+        dn = self.dn
+        clist, row = dn["clist"], dn["row"]
+        m = len(clist)
+        uf = oracle._UF(m)
+        f = forests.numpy().reshape(n_forests, m) if m else np.zeros((n_forests, 0), np.int32)
+        for r in range(n_forests):
+            for a in range(m):
+                uf.union(a, int(f[r, a]))
+        keyc = np.array([clist[uf.find(a)] for a in range(m)], np.int64)
+        cnt = dn["counts"]
+        blist = np.nonzero((cnt >= 2) & (cnt < dn["ms"]))[0]
+        bmine = (np.arange(len(blist)) // 2048) % dn["world"] == dn["rank"]
+        best = np.full(len(blist), 0x7FFFFFFF, np.int64)
+        off, nbr = dn["off"], dn["nbr"]
+        for k in np.nonzero(bmine)[0]:
+            p = blist[k]
+            ks = [keyc[row[q]] for q in nbr[off[p]:off[p + 1]] if row[q] >= 0]
+            if ks:
+                best[k] = min(ks)
+        dn.update(keyc=keyc, blist=blist)
+        return torch.from_numpy(best.astype(np.int32))
+
+    def dense_finish(self, best, n):
+        dn = self.dn
+        key = np.full(n, 0xFFFFFFFF, np.int64)
+        key[dn["clist"]] = dn["keyc"]
+        b = best.numpy().astype(np.int64)
+        key[dn["blist"]] = np.where(b == 0x7FFFFFFF, 0xFFFFFFFF, b)
+        roots = np.unique(key[key != 0xFFFFFFFF])
+        labels = np.full(n, -1, np.int32)
+        m = key != 0xFFFFFFFF
+        labels[m] = np.searchsorted(roots, key[m])
+        core = (dn["counts"] >= dn["ms"]).astype(np.uint8)
+        return torch.from_numpy(labels), torch.from_numpy(core), len(roots)
+
     def scatter_results(self, pairs, gid_base, n):
         p = pairs.numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
         idx = p[:, 0] - gid_base

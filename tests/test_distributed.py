@@ -146,3 +146,38 @@ def test_train_threads_local_comm():
     labels = np.concatenate([r.local_labels.numpy() for r in res])
     np.testing.assert_array_equal(labels, g["sk_labels"])
     assert {r.n_clusters for r in res} == {int(g["sk_labels"].max()) + 1}
+
+
+def _dense_blobs(n=6000, d=8, seed=5):
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-4, 4, size=(6, d))
+    X = c[rng.integers(0, 6, n)] + rng.normal(scale=0.35, size=(n, d))
+    X[: n // 20] = rng.uniform(-5, 5, size=(n // 20, d))   # noise
+    return X.astype(np.float32)
+
+
+@pytest.mark.parametrize("case,world,api", [("c3_5k", 2, False), ("c3_5k", 3, True),
+                                            ("blobs8", 2, False), ("blobs8", 3, True)])
+def test_sharded_dense_equals_sklearn(tmp_path, case, world, api):
+    """d > 4 over ranks (distributed._train_dense): slices all-gathered, the
+    count / link / border stages split by row chunks with a sum, a forest
+    gather and a min between them.  Labels equal sklearn's (the golden C3
+    slice) or the oracle's (8-D blobs with > 2048 core points, so every
+    rank's link share is non-empty); KD boxes equal one process's."""
+    if case == "c3_5k":
+        g = load_golden("c3_5k")
+        X, eps, ms, P = g["X"], float(g["eps"]), int(g["min_samples"]), int(g["P"])
+        want, core = g["sk_labels"], g["sk_core"].astype(np.uint8)
+    else:
+        X, eps, ms, P = _dense_blobs(), 0.9, 8, 4
+        want, core, _, _ = oracle.dbscan(X, eps, ms)
+        assert core.sum() > 2048
+    out = run_world(world, X, eps, ms, 0, P, str(tmp_path), api=api)
+    assert (out["seen"] == 1).all()
+    np.testing.assert_array_equal(out["labels"], want)
+    np.testing.assert_array_equal(out["core"], core)
+    np.testing.assert_array_equal(out["loc_labels"], want)
+    assert out["ncl"] == {int(want.max()) + 1}
+    kd = oracle.kd_partition(X, P, sums="exact")
+    for sp in out["splits"]:
+        np.testing.assert_array_equal(sp, np.array(kd["splits"], np.float64))

@@ -730,3 +730,81 @@ def test_c4_partition_invariance_large(native):
     u, fi = np.unique(lab[idx], return_index=True)
     assert np.array_equal(u, np.arange(ref.n_clusters_))
     assert np.all(np.diff(idx[fi]) > 0)
+
+
+# ------------------------------------------------------------ sharded dense (d > 4)
+def _dense_stages(native, Xd, eps, ms, metric, W, full=False):
+    """W ranks simulated in one process: one context each on cuda:0, the
+    collectives done by hand (sum of counts, concatenation of the forests,
+    min of the border keys) — pd_dense_* exactly as distributed._train_dense
+    drives them."""
+    lo = Xd.min(0).values.double().cpu().numpy()
+    hi = Xd.max(0).values.double().cpu().numpy()
+    dbox = np.stack([lo, hi])
+    ctxs = [native.Context(0) for _ in range(W)]
+    for c in ctxs:
+        c.set_option(native.PD_OPT_FULL_COUNTS, int(full))
+    parts = [native.dense_count(Xd, eps, ms, metric, dbox, r, W, ctx=ctxs[r]) for r in range(W)]
+    cnt = torch.stack(parts).sum(0).to(torch.int32)
+    forests = torch.cat([native.dense_link(cnt, ctx=c) for c in ctxs])
+    n = Xd.shape[0]
+    best = torch.stack([native.dense_border(forests, W, n, ctx=c) for c in ctxs]).min(0).values \
+        if n else torch.empty(0, dtype=torch.int32, device=Xd.device)
+    outs = [native.dense_finish(best, n, Xd.device, want_counts=full, ctx=c) for c in ctxs]
+    for o in outs[1:]:   # every rank ends with the same answer
+        assert torch.equal(o[0], outs[0][0]) and o[3] == outs[0][3]
+    return outs[0], parts
+
+
+DENSE_SHARD = [("c3_60k", 4, "euclidean"), ("c3_60k", 8, "euclidean"), ("d5_blobs", 3, "euclidean"),
+               ("d8_cityblock", 2, "cityblock"), ("d100_f64", 3, "euclidean")]
+
+
+@pytest.mark.parametrize("name,W,metric", DENSE_SHARD, ids=[f"{c[0]}-w{c[1]}" for c in DENSE_SHARD])
+def test_dense_sharded_stages_match_oracle(native, name, W, metric):
+    """The sharded dense stages over W simulated ranks give the oracle's
+    counts, core flags and labels; each rank's count share is non-trivial."""
+    from pypardis_amd import synth
+    if name == "c3_60k":
+        X, eps, ms = synth.make_config("C3", n=60_000)[0], 0.114028, 10
+    else:
+        case = {c[0]: c for c in DENSE}[name]
+        X, eps, ms = np.ascontiguousarray(case[1]()), case[2], case[3]
+    (lab, core, cnt, ncl), parts = _dense_stages(native, _dev(X), eps, ms,
+                                                 native.metric_code(metric), W, full=True)
+    lab_o, core_o, cnt_o, nc_o = oracle.dbscan(X, eps, ms, metric)
+    assert np.array_equal(cnt.cpu().numpy().astype(np.int64), cnt_o)
+    assert np.array_equal(lab.cpu().numpy().astype(np.int64), lab_o) and ncl == nc_o
+    assert np.array_equal(core.cpu().numpy(), core_o)
+    if len(X) >= 2048 * W:
+        for p in parts:   # every rank computed some rows, and only its own
+            assert int((p > 0).sum()) > 0
+
+
+def test_dense_sharded_single_rank_equals_cluster(native):
+    """Rank 0 of 1 through pd_dense_* equals pd_cluster; edge cases: no core
+    point, one point, empty input."""
+    from pypardis_amd import synth
+    X = synth.make_config("C3", n=20_000)[0]
+    Xd = _dev(X)
+    lab1, core1, _, nc1 = native.cluster(Xd, 0.114028, 10)
+    (lab, core, _, ncl), _ = _dense_stages(native, Xd, 0.114028, 10, 0, 1)
+    assert torch.equal(lab, lab1) and torch.equal(core, core1) and ncl == nc1
+    (lab, _, _, ncl), _ = _dense_stages(native, Xd, 1e-6, 10, 0, 3)    # nothing core
+    assert ncl == 0 and int((lab != -1).sum()) == 0
+    (lab, _, _, ncl), _ = _dense_stages(native, Xd[:1].contiguous(), 0.5, 1, 0, 2)
+    assert ncl == 1 and lab.tolist() == [0]
+
+
+def test_dense_sharded_process_group_native(native, tmp_path):
+    """dbscan.DBSCAN(...).train(slice) with 64-D points in a gloo group of 3
+    ranks sharing cuda:0: labels equal the single-device dense path."""
+    from dist_worker import run_world
+    from pypardis_amd import synth
+    X = synth.make_config("C3", n=40_000)[0]
+    lab1, core1, _, nc1 = native.cluster(_dev(X), 0.114028, 10)
+    out = run_world(3, X, 0.114028, 10, 0, 4, str(tmp_path), native=True, api=True)
+    np.testing.assert_array_equal(out["loc_labels"], lab1.cpu().numpy().astype(np.int64))
+    np.testing.assert_array_equal(out["loc_core"], core1.cpu().numpy())
+    for z in out["ranks"]:
+        assert int(z["n_clusters_"]) == nc1

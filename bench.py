@@ -254,23 +254,27 @@ def grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages):
     return roof, stage
 
 
-def dense_roofline(n, d, t_cnt, cells, pmc, pmc_src):
+def dense_roofline(n, d, t_cnt, cells, pmc, pmc_src, refined=None):
     # dense tiles (dense.hip): the count pass's Gram tiles, 2 d flops per pair
     # over the 64 x 64 wave tiles it computes (the engine reports them in
     # cells_n; the projection window prunes the rest of the n^2 pairs); the
-    # MFMA executes 3 split-bf16 products with d padded to 16 ks
+    # MFMA executes the hi.hi screen on every tile (d padded to 16 ks) and the
+    # two remaining split-bf16 products on the tiles the screen keeps
+    # (grid_cells)
     ks = 1 if d <= 16 else 2 if d <= 32 else 4 if d <= 64 else 8
     n_pad = -(-n // 64) * 64
     tiles = cells if cells > 0 else (n_pad // 64) ** 2
+    refined = tiles if refined is None else refined
     alg = 2.0 * d * 64 * 64 * tiles
-    exe = 3 * 2.0 * 64 * 64 * 16 * ks * tiles
+    exe = 2.0 * 64 * 64 * 16 * ks * (tiles + 2 * refined)
     achieved = alg / (t_cnt * 1e-3) / 1e12
     roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS,
             "frac_kind": "algorithmic: 2 d flops per computed pair", "traffic": None,
             "kernel": "tile_kernel (count pass)", "kernel_ms": t_cnt,
             "algorithmic_flops": alg, "mfma_executed_flops": exe,
-            "wave_tiles": tiles, "tiles_all_pairs": (n_pad // 64) ** 2,
+            "wave_tiles": tiles, "refined_tiles": refined,
+            "tiles_all_pairs": (n_pad // 64) ** 2,
             "tile_fraction": tiles / (n_pad // 64) ** 2,
             "mfma_executed_tflops": exe / (t_cnt * 1e-3) / 1e12,
             "mfma_utilisation": exe / (t_cnt * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS,
@@ -401,7 +405,7 @@ def main():
         for k, v in t.items():
             stage_sum[k] = stage_sum.get(k, 0.0) + v
         count_ms.append(t["count"])
-        rec, cells = int(t["records"]), int(t["cells_n"])
+        rec, cells, gcells = int(t["records"]), int(t["cells_n"]), int(t["grid_cells"])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -442,8 +446,8 @@ def main():
             roof, stage_roof = grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages)
             dtype = f"{'f32' if Xd.dtype == torch.float32 else 'f64'} coords, f64 predicate"
         else:
-            roof = dense_roofline(n, d, t_cnt, cells, pmc, pmc_src)
-            dtype = "bf16x3 (split bf16 MFMA, fp32 accumulate) + f64 recheck"
+            roof = dense_roofline(n, d, t_cnt, cells, pmc, pmc_src, refined=gcells)
+            dtype = "bf16 hi.hi screen, split-bf16 x3 where it keeps a pair (fp32 accumulate), f64 recheck"
         if args.config == "C2" and n == cfgd["n"]:
             metric = BASELINE_METRIC
         else:

@@ -101,7 +101,11 @@ enum pd_option {
                                 core record tests in the centre-row union (0 = all).  Default -1:
                                 mode 6 takes 4 when cells hold <= 4 records on average, else 16
                                 (modes 3/5: 16).  A heuristic either way: the cell verify proves
-                                or tests every edge, so labels are the same */
+                                or tests every edge, so labels are the same */,
+    PD_OPT_DIR_BUDGET = 14    /* bytes the bbox-sized eps-grid directory may take (20 B per 64
+                                cells); beyond it every cell grows by a common factor until it
+                                fits (exact at any width >= eps; more candidates per record).
+                                Default 32 GiB (PD_T_GRID_GROW reports the factor) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */
@@ -111,7 +115,10 @@ enum pd_timing_slot {
     PD_T_KEY_BITS, PD_T_CORE_RECORDS,
     /* PD_OPT_SWEEP_STATS counters */
     PD_T_S_COUNT_CAND, PD_T_S_LINK_CAND, PD_T_S_LINK_HIT, PD_T_S_LINK_CORE, PD_T_S_LINK_SAME,
-    PD_T_S_LINK_FIND_SAME, PD_T_S_LINK_UNIONS, PD_T_S_VERIFY_PAIRS, PD_T_NSLOTS
+    PD_T_S_LINK_FIND_SAME, PD_T_S_LINK_UNIONS, PD_T_S_VERIFY_PAIRS,
+    PD_T_GRID_GROW,            /* cell width / eps of the last grid train (1 unless the
+                                  directory budget made the cells grow) */
+    PD_T_NSLOTS
 };
 
 typedef struct pd_ctx pd_ctx;

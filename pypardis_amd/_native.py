@@ -27,12 +27,13 @@ PD_OPT_BORDER_ROOTS = 10
 PD_OPT_DENSE_PRUNE = 11
 PD_OPT_COUNT_ROTATE = 12
 PD_OPT_CENTRE_WINDOW = 13
+PD_OPT_DIR_BUDGET = 14
 SWEEP_VARIANT_DEFAULT = 5
 LINK_MODE_DEFAULT = 6
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
                 "s_count_cand", "s_link_cand", "s_link_hit", "s_link_core", "s_link_same",
-                "s_link_find_same", "s_link_unions", "s_verify_pairs"]
+                "s_link_find_same", "s_link_unions", "s_verify_pairs", "grid_grow"]
 
 # every symbol include/pardis.h declares (tests/test_abi.py checks the .so)
 EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",

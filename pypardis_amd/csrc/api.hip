@@ -158,6 +158,9 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         } else if (option == PD_OPT_CENTRE_WINDOW) {
             if (value > 0x7FFFFFFF) throw Error(PD_EINVAL, "centre window too large");
             ctx->c.centre_window = value < 0 ? -1 : (int)value;   // < 0: automatic
+        } else if (option == PD_OPT_DIR_BUDGET) {
+            if (value < 16) throw Error(PD_EINVAL, "directory budget must be >= 16 bytes");
+            ctx->c.dir_budget = value;
         } else if (option == PD_OPT_XSUB) {
             if (value < 1 || value > 16) throw Error(PD_EINVAL, "xsub must be in [1, 16]");
             ctx->c.xsub = (int)value;
@@ -179,7 +182,7 @@ int32_t pd_ctx_timings(pd_ctx* ctx, double* out, int32_t n) {
                                        (double)t.sweep[0], (double)t.sweep[1],
                                        (double)t.sweep[2], (double)t.sweep[3],
                                        (double)t.sweep[4], (double)t.sweep[5],
-                                       (double)t.sweep[6], (double)t.sweep[7]};
+                                       (double)t.sweep[6], (double)t.sweep[7], t.grid_grow};
         for (int i = 0; i < n && i < PD_T_NSLOTS; ++i) out[i] = v[i];
     });
 }

@@ -55,6 +55,14 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 enum { kCount = 0, kLink = 1, kBorder = 2 };
 constexpr int kTile = 64;                 // points per wave tile (2 MFMA tiles of 32)
 constexpr float kBandC = 1.0f / 8192.0f;  // error band c (see header)
+// Count pass screen: hi.hi alone (one MFMA per k-step instead of three) is
+// within 2^-8 (1 + 2^-10) |x||y| + 2^-17 s of the dot product (bf16 rounds
+// each coordinate by <= 2^-9 of itself; products exact, fp32 accumulation
+// over <= 128 terms), i.e. d2 within 2^-8 * 1.01 s.  A tile where no pair
+// passes the band c' = 2^-7 holds no neighbour (a 1.9x margin), so only
+// tiles that can hold one fetch the lo fragments and finish the split
+// product; C3 pairs lie ~100 eps^2 apart, so most tiles stop at the screen.
+constexpr float kScreenC = 1.0f / 128.0f;
 constexpr float kPadNorm = 1.0e30f;       // norm of padding rows: never a neighbour
 
 inline unsigned nblocks(uint64_t n, unsigned per = kBlock) {
@@ -170,7 +178,8 @@ struct TileArgs {
     uint32_t band, nband, sub, nsub;
     uint32_t whole_bands;       // 1: one run per band (the overflow path), for tests
     double win;
-    unsigned long long* tiles;  // wave tiles computed (null: not counted)
+    unsigned long long* tiles;  // [2]: wave tiles computed, of which refined past the
+                                // count screen (null: not counted)
     // sharded train: this device computes the I rows of the chunks
     // (kShardChunk rows each) c with c % shard_world == shard_rank
     uint32_t shard_rank, shard_world;
@@ -238,10 +247,13 @@ constexpr int tile_threads(int) { return 256; }
 constexpr int kCountQT = 2;   // query tiles (of 32) per wave in the count pass (4: one
                               // wave per SIMD, measured 125 vs 74 ms on C3)
 
-template <int KS>
+// LO: the lo fragments are staged too (link / border); the count pass
+// stages hi only and reads lo from global memory for the tiles its screen
+// keeps (half the streamed bytes per tile).
+template <int KS, bool LO>
 struct TileLds {
     bf16x8 hi[2][2][KS][64];   // [buffer][row group][k-step][lane]
-    bf16x8 lo[2][2][KS][64];
+    bf16x8 lo[LO ? 2 : 1][LO ? 2 : 1][LO ? KS : 1][LO ? 64 : 1];
     float nta[2][kTile];       // -ta_j = -(1+c)|x_j|^2 / 2
 };
 
@@ -252,9 +264,10 @@ template <typename T, int MODE, int KS, int QT>
 __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_eu((KS >= 8 || QT > 2) ? 1 : 2))) void tile_kernel(TileArgs<T> A) {
     constexpr int TB = tile_threads(KS);
     constexpr int QW = 32 * QT;                  // query rows per wave
-    constexpr int NC = 2 * 2 * KS * 64;          // 16-byte chunks per tile (hi + lo)
+    constexpr bool LO = MODE != kCount;          // lo staged with hi (see TileLds)
+    constexpr int NC = (LO ? 2 : 1) * 2 * KS * 64;   // 16-byte chunks per staged tile
     constexpr int NCH = (NC + TB - 1) / TB;      // per thread
-    __shared__ TileLds<KS> S;
+    __shared__ TileLds<KS, LO> S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // block -> query rows.  Pruned count: bands are dealt round-robin to the
     // 8 XCDs (dispatch puts block id b on XCD b % 8), a band's blocks kept
@@ -281,7 +294,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
     // the wave's 32 QT query points: B operand fragments, kept in registers
     bf16x8 bh[QT][KS], bl[QT][KS];
     uint32_t iq[QT];
-    float ai[QT], bi[QT];
+    float ai[QT], bi[QT], bc[QT];
     bool ok[QT];
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
@@ -296,6 +309,10 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
         const float nI = wave_ok ? A.I.norm[iq[t]] : kPadNorm;
         ai[t] = ((1.0f + kBandC) * nI - A.elo) * 0.5f;
         bi[t] = ((1.0f - kBandC) * nI - A.ehi) * 0.5f - kBandC * 1.001f * nJmax;
+        // screen: acc_hh - ta_j >= ((1-c')|x_i|^2 - ehi)/2 - ((c'+c)/2)|x_j|^2,
+        // widened by max |x_j|^2
+        bc[t] = ((1.0f - kScreenC) * nI - A.ehi) * 0.5f -
+                (0.5f * (kScreenC + kBandC)) * 1.001f * nJmax;
     }
     uint32_t cnt[QT], best[QT];
 #pragma unroll
@@ -410,7 +427,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
     }
     __syncthreads();
     const uint32_t nseg = nseg_s;
-    uint32_t ntiles = 0;
+    uint32_t ntiles = 0, nrefined = 0;
     // cursor over the tiles of the segments; false at the end
     auto seek = [&](uint32_t& sg, uint32_t& j) -> bool {
         while (sg < nseg) {
@@ -436,7 +453,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
             const int half = c / (2 * KS * 64);            // 0 hi, 1 lo
             const int w = c % (2 * KS * 64);               // (row group, k-step, lane)
             const uint64_t o = (uint64_t)(j0 / 32) * KS * 64 + w;
-            st.v[q] = half ? A.J.lo[o] : A.J.hi[o];
+            st.v[q] = (LO && half) ? A.J.lo[o] : A.J.hi[o];
         }
         if (threadIdx.x < kTile) st.n = A.J.norm[j0 + threadIdx.x];
     };
@@ -447,7 +464,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
             if (NC % TB != 0 && c >= NC) break;
             const int half = c / (2 * KS * 64);
             const int w = c % (2 * KS * 64);
-            bf16x8* dst = half ? &S.lo[buf][0][0][0] : &S.hi[buf][0][0][0];
+            bf16x8* dst = (LO && half) ? &S.lo[LO ? buf : 0][0][0][0] : &S.hi[buf][0][0][0];
             dst[w] = st.v[q];
         }
         if (threadIdx.x < kTile) S.nta[buf][threadIdx.x] = -((1.0f + kBandC) * 0.5f) * st.n;
@@ -486,32 +503,80 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
                     nt[u][4 * q + 3] = v.w;
                 }
             f32x16 acc[2][QT];
+            bool refine = true;
+            if constexpr (LO) {
 #pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                bf16x8 ah[2], al[2];
+                for (int s = 0; s < KS; ++s) {
+                    bf16x8 ah[2], al[2];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    ah[u] = S.hi[buf][u][s][lane];
-                    al[u] = S.lo[buf][u][s][lane];
-                }
-#pragma unroll
-                for (int u = 0; u < 2; ++u)
-#pragma unroll
-                    for (int t = 0; t < QT; ++t) {
-                        acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                            ah[u], bh[t][s], s == 0 ? nt[u] : acc[u][t], 0, 0, 0);
-                        acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bl[t][s],
-                                                                            acc[u][t], 0, 0, 0);
-                        acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[u], bh[t][s],
-                                                                            acc[u][t], 0, 0, 0);
+                    for (int u = 0; u < 2; ++u) {
+                        ah[u] = S.hi[buf][u][s][lane];
+                        al[u] = S.lo[LO ? buf : 0][LO ? u : 0][LO ? s : 0][LO ? lane : 0];
                     }
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int t = 0; t < QT; ++t) {
+                            acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                ah[u], bh[t][s], s == 0 ? nt[u] : acc[u][t], 0, 0, 0);
+                            acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[u], bl[t][s],
+                                                                                acc[u][t], 0, 0, 0);
+                            acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[u], bh[t][s],
+                                                                                acc[u][t], 0, 0, 0);
+                        }
+                }
+            } else {
+                // count pass: the hi.hi screen (kScreenC), then the rest of the
+                // split product only where the screen leaves a candidate pair
+#pragma unroll
+                for (int s = 0; s < KS; ++s) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const bf16x8 ah = S.hi[buf][u][s][lane];
+#pragma unroll
+                        for (int t = 0; t < QT; ++t)
+                            acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                ah, bh[t][s], s == 0 ? nt[u] : acc[u][t], 0, 0, 0);
+                    }
+                }
+                bool mb = false;
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int t = 0; t < QT; ++t) mb |= acc[u][t][r] >= bc[t];
+                refine = __any(mb);
+                nrefined += refine ? 1u : 0u;
+                if (refine) {
+                    bf16x8 al[2][KS];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int s = 0; s < KS; ++s)
+                            al[u][s] = A.J.lo[((uint64_t)(j0 / 32 + u) * KS + s) * 64 + lane];
+#pragma unroll
+                    for (int s = 0; s < KS; ++s)
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const bf16x8 ah = S.hi[buf][u][s][lane];
+#pragma unroll
+                            for (int t = 0; t < QT; ++t) {
+                                acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                    ah, bl[t][s], acc[u][t], 0, 0, 0);
+                                acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                    al[u][s], bh[t][s], acc[u][t], 0, 0, 0);
+                            }
+                        }
+                }
             }
             // element e of block q of m-tile u: row j = j0 + 32u + 8q + 4h + e
             uint64_t band[QT];
 #pragma unroll
             for (int t = 0; t < QT; ++t) band[t] = 0ull;
-            bool walk = true;
+            bool walk = refine;
             if constexpr (MODE == kCount) {
+              if (refine) {
                 uint32_t ci[QT], cm[QT];
 #pragma unroll
                 for (int t = 0; t < QT; ++t) ci[t] = cm[t] = 0u;
@@ -548,6 +613,7 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
                                 band[t] |= b ? (1ull << (16 * u + r)) : 0ull;
                             }
                 }
+              }
             } else {
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
@@ -597,7 +663,10 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
         if (!have) break;
         step(stA, stB);
     }
-    if (A.tiles && lane == 0 && ntiles) atomicAdd(A.tiles, (unsigned long long)ntiles);
+    if (A.tiles && lane == 0 && ntiles) {
+        atomicAdd(A.tiles, (unsigned long long)ntiles);
+        if (nrefined) atomicAdd(A.tiles + 1, (unsigned long long)nrefined);
+    }
     // lanes l and l + 32 hold the same query column
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
@@ -1058,8 +1127,8 @@ void count_stage(Ctx& ctx, TrainArgs& a, int rank, int world) {
         const FragSet Fs = make_frags<T>(ctx, "dn_all", X, d, sid, n, G, s);
         uint32_t* cs = ctx.arena.get<uint32_t>("dn_cnt_sorted", n);
         if (world > 1) PD_HIP(hipMemsetAsync(cs, 0, sizeof(uint32_t) * n, s));
-        dtiles = ctx.arena.get<unsigned long long>("dn_tiles", 1);
-        PD_HIP(hipMemsetAsync(dtiles, 0, sizeof(unsigned long long), s));
+        dtiles = ctx.arena.get<unsigned long long>("dn_tiles", 2);
+        PD_HIP(hipMemsetAsync(dtiles, 0, 2 * sizeof(unsigned long long), s));
         A.I = A.J = Fs;
         A.p3 = ps;
         A.bp1 = bp1;
@@ -1190,13 +1259,16 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
     DenseState& ds = ctx.dn;
     ctx.t.records = ds.n;
     ctx.t.core_records = ds.n_core;
-    ctx.t.cells_n = 0;   // dense: wave tiles computed by the count pass (timing on)
-    if (ds.tiles && ctx.timing) {
-        unsigned long long nt = 0;
-        PD_HIP(hipMemcpy(&nt, ds.tiles, sizeof(nt), hipMemcpyDeviceToHost));
-        ctx.t.cells_n = (int64_t)nt;
-    }
+    // dense (timing on): cells_n = wave tiles the count pass computed,
+    // grid_cells = those its hi.hi screen passed on to the full split product
+    ctx.t.cells_n = 0;
     ctx.t.grid_cells = 0;
+    if (ds.tiles && ctx.timing) {
+        unsigned long long nt[2] = {0, 0};
+        PD_HIP(hipMemcpy(nt, ds.tiles, sizeof(nt), hipMemcpyDeviceToHost));
+        ctx.t.cells_n = (int64_t)nt[0];
+        ctx.t.grid_cells = (int64_t)nt[1];
+    }
     if (ctx.timing) {
         ctx.t.count = ev.span(0, 1);
         ctx.t.link = ev.span(1, 2);

@@ -3040,57 +3040,84 @@ void train(Ctx& ctx, TrainArgs& a) {
         }
         return;
     }
-    // per-neighbourhood grids
-    const double cw = a.eps * (1.0 + 1.0 / 1048576.0);
+    // per-neighbourhood grids.  Cells are eps (eps/xsub along axis 0) wide;
+    // when the bbox-sized directory (20 B per 64 cells: occupancy word +
+    // word root) would pass the budget (PD_OPT_DIR_BUDGET, default 32 GiB),
+    // every cell grows by a common factor k >= 1 until it fits.  Any width >=
+    // eps is exact: the sweeps derive their candidate ranges from the cell
+    // geometry (chords along axis 0, rows +-1 beyond it) and the cell verify
+    // covers +-xsub axis-0 cells of width >= eps/xsub; wider cells only add
+    // candidates (globe-sized extents at a small eps).
     const int xsub = ctx.xsub < 1 ? 1 : ctx.xsub;
     std::vector<PartGrid> parts(a.P);
     uint64_t G = 0;
-    for (int L = 0; L < a.P; ++L) {
-        PartGrid& g = parts[L];
-        std::memset(&g, 0, sizeof(g));
-        for (int j = 0; j < d; ++j) {
-            g.cs[j] = j == 0 ? cw / (double)xsub : cw;
-            g.inv[j] = j == 0 ? (double)xsub / cw : 1.0 / cw;
-        }
-        g.base = G;
-        bool empty = false;
-        long double cells = 1;
-        for (int j = 0; j < d; ++j) {
-            g.elo[j] = a.ebox[(size_t)L * 2 * d + j];
-            g.ehi[j] = a.ebox[(size_t)L * 2 * d + d + j];
-            const double lo = std::max(g.elo[j], box[j]);
-            const double hi = std::min(g.ehi[j], box[d + j]);
-            if (!(lo <= hi)) empty = true;
-            g.lo[j] = lo;
-            if (!empty) {
-                const double nc = std::floor((hi - lo) * g.inv[j]) + 1.0;
-                if (!(nc < 4.0e18)) throw Error(-5, "grid too large along one axis");
-                g.nc[j] = (int64_t)nc;
-                cells *= (long double)g.nc[j];
-            }
-        }
-        for (int j = 0; j < d; ++j) {
-            float fl = (float)g.elo[j], fh = (float)g.ehi[j];
-            if ((double)fl < g.elo[j]) fl = std::nextafter(fl, INFINITY);
-            if ((double)fh > g.ehi[j]) fh = std::nextafter(fh, -INFINITY);
-            g.flo[j] = fl;
-            g.fhi[j] = fh;
-        }
-        if (empty) {
+    const long double budget = (long double)ctx.dir_budget;
+    double grow = 1.0;
+    for (int attempt = 0;; ++attempt) {
+        const double cw = a.eps * (1.0 + 1.0 / 1048576.0) * grow;
+        G = 0;
+        bool too_big = false;
+        long double gsum = 0;
+        for (int L = 0; L < a.P && !too_big; ++L) {
+            PartGrid& g = parts[L];
+            std::memset(&g, 0, sizeof(g));
             for (int j = 0; j < d; ++j) {
-                g.nc[j] = 0;
-                g.elo[j] = g.flo[j] = INFINITY;   // a box no point is in
-                g.ehi[j] = g.fhi[j] = -INFINITY;
+                g.cs[j] = j == 0 ? cw / (double)xsub : cw;
+                g.inv[j] = j == 0 ? (double)xsub / cw : 1.0 / cw;
             }
-            continue;
+            g.base = G;
+            bool empty = false;
+            long double cells = 1;
+            for (int j = 0; j < d; ++j) {
+                g.elo[j] = a.ebox[(size_t)L * 2 * d + j];
+                g.ehi[j] = a.ebox[(size_t)L * 2 * d + d + j];
+                const double lo = std::max(g.elo[j], box[j]);
+                const double hi = std::min(g.ehi[j], box[d + j]);
+                if (!(lo <= hi)) empty = true;
+                g.lo[j] = lo;
+                if (!empty) {
+                    const double nc = std::floor((hi - lo) * g.inv[j]) + 1.0;
+                    if (!(nc < 4.0e18)) {
+                        too_big = true;
+                        break;
+                    }
+                    g.nc[j] = (int64_t)nc;
+                    cells *= (long double)g.nc[j];
+                }
+            }
+            if (too_big) break;
+            for (int j = 0; j < d; ++j) {
+                float fl = (float)g.elo[j], fh = (float)g.ehi[j];
+                if ((double)fl < g.elo[j]) fl = std::nextafter(fl, INFINITY);
+                if ((double)fh > g.ehi[j]) fh = std::nextafter(fh, -INFINITY);
+                g.flo[j] = fl;
+                g.fhi[j] = fh;
+            }
+            if (empty) {
+                for (int j = 0; j < d; ++j) {
+                    g.nc[j] = 0;
+                    g.elo[j] = g.flo[j] = INFINITY;   // a box no point is in
+                    g.ehi[j] = g.fhi[j] = -INFINITY;
+                }
+                continue;
+            }
+            gsum += cells;
+            if (gsum > 4.0e18L) {
+                too_big = true;
+                break;
+            }
+            G += (uint64_t)cells;
         }
-        if (cells > 4.0e18L) throw Error(-5, "grid too large (sum of cells > 4e18)");
-        G += (uint64_t)cells;
-        if ((long double)G > 4.0e18L) throw Error(-5, "grid too large");
+        const long double dir_bytes = too_big ? 1e30L : gsum / 64.0L * 20.0L;
+        if (dir_bytes <= budget) break;
+        if (attempt >= 64 || !std::isfinite(grow * 2.0))
+            throw Error(-5, "eps-grid directory does not fit the budget at any cell size");
+        // the directory shrinks by k^d: aim below the budget in one step
+        double k = too_big ? 1024.0
+                           : (double)std::pow((double)(dir_bytes / budget), 1.0 / (double)d) * 1.01;
+        grow *= std::max(k, 1.25);
     }
-    // directory: G/64 words of 12 B; refuse beyond 64 GiB (future: hashed rows)
-    if ((long double)G / 64.0L * 12.0L > 64.0L * (1ull << 30))
-        throw Error(-5, "eps-grid directory would exceed 64 GiB; eps too small for the extent");
+    ctx.t.grid_grow = grow;
     int key_bits = 1;
     while (key_bits < 64 && ((G - (G ? 1 : 0)) >> key_bits)) ++key_bits;
     if (a.dtype == 0) {

@@ -50,6 +50,7 @@ struct Timings {
     // core hits, hits already under the root, finds that met the root, unions;
     // cell pairs tested record by record (link mode 3)
     int64_t sweep[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double grid_grow = 1.0;      // cell width / eps (PD_OPT_DIR_BUDGET)
 };
 
 // Device state carried from phase A (local clustering) to phase B (border
@@ -129,6 +130,7 @@ struct Ctx {
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
     bool border_roots = false;   // border sweep's single-root fast path (tuning)
+    int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow
     int dense_prune = 1;         // dense count pass: projection-window tiles only (2: per-band runs)
     int variant = 5;             // PD_OPT_SWEEP_VARIANT: batched count + border, row-wise link
     Timings t;

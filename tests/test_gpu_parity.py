@@ -808,3 +808,54 @@ def test_dense_sharded_process_group_native(native, tmp_path):
     np.testing.assert_array_equal(out["loc_core"], core1.cpu().numpy())
     for z in out["ranks"]:
         assert int(z["n_clusters_"]) == nc1
+
+
+# ------------------------------------------------------------ directory budget
+@pytest.mark.parametrize("name,budget", [("b2d_20k", 4096), ("b3d_20k", 4096), ("c0", 32),
+                                         ("lattice_900", 32), ("c0_p5_cityblock", 32)])
+def test_grid_growth_is_exact(native, name, budget):
+    """Cells wider than eps (the directory budget forces them to grow) give
+    sklearn's counts, core flags and labels — through pd_cluster and through
+    the partitioned train (halo, merge, border)."""
+    from pypardis_amd import DBSCAN
+    g = load_golden(name)
+    ctx = native.context()
+    ctx.set_option(native.PD_OPT_DIR_BUDGET, budget)
+    try:
+        lab, core, ncl, cnt = _cluster(native, g["X"], float(g["eps"]), int(g["min_samples"]),
+                                       _metric(g), full=True)
+        grow = ctx.timings()["grid_grow"]
+        P = int(g["max_partitions"])
+        m = DBSCAN(eps=float(g["eps"]), min_samples=int(g["min_samples"]), metric=_metric(g),
+                   max_partitions=P if P > 0 else None).train(_dev(g["X"]))
+    finally:
+        ctx.set_option(native.PD_OPT_DIR_BUDGET, 32 << 30)
+    assert grow > 1.5, grow
+    assert np.array_equal(cnt, g["sk_counts"])
+    assert np.array_equal(core, g["sk_core"])
+    assert np.array_equal(lab, g["sk_labels"]) and ncl == int(g["sk_labels"].max()) + 1
+    assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), g["sk_labels"])
+
+
+@pytest.mark.parametrize("d", [2, 3, 4])
+def test_globe_sized_extent(native, d):
+    """Clusters 1e7 eps apart on every axis (a bbox-sized directory of 1e14 -
+    1e28 cells): the cells grow to the default 32 GiB budget and the answer
+    still equals the oracle's (dense clusters, noise, a chain across cells)."""
+    rng = np.random.default_rng(40 + d)
+    eps = 0.01
+    parts = [rng.normal(scale=0.02, size=(3000, d)) + c
+             for c in (np.zeros(d), np.full(d, 1e5), np.r_[1e5, np.zeros(d - 1)])]
+    chain = np.zeros((400, d))
+    chain[:, 0] = -1.0 - 0.009 * np.arange(400)   # spacing < eps: one chain cluster
+    noise = rng.uniform(-2e5, 2e5, size=(500, d))
+    X = np.concatenate(parts + [chain, noise]).astype(np.float64)
+    lab_o, core_o, cnt_o, nc_o = oracle.dbscan(X, eps, 5)
+    lab, core, ncl, cnt = _cluster(native, X, eps, 5, full=True)
+    assert native.context().timings()["grid_grow"] > 1.0
+    assert np.array_equal(cnt, cnt_o)
+    assert np.array_equal(core, core_o)
+    assert np.array_equal(lab, lab_o) and ncl == nc_o
+    from pypardis_amd import DBSCAN
+    m = DBSCAN(eps=eps, min_samples=5, max_partitions=8).train(_dev(X))
+    assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)

@@ -577,18 +577,18 @@ def test_sharded_native_large(native, tmp_path):
 # ------------------------------------------------------------ dense (d > 4) path
 DENSE = [
     # (name, X builder, eps, min_samples, metric, max_partitions)
-    ("c3_30k", lambda: __import__("pypardis_amd").synth.make_config("C3", n=30_000)[0],
+    ("c3_30k", lambda: __import__("pypardis_amd.synth").synth.make_config("C3", n=30_000)[0],
      0.114028, 10, "euclidean", 1),
-    ("c3_wide_eps", lambda: __import__("pypardis_amd").synth.make_config("C3", n=8_000)[0],
+    ("c3_wide_eps", lambda: __import__("pypardis_amd.synth").synth.make_config("C3", n=8_000)[0],
      0.9, 25, "euclidean", 3),
-    ("d5_blobs", lambda: __import__("pypardis_amd").synth.blobs_noise(
+    ("d5_blobs", lambda: __import__("pypardis_amd.synth").synth.blobs_noise(
         20_000, 5, side=6.0, n_centers=8, sigma=0.4, seed=71), 0.3, 8, "euclidean", 1),
-    ("d100_f64", lambda: __import__("pypardis_amd").synth.blobs_noise(
+    ("d100_f64", lambda: __import__("pypardis_amd.synth").synth.blobs_noise(
         6_000, 100, side=4.0, n_centers=6, sigma=0.15, seed=72).astype(np.float64) + 1e3,
      1.6, 5, "euclidean", 1),
-    ("d200_brute", lambda: __import__("pypardis_amd").synth.blobs_noise(
+    ("d200_brute", lambda: __import__("pypardis_amd.synth").synth.blobs_noise(
         3_000, 200, side=3.0, n_centers=4, sigma=0.1, seed=73), 2.0, 5, "euclidean", 1),
-    ("d8_cityblock", lambda: __import__("pypardis_amd").synth.blobs_noise(
+    ("d8_cityblock", lambda: __import__("pypardis_amd.synth").synth.blobs_noise(
         8_000, 8, side=5.0, n_centers=6, sigma=0.3, seed=74), 1.2, 6, "cityblock", 1),
 ]
 

@@ -502,6 +502,10 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     roots = ops.select_roots(keys, gid) if nr else ops.empty(0, torch.int32)
     all_roots = comm.all_gather_var(roots).to(dev).contiguous()
     ops.sort(all_roots)
+    # one root per cluster over all ranks: only owned records carry keys
+    # (shard.hip IsRoot); a duplicate would double-count a cluster
+    if all_roots.shape[0] > 1 and bool((all_roots[1:] == all_roots[:-1]).any()):
+        raise RuntimeError("sharded train: a cluster root was selected on two ranks")
     labels = ops.rank_labels(keys, all_roots) if nr else ops.empty(0, torch.int32)
     own = owner >= 0
     lap("phase_b")

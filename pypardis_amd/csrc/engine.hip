@@ -1812,25 +1812,35 @@ __device__ __forceinline__ void word_merge(uint32_t* wroot, uint64_t w, uint32_t
 // their cell roots by a segmented shuffle scan and the segment's last lane
 // merges the result into the word atomically (a word can span two waves).
 // wroot must start at kNone.
+// Mode 6 tiers: a thread walks a cell of <= kMidCell records, a wave one of
+// <= kWordBig (mid_cell_word_root_kernel), a block a larger one
+// (big_cell_word_root_kernel).  A thread walking up to 256 records held its
+// whole wave on C4's dense cells: 55 ms of the 1B-point link.
+constexpr uint32_t kMidCell = 16, kWordBig = 1024;
+
 template <typename K>
 __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
     const uint32_t* __restrict__ cstart, const uint32_t* __restrict__ ncells,
     const K* __restrict__ keys, uint32_t* __restrict__ par, uint32_t* __restrict__ croot,
-    uint32_t* __restrict__ wroot, uint32_t* __restrict__ big, uint32_t* __restrict__ nbig) {
+    uint32_t* __restrict__ wroot, uint32_t* __restrict__ mid, uint32_t* __restrict__ nmid,
+    uint32_t* __restrict__ big, uint32_t* __restrict__ nbig) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const uint32_t nc = *ncells;
     uint32_t v = kNone;
     uint64_t word = ~0ull;
+    uint32_t sz = 0, s = 0;
     if (c < nc) {
-        const uint32_t s = cstart[c], e = cstart[c + 1];
+        s = cstart[c];
+        sz = cstart[c + 1] - s;
         word = (uint64_t)keys[s] >> 6;
-        if (e - s > kBigCell) {
-            big[atomicAdd(nbig, 1u)] = c;   // its root joins the word in big_cell_word_root
-        } else {
-            for (uint32_t r = s; r < e; ++r) v = root_merge(v, core_root(par, r));
-            croot[c] = v;
-        }
+    }
+    // the larger cells' roots join their words in the mid / big kernels
+    wave_append(mid, nmid, sz > kMidCell && sz <= kWordBig, c);
+    wave_append(big, nbig, sz > kWordBig, c);
+    if (c < nc && sz <= kMidCell) {
+        for (uint32_t r = s; r < s + sz; ++r) v = root_merge(v, core_root(par, r));
+        croot[c] = v;
     }
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1840,6 +1850,28 @@ __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
     }
     const uint64_t next = (uint64_t)__shfl_down((long long)word, 1, 64);
     if (c < nc && (lane == 63 || next != word)) word_merge(wroot, word, v);
+}
+
+template <typename K>
+__global__ __launch_bounds__(kBlock) void mid_cell_word_root_kernel(
+    const uint32_t* __restrict__ cstart, const K* __restrict__ keys,
+    const uint32_t* __restrict__ mid, const uint32_t* __restrict__ nmid,
+    uint32_t* __restrict__ par, uint32_t* __restrict__ croot, uint32_t* __restrict__ wroot) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nm = *nmid;
+    const uint32_t nw = gridDim.x * (kBlock / 64);
+    for (uint32_t i = (blockIdx.x * kBlock + threadIdx.x) >> 6; i < nm; i += nw) {
+        const uint32_t c = mid[i];
+        const uint32_t s = cstart[c], e = cstart[c + 1];
+        uint32_t v = kNone;
+        for (uint32_t r = s + lane; r < e; r += 64) v = root_merge(v, core_root(par, r));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v = root_merge(v, (uint32_t)__shfl_xor((int)v, o, 64));
+        if (lane == 0) {
+            croot[c] = v;
+            word_merge(wroot, (uint64_t)keys[s] >> 6, v);
+        }
+    }
 }
 
 template <typename K>
@@ -2636,12 +2668,15 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
         uint32_t* wroot = ctx.arena.get<uint32_t>("word_root", W);
         if (mode == 6) {   // cell and word roots in one pass
-            uint32_t* big = ctx.arena.get<uint32_t>("big_cells", R / (kBigCell + 1) + 1);
-            uint32_t* nbig = ctx.arena.get<uint32_t>("big_count", 4);
-            PD_HIP(hipMemsetAsync(nbig, 0, sizeof(uint32_t), s));
+            uint32_t* big = ctx.arena.get<uint32_t>("big_cells", R / (kWordBig + 1) + 1);
+            uint32_t* mid = ctx.arena.get<uint32_t>("mid_cells", R / (kMidCell + 1) + 1);
+            uint32_t* nbig = ctx.arena.get<uint32_t>("big_count", 4);   // [0] big, [1] mid
+            PD_HIP(hipMemsetAsync(nbig, 0, 2 * sizeof(uint32_t), s));
             PD_HIP(hipMemsetAsync(wroot, 0xFF, sizeof(uint32_t) * W, s));
             hipLaunchKernelGGL((cell_word_root_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                               cstart, dncells, keys, par, croot, wroot, big, nbig);
+                               cstart, dncells, keys, par, croot, wroot, mid, nbig + 1, big, nbig);
+            hipLaunchKernelGGL((mid_cell_word_root_kernel<K>), dim3(2048), dim3(kBlock), 0, s,
+                               cstart, keys, mid, nbig + 1, par, croot, wroot);
             hipLaunchKernelGGL((big_cell_word_root_kernel<K>), dim3(1024), dim3(kBlock), 0, s,
                                cstart, keys, big, nbig, par, croot, wroot);
         } else {

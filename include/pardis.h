@@ -331,6 +331,24 @@ int32_t pd_dense_border(pd_ctx* ctx, const uint32_t* forests, int32_t n_forests,
 int32_t pd_dense_finish(pd_ctx* ctx, const int32_t* best, int32_t* labels, uint8_t* core,
                         uint32_t* counts, int64_t* n_clusters_host, void* stream);
 
+/* The whole KD partition of one device (R:dbscan/partition.py:139-183 with
+ * min_var_split, exact sums) as one chain of launches and one host sync: the
+ * per-level decisions (largest-variance axis, the seven bounds, the balanced
+ * boundary — R:dbscan/partition.py:86-95,58-65) run on the device in the host
+ * path's fp64 operation order, so the splits equal pd_kd_pass + pd_kd_counts
+ * + host decisions bit for bit.  Levels of the BFS schedule: level l splits
+ * level_sizes[l] labels, cur[] -> newlab[] (concatenated over levels, the
+ * first level's single label 0).  labels (device int32[n], all 0 on entry)
+ * end as the partition labels.  trace_host: 13 doubles per split — axis,
+ * mean, variance, n_less for the 7 bounds, n, candidate index, boundary.
+ * lohi_host: bbox (2 d); *bad_host: non-finite coordinates.  d <= 4, labels
+ * < 256, 16-byte aligned X / labels; PD_EUNSUPPORTED otherwise (use the
+ * per-pass entry points). */
+int32_t pd_kd_build(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                    int32_t* labels, int32_t n_levels, const int32_t* level_sizes_host,
+                    const int32_t* cur_host, const int32_t* newlab_host, double* trace_host,
+                    double* lohi_host, int64_t* bad_host, void* stream);
+
 /* ---- RCCL collectives of the sharded train (one rank per device).  They
  * replace Spark's data movement: partitionBy shuffle (R:dbscan/dbscan.py:
  * 114-118) -> pd_comm_all_to_all_v; collect / broadcast of the cluster-id map

@@ -45,7 +45,7 @@ EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
            "pd_comm_unique_id", "pd_comm_init", "pd_comm_init_all", "pd_comm_destroy",
            "pd_comm_all_reduce", "pd_comm_all_gather_v", "pd_comm_all_to_all_v",
            "pd_comm_broadcast", "pd_dense_count", "pd_dense_link", "pd_dense_border",
-           "pd_dense_finish"]
+           "pd_dense_finish", "pd_kd_build"]
 
 
 class PardisError(RuntimeError):
@@ -116,6 +116,7 @@ def load():
             "pd_dense_link": ([P, P, P, P, P], I32),
             "pd_dense_border": ([P, P, I32, P, P, P], I32),
             "pd_dense_finish": ([P, P, P, P, P, P, P], I32),
+            "pd_kd_build": ([P, P, I32, I64, I32, P, I32, P, P, P, P, P, P, P], I32),
         }
         for name, (args, res) in sig.items():
             f = getattr(lib, name)
@@ -291,6 +292,31 @@ def kd_pass(X, labels, split=None, sel=(), labels_zero=False, bbox=False, ctx=No
     if bbox:
         return out, lohi[:d], lohi[d:], int(bad[0])
     return out
+
+
+PD_EUNSUPPORTED = -5
+KD_TRACE = 13
+
+
+def kd_build(X, labels, levels, ctx=None):
+    """pd_kd_build: the whole min_var BFS in one launch chain.  levels: the
+    BFS schedule (lists of (cur, new) label pairs).  Returns (lo, hi, bad,
+    trace (n_splits, 13)); raises PardisError(PD_EUNSUPPORTED) when the
+    fused path does not apply."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    sizes = np.array([len(lv) for lv in levels], np.int32)
+    cur = np.array([c for lv in levels for c, _ in lv], np.int32)
+    new = np.array([nl for lv in levels for _, nl in lv], np.int32)
+    trace = np.zeros((len(cur), KD_TRACE), np.float64)
+    lohi = np.zeros(2 * d, np.float64)
+    bad = np.zeros(1, np.int64)
+    _check(load().pd_kd_build(ctx.ptr, X.data_ptr(), dt, n, d, labels.data_ptr(), len(sizes),
+                              sizes.ctypes.data, cur.ctypes.data, new.ctypes.data,
+                              trace.ctypes.data, lohi.ctypes.data, bad.ctypes.data,
+                              _stream(X.device)))
+    return lohi[:d], lohi[d:], int(bad[0]), trace
 
 
 def round_dd(dd):

@@ -522,6 +522,20 @@ int32_t pd_scatter_results(pd_ctx* ctx, const uint32_t* pairs, int64_t m, uint32
     });
 }
 
+int32_t pd_kd_build(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, int32_t* labels,
+                    int32_t n_levels, const int32_t* sizes, const int32_t* cur, const int32_t* newlab,
+                    double* trace, double* lohi, int64_t* bad, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (n == 0) throw Error(PD_EINVAL, "kd_build of an empty set");
+        if (!labels || n_levels < 1 || !sizes || !cur || !newlab || !trace || !lohi)
+            throw Error(PD_EINVAL, "null argument");
+        if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "kd_build: d > 4");
+        kd_build(ctx->c, X, dtype, n, d, labels, n_levels, sizes, cur, newlab, trace, lohi, bad,
+                 (hipStream_t)stream);
+    });
+}
+
 // ---------------------------------------------------------------- sharded dense train
 
 int32_t pd_dense_count(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, double eps,

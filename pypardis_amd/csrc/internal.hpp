@@ -210,6 +210,11 @@ void kd_pass(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labe
              bool labels_zero, int n_split, const int32_t* ssel, const int32_t* saxis,
              const double* sbound, const int32_t* snew, int n_sel, const int32_t* sel,
              double* out_dd, double* lohi, int64_t* bad, hipStream_t s);
+// The whole min_var BFS (exact sums) in one launch chain, the level
+// decisions on the device; trace: 13 doubles per split (kd.hip kd_build).
+void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels, int n_levels,
+              const int32_t* sizes, const int32_t* cur, const int32_t* newl, double* trace_out,
+              double* lohi, int64_t* bad, hipStream_t s);
 void kd_moments_dd(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                    int n_sel, const int32_t* sel_host, double* out_host, hipStream_t s);
 void route(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P, const double* ebox_host,

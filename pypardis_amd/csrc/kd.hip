@@ -1363,6 +1363,244 @@ void kd_split(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
     sync(s);
 }
 
+// ---------------------------------------------------------------- device-decided KD
+// The whole min_var BFS of one device as one chain of launches with a single
+// host sync at the end (R:dbscan/partition.py:139-183): the level decisions
+// the host made between passes — the largest-variance axis and the seven
+// candidate bounds (R:dbscan/partition.py:86-95, 58-59), the first bound that
+// minimises |#left - #right| (:60-65) — run as one-thread-per-split kernels
+// with the host's fp64 operation order (partition.level_axes /
+// level_boundaries: same divisions, products and argmax/argmin tie rules),
+// so the splits equal the host path's bit for bit.
+// trace per split: axis, mean, var, cnt[8] (n_less per bound, n), cand, boundary.
+constexpr int kTrace = 13;
+
+__global__ void kdb_axes_kernel(const double* __restrict__ mom, int S, int D, int G,
+                                int32_t* __restrict__ axis, double* __restrict__ bounds,
+                                double* __restrict__ trace) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= S) return;
+    const double* p = mom + (size_t)k * G;
+    const double c = p[0];
+    int a = 0;
+    double best = 0.0, ma = 0.0, va = 0.0;
+    for (int j = 0; j < D; ++j) {
+        // partition.round_dd: hi + lo; level_axes: m = s / c, v = q / c - m * m
+        const double sj = __dadd_rn(p[1 + 2 * j], p[2 + 2 * j]);
+        const double qj = __dadd_rn(p[1 + 2 * D + 2 * j], p[2 + 2 * D + 2 * j]);
+        const double m = __ddiv_rn(sj, c);
+        const double v = __dsub_rn(__ddiv_rn(qj, c), __dmul_rn(m, m));
+        // np.argmax: the first NaN if any, else the first maximum
+        const bool take = j == 0 || (!isnan(best) && (isnan(v) || v > best));
+        if (take) {
+            best = v;
+            a = j;
+            ma = m;
+            va = v;
+        }
+    }
+    // partition._bounds: std = sqrt(v) (0 for v < 0, NaN stays NaN);
+    // bound i = mean + ((i - 3) * 0.3) * std
+    const double sd = isnan(va) ? va : (va >= 0.0 ? __dsqrt_rn(va) : 0.0);
+    for (int i = 0; i < 7; ++i)
+        bounds[(size_t)k * 7 + i] = __dadd_rn(ma, __dmul_rn(__dmul_rn((double)(i - 3), 0.3), sd));
+    axis[k] = a;
+    double* t = trace + (size_t)k * kTrace;
+    t[0] = (double)a;
+    t[1] = ma;
+    t[2] = va;
+}
+
+__global__ void kdb_boundary_kernel(const unsigned long long* __restrict__ cnt, int S,
+                                    const double* __restrict__ bounds,
+                                    double* __restrict__ boundary, double* __restrict__ trace) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= S) return;
+    const unsigned long long* c = cnt + (size_t)k * 8;
+    const double tot = (double)c[7];
+    // level_boundaries: |2.0 * n_less - n|, np.argmin (first minimum)
+    int bi = 0;
+    double best = fabs(__dsub_rn(__dmul_rn(2.0, (double)c[0]), tot));
+    for (int i = 1; i < 7; ++i) {
+        const double v = fabs(__dsub_rn(__dmul_rn(2.0, (double)c[i]), tot));
+        if (v < best) {
+            best = v;
+            bi = i;
+        }
+    }
+    boundary[k] = bounds[(size_t)k * 7 + bi];
+    double* t = trace + (size_t)k * kTrace;
+    for (int i = 0; i < 8; ++i) t[3 + i] = (double)c[i];
+    t[11] = (double)bi;
+    t[12] = boundary[k];
+}
+
+namespace {
+// run_pass without the host sync: the finished quantities stay on the device
+// (fin: NG x G moments, then the bbox; may be null when the pass has none).
+template <typename T, int D, bool LAB, bool SP, int NG, bool BB>
+void run_pass_dev(Ctx& ctx, const T* X, int64_t n, int32_t* labels, const SplitTab& sp, int4 sel,
+                  double* fin, hipStream_t s) {
+    constexpr int G = 1 + 4 * D, WM = NG * G, W = WM + (BB ? 2 * D + 1 : 0);
+    constexpr int TP = 4 * kBlock * ((sizeof(T) * D <= 16) ? 2 : 1);
+    static int resident = 0;
+    if (!resident) {
+        int per_cu = 0, dev = 0, cus = 0;
+        PD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(&kd_pass_kernel<T, D, LAB, SP, NG, BB>), kBlock, 0));
+        PD_HIP(hipGetDevice(&dev));
+        PD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        resident = std::max(1, per_cu) * std::max(1, cus);
+    }
+    const int nb = (int)std::min<int64_t>(resident, std::max<int64_t>(1, (n + TP - 1) / TP));
+    double* part = ctx.arena.get<double>("pass_part", (size_t)nb * (W > 0 ? W : 1));
+    hipLaunchKernelGGL((kd_pass_kernel<T, D, LAB, SP, NG, BB>), dim3(nb), dim3(kBlock), 0, s,
+                       X, (uint64_t)n, labels, sp, sel, part);
+    PD_HIP(hipGetLastError());
+    if constexpr (W > 0) {
+        hipLaunchKernelGGL(kd_finish_kernel, dim3(1), dim3(kBlock), 0, s, part, nb, WM, G, D, W,
+                           fin);
+        PD_HIP(hipGetLastError());
+    }
+}
+}  // namespace
+
+void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels, int n_levels,
+              const int32_t* sizes, const int32_t* cur, const int32_t* newl, double* trace_out,
+              double* lohi, int64_t* bad, hipStream_t s) {
+    if (n <= 0 || n_levels <= 0) throw Error(-1, "kd_build: no points or no levels");
+    if (ctx.seq_moments || !vec_ok(d, X, labels))
+        throw Error(-5, "kd_build: d <= 4, 16-byte aligned inputs and exact sums only");
+    // per level: slot_of[ntab] | axis[S] | newlab[S] | (pad 8) bounds[7 S] | boundary[S]
+    std::vector<size_t> off(n_levels + 1, 0), off_d(n_levels, 0), first(n_levels, 0);
+    std::vector<int> ntab(n_levels, 1);
+    int total = 0;
+    for (int l = 0; l < n_levels; ++l) {
+        const int S = sizes[l];
+        if (S < 1 || S > kTabLds) throw Error(-5, "kd_build: level too wide");
+        first[l] = total;
+        for (int k = 0; k < S; ++k) {
+            const int L = cur[total + k], N = newl[total + k];
+            if (L < 0 || L >= kTabLds || N < 0) throw Error(-5, "kd_build: labels beyond the LDS tables");
+            ntab[l] = std::max(ntab[l], L + 1);
+        }
+        const size_t ints = (size_t)ntab[l] + 2 * S;
+        off_d[l] = off[l] + ((sizeof(int32_t) * ints + 7) & ~size_t(7));
+        off[l + 1] = off_d[l] + sizeof(double) * 8 * S;
+        total += S;
+    }
+    char* h = (char*)pinned(ctx, off[n_levels] + sizeof(double) * ((size_t)total * kTrace + 16));
+    std::memset(h, 0, off[n_levels]);
+    for (int l = 0; l < n_levels; ++l) {
+        int32_t* slot = (int32_t*)(h + off[l]);
+        const int S = sizes[l];
+        for (int k = 0; k < ntab[l]; ++k) slot[k] = -1;
+        for (int k = 0; k < S; ++k) {
+            slot[cur[first[l] + k]] = k;
+            slot[ntab[l] + S + k] = newl[first[l] + k];   // newlab after axis
+        }
+    }
+    char* dt = ctx.arena.get<char>("kdb_tables", off[n_levels] + 64);
+    PD_HIP(hipMemcpyAsync(dt, h, off[n_levels], hipMemcpyHostToDevice, s));
+    struct Lv {
+        int32_t *slot, *axis, *newlab;
+        double *bounds, *boundary;
+    };
+    std::vector<Lv> lv(n_levels);
+    for (int l = 0; l < n_levels; ++l) {
+        const int S = sizes[l];
+        lv[l].slot = (int32_t*)(dt + off[l]);
+        lv[l].axis = lv[l].slot + ntab[l];
+        lv[l].newlab = lv[l].axis + S;
+        lv[l].bounds = (double*)(dt + off_d[l]);
+        lv[l].boundary = lv[l].bounds + 7 * S;
+    }
+    double* trace = ctx.arena.get<double>("kdb_trace", (size_t)total * kTrace);
+    unsigned long long* dcnt = ctx.arena.get<unsigned long long>("kdb_cnt", (size_t)kTabLds * 8);
+    dispatch_t(dtype, [&](auto tp) {
+        using T = std::remove_pointer_t<decltype(tp)>;
+        dispatch_d(d, [&](auto Dc) {
+            constexpr int D = decltype(Dc)::value;
+            constexpr int G = 1 + 4 * D;
+            const T* Xt = (const T*)X;
+            double* fin0 = ctx.arena.get<double>("kdb_fin0", G + 2 * D + 1);
+            double* mom = ctx.arena.get<double>("kdb_mom", (size_t)kTabLds * G);
+            const SplitTab none{nullptr, 0, nullptr, nullptr, nullptr, 0};
+            run_pass_dev<T, D, false, false, 1, true>(ctx, Xt, n, labels, none,
+                                                      make_int4(cur[0], -2, -2, -2), fin0, s);
+            for (int l = 0; l < n_levels; ++l) {
+                const int S = sizes[l];
+                const int32_t* sel = cur + first[l];
+                const double* m = fin0;
+                if (l > 0) {
+                    const Lv& p = lv[l - 1];
+                    const SplitTab sp{p.slot, ntab[l - 1], p.axis, p.boundary, p.newlab, sizes[l - 1]};
+                    for (int g0 = 0; g0 < S; g0 += kGroup) {
+                        const int ng = std::min(S - g0, kGroup);
+                        int4 sl = make_int4(-2, -2, -2, -2);
+                        for (int g = 0; g < ng; ++g) (&sl.x)[g] = sel[g0 + g];
+                        dispatch_ng(ng, [&](auto NGc) {
+                            constexpr int NG = decltype(NGc)::value;
+                            if (g0 == 0)
+                                run_pass_dev<T, D, true, true, NG, false>(ctx, Xt, n, labels, sp, sl,
+                                                                          mom, s);
+                            else
+                                run_pass_dev<T, D, true, false, NG, false>(
+                                    ctx, Xt, n, labels, none, sl, mom + (size_t)g0 * G, s);
+                        });
+                    }
+                    m = mom;
+                }
+                double* tr = trace + (size_t)first[l] * kTrace;
+                hipLaunchKernelGGL(kdb_axes_kernel, dim3(1), dim3(kTabLds), 0, s, m, S, D, G,
+                                   lv[l].axis, lv[l].bounds, tr);
+                PD_HIP(hipMemsetAsync(dcnt, 0, sizeof(unsigned long long) * S * 8, s));
+                const unsigned nb4 = grid_for((n + 3) / 4, 2048);
+                if (S <= 4) {
+                    auto go = [&](auto NSc) {
+                        constexpr int NS = decltype(NSc)::value;
+                        hipLaunchKernelGGL((counts_reg_kernel<T, D, NS>), dim3(nb4), dim3(kBlock), 0,
+                                           s, Xt, (uint64_t)n, labels, lv[l].slot, ntab[l],
+                                           lv[l].axis, lv[l].bounds, S, dcnt);
+                    };
+                    if (S == 1)
+                        go(std::integral_constant<int, 1>{});
+                    else if (S == 2)
+                        go(std::integral_constant<int, 2>{});
+                    else
+                        go(std::integral_constant<int, 4>{});
+                } else {
+                    int rep = kRep;
+                    while (rep > 1 && (size_t)rep * S * 8 * sizeof(unsigned int) > 48 * 1024) rep >>= 1;
+                    hipLaunchKernelGGL((counts4_kernel<T, D>), dim3(nb4), dim3(kBlock),
+                                       sizeof(unsigned int) * rep * S * 8, s, Xt, (uint64_t)n, labels,
+                                       lv[l].slot, ntab[l], lv[l].axis, lv[l].bounds, S, 0, rep,
+                                       dcnt);
+                }
+                PD_HIP(hipGetLastError());
+                hipLaunchKernelGGL(kdb_boundary_kernel, dim3(1), dim3(kTabLds), 0, s, dcnt, S,
+                                   lv[l].bounds, lv[l].boundary, tr);
+                PD_HIP(hipGetLastError());
+            }
+            // the last level's split alone
+            const Lv& p = lv[n_levels - 1];
+            const SplitTab sp{p.slot, ntab[n_levels - 1], p.axis, p.boundary, p.newlab,
+                              sizes[n_levels - 1]};
+            run_pass_dev<T, D, true, true, 0, false>(ctx, Xt, n, labels, sp,
+                                                     make_int4(-2, -2, -2, -2), nullptr, s);
+            // one copy back: the trace and the bbox
+            double* ht = (double*)(h + off[n_levels]);
+            PD_HIP(hipMemcpyAsync(ht, trace, sizeof(double) * total * kTrace, hipMemcpyDeviceToHost, s));
+            PD_HIP(hipMemcpyAsync(ht + (size_t)total * kTrace, fin0 + G, sizeof(double) * (2 * D + 1),
+                                  hipMemcpyDeviceToHost, s));
+            sync(s);
+            std::memcpy(trace_out, ht, sizeof(double) * total * kTrace);
+            for (int j = 0; j < 2 * D; ++j) lohi[j] = ht[(size_t)total * kTrace + j];
+            if (bad) *bad = (int64_t)ht[(size_t)total * kTrace + 2 * D];
+        });
+    });
+}
+
 void kd_radix_hist(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                    int n_sel, const int32_t* sel, const int32_t* axis, const uint64_t* prefix,
                    int shift, int64_t* out, hipStream_t s) {

@@ -52,6 +52,12 @@ def _split_schedule(max_partitions):
     return levels
 
 
+# KDPartitioner's exact min_var path: the level decisions on the device
+# (pd_kd_build, one host sync per partition) instead of one host round trip
+# per pass; False forces the per-pass path (same splits; tests compare them).
+DEVICE_DECISIONS = True
+
+
 def _bounds(mean, variance):
     """R:dbscan/partition.py:58-59, same expression order in fp64."""
     std_dev = np.sqrt(np.float64(variance) if variance >= 0 else np.float64(0.0)) \
@@ -280,6 +286,25 @@ class KDPartitioner(object):
         self.labels = torch.zeros(self.points.n, dtype=torch.int32, device=X.device)
         levels = _split_schedule(self.max_partitions)
         first = None
+        trace = None
+        if levels and self._fused() and DEVICE_DECISIONS:
+            # the whole BFS in one launch chain (pd_kd_build): the level
+            # decisions run on the device, bit-identical to the host's
+            try:
+                lo, hi, bad, trace = _native.kd_build(X, self.labels, levels)
+            except _native.PardisError as e:
+                if e.code != _native.PD_EUNSUPPORTED:
+                    raise
+        if trace is not None:
+            if bad:
+                raise ValueError("Input contains NaN or infinity.")
+            self.data_box = (lo, hi)
+            self.splits = []
+            self._apply_trace(BoundingBox(k=self.k).union(BoundingBox(lo, hi)), levels, trace)
+            self.partitions = {L: PartitionView(self.points, self.labels, L)
+                               for L in sorted(self.bounding_boxes)}
+            self.result = _Union(self.partitions)
+            return
         if levels and self._fused():
             # the bbox rides on the first level's moments pass (one read of X)
             first, lo, hi, bad = _native.kd_pass(X, self.labels, sel=[0], labels_zero=True,
@@ -295,6 +320,17 @@ class KDPartitioner(object):
         self.partitions = {L: PartitionView(self.points, self.labels, L)
                            for L in sorted(self.bounding_boxes)}
         self.result = _Union(self.partitions)
+
+    def _apply_trace(self, box, levels, trace):
+        """Boxes and split trace from pd_kd_build's per-split records."""
+        self.bounding_boxes = {0: box}
+        k = 0
+        for level in levels:
+            t = trace[k:k + len(level)]
+            k += len(level)
+            apply_level(self.bounding_boxes, self.splits, level, t[:, 0].astype(np.int64).tolist(),
+                        t[:, 1], t[:, 2], t[:, 3:11].astype(np.int64),
+                        t[:, 11].astype(np.int64).tolist(), t[:, 12])
 
     def _fused(self):
         return self.split_method == 'min_var' and self.sums == 'exact'

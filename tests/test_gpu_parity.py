@@ -859,3 +859,53 @@ def test_globe_sized_extent(native, d):
     from pypardis_amd import DBSCAN
     m = DBSCAN(eps=eps, min_samples=5, max_partitions=8).train(_dev(X))
     assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)
+
+
+# ------------------------------------------------------------ device-decided KD
+KD_DEV = [("c2_1m", 8), ("c2_1m", 13), ("c2_1m", 64), ("c4_500k", 16), ("f64_300k", 5),
+          ("ident_5k", 8), ("tiny_7", 4), ("d1_200k", 32), ("d4_300k", 256)]
+
+
+def _kd_case(name):
+    from pypardis_amd import synth
+    rng = np.random.default_rng(11)
+    if name == "c2_1m":
+        return synth.make_config("C2", n=1_000_000)[0]
+    if name == "c4_500k":
+        return synth.gps_skew(500_000, seed=8, n_cities=200).numpy()
+    if name == "f64_300k":
+        return rng.normal(size=(300_000, 3)) * np.array([1.0, 1e-3, 5.0]) + 1e4
+    if name == "ident_5k":
+        return np.full((5_000, 2), 0.5, np.float32)
+    if name == "tiny_7":
+        return rng.normal(size=(7, 3)).astype(np.float32)
+    if name == "d1_200k":
+        return rng.uniform(-1, 1, size=(200_000, 1)).astype(np.float32)
+    return rng.normal(size=(300_000, 4)).astype(np.float32)
+
+
+@pytest.mark.parametrize("name,P", KD_DEV, ids=[f"{c[0]}-P{c[1]}" for c in KD_DEV])
+def test_kd_device_decisions_equal_host(native, name, P):
+    """pd_kd_build (level decisions on the device, one sync) gives the per-pass
+    host-decided path's split trace, boxes and labels bit for bit — levels of
+    1..128 splits, fp32 / fp64, zero variance, fewer points than partitions."""
+    from pypardis_amd import KDPartitioner, partition
+    X = _kd_case(name)
+    Xd = _dev(X)
+    a = KDPartitioner(Xd, P)
+    partition.DEVICE_DECISIONS = False
+    try:
+        b = KDPartitioner(Xd, P)
+    finally:
+        partition.DEVICE_DECISIONS = True
+    sa, fa = _kd_arrays(a.splits)
+    sb, fb = _kd_arrays(b.splits)
+    assert np.array_equal(sa, sb)
+    assert np.array_equal(fa, fb, equal_nan=True)
+    assert np.array_equal(a.box_array(), b.box_array(), equal_nan=True)
+    assert torch.equal(a.labels, b.labels)
+    assert a.data_box[0].tolist() == b.data_box[0].tolist()
+    if name == "c2_1m" and P == 8:   # and the oracle's exact restatement
+        ref = oracle.kd_partition(X, P, sums="exact")
+        assert np.array_equal(sa, _kd_arrays(ref["splits"])[0])
+        assert np.array_equal(a.labels.cpu().numpy(), ref["owner"])

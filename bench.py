@@ -56,9 +56,11 @@ sys.path.insert(0, HERE)
 HBM_PEAK_GBS = 8000.0
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md; no sparsity)
 BASELINE_METRIC = "points clustered/sec (whole node), 100M 3-D pts, 1/2/4/8 GPUs; % HBM roofline"
-LINK_KERNELS = ("init_kernel", "flatten_kernel", "window_link_kernel", "centre_link_kernel",
-                "link_kernel", "link2_kernel", "cell_root_kernel", "word_root_kernel",
-                "verify_screen_kernel", "flag_list_kernel", "cell_verify_kernel", "pair_kernel")
+LINK_KERNELS = ("init_kernel", "flatten_kernel", "window_link_kernel", "window_uf_kernel",
+                "centre_link_kernel", "link_kernel", "link2_kernel", "cell_root_kernel",
+                "big_cell_root_kernel", "cell_word_root_kernel", "mid_cell_word_root_kernel",
+                "big_cell_word_root_kernel", "word_root_kernel", "verify_screen_kernel",
+                "flag_list_kernel", "cell_verify_kernel", "pair_kernel")
 
 
 def parse():

@@ -425,6 +425,12 @@ def main():
         ctx.set_option(_native.PD_OPT_SWEEP_STATS, 0)
         sweep = {k: int(v) for k, v in ctx.timings().items()
                  if k.startswith("s_") or k in ("records", "core_records")}
+        # the default link (mode 6) tallies candidates, hits and unions only;
+        # the other s_link_* slots belong to modes 0-3
+        if args.link_mode in (None, 5, 6):
+            for k in ("s_link_core", "s_link_same", "s_link_find_same"):
+                if not sweep.get(k):
+                    sweep.pop(k, None)
     ms_step = 1e3 * el / args.steps
     value = n * args.steps / el
     ncl = m.n_clusters_

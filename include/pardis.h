@@ -192,6 +192,19 @@ int32_t pd_train(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d
                  const double* data_box_host, const int32_t* owner, int32_t* labels,
                  uint8_t* core, uint32_t* counts, int64_t* n_clusters_host, void* stream);
 
+/* pd_train with the KD split tree instead of the owner labels
+ * (R:dbscan/partition.py:151-152 replayed per point inside the halo pass:
+ * level l, a point whose label has a split moves to newlab when v[axis] >=
+ * boundary): no owner array, no final split pass.  The tree in BFS order as
+ * pd_kd_build's: level_sizes_host[l] splits, then per split cur / axis /
+ * boundary / newlab (host).  d <= 4, <= 16 levels. */
+int32_t pd_train_tree(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, double eps,
+                      int32_t min_samples, int32_t metric, int32_t P, const double* ebox,
+                      const double* data_box, int32_t n_levels, const int32_t* level_sizes_host,
+                      const int32_t* cur_host, const int32_t* axis_host,
+                      const double* boundary_host, const int32_t* newlab_host, int32_t* labels,
+                      uint8_t* core, uint32_t* counts, int64_t* n_clusters, void* stream);
+
 /* ---- sharded train (one process per device; the caller moves the buffers
  * between devices, e.g. torch.distributed over RCCL).  Replaces Spark's
  * partitionBy shuffle of the halo records (R:dbscan/dbscan.py:114-118) and the
@@ -343,11 +356,13 @@ int32_t pd_dense_finish(pd_ctx* ctx, const int32_t* best, int32_t* labels, uint8
  * mean, variance, n_less for the 7 bounds, n, candidate index, boundary.
  * lohi_host: bbox (2 d); *bad_host: non-finite coordinates.  d <= 4, labels
  * < 256, 16-byte aligned X / labels; PD_EUNSUPPORTED otherwise (use the
- * per-pass entry points). */
+ * per-pass entry points).  final_split = 0 leaves the last level's split
+ * unapplied (labels then hold the previous level's; pd_train_tree replays
+ * the tree itself, pd_kd_split applies it when the labels are wanted). */
 int32_t pd_kd_build(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
                     int32_t* labels, int32_t n_levels, const int32_t* level_sizes_host,
-                    const int32_t* cur_host, const int32_t* newlab_host, double* trace_host,
-                    double* lohi_host, int64_t* bad_host, void* stream);
+                    const int32_t* cur_host, const int32_t* newlab_host, int32_t final_split,
+                    double* trace_host, double* lohi_host, int64_t* bad_host, void* stream);
 
 /* ---- RCCL collectives of the sharded train (one rank per device).  They
  * replace Spark's data movement: partitionBy shuffle (R:dbscan/dbscan.py:

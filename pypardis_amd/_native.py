@@ -45,7 +45,7 @@ EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
            "pd_comm_unique_id", "pd_comm_init", "pd_comm_init_all", "pd_comm_destroy",
            "pd_comm_all_reduce", "pd_comm_all_gather_v", "pd_comm_all_to_all_v",
            "pd_comm_broadcast", "pd_dense_count", "pd_dense_link", "pd_dense_border",
-           "pd_dense_finish", "pd_kd_build"]
+           "pd_dense_finish", "pd_kd_build", "pd_train_tree"]
 
 
 class PardisError(RuntimeError):
@@ -116,7 +116,9 @@ def load():
             "pd_dense_link": ([P, P, P, P, P], I32),
             "pd_dense_border": ([P, P, I32, P, P, P], I32),
             "pd_dense_finish": ([P, P, P, P, P, P, P], I32),
-            "pd_kd_build": ([P, P, I32, I64, I32, P, I32, P, P, P, P, P, P, P], I32),
+            "pd_kd_build": ([P, P, I32, I64, I32, P, I32, P, P, P, I32, P, P, P, P], I32),
+            "pd_train_tree": ([P, P, I32, I64, I32, D, I32, I32, I32, P, P, I32, P, P, P, P, P, P, P,
+                               P, P, P], I32),
         }
         for name, (args, res) in sig.items():
             f = getattr(lib, name)
@@ -298,7 +300,7 @@ PD_EUNSUPPORTED = -5
 KD_TRACE = 13
 
 
-def kd_build(X, labels, levels, ctx=None):
+def kd_build(X, labels, levels, final_split=True, ctx=None):
     """pd_kd_build: the whole min_var BFS in one launch chain.  levels: the
     BFS schedule (lists of (cur, new) label pairs).  Returns (lo, hi, bad,
     trace (n_splits, 13)); raises PardisError(PD_EUNSUPPORTED) when the
@@ -314,8 +316,8 @@ def kd_build(X, labels, levels, ctx=None):
     bad = np.zeros(1, np.int64)
     _check(load().pd_kd_build(ctx.ptr, X.data_ptr(), dt, n, d, labels.data_ptr(), len(sizes),
                               sizes.ctypes.data, cur.ctypes.data, new.ctypes.data,
-                              trace.ctypes.data, lohi.ctypes.data, bad.ctypes.data,
-                              _stream(X.device)))
+                              int(bool(final_split)), trace.ctypes.data, lohi.ctypes.data,
+                              bad.ctypes.data, _stream(X.device)))
     return lohi[:d], lohi[d:], int(bad[0]), trace
 
 
@@ -406,6 +408,34 @@ def train(X, eps, min_samples, metric, ebox, owner=None, data_box=None, want_cou
                            owner.data_ptr() if owner is not None else None, labels.data_ptr(),
                            core.data_ptr(), counts.data_ptr() if counts is not None else None,
                            ncl.ctypes.data, _stream(X.device)))
+    return labels, core, counts, int(ncl[0])
+
+
+def train_tree(X, eps, min_samples, metric, ebox, tree, data_box=None, want_counts=False,
+               ctx=None):
+    """pd_train_tree: pd_train with the KD split tree (sizes, cur, axis,
+    boundary, new) replayed per point instead of owner labels."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    ebox = np.ascontiguousarray(ebox, np.float64)
+    sizes, cur, axis, bound, new = (np.ascontiguousarray(tree[0], np.int32),
+                                    np.ascontiguousarray(tree[1], np.int32),
+                                    np.ascontiguousarray(tree[2], np.int32),
+                                    np.ascontiguousarray(tree[3], np.float64),
+                                    np.ascontiguousarray(tree[4], np.int32))
+    labels = torch.empty(n, dtype=torch.int32, device=X.device)
+    core = torch.empty(n, dtype=torch.uint8, device=X.device)
+    counts = torch.empty(n, dtype=torch.int32, device=X.device) if want_counts else None
+    dbox = None if data_box is None else np.ascontiguousarray(data_box, np.float64).reshape(2 * d)
+    ncl = np.zeros(1, np.int64)
+    _check(load().pd_train_tree(ctx.ptr, X.data_ptr(), dt, n, d, float(eps), int(min_samples),
+                                int(metric), ebox.shape[0], ebox.ctypes.data,
+                                dbox.ctypes.data if dbox is not None else None, len(sizes),
+                                sizes.ctypes.data, cur.ctypes.data, axis.ctypes.data,
+                                bound.ctypes.data, new.ctypes.data, labels.data_ptr(),
+                                core.data_ptr(), counts.data_ptr() if counts is not None else None,
+                                ncl.ctypes.data, _stream(X.device)))
     return labels, core, counts, int(ncl[0])
 
 

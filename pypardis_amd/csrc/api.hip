@@ -309,6 +309,46 @@ int32_t pd_train(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d
     });
 }
 
+int32_t pd_train_tree(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, double eps,
+                      int32_t min_samples, int32_t metric, int32_t P, const double* ebox,
+                      const double* data_box, int32_t n_levels, const int32_t* level_sizes,
+                      const int32_t* cur, const int32_t* axis, const double* boundary,
+                      const int32_t* newlab, int32_t* labels, uint8_t* core, uint32_t* counts,
+                      int64_t* n_clusters, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (!ebox) throw Error(PD_EINVAL, "null ebox");
+        if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "pd_train_tree: d > 4 (use pd_train)");
+        if (n_levels < 0 || n_levels > 16 ||
+            (n_levels && (!level_sizes || !cur || !axis || !boundary || !newlab)))
+            throw Error(PD_EINVAL, "bad split tree");
+        if (P > 1 && n_levels == 0) throw Error(PD_EINVAL, "P > 1 needs the split tree");
+        TrainArgs a;
+        a.X = X;
+        a.dtype = dtype;
+        a.n = n;
+        a.d = d;
+        a.eps = eps;
+        a.min_samples = min_samples;
+        a.metric = metric;
+        a.P = P;
+        a.ebox = ebox;
+        a.data_box = data_box;
+        a.tree_levels = n_levels;
+        a.tree_sizes = level_sizes;
+        a.tree_cur = cur;
+        a.tree_axis = axis;
+        a.tree_bound = boundary;
+        a.tree_new = newlab;
+        a.labels = labels;
+        a.core = core;
+        a.counts = counts;
+        a.stream = (hipStream_t)stream;
+        train(ctx->c, a);
+        if (n_clusters) *n_clusters = a.n_clusters;
+    });
+}
+
 int32_t pd_cluster(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, double eps,
                    int32_t min_samples, int32_t metric, int32_t* labels, uint8_t* core,
                    uint32_t* counts, int64_t* n_clusters, void* stream) {
@@ -524,15 +564,15 @@ int32_t pd_scatter_results(pd_ctx* ctx, const uint32_t* pairs, int64_t m, uint32
 
 int32_t pd_kd_build(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, int32_t* labels,
                     int32_t n_levels, const int32_t* sizes, const int32_t* cur, const int32_t* newlab,
-                    double* trace, double* lohi, int64_t* bad, void* stream) {
+                    int32_t final_split, double* trace, double* lohi, int64_t* bad, void* stream) {
     return guard(ctx, [&] {
         check_common(ctx, X, n, d);
         if (n == 0) throw Error(PD_EINVAL, "kd_build of an empty set");
         if (!labels || n_levels < 1 || !sizes || !cur || !newlab || !trace || !lohi)
             throw Error(PD_EINVAL, "null argument");
         if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "kd_build: d > 4");
-        kd_build(ctx->c, X, dtype, n, d, labels, n_levels, sizes, cur, newlab, trace, lohi, bad,
-                 (hipStream_t)stream);
+        kd_build(ctx->c, X, dtype, n, d, labels, n_levels, sizes, cur, newlab, final_split != 0,
+                 trace, lohi, bad, (hipStream_t)stream);
     });
 }
 

@@ -493,6 +493,41 @@ __device__ __forceinline__ int part_of_wave(const uint32_t* __restrict__ ps, int
 }
 
 // ------------------------------------------------------------------ kernels
+// The KD partition's split tree (pd_train_tree): a point's owner label is
+// found by replaying the BFS splits on its coordinates — level l, the label's
+// slot: v[axis] >= boundary moves it to the new label (the kd_pass split,
+// R:dbscan/partition.py:66-68) — so pd_train needs no owner array and the
+// partitioner no final split pass.
+struct KdTree {
+    int nl = 0;                  // levels (0: no tree)
+    int ntab[16], toff[16], eoff[16];
+    int nslot = 0, ne = 0;       // table sizes
+    const int32_t* slot;         // per level: label -> slot (-1: not split)
+    const int32_t* ax_new;       // per split: axis, new label
+    const double* bound;         // per split: boundary
+};
+// tables up to this size are staged in LDS by halo_write_kernel (P <= 64)
+constexpr int kTreeSlots = 256, kTreeSplits = 128;
+
+template <typename T, int D>
+__device__ __forceinline__ int tree_owner(const KdTree& t, const int32_t* slot,
+                                          const int32_t* ax_new, const double* bound,
+                                          const T (&v)[D]) {
+    int lab = 0;
+    for (int l = 0; l < t.nl; ++l) {
+        if (lab >= t.ntab[l]) continue;
+        const int sl = slot[t.toff[l] + lab];
+        if (sl < 0) continue;
+        const int e = t.eoff[l] + sl;
+        const int ax = ax_new[2 * e];
+        T x = v[0];
+#pragma unroll
+        for (int j = 1; j < D; ++j) x = ax == j ? v[j] : x;
+        if ((double)x >= bound[e]) lab = ax_new[2 * e + 1];
+    }
+    return lab;
+}
+
 // Halo records (R:dbscan/dbscan.py:136-151) in two ordered passes over the
 // points: halo_tile_kernel counts each tile's records (a tile = one block's
 // 4·256 points), the host scans the tile counts (rocPRIM), and
@@ -596,8 +631,8 @@ __device__ __forceinline__ K key_of(const T (&tv)[D], const KeyGrid<D>& g) {
 template <typename T, int D, typename K, bool MASK>
 __global__ __launch_bounds__(kBlock) void halo_write_kernel(
     const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
-    const int32_t* __restrict__ owner, const uint64_t* __restrict__ tile_off, K* __restrict__ keys,
-    uint32_t* __restrict__ vals) {
+    const int32_t* __restrict__ owner, KdTree tree, const uint64_t* __restrict__ tile_off,
+    K* __restrict__ keys, uint32_t* __restrict__ vals) {
     uint64_t idx[4];
     T v[4][D];
     unsigned long long m[4];
@@ -618,6 +653,14 @@ __global__ __launch_bounds__(kBlock) void halo_write_kernel(
     }
     __shared__ uint32_t ws[kBlock / 64];
     __shared__ KeyGrid<D> kg[MASK ? 64 : 1];
+    __shared__ int32_t t_slot[MASK ? kTreeSlots : 1], t_axn[MASK ? 2 * kTreeSplits : 1];
+    __shared__ double t_bd[MASK ? kTreeSplits : 1];
+    const bool tree_lds = MASK && tree.nl && tree.nslot <= kTreeSlots && tree.ne <= kTreeSplits;
+    if (tree_lds) {
+        for (int k = threadIdx.x; k < tree.nslot; k += kBlock) t_slot[k] = tree.slot[k];
+        for (int k = threadIdx.x; k < 2 * tree.ne; k += kBlock) t_axn[k] = tree.ax_new[k];
+        for (int k = threadIdx.x; k < tree.ne; k += kBlock) t_bd[k] = tree.bound[k];
+    }
     if (lane == 0) ws[w] = wtot;
     if constexpr (MASK) {
         for (int L = threadIdx.x; L < P; L += kBlock) {
@@ -637,7 +680,11 @@ __global__ __launch_bounds__(kBlock) void halo_write_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         if (!cnt[q]) continue;
-        const int own = owner ? owner[idx[q]] : 0;   // P == 1: neighbourhood 0
+        // P == 1: neighbourhood 0
+        const int own = owner  ? owner[idx[q]]
+                        : !tree.nl ? 0
+                        : tree_lds ? tree_owner<T, D>(tree, t_slot, t_axn, t_bd, v[q])
+                                   : tree_owner<T, D>(tree, tree.slot, tree.ax_new, tree.bound, v[q]);
         const uint32_t tag = (uint32_t)idx[q] | (cnt[q] >= 2 ? kDupBit : 0u);
         uint64_t o = wbase + ex[q];
         if constexpr (MASK) {
@@ -2500,12 +2547,60 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     uint32_t* vals = ctx.arena.get<uint32_t>("vals", R);
     K* keys2 = ctx.arena.get<K>("keys2", R);
     uint32_t* vals2 = ctx.arena.get<uint32_t>("vals2", R);
+    KdTree tree;
+    if (!a.owner && a.tree_levels > 0) {
+        // upload the split tree: per level a label -> slot table, per split
+        // (axis, new label) and the boundary
+        const int nl = a.tree_levels;
+        if (nl > 16) throw Error(-5, "KD split tree deeper than 16 levels");
+        std::vector<int> ntab(nl, 1), toff(nl, 0), eoff(nl, 0);
+        int nslot = 0, ne = 0;
+        for (int l = 0; l < nl; ++l) {
+            for (int k = 0; k < a.tree_sizes[l]; ++k)
+                ntab[l] = std::max(ntab[l], a.tree_cur[ne + k] + 1);
+            toff[l] = nslot;
+            eoff[l] = ne;
+            nslot += ntab[l];
+            ne += a.tree_sizes[l];
+        }
+        const size_t ib = sizeof(int32_t) * ((size_t)nslot + 2 * ne);
+        const size_t db = (ib + 7) & ~size_t(7);
+        char* h = (char*)pinned(ctx, db + sizeof(double) * ne);
+        int32_t* hs = (int32_t*)h;
+        int32_t* hx = hs + nslot;
+        double* hb = (double*)(h + db);
+        for (int k = 0; k < nslot; ++k) hs[k] = -1;
+        for (int l = 0; l < nl; ++l)
+            for (int k = 0; k < a.tree_sizes[l]; ++k) {
+                const int e = eoff[l] + k, L = a.tree_cur[e];
+                if (L < 0 || a.tree_axis[e] < 0 || a.tree_axis[e] >= D)
+                    throw Error(-1, "bad KD split tree");
+                hs[toff[l] + L] = k;
+                hx[2 * e] = a.tree_axis[e];
+                hx[2 * e + 1] = a.tree_new[e];
+                hb[e] = a.tree_bound[e];
+            }
+        char* dt = ctx.arena.get<char>("kd_tree", db + sizeof(double) * ne);
+        PD_HIP(hipMemcpyAsync(dt, h, db + sizeof(double) * ne, hipMemcpyHostToDevice, s));
+        sync(s);   // the pinned block is reused by later uploads (the halo scan already synced)
+        tree.nl = nl;
+        for (int l = 0; l < nl; ++l) {
+            tree.ntab[l] = ntab[l];
+            tree.toff[l] = toff[l];
+            tree.eoff[l] = eoff[l];
+        }
+        tree.nslot = nslot;
+        tree.ne = ne;
+        tree.slot = (const int32_t*)dt;
+        tree.ax_new = (const int32_t*)dt + nslot;
+        tree.bound = (const double*)(dt + db);
+    }
     if (P <= 64)
         hipLaunchKernelGGL((halo_write_kernel<T, D, K, true>), dim3(htiles), dim3(kBlock), 0, s, X,
-                           n, parts, P, a.owner, toff, keys, vals);
+                           n, parts, P, a.owner, tree, toff, keys, vals);
     else
         hipLaunchKernelGGL((halo_write_kernel<T, D, K, false>), dim3(htiles), dim3(kBlock), 0, s,
-                           X, n, parts, P, a.owner, toff, keys, vals);
+                           X, n, parts, P, a.owner, tree, toff, keys, vals);
     PD_HIP(hipGetLastError());
     tm.mark();   // 1
 

@@ -167,6 +167,14 @@ struct TrainArgs {
     const uint32_t* map_keys = nullptr;
     int64_t n_map = 0;
     uint32_t* keys_out = nullptr;     // device out, n: cluster key per owned point (phase 2)
+    // pd_train_tree: the KD split tree instead of `owner` (host arrays, BFS
+    // order: tree_sizes[l] splits at level l, cur -> new when v[axis] >= bound)
+    int tree_levels = 0;
+    const int32_t* tree_sizes = nullptr;
+    const int32_t* tree_cur = nullptr;
+    const int32_t* tree_axis = nullptr;
+    const double* tree_bound = nullptr;
+    const int32_t* tree_new = nullptr;
     int64_t n_exports = 0;            // out (phase 1)
 };
 
@@ -213,8 +221,8 @@ void kd_pass(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labe
 // The whole min_var BFS (exact sums) in one launch chain, the level
 // decisions on the device; trace: 13 doubles per split (kd.hip kd_build).
 void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels, int n_levels,
-              const int32_t* sizes, const int32_t* cur, const int32_t* newl, double* trace_out,
-              double* lohi, int64_t* bad, hipStream_t s);
+              const int32_t* sizes, const int32_t* cur, const int32_t* newl, bool final_split,
+              double* trace_out, double* lohi, int64_t* bad, hipStream_t s);
 void kd_moments_dd(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                    int n_sel, const int32_t* sel_host, double* out_host, hipStream_t s);
 void route(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P, const double* ebox_host,

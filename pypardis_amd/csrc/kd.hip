@@ -1466,8 +1466,8 @@ void run_pass_dev(Ctx& ctx, const T* X, int64_t n, int32_t* labels, const SplitT
 }  // namespace
 
 void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels, int n_levels,
-              const int32_t* sizes, const int32_t* cur, const int32_t* newl, double* trace_out,
-              double* lohi, int64_t* bad, hipStream_t s) {
+              const int32_t* sizes, const int32_t* cur, const int32_t* newl, bool final_split,
+              double* trace_out, double* lohi, int64_t* bad, hipStream_t s) {
     if (n <= 0 || n_levels <= 0) throw Error(-1, "kd_build: no points or no levels");
     if (ctx.seq_moments || !vec_ok(d, X, labels))
         throw Error(-5, "kd_build: d <= 4, 16-byte aligned inputs and exact sums only");
@@ -1582,12 +1582,15 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                                    lv[l].bounds, lv[l].boundary, tr);
                 PD_HIP(hipGetLastError());
             }
-            // the last level's split alone
-            const Lv& p = lv[n_levels - 1];
-            const SplitTab sp{p.slot, ntab[n_levels - 1], p.axis, p.boundary, p.newlab,
-                              sizes[n_levels - 1]};
-            run_pass_dev<T, D, true, true, 0, false>(ctx, Xt, n, labels, sp,
-                                                     make_int4(-2, -2, -2, -2), nullptr, s);
+            // the last level's split alone (or left to the caller: pd_train_tree
+            // replays the split tree, the labels are then applied lazily)
+            if (final_split) {
+                const Lv& p = lv[n_levels - 1];
+                const SplitTab sp{p.slot, ntab[n_levels - 1], p.axis, p.boundary, p.newlab,
+                                  sizes[n_levels - 1]};
+                run_pass_dev<T, D, true, true, 0, false>(ctx, Xt, n, labels, sp,
+                                                         make_int4(-2, -2, -2, -2), nullptr, s);
+            }
             // one copy back: the trace and the bbox
             double* ht = (double*)(h + off[n_levels]);
             PD_HIP(hipMemcpyAsync(ht, trace, sizeof(double) * total * kTrace, hipMemcpyDeviceToHost, s));

@@ -267,10 +267,17 @@ class DBSCAN(object):
                                for L, box in sorted(parts.bounding_boxes.items())}
         self.neighbors = _Neighborhoods(points, self.expanded_boxes)
         ebox = np.stack([self.expanded_boxes[L].as_array() for L in sorted(self.expanded_boxes)])
-        owner = parts.labels if len(ebox) > 1 else None
         lo, hi = parts.data_box
-        labels, core, _, ncl = _native.train(points.X, self.eps, self.min_samples, metric, ebox,
-                                             owner=owner, data_box=np.stack([lo, hi]))
+        tree = parts.split_tree() if len(ebox) > 1 and points.d <= 4 else None
+        if tree is not None:
+            # the owner of each point is found by replaying the KD splits in
+            # the halo pass (no owner array, no final split pass)
+            labels, core, _, ncl = _native.train_tree(points.X, self.eps, self.min_samples, metric,
+                                                      ebox, tree, data_box=np.stack([lo, hi]))
+        else:
+            owner = parts.labels if len(ebox) > 1 else None
+            labels, core, _, ncl = _native.train(points.X, self.eps, self.min_samples, metric,
+                                                 ebox, owner=owner, data_box=np.stack([lo, hi]))
         self.labels_ = labels
         self.core_sample_mask_ = core
         self.n_clusters_ = ncl

@@ -71,8 +71,12 @@ class PartitionView(object):
 
     def __init__(self, points, labels, label):
         self.points = points
-        self.labels = labels
+        self._labels = labels   # tensor, or the partitioner (labels on first use)
         self.label = int(label)
+
+    @property
+    def labels(self):
+        return self._labels.labels if isinstance(self._labels, KDPartitioner) else self._labels
 
     def indices(self):
         return torch.nonzero(self.labels == self.label).flatten()
@@ -283,7 +287,9 @@ class KDPartitioner(object):
             # astronomically large in high dimension; it would never finish
             raise ValueError(f"max_partitions={self.max_partitions} (> 65536; the default is "
                              "4**k): pass max_partitions explicitly")
-        self.labels = torch.zeros(self.points.n, dtype=torch.int32, device=X.device)
+        self._labels = torch.zeros(self.points.n, dtype=torch.int32, device=X.device)
+        self._pending = None    # the last level's split, applied on first use
+        self._tree = None       # (sizes, cur, axis, boundary, new): pd_train_tree
         levels = _split_schedule(self.max_partitions)
         first = None
         trace = None
@@ -291,7 +297,8 @@ class KDPartitioner(object):
             # the whole BFS in one launch chain (pd_kd_build): the level
             # decisions run on the device, bit-identical to the host's
             try:
-                lo, hi, bad, trace = _native.kd_build(X, self.labels, levels)
+                lo, hi, bad, trace = _native.kd_build(X, self._labels, levels,
+                                                      final_split=False)
             except _native.PardisError as e:
                 if e.code != _native.PD_EUNSUPPORTED:
                     raise
@@ -301,13 +308,20 @@ class KDPartitioner(object):
             self.data_box = (lo, hi)
             self.splits = []
             self._apply_trace(BoundingBox(k=self.k).union(BoundingBox(lo, hi)), levels, trace)
-            self.partitions = {L: PartitionView(self.points, self.labels, L)
+            last = trace[len(trace) - len(levels[-1]):]
+            self._pending = ([c for c, _ in levels[-1]], last[:, 0].astype(np.int32).tolist(),
+                             last[:, 12].tolist(), [nl for _, nl in levels[-1]])
+            self._tree = (np.array([len(lv) for lv in levels], np.int32),
+                          np.array([c for lv in levels for c, _ in lv], np.int32),
+                          trace[:, 0].astype(np.int32), trace[:, 12].copy(),
+                          np.array([nl for lv in levels for _, nl in lv], np.int32))
+            self.partitions = {L: PartitionView(self.points, self, L)
                                for L in sorted(self.bounding_boxes)}
             self.result = _Union(self.partitions)
             return
         if levels and self._fused():
             # the bbox rides on the first level's moments pass (one read of X)
-            first, lo, hi, bad = _native.kd_pass(X, self.labels, sel=[0], labels_zero=True,
+            first, lo, hi, bad = _native.kd_pass(X, self._labels, sel=[0], labels_zero=True,
                                                  bbox=True)
         else:
             lo, hi, bad = _native.bbox(X)
@@ -317,9 +331,22 @@ class KDPartitioner(object):
         box = BoundingBox(k=self.k).union(BoundingBox(lo, hi))
         self.splits = []
         self._create_partitions(box, levels, first)
-        self.partitions = {L: PartitionView(self.points, self.labels, L)
+        self.partitions = {L: PartitionView(self.points, self._labels, L)
                            for L in sorted(self.bounding_boxes)}
         self.result = _Union(self.partitions)
+
+    @property
+    def labels(self):
+        """KD label of every point (device int32, input order)."""
+        if self._pending is not None:
+            sel, axes, boundary, new = self._pending
+            self._pending = None
+            _native.kd_split(self.points.X, self._labels, sel, axes, boundary, new)
+        return self._labels
+
+    def split_tree(self):
+        """The BFS split tree for pd_train_tree (device-decided path), else None."""
+        return self._tree
 
     def _apply_trace(self, box, levels, trace):
         """Boxes and split trace from pd_kd_build's per-split records."""
@@ -336,7 +363,7 @@ class KDPartitioner(object):
         return self.split_method == 'min_var' and self.sums == 'exact'
 
     def _create_partitions(self, box, levels, first=None):
-        X, labels = self.points.X, self.labels
+        X, labels = self.points.X, self._labels
         self.bounding_boxes = {0: box}
         if self._fused():
             # per level two streaming passes: pd_kd_pass (the previous

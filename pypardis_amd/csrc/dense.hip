@@ -539,13 +539,17 @@ __global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_e
                                 ah, bh[t][s], s == 0 ? nt[u] : acc[u][t], 0, 0, 0);
                     }
                 }
+                // per query column t one maximum over the tile's 32 rows
+                // (3-input max: half the VALU work of a compare per element;
+                // the accumulators are finite), then one compare
                 bool mb = false;
 #pragma unroll
-                for (int r = 0; r < 16; ++r)
+                for (int t = 0; t < QT; ++t) {
+                    float m0 = fmaxf(acc[0][t][0], acc[1][t][0]);
 #pragma unroll
-                    for (int u = 0; u < 2; ++u)
-#pragma unroll
-                        for (int t = 0; t < QT; ++t) mb |= acc[u][t][r] >= bc[t];
+                    for (int r = 1; r < 16; ++r) m0 = fmaxf(fmaxf(m0, acc[0][t][r]), acc[1][t][r]);
+                    mb |= m0 >= bc[t];
+                }
                 refine = __any(mb);
                 nrefined += refine ? 1u : 0u;
                 if (refine) {

@@ -243,7 +243,9 @@ __device__ __forceinline__ void tile_hit(const TileArgs<T>& A, uint32_t i, uint3
 // Threads per tile block: 4 waves share each streamed tile.  (8 waves per
 // block halve the streamed bytes per MFMA but measured slower on C3: 125 vs
 // 110 ms — an 8-wave barrier per tile, one block per CU.)
-constexpr int tile_threads(int) { return 256; }
+constexpr int kCountWaves = 4;   // waves per count-pass block (each staged tile feeds them all; 8:
+                                 // 41.4 vs 36.1 ms on C3 — wider windows per block, more tiles)
+constexpr int tile_threads(int, int mode) { return mode == kCount ? 64 * kCountWaves : 256; }
 constexpr int kCountQT = 2;   // query tiles (of 32) per wave in the count pass (4: one
                               // wave per SIMD, measured 125 vs 74 ms on C3)
 
@@ -261,8 +263,8 @@ struct TileLds {
 // doubles the MFMA work per streamed byte (each staged tile feeds 2 x 4 x 3 x
 // KS MFMAs per wave) at one wave per SIMD.
 template <typename T, int MODE, int KS, int QT>
-__global__ __launch_bounds__(tile_threads(KS)) __attribute__((amdgpu_waves_per_eu((KS >= 8 || QT > 2) ? 1 : 2))) void tile_kernel(TileArgs<T> A) {
-    constexpr int TB = tile_threads(KS);
+__global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu((KS >= 8 || QT > 2) ? 1 : 2))) void tile_kernel(TileArgs<T> A) {
+    constexpr int TB = tile_threads(KS, MODE);
     constexpr int QW = 32 * QT;                  // query rows per wave
     constexpr bool LO = MODE != kCount;          // lo staged with hi (see TileLds)
     constexpr int NC = (LO ? 2 : 1) * 2 * KS * 64;   // 16-byte chunks per staged tile
@@ -926,7 +928,7 @@ void run_tiles(const TileArgs<T>& A, const Geometry& G, int metric, hipStream_t 
     if (A.I.m == 0 || A.J.m == 0) return;
     if (G.mfma) {
         auto launch = [&](auto ks) {
-            constexpr int KS = decltype(ks)::value, TB = tile_threads(KS);
+            constexpr int KS = decltype(ks)::value, TB = tile_threads(KS, MODE);
             // the count pass (the bulk of the MFMA work) takes 4 query tiles per
             // wave where the registers allow it
             constexpr int QT = (MODE == kCount && KS <= 4) ? kCountQT : 2;

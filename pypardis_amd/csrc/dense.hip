@@ -266,7 +266,10 @@ template <typename T, int MODE, int KS, int QT>
 __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu((KS >= 8 || QT > 2) ? 1 : 2))) void tile_kernel(TileArgs<T> A) {
     constexpr int TB = tile_threads(KS, MODE);
     constexpr int QW = 32 * QT;                  // query rows per wave
-    constexpr bool LO = MODE != kCount;          // lo staged with hi (see TileLds)
+    // every mode screens with hi.hi and reads lo from global memory for the
+    // tiles it keeps (link / border too: their core x core and border x core
+    // pairs are as far apart as the count pass's); LO = true would stage lo
+    constexpr bool LO = false;
     constexpr int NC = (LO ? 2 : 1) * 2 * KS * 64;   // 16-byte chunks per staged tile
     constexpr int NCH = (NC + TB - 1) / TB;      // per thread
     __shared__ TileLds<KS, LO> S;
@@ -620,7 +623,7 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
                             }
                 }
               }
-            } else {
+            } else if (refine) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
 #pragma unroll

@@ -76,6 +76,8 @@ def parse():
                     help="CPU baseline sample size (default 1M; 10M for C4; 20k for d > 15)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--link-mode", type=int, default=None, help="PD_OPT_LINK_MODE override")
+    ap.add_argument("--dir-budget", type=int, default=None,
+                    help="PD_OPT_DIR_BUDGET override (bytes of the eps-grid directory)")
     ap.add_argument("--sweep-variant", type=int, default=None,
                     help="PD_OPT_SWEEP_VARIANT override (bit 0 count, 1 link, 2 border)")
     ap.add_argument("--count-rotate", type=int, default=None,
@@ -374,7 +376,8 @@ def main():
                      (_native.PD_OPT_CENTRE_WINDOW, args.centre_window),
                      (_native.PD_OPT_COUNT_ROTATE, args.count_rotate),
                      (_native.PD_OPT_LINK_MODE, args.link_mode),
-                     (_native.PD_OPT_JUMP_ROUNDS, args.jump_rounds)):
+                     (_native.PD_OPT_JUMP_ROUNDS, args.jump_rounds),
+                     (_native.PD_OPT_DIR_BUDGET, args.dir_budget)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None

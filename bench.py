@@ -409,7 +409,9 @@ def main():
         t = ctx.timings()
         for k, v in t.items():
             stage_sum[k] = stage_sum.get(k, 0.0) + v
-        count_ms.append(t["count"])
+        # the roofline kernel's own event time (dense: the tile kernel alone;
+        # grid: the count stage is the count2 launch)
+        count_ms.append(t["count_kernel"] if t.get("count_kernel", 0) > 0 else t["count"])
         rec, cells, gcells = int(t["records"]), int(t["cells_n"]), int(t["grid_cells"])
     torch.cuda.synchronize()
     if world > 1:

@@ -118,6 +118,8 @@ enum pd_timing_slot {
     PD_T_S_LINK_FIND_SAME, PD_T_S_LINK_UNIONS, PD_T_S_VERIFY_PAIRS,
     PD_T_GRID_GROW,            /* cell width / eps of the last grid train (1 unless the
                                   directory budget made the cells grow) */
+    PD_T_COUNT_KERNEL,         /* dense path: ms of the count pass's tile kernel alone
+                                  (PD_T_COUNT includes its projection sorts) */
     PD_T_NSLOTS
 };
 

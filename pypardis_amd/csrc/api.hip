@@ -182,7 +182,8 @@ int32_t pd_ctx_timings(pd_ctx* ctx, double* out, int32_t n) {
                                        (double)t.sweep[0], (double)t.sweep[1],
                                        (double)t.sweep[2], (double)t.sweep[3],
                                        (double)t.sweep[4], (double)t.sweep[5],
-                                       (double)t.sweep[6], (double)t.sweep[7], t.grid_grow};
+                                       (double)t.sweep[6], (double)t.sweep[7], t.grid_grow,
+                                       (double)t.count_kernel};
         for (int i = 0; i < n && i < PD_T_NSLOTS; ++i) out[i] = v[i];
     });
 }

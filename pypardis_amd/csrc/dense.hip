@@ -1150,7 +1150,14 @@ void count_stage(Ctx& ctx, TrainArgs& a, int rank, int world) {
         A.win = a.eps * (1.0 + 1.0 / 1048576.0) + 16.0 * amax * DBL_EPSILON;
         A.tiles = dtiles;
         A.cnt = cs;
+        // the roofline kernel's own time (events around the launch alone)
+        if (ctx.timing) {
+            for (int k = 14; k < 16; ++k)
+                if (!ctx.ev[k]) PD_HIP(hipEventCreate(&ctx.ev[k]));
+            PD_HIP(hipEventRecord(ctx.ev[14], s));
+        }
         run_tiles<T, kCount>(A, G, a.metric, s);
+        if (ctx.timing) PD_HIP(hipEventRecord(ctx.ev[15], s));
         hipLaunchKernelGGL(scatter_cnt_kernel, dim3(nblocks(n)), dim3(kBlock), 0, s, cs, sid, n,
                            cnt);
         PD_HIP(hipGetLastError());
@@ -1277,6 +1284,12 @@ void run_dense(Ctx& ctx, TrainArgs& a) {
         PD_HIP(hipMemcpy(nt, ds.tiles, sizeof(nt), hipMemcpyDeviceToHost));
         ctx.t.cells_n = (int64_t)nt[0];
         ctx.t.grid_cells = (int64_t)nt[1];
+    }
+    ctx.t.count_kernel = 0;
+    if (ctx.timing && ds.tiles && ctx.ev[14] && ctx.ev[15]) {
+        float ms = 0;
+        PD_HIP(hipEventElapsedTime(&ms, ctx.ev[14], ctx.ev[15]));
+        ctx.t.count_kernel = ms;
     }
     if (ctx.timing) {
         ctx.t.count = ev.span(0, 1);

@@ -51,6 +51,7 @@ struct Timings {
     // cell pairs tested record by record (link mode 3)
     int64_t sweep[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     double grid_grow = 1.0;      // cell width / eps (PD_OPT_DIR_BUDGET)
+    float count_kernel = 0;      // dense path: the count pass's tile kernel alone (ms)
 };
 
 // Device state carried from phase A (local clustering) to phase B (border

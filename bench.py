@@ -451,6 +451,8 @@ def main():
         stages = {k: round(v / args.steps, 3) for k, v in stage_sum.items()
                   if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records")
                   and not k.startswith("s_")}
+        if not stages.get("count_kernel"):
+            stages.pop("count_kernel", None)   # dense path only
         # KD partition + host work around pd_train (wall time, not events)
         stages["outside_train"] = round(ms_step - stages.get("total", 0.0), 3)
         pmc, pmc_src = load_pmc(args.config)

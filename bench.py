@@ -211,6 +211,8 @@ def cpu_baseline(cfg_name, n_sample, n_full, d):
 
 def grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages):
     alg_bytes, per = b_nc(rec, cells, d)
+    if not t_cnt > 0:   # no kernel time recorded (never expected): no rate, no crash
+        t_cnt = 1e30
     achieved = alg_bytes / (t_cnt * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
@@ -271,6 +273,8 @@ def dense_roofline(n, d, t_cnt, cells, pmc, pmc_src, refined=None):
     refined = tiles if refined is None else refined
     alg = 2.0 * d * 64 * 64 * tiles
     exe = 2.0 * 64 * 64 * 16 * ks * (tiles + 2 * refined)
+    if not t_cnt > 0:   # no kernel time recorded (never expected): no rate, no crash
+        t_cnt = 1e30
     achieved = alg / (t_cnt * 1e-3) / 1e12
     roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS,

@@ -1326,10 +1326,23 @@ void dense_count(Ctx& ctx, TrainArgs& a, int rank, int world, uint32_t* counts_o
     if (a.n >= 0x7FFFFFFFll) throw Error(-5, "sharded dense path: n must be < 2^31 - 1");
     if (world < 1 || rank < 0 || rank >= world) throw Error(-1, "bad rank / world");
     ctx.st.valid = false;
+    ctx.t = Timings{};
     by_dtype(a.dtype, [&](auto t) { count_stage<decltype(t)>(ctx, a, rank, world); });
     if (a.n)
         PD_HIP(hipMemcpyAsync(counts_out, ctx.dn.cnt, sizeof(uint32_t) * a.n,
                               hipMemcpyDeviceToDevice, a.stream));
+    if (ctx.timing && ctx.dn.tiles && ctx.ev[14] && ctx.ev[15]) {
+        // this rank's share of the count pass (PD_T_COUNT / PD_T_COUNT_KERNEL)
+        sync(a.stream);
+        float ms = 0;
+        PD_HIP(hipEventElapsedTime(&ms, ctx.ev[14], ctx.ev[15]));
+        unsigned long long nt[2] = {0, 0};
+        PD_HIP(hipMemcpy(nt, ctx.dn.tiles, sizeof(nt), hipMemcpyDeviceToHost));
+        ctx.t.count = ctx.t.count_kernel = ms;
+        ctx.t.records = a.n;
+        ctx.t.cells_n = (int64_t)nt[0];
+        ctx.t.grid_cells = (int64_t)nt[1];
+    }
 }
 
 uint32_t dense_link(Ctx& ctx, const uint32_t* counts, uint32_t* forest_out, hipStream_t s) {

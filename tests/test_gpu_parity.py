@@ -909,3 +909,20 @@ def test_kd_device_decisions_equal_host(native, name, P):
         ref = oracle.kd_partition(X, P, sums="exact")
         assert np.array_equal(sa, _kd_arrays(ref["splits"])[0])
         assert np.array_equal(a.labels.cpu().numpy(), ref["owner"])
+
+
+@pytest.mark.parametrize("P", [300, 1000])
+def test_train_many_partitions_fallbacks(native, P):
+    """Many partitions: P = 300 keeps the device-decided KD (split labels <
+    256) with the split tree replayed from global memory in the unmasked
+    halo kernel (P > 64); P = 1000 has split labels beyond the LDS tables, so
+    KDPartitioner falls back to the per-pass path and DBSCAN.train to owner
+    labels — labels the oracle's either way."""
+    from pypardis_amd import DBSCAN, synth
+    X, cfg = synth.make_config("C2", n=200_000)
+    lab_o, core_o, _, nc_o = oracle.dbscan(X, cfg["eps"], cfg["min_samples"])
+    m = DBSCAN(eps=cfg["eps"], min_samples=cfg["min_samples"], max_partitions=P).train(_dev(X))
+    assert (m.partitioner.split_tree() is None) == (P > 512)
+    assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)
+    assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_o)
+    assert m.n_clusters_ == nc_o and len(m.bounding_boxes) == P

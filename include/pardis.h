@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PD_ABI_VERSION 2
+#define PD_ABI_VERSION 3
 
 enum pd_status {
     PD_OK = 0,
@@ -84,7 +84,10 @@ enum pd_option {
                                identical): bit 0 count, bit 1 link, bit 2 border; a set bit
                                selects the batched lane kernel (wave-uniform grid in scalar
                                registers, three rows swept as one list), a clear bit the
-                               row-by-row kernel.  Default 5 (the measured best on MI355X). */
+                               row-by-row kernel; bit 3 (count) the persistent-lane kernel
+                               (lanes take the next record of their wave's chunk when they
+                               finish; overrides bit 0).  Default 13 (the measured best on
+                               MI355X). */
     PD_OPT_BORDER_ROOTS = 10, /* batched border sweep: skip or stop early where the stencil's
                                 directory words hold at most one cluster root (tuning; same
                                 labels; default 0 — slower on C2) */
@@ -257,7 +260,8 @@ int32_t pd_pack(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
                 int64_t capacity, int64_t* m_host, void* stream);
 
 /* Phase A on this device's neighbourhoods (arguments as pd_train; gid[n] =
- * global id of each local point, xr[n] = point also lives on another device).
+ * global id of each local point (null: the identity, a one-rank group), xr[n]
+ * = point also lives on another device (null: none does)).
  * *n_exports_host = number of (global id, component key) exports. */
 int32_t pd_train_begin(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
                        double eps, int32_t min_samples, int32_t metric, int32_t P,
@@ -366,6 +370,73 @@ int32_t pd_kd_build(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_
                     const int32_t* cur_host, const int32_t* newlab_host, int32_t final_split,
                     double* trace_host, double* lohi_host, int64_t* bad_host, void* stream);
 
+/* ---- Sharded train, device-resident variant (no host round trip per KD
+ * level, one ordered pass per exchange side).  The KD partition of
+ * R:dbscan/partition.py:139-183 (min_var_split, exact sums) split at its
+ * collectives: per level l of the BFS schedule (as pd_kd_build's)
+ *   pd_kdx_moments  -> out: this slice's partials, S_l x (1 + 4d) doubles (+ the
+ *                      bbox, 2d + 1 doubles, on level 0)  [caller: all-gather,
+ *                      rank order -> n_ranks x len]
+ *   pd_kdx_axes     <- the gathered partials: exact rank-order fold, the split
+ *                      axes and 7 bounds (R:dbscan/partition.py:86-95,58-59)
+ *   pd_kdx_counts   -> out: S_l x 8 u64 n_less / n of this slice
+ *                      [caller: all-reduce SUM, u64]
+ *   pd_kdx_boundary <- the summed counts: the balanced bound (:60-65)
+ * then pd_kdx_end: the last level's split (final_split), the trace (13 doubles
+ * per split, as pd_kd_build) and the global bbox to the host (one sync).  The
+ * splits equal the single-device pd_kd_build's bit for bit.  Every rank calls
+ * every step (an empty slice contributes zeros).  d <= 4. */
+int32_t pd_kdx_begin(pd_ctx* ctx, int32_t d, int32_t n_levels, const int32_t* level_sizes_host,
+                     const int32_t* cur_host, const int32_t* newlab_host, void* stream);
+int32_t pd_kdx_moments(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                       int32_t* labels, int32_t level, double* out, void* stream);
+int32_t pd_kdx_axes(pd_ctx* ctx, const double* gathered, int32_t n_ranks, int32_t level,
+                    void* stream);
+int32_t pd_kdx_counts(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                      const int32_t* labels, int32_t level, uint64_t* out, void* stream);
+int32_t pd_kdx_boundary(pd_ctx* ctx, const uint64_t* counts, int32_t level, void* stream);
+int32_t pd_kdx_end(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                   int32_t* labels, int32_t final_split, double* trace_host, double* lohi_host,
+                   int64_t* bad_host, void* stream);
+
+/* The partitionBy shuffle of the halo records (R:dbscan/dbscan.py:114-118) in
+ * two ordered passes over the slice.  pd_route2: destination mask of every
+ * point (kept in the context) and counts_host[2 r] = points routed to rank r,
+ * counts_host[2 r + 1] = those of them rank r owns (kdlab's partition lives
+ * there) — the sizes of the results that come back.  pd_pack2 (same context,
+ * next call): every point written to each of its destinations in ascending
+ * local index, into per-destination buffers given as host arrays of device
+ * pointers (coords[r], gid[r], owner[r], xr[r]; null where nothing is routed):
+ * pack the self block straight into the receive buffers and the rest into
+ * the send buffers of pd_comm_exchange.  Fields as pd_pack. */
+int32_t pd_route2(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, int32_t P,
+                  const double* ebox_host, const int32_t* part_rank_host, const int32_t* kdlab,
+                  int32_t n_ranks, int64_t* counts_host, void* stream);
+int32_t pd_pack2(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                 const int32_t* kdlab, int32_t P, const int32_t* part_rank_host,
+                 const int32_t* local_index_host, uint32_t gid_base, int32_t n_ranks,
+                 void* const* coords_host, uint32_t* const* gid_host, int32_t* const* owner_host,
+                 uint8_t* const* xr_host, void* stream);
+
+/* Results back to the ranks holding the points (R:dbscan/dbscan.py:162-164):
+ * after pd_train_end (keys) and the gathered, sorted roots of all ranks.  The
+ * nr records arrived grouped by source rank (src_offsets_host[n_ranks + 1]);
+ * the owned ones of this rank's own block are written straight into
+ * labels[n_local] / core_out (gid - gid_base), the others compacted in order
+ * as pairs (gid, (label + 1) | core << 31) — block by block, i.e. destination
+ * by destination — expect_remote of them (the exchanged owned counts).  gid
+ * may be null (identity: a one-rank group).  pd_results_scatter adds the
+ * pairs received from the other ranks and checks (one sync) that every point
+ * got exactly one label and every key has a root: PD_EINVAL otherwise. */
+int32_t pd_results(pd_ctx* ctx, int64_t nr, const uint32_t* keys, const uint8_t* core,
+                   const int32_t* owner, const uint32_t* gid, const uint32_t* roots,
+                   int64_t n_roots, int64_t n_total, uint32_t gid_base, int64_t n_local,
+                   int32_t n_ranks, int32_t rank, const int64_t* src_offsets_host,
+                   int64_t expect_remote, int32_t* labels, uint8_t* core_out, uint32_t* pairs,
+                   void* stream);
+int32_t pd_results_scatter(pd_ctx* ctx, const uint32_t* pairs, int64_t m, uint32_t gid_base,
+                           int64_t n, int32_t* labels, uint8_t* core, void* stream);
+
 /* ---- RCCL collectives of the sharded train (one rank per device).  They
  * replace Spark's data movement: partitionBy shuffle (R:dbscan/dbscan.py:
  * 114-118) -> pd_comm_all_to_all_v; collect / broadcast of the cluster-id map
@@ -399,6 +470,24 @@ int32_t pd_comm_all_to_all_v(pd_comm* comm, const void* send, const int64_t* sen
                              void* stream);
 int32_t pd_comm_broadcast(pd_comm* comm, void* buf, int64_t count, int32_t elem, int32_t root,
                           void* stream);
+/* n_fields buffers exchanged in ONE group (the halo-record fields of the
+ * partitionBy shuffle): block r of field f = rec_bytes[f] * counts[r] bytes at
+ * rec_bytes[f] * offsets[r] (send grouped by destination, recv by source;
+ * all host arrays of n_ranks).  skip_self != 0: the self blocks are already in
+ * place in recv (pd_pack2 wrote them). */
+int32_t pd_comm_exchange(pd_comm* comm, int32_t n_fields, const void* const* send_host,
+                         void* const* recv_host, const int64_t* rec_bytes_host,
+                         const int64_t* send_counts_host, const int64_t* send_offsets_host,
+                         const int64_t* recv_counts_host, const int64_t* recv_offsets_host,
+                         int32_t skip_self, void* stream);
+/* ncclCommAbort: releases every rank blocked on this communicator (a rank of
+ * a one-process group failed); the communicator is unusable afterwards. */
+int32_t pd_comm_abort(pd_comm* comm);
+/* The check pd_comm_init / pd_comm_init_all run when n_ranks > 1 (unless
+ * PD_COMM_SELF_CHECK=0): one all_to_all_v (uneven and zero-sized blocks) and
+ * one all_gather_v with a known rank pattern, verified on the device;
+ * PD_ERCCL on a mismatch.  Collective; callable at any n_ranks. */
+int32_t pd_comm_self_check(pd_comm* comm);
 
 #ifdef __cplusplus
 }

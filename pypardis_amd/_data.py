@@ -67,6 +67,8 @@ def _to_tensor(X, device):
 
 
 def _keys(keys):
+    if isinstance(keys, torch.Tensor):
+        keys = keys.detach().cpu().numpy()
     try:
         a = np.asarray(keys)
         if a.dtype.kind in "iu":
@@ -88,6 +90,9 @@ def _is_keys_and_matrix(data):
     keys, X = data
     if not isinstance(X, (np.ndarray, torch.Tensor)) or X.ndim not in (1, 2):
         return False
+    if isinstance(keys, (np.ndarray, torch.Tensor)):
+        # a 1-D key array (its elements are 0-d arrays / tensors, not scalars)
+        return keys.ndim == 1 and len(keys) == len(X)
     try:
         return len(keys) == len(X) and all(np.isscalar(k) for k in keys[:8])
     except TypeError:

@@ -28,7 +28,7 @@ PD_OPT_DENSE_PRUNE = 11
 PD_OPT_COUNT_ROTATE = 12
 PD_OPT_CENTRE_WINDOW = 13
 PD_OPT_DIR_BUDGET = 14
-SWEEP_VARIANT_DEFAULT = 5
+SWEEP_VARIANT_DEFAULT = 13
 LINK_MODE_DEFAULT = 6
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
@@ -46,7 +46,10 @@ EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
            "pd_comm_unique_id", "pd_comm_init", "pd_comm_init_all", "pd_comm_destroy",
            "pd_comm_all_reduce", "pd_comm_all_gather_v", "pd_comm_all_to_all_v",
            "pd_comm_broadcast", "pd_dense_count", "pd_dense_link", "pd_dense_border",
-           "pd_dense_finish", "pd_kd_build", "pd_train_tree"]
+           "pd_dense_finish", "pd_kd_build", "pd_train_tree", "pd_kdx_begin", "pd_kdx_moments",
+           "pd_kdx_axes", "pd_kdx_counts", "pd_kdx_boundary", "pd_kdx_end", "pd_route2",
+           "pd_pack2", "pd_results", "pd_results_scatter", "pd_comm_exchange", "pd_comm_abort",
+           "pd_comm_self_check"]
 
 
 class PardisError(RuntimeError):
@@ -120,6 +123,20 @@ def load():
             "pd_kd_build": ([P, P, I32, I64, I32, P, I32, P, P, P, I32, P, P, P, P], I32),
             "pd_train_tree": ([P, P, I32, I64, I32, D, I32, I32, I32, P, P, I32, P, P, P, P, P, P, P,
                                P, P, P], I32),
+            "pd_kdx_begin": ([P, I32, I32, P, P, P, P], I32),
+            "pd_kdx_moments": ([P, P, I32, I64, I32, P, I32, P, P], I32),
+            "pd_kdx_axes": ([P, P, I32, I32, P], I32),
+            "pd_kdx_counts": ([P, P, I32, I64, I32, P, I32, P, P], I32),
+            "pd_kdx_boundary": ([P, P, I32, P], I32),
+            "pd_kdx_end": ([P, P, I32, I64, I32, P, I32, P, P, P, P], I32),
+            "pd_route2": ([P, P, I32, I64, I32, I32, P, P, P, I32, P, P], I32),
+            "pd_pack2": ([P, P, I32, I64, I32, P, I32, P, P, U32, I32, P, P, P, P, P], I32),
+            "pd_results": ([P, I64, P, P, P, P, P, I64, I64, U32, I64, I32, I32, P, I64, P, P, P,
+                            P], I32),
+            "pd_results_scatter": ([P, P, I64, U32, I64, P, P, P], I32),
+            "pd_comm_exchange": ([P, I32, P, P, P, P, P, P, P, I32, P], I32),
+            "pd_comm_abort": ([P], I32),
+            "pd_comm_self_check": ([P], I32),
         }
         for name, (args, res) in sig.items():
             f = getattr(lib, name)
@@ -494,6 +511,132 @@ def pack(X, mask, dest, kdlab, part_rank, local_index, gid_base, out, ctx=None):
     return int(m[0])
 
 
+# ---- device-decided sharded KD (pd_kdx_*): tensors stay on the device
+def _ptr(t):
+    return t.data_ptr() if t is not None and t.numel() else None
+
+
+def kdx_begin(d, levels, device, ctx=None):
+    ctx = ctx or context(device)
+    sizes = np.array([len(lv) for lv in levels], np.int32)
+    cur = np.array([c for lv in levels for c, _ in lv], np.int32)
+    new = np.array([nl for lv in levels for _, nl in lv], np.int32)
+    _check(load().pd_kdx_begin(ctx.ptr, int(d), len(levels), sizes.ctypes.data, cur.ctypes.data,
+                               new.ctypes.data, _stream(device)))
+
+
+def kdx_part_len(S, d, level):
+    return S * (1 + 4 * d) + (2 * d + 1 if level == 0 else 0)
+
+
+def kdx_moments(X, labels, level, S, ctx=None):
+    """This slice's moment partials of level `level` (device float64)."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    out = torch.empty(kdx_part_len(S, d, level), dtype=torch.float64, device=X.device)
+    _check(load().pd_kdx_moments(ctx.ptr, X.data_ptr() if n else None, dt, n, d, _ptr(labels),
+                                 int(level), out.data_ptr(), _stream(X.device)))
+    return out
+
+
+def kdx_axes(gathered, n_ranks, level, ctx=None):
+    g = gathered.contiguous()
+    ctx = ctx or context(g.device.index)
+    _check(load().pd_kdx_axes(ctx.ptr, g.data_ptr(), int(n_ranks), int(level), _stream(g.device)))
+
+
+def kdx_counts(X, labels, level, S, ctx=None):
+    """This slice's n_less / n per split of the level (device int64, S x 8)."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    out = torch.empty(8 * S, dtype=torch.int64, device=X.device)
+    _check(load().pd_kdx_counts(ctx.ptr, X.data_ptr() if n else None, dt, n, d, _ptr(labels),
+                                int(level), out.data_ptr(), _stream(X.device)))
+    return out
+
+
+def kdx_boundary(counts, level, ctx=None):
+    c = counts.contiguous()
+    ctx = ctx or context(c.device.index)
+    _check(load().pd_kdx_boundary(ctx.ptr, c.data_ptr(), int(level), _stream(c.device)))
+
+
+def kdx_end(X, labels, n_splits, final_split, ctx=None):
+    """-> (trace (n_splits, 13), lo, hi, non-finite count) on the host."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    trace = np.zeros((n_splits, 13), np.float64)
+    lohi = np.zeros(2 * d, np.float64)
+    bad = np.zeros(1, np.int64)
+    _check(load().pd_kdx_end(ctx.ptr, X.data_ptr() if n else None, dt, n, d, _ptr(labels),
+                             1 if final_split else 0, trace.ctypes.data, lohi.ctypes.data,
+                             bad.ctypes.data, _stream(X.device)))
+    return trace, lohi[:d].copy(), lohi[d:].copy(), int(bad[0])
+
+
+def route2(X, ebox, part_rank, kdlab, n_ranks, ctx=None):
+    """Destination masks (kept in the context for pack2) and per rank
+    (points routed there, of which it owns) — int64 (n_ranks, 2), host."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    ebox = np.ascontiguousarray(ebox, np.float64)
+    part_rank = np.ascontiguousarray(part_rank, np.int32)
+    counts = np.zeros((n_ranks, 2), np.int64)
+    _check(load().pd_route2(ctx.ptr, X.data_ptr() if n else None, dt, n, d, ebox.shape[0],
+                            ebox.ctypes.data, part_rank.ctypes.data, _ptr(kdlab), int(n_ranks),
+                            counts.ctypes.data, _stream(X.device)))
+    return counts
+
+
+def pack2(X, kdlab, part_rank, local_index, gid_base, outs, ctx=None):
+    """outs[r] = (coords (m_r, d), gid int32[m_r], owner int32[m_r], xr uint8[m_r])
+    device views, one per rank (after route2 on the same context)."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    W = len(outs)
+    part_rank = np.ascontiguousarray(part_rank, np.int32)
+    local_index = np.ascontiguousarray(local_index, np.int32)
+    tabs = [np.array([_ptr(o[f]) or 0 for o in outs], np.uint64) for f in range(4)]
+    _check(load().pd_pack2(ctx.ptr, X.data_ptr() if n else None, dt, n, d, _ptr(kdlab),
+                           len(part_rank), part_rank.ctypes.data, local_index.ctypes.data,
+                           int(gid_base), W, tabs[0].ctypes.data, tabs[1].ctypes.data,
+                           tabs[2].ctypes.data, tabs[3].ctypes.data, _stream(X.device)))
+
+
+def results(keys, core, owner, gid, roots, n_total, gid_base, n_local, n_ranks, rank, src_off,
+            expect_remote, device, ctx=None):
+    """Labels / core flags of this rank's points from the owned records of its
+    own block; the other owned records as (gid, (label + 1) | core << 31)
+    pairs, block by block.  -> (labels int32[n_local], core uint8[n_local],
+    pairs int32 (expect_remote, 2)), all on the device."""
+    ctx = ctx or context(device)
+    nr = keys.shape[0]
+    labels = torch.empty(max(n_local, 1), dtype=torch.int32, device=device)
+    core_out = torch.empty(max(n_local, 1), dtype=torch.uint8, device=device)
+    pairs = torch.empty((max(expect_remote, 1), 2), dtype=torch.int32, device=device)
+    src = np.ascontiguousarray(src_off, np.int64)
+    _check(load().pd_results(ctx.ptr, nr, _ptr(keys), _ptr(core), _ptr(owner), _ptr(gid),
+                             _ptr(roots), roots.shape[0], int(n_total), int(gid_base),
+                             int(n_local), int(n_ranks), int(rank), src.ctypes.data,
+                             int(expect_remote), labels.data_ptr(), core_out.data_ptr(),
+                             pairs.data_ptr(), _stream(device)))
+    return labels[:n_local], core_out[:n_local], pairs[:expect_remote]
+
+
+def results_scatter(pairs, gid_base, labels, core, ctx=None):
+    device = labels.device
+    ctx = ctx or context(device.index)
+    m = pairs.shape[0]
+    p = pairs.contiguous()
+    _check(load().pd_results_scatter(ctx.ptr, _ptr(p), m, int(gid_base), labels.shape[0],
+                                     _ptr(labels), _ptr(core), _stream(device)))
+
+
 def train_begin(X, eps, min_samples, metric, ebox, owner, gid, xr, data_box, ctx=None):
     """Phase A of a sharded train; returns the number of exports."""
     dt = _check_points(X)
@@ -505,7 +648,7 @@ def train_begin(X, eps, min_samples, metric, ebox, owner, gid, xr, data_box, ctx
     _check(load().pd_train_begin(ctx.ptr, X.data_ptr() if n else None, dt, n, d, float(eps),
                                  int(min_samples), int(metric), ebox.shape[0], ebox.ctypes.data,
                                  dbox.ctypes.data, owner.data_ptr() if n else None,
-                                 gid.data_ptr() if n else None, xr.data_ptr() if n else None,
+                                 _ptr(gid) if n else None, _ptr(xr) if n else None,
                                  ne.ctypes.data, _stream(X.device)))
     return int(ne[0])
 
@@ -750,6 +893,38 @@ class Comm:
                                            rc.ctypes.data, self._elem(send),
                                            _stream(self.device)))
         return out
+
+    def exchange(self, sends, recvs, send_counts, recv_counts, skip_self=True):
+        """Fields exchanged in one group: sends[f] rows grouped by destination
+        (send_counts), recvs[f] rows grouped by source (recv_counts); with
+        skip_self the self block is already in place in recvs[f]."""
+        W = self.world
+        sc = np.ascontiguousarray(send_counts, np.int64)
+        rc = np.ascontiguousarray(recv_counts, np.int64)
+        # send buffers hold the other ranks' blocks only when the self block
+        # was packed in place
+        se = sc.copy()
+        if skip_self:
+            se[self.rank] = 0
+        so = np.ascontiguousarray(np.concatenate([[0], np.cumsum(se)[:-1]]), np.int64)
+        ro = np.ascontiguousarray(np.concatenate([[0], np.cumsum(rc)[:-1]]), np.int64)
+        rb = np.array([t.element_size() * (int(np.prod(t.shape[1:])) if t.dim() > 1 else 1)
+                       for t in recvs], np.int64)
+        sp = np.array([_ptr(t) or 0 for t in sends], np.uint64)
+        rp = np.array([_ptr(t) or 0 for t in recvs], np.uint64)
+        if len(sends) != len(recvs) or len(sc) != W or len(rc) != W:
+            raise ValueError("exchange: one send and one recv per field, counts per rank")
+        _check(load().pd_comm_exchange(self.ptr, len(sends), sp.ctypes.data, rp.ctypes.data,
+                                       rb.ctypes.data, sc.ctypes.data, so.ctypes.data,
+                                       rc.ctypes.data, ro.ctypes.data, 1 if skip_self else 0,
+                                       _stream(self.device)))
+
+    def abort(self):
+        if self.ptr:
+            load().pd_comm_abort(self.ptr)
+
+    def self_check(self):
+        _check(load().pd_comm_self_check(self.ptr))
 
     def broadcast(self, t, root=0):
         _check(load().pd_comm_broadcast(self.ptr, t.data_ptr(), t.numel(), self._elem(t),

@@ -150,7 +150,7 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         } else if (option == PD_OPT_BORDER_ROOTS)
             ctx->c.border_roots = value != 0;
         else if (option == PD_OPT_SWEEP_VARIANT) {
-            if (value < 0 || value > 7) throw Error(PD_EINVAL, "sweep variant is a 3-bit mask");
+            if (value < 0 || value > 15) throw Error(PD_EINVAL, "sweep variant is a 4-bit mask");
             ctx->c.variant = (int)value;
         } else if (option == PD_OPT_COUNT_ROTATE) {
             if (value < 0 || value > 0x7FFFFFFF) throw Error(PD_EINVAL, "count rotate must be >= 0");
@@ -458,7 +458,8 @@ int32_t pd_train_begin(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int
     return guard(ctx, [&] {
         check_common(ctx, X, n, d);
         if (!ebox) throw Error(PD_EINVAL, "null ebox");
-        if (n > 0 && (!owner || !gid || !xr)) throw Error(PD_EINVAL, "owner, gid and xr required");
+        // gid null: identity (one rank); xr null: no point lives on another rank
+        if (n > 0 && !owner) throw Error(PD_EINVAL, "owner required");
         TrainArgs a;
         a.X = X;
         a.dtype = dtype;
@@ -577,6 +578,115 @@ int32_t pd_kd_build(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_
     });
 }
 
+// ---------------------------------------------------------------- sharded device-decided KD
+int32_t pd_kdx_begin(pd_ctx* ctx, int32_t d, int32_t n_levels, const int32_t* sizes,
+                     const int32_t* cur, const int32_t* newlab, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || !sizes || !cur || !newlab) throw Error(PD_EINVAL, "null argument");
+        kdx_begin(ctx->c, d, n_levels, sizes, cur, newlab, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_kdx_moments(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                       int32_t* labels, int32_t level, double* out, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (!out || (n && !labels)) throw Error(PD_EINVAL, "null argument");
+        kdx_moments(ctx->c, X, dtype, n, d, labels, level, out, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_kdx_axes(pd_ctx* ctx, const double* gathered, int32_t n_ranks, int32_t level,
+                    void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || !gathered) throw Error(PD_EINVAL, "null argument");
+        kdx_axes(ctx->c, gathered, n_ranks, level, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_kdx_counts(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                      const int32_t* labels, int32_t level, uint64_t* out, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (!out || (n && !labels)) throw Error(PD_EINVAL, "null argument");
+        kdx_counts(ctx->c, X, dtype, n, d, labels, level, (unsigned long long*)out,
+                   (hipStream_t)stream);
+    });
+}
+
+int32_t pd_kdx_boundary(pd_ctx* ctx, const uint64_t* counts, int32_t level, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || !counts) throw Error(PD_EINVAL, "null argument");
+        kdx_boundary(ctx->c, (const unsigned long long*)counts, level, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_kdx_end(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, int32_t* labels,
+                   int32_t final_split, double* trace, double* lohi, int64_t* bad, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (!trace || !lohi || (n && !labels)) throw Error(PD_EINVAL, "null argument");
+        kdx_end(ctx->c, X, dtype, n, d, labels, final_split != 0, trace, lohi, bad,
+                (hipStream_t)stream);
+    });
+}
+
+// ---------------------------------------------------------------- one-pass exchange, results
+int32_t pd_route2(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, int32_t P,
+                  const double* ebox, const int32_t* part_rank, const int32_t* kdlab,
+                  int32_t n_ranks, int64_t* counts, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "d > 4");
+        if (!ebox || !part_rank || !counts || (n && !kdlab)) throw Error(PD_EINVAL, "null argument");
+        route2(ctx->c, X, dtype, n, d, P, ebox, part_rank, kdlab, n_ranks, counts,
+               (hipStream_t)stream);
+    });
+}
+
+int32_t pd_pack2(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                 const int32_t* kdlab, int32_t P, const int32_t* part_rank,
+                 const int32_t* local_index, uint32_t gid_base, int32_t n_ranks,
+                 void* const* coords, uint32_t* const* gid, int32_t* const* owner,
+                 uint8_t* const* xr, void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "d > 4");
+        if (P < 1 || !part_rank || !local_index || !coords || !gid || !owner || !xr ||
+            (n && !kdlab))
+            throw Error(PD_EINVAL, "null argument");
+        pack2(ctx->c, X, dtype, n, d, kdlab, P, part_rank, local_index, gid_base, n_ranks, coords,
+              gid, owner, xr, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_results(pd_ctx* ctx, int64_t nr, const uint32_t* keys, const uint8_t* core,
+                   const int32_t* owner, const uint32_t* gid, const uint32_t* roots, int64_t n_roots,
+                   int64_t n_total, uint32_t gid_base, int64_t n_local, int32_t n_ranks,
+                   int32_t rank, const int64_t* src_offsets, int64_t expect_remote,
+                   int32_t* labels, uint8_t* core_out, uint32_t* pairs, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || !src_offsets || nr < 0 || n_local < 0 || n_roots < 0 || expect_remote < 0)
+            throw Error(PD_EINVAL, "bad argument");
+        if (nr && (!keys || !owner)) throw Error(PD_EINVAL, "null argument");
+        if (n_roots && !roots) throw Error(PD_EINVAL, "null roots");
+        if (n_local && !labels) throw Error(PD_EINVAL, "null labels");
+        if (expect_remote && !pairs) throw Error(PD_EINVAL, "null pairs");
+        results(ctx->c, nr, keys, core, owner, gid, roots, n_roots, n_total, gid_base, n_local,
+                n_ranks, rank, src_offsets, expect_remote, labels, core_out, pairs,
+                (hipStream_t)stream);
+    });
+}
+
+int32_t pd_results_scatter(pd_ctx* ctx, const uint32_t* pairs, int64_t m, uint32_t gid_base,
+                           int64_t n, int32_t* labels, uint8_t* core, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || m < 0 || n < 0 || (m && !pairs) || (n && !labels))
+            throw Error(PD_EINVAL, "bad argument");
+        results_scatter(ctx->c, pairs, m, gid_base, n, labels, core, (hipStream_t)stream);
+    });
+}
+
 // ---------------------------------------------------------------- sharded dense train
 
 int32_t pd_dense_count(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d, double eps,
@@ -687,6 +797,29 @@ int32_t pd_comm_all_to_all_v(pd_comm* comm, const void* send, const int64_t* sen
         if (!send_counts || !recv_counts) throw Error(PD_EINVAL, "null counts");
         comm_all_to_all_v(comm->c, send, send_counts, recv, recv_counts, elem, (hipStream_t)stream);
     });
+}
+
+int32_t pd_comm_exchange(pd_comm* comm, int32_t n_fields, const void* const* send,
+                         void* const* recv, const int64_t* rec_bytes, const int64_t* send_counts,
+                         const int64_t* send_offsets, const int64_t* recv_counts,
+                         const int64_t* recv_offsets, int32_t skip_self, void* stream) {
+    return comm_guard(comm, [&] {
+        if (n_fields < 1 || n_fields > 16 || !send || !recv || !rec_bytes || !send_counts ||
+            !send_offsets || !recv_counts || !recv_offsets)
+            throw Error(PD_EINVAL, "bad argument");
+        comm_exchange(comm->c, n_fields, send, recv, rec_bytes, send_counts, send_offsets,
+                      recv_counts, recv_offsets, skip_self != 0, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_comm_abort(pd_comm* comm) {
+    if (!comm) return PD_OK;
+    comm_abort(comm->c);
+    return PD_OK;
+}
+
+int32_t pd_comm_self_check(pd_comm* comm) {
+    return comm_guard(comm, [&] { comm_self_check(&comm->c, 1); });
 }
 
 int32_t pd_comm_broadcast(pd_comm* comm, void* buf, int64_t count, int32_t elem, int32_t root,

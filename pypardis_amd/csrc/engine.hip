@@ -1504,6 +1504,279 @@ __global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs
     if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
 }
 
+// ------------------------------------------------------------------ persistent-lane count
+// count3_kernel (PD_OPT_SWEEP_VARIANT bit 3, the default): the same answer as
+// count2_kernel — neighbour count with the min_samples early exit, core flag,
+// the two smallest neighbours seen — reorganised for instruction issue, which
+// is what bounds the count sweep (PMC, C2: 2086 VALU instructions per 64-record
+// wave at ~5.4 ms of pure issue time for a 7 ms kernel):
+//   * lanes are persistent within a wave: each wave owns kChunk consecutive
+//     records and a lane that finishes its record (early exit or last row)
+//     takes the next one, so a wave no longer runs at the pace of its slowest
+//     lane (count2: ~30 % of lane-slots did work);
+//   * a lane walks its record's rows one at a time (centre row first); a row's
+//     candidate range costs ~60 instructions instead of ~130: the chord of the
+//     eps-ball is taken in fp32 from the in-cell fraction (distances shrunk by
+//     2^-16 relative + 2^-20 of a cell, the chord grown by 2^-16 + 2^-16 cells:
+//     a superset of the fp64 chord, so no neighbour is ever cut; the fp64 cell
+//     index itself is the one the record keys were built with), the row's key
+//     is the query cell's key plus integer offsets, rows outside the grid have
+//     an infinite distance.
+// A lane's state: its record (query point, Pred), the next row q, the current
+// candidate range [j, e) and, for a long rotated centre row, the wrapped part
+// [ws, we).
+constexpr uint32_t kChunk = 256;   // records per wave (4 per lane on average)
+
+template <int D>
+struct RowGeo {
+    uint64_t kc;             // key of the query cell
+    int32_t lim_lo, lim_hi;  // axis-0 offsets that stay inside the grid
+    float f0;                // in-cell fraction along axis 0
+    float tl[D], th[D];      // (j >= 1) distance to the lower / upper row (squared for
+                             // euclidean; +inf: no such row)
+};
+
+// Row q's axis offsets (-1, 0, +1) for axes 1.., centre row first: digit t of
+// q in base 3 (axis 1 fastest) -> offset 0, -1, +1 for t = 0, 1, 2.
+template <int D>
+__device__ __forceinline__ int row_off(int q, int j) {
+    int t = q;
+    for (int k = 1; k < j; ++k) t /= 3;
+    t %= 3;
+    return t == 0 ? 0 : (t == 1 ? -1 : 1);
+}
+
+template <typename T, int D, int M, bool U>
+struct Count3Grid {
+    // neighbourhood grid fields (U: wave-uniform, scalar registers)
+    double lo[D], inv[D];
+    double cs[D];
+    int64_t nc[D];
+    uint64_t base;
+    uint64_t S[D];           // key strides
+    float wsc, wsl;          // chord -> axis-0 cells: w * wsc + wsl
+    __device__ __forceinline__ void load(const PartGrid* gp) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            lo[j] = U ? uniform_f64(gp->lo[j]) : gp->lo[j];
+            inv[j] = U ? uniform_f64(gp->inv[j]) : gp->inv[j];
+            cs[j] = U ? uniform_f64(gp->cs[j]) : gp->cs[j];
+            nc[j] = U ? uniform_i64(gp->nc[j]) : gp->nc[j];
+        }
+        base = U ? (uint64_t)uniform_i64((int64_t)gp->base) : gp->base;
+        uint64_t s = 1;
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            S[j] = s;
+            s *= (uint64_t)nc[j];
+        }
+        wsc = (float)(inv[0] * (1.0 + 1.0 / 65536.0));
+        wsl = 1.0f / 65536.0f;
+    }
+};
+
+template <typename T, int D, int M, bool U>
+__device__ __forceinline__ RowGeo<D> row_geo(const Count3Grid<T, D, M, U>& g, const double (&a)[D]) {
+    RowGeo<D> R;
+    uint64_t lin = 0;
+#pragma unroll
+    for (int j = D - 1; j >= 0; --j) {
+        const double u = (a[j] - g.lo[j]) * g.inv[j];
+        // the cell index exactly as the record keys were built (key_of)
+        int64_t c = (int64_t)floor(u);
+        c = c < 0 ? 0 : c;
+        c = c >= g.nc[j] ? g.nc[j] - 1 : c;
+        lin = lin * (uint64_t)g.nc[j] + (uint64_t)c;
+        double fr = u - (double)c;
+        fr = fr < 0.0 ? 0.0 : (fr > 1.0 ? 1.0 : fr);
+        const float f = (float)fr;
+        if (j == 0) {
+            R.f0 = f;
+            R.lim_lo = -(int32_t)(c < 64 ? c : 64);
+            const int64_t up = g.nc[0] - 1 - c;
+            R.lim_hi = (int32_t)(up < 64 ? up : 64);
+        } else {
+            const float csf = (float)g.cs[j];
+            const float shrink = 1.0f - 1.0f / 65536.0f, abs_s = csf * (1.0f / 1048576.0f);
+            float dl = fmaxf(f * csf * shrink - abs_s, 0.0f);
+            float dh = fmaxf((1.0f - f) * csf * shrink - abs_s, 0.0f);
+            if constexpr (M == 0) {
+                dl *= dl;
+                dh *= dh;
+            }
+            R.tl[j] = c > 0 ? dl : INFINITY;
+            R.th[j] = c < g.nc[j] - 1 ? dh : INFINITY;
+        }
+    }
+    R.kc = g.base + lin;
+    return R;
+}
+
+// Candidate record range [s, e) of row q (e <= s: empty).
+template <typename T, int D, int M, bool U>
+__device__ __forceinline__ void row_range3(const Cells& C, const Count3Grid<T, D, M, U>& g,
+                                           const RowGeo<D>& R, float e2, int q, uint32_t& s,
+                                           uint32_t& e) {
+    float d2 = 0.0f;
+    int64_t koff = 0;
+#pragma unroll
+    for (int j = 1; j < D; ++j) {
+        const int o = row_off<D>(q, j);
+        d2 += o < 0 ? R.tl[j] : (o > 0 ? R.th[j] : 0.0f);
+        koff += o < 0 ? -(int64_t)g.S[j] : (o > 0 ? (int64_t)g.S[j] : 0);
+    }
+    const bool ok = d2 <= e2;
+    float w;
+    if constexpr (M == 0)
+        w = __builtin_sqrtf(fmaxf(e2 - d2, 0.0f));
+    else
+        w = fmaxf(e2 - d2, 0.0f);
+    const float wc = w * g.wsc + g.wsl;
+    int32_t dx0 = (int32_t)floorf(R.f0 - wc), dx1 = (int32_t)floorf(R.f0 + wc);
+    dx0 = dx0 > R.lim_lo ? dx0 : R.lim_lo;
+    dx1 = dx1 < R.lim_hi ? dx1 : R.lim_hi;
+    const uint64_t rb = R.kc + (uint64_t)koff;
+    const uint64_t k0 = ok ? rb + (uint64_t)(int64_t)dx0 : R.kc;
+    const uint64_t k1 = ok ? rb + (uint64_t)(int64_t)(dx1 + 1) : R.kc;
+    const uint4 w0 = C.dir[k0 >> 6], w1 = C.dir[k1 >> 6];
+    const uint32_t i0 = dir_rank(w0, k0), i1 = dir_rank(w1, k1);
+    s = C.cstart[i0];
+    e = C.cstart[i1];
+    e = e > s ? e : s;
+}
+
+template <typename T, int D, int M, bool ST, bool U>
+__device__ __forceinline__ void count3_wave(const T* __restrict__ Xs, uint32_t c0, uint32_t c1,
+                                            const Cells& C, int L0, double eps, double eps2,
+                                            float lo, float hi, uint32_t ms, int full,
+                                            uint32_t rot_min, uint8_t* __restrict__ core,
+                                            uint32_t* __restrict__ mn_out,
+                                            uint32_t* __restrict__ cnt_out,
+                                            unsigned long long* __restrict__ stats) {
+    constexpr int NR = NRows<D>::v;
+    const int lane = threadIdx.x & 63;
+    const uint32_t stop = full ? 0xFFFFFFFFu : ms;
+    // fp32 threshold of the row test: eps^2 (eps) rounded up
+    float e2 = M == 0 ? (float)eps2 : (float)eps;
+    e2 = e2 * (1.0f + 1.0f / 65536.0f);
+    Count3Grid<T, D, M, U> g;
+    if constexpr (U) g.load(C.parts + L0);
+    Pred<T, D, M> pr;
+    RowGeo<D> geo;
+    uint32_t r = kNone, cnt = 0, mn = kNone, mn2 = kNone, n_cand = 0;
+    uint32_t j = 0, e = 0, ws = 0, we = 0;
+    int q = NR;
+    uint32_t next = c0;   // wave-uniform: next record to hand out
+    bool active = true;
+    while (true) {
+        // ---- advance lanes whose range is spent: wrap, next row, or next record
+        bool need = active && (j >= e || cnt >= stop);
+        while (__any(need)) {
+            if (need && j >= e && we > ws && cnt < stop) {   // the wrapped part of the centre row
+                j = ws;
+                e = we;
+                ws = we = 0;
+                need = false;
+            }
+            const bool fin = need && (cnt >= stop || q >= NR);
+            if (fin && r != kNone) {
+                core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
+                reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, mn2);
+                if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
+            }
+            const unsigned long long b = __ballot(fin);
+            const uint32_t pos = next + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+            next += (uint32_t)__popcll(b);
+            if (fin) {
+                if (pos < c1) {
+                    r = pos;
+                    double a[D];
+                    load_rec<T, D>(Xs, r, a);
+                    pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
+                    if constexpr (!U) {
+                        const int L = part_of(C.part_start, C.P, r);
+                        g.load(C.parts + L);
+                    }
+                    geo = row_geo<T, D, M, U>(g, a);
+                    cnt = 0;
+                    mn = mn2 = kNone;
+                    q = 0;
+                } else {
+                    r = kNone;
+                    active = false;
+                    need = false;
+                }
+                j = e = ws = we = 0;
+            }
+            if (need && q < NR) {   // the next row (new records start at the centre row)
+                uint32_t s, en;
+                row_range3<T, D, M, U>(C, g, geo, e2, q, s, en);
+                j = s;
+                e = en;
+                // a long centre row: start at record r & ~(kRotAlign - 1) when it
+                // lies in the row, and wrap (count2_kernel's rotation)
+                if (q == 0 && en - s > rot_min) {
+                    const uint32_t v = r & ~(kRotAlign - 1u);
+                    if (v > s && v < en) {
+                        j = v;
+                        ws = s;
+                        we = v;
+                    }
+                }
+                ++q;
+            }
+            need = active && (j >= e || cnt >= stop);
+        }
+        if (!__any(active)) break;
+        // ---- four candidates of the current range
+        if (active) {
+            uint32_t jj[4];
+            T b[4][D];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                jj[u] = j + u;
+                load_raw<T, D>(Xs, jj[u] < e ? jj[u] : j, b[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const bool h = jj[u] < e && pr(b[u]);
+                cnt += h ? 1u : 0u;
+                const uint32_t x = h ? jj[u] : kNone;
+                mn2 = min(mn2, max(mn, x));   // the two smallest hits
+                mn = min(mn, x);
+            }
+            if constexpr (ST) n_cand += (e - j < 4u ? e - j : 4u);
+            j += 4;
+        }
+    }
+    if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
+}
+
+template <typename T, int D, int M, bool ST>
+__global__ __launch_bounds__(kBlock) void count3_kernel(const T* __restrict__ Xs, uint32_t R,
+                                                        Cells C, double eps, double eps2,
+                                                        float lo, float hi, uint32_t ms, int full,
+                                                        uint32_t rot_min,
+                                                        uint8_t* __restrict__ core,
+                                                        uint32_t* __restrict__ mn_out,
+                                                        uint32_t* __restrict__ cnt_out,
+                                                        unsigned long long* __restrict__ stats) {
+    const uint32_t wv = xcd_block(blockIdx.x, gridDim.x) * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t c0l = (uint64_t)wv * kChunk;
+    if (c0l >= R) return;
+    const uint32_t c0 = (uint32_t)c0l;
+    const uint32_t c1 = (uint32_t)(c0l + kChunk < R ? c0l + kChunk : R);
+    // one neighbourhood for the whole chunk (all but at most P - 1 chunks):
+    // grid in scalar registers
+    const int L0 = part_of(C.part_start, C.P, c0);
+    if (C.part_start[L0 + 1] >= c1)
+        count3_wave<T, D, M, ST, true>(Xs, c0, c1, C, L0, eps, eps2, lo, hi, ms, full, rot_min,
+                                       core, mn_out, cnt_out, stats);
+    else
+        count3_wave<T, D, M, ST, false>(Xs, c0, c1, C, L0, eps, eps2, lo, hi, ms, full, rot_min,
+                                        core, mn_out, cnt_out, stats);
+}
+
 // ------------------------------------------------------------------ link mode 3
 // (1) on the forest of the count pass's smallest neighbours (init_kernel),
 // union over the centre row only (each core record with the core records of
@@ -2463,7 +2736,12 @@ template <typename T, int D, int M, bool ST>
 void launch_count(int variant, hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double eps,
                   double eps2, float lo, float hi, uint32_t ms, int full, uint32_t rot_min,
                   uint8_t* core, uint32_t* mn, uint32_t* cnt, unsigned long long* st) {
-    if (variant & 1)
+    if (variant & 8) {   // persistent lanes, kChunk records per wave
+        const uint64_t waves = ((uint64_t)R + kChunk - 1) / kChunk;
+        const unsigned nb = (unsigned)((waves + kBlock / 64 - 1) / (kBlock / 64));
+        hipLaunchKernelGGL((count3_kernel<T, D, M, ST>), dim3(nb ? nb : 1), dim3(kBlock), 0, s, Xs,
+                           R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
+    } else if (variant & 1)
         hipLaunchKernelGGL((count2_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
                            C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
     else

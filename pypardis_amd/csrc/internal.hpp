@@ -112,6 +112,33 @@ struct DenseState {
     unsigned long long* tiles = nullptr;
 };
 
+// Device-decided KD partition of a sharded train (pd_kdx_*, kd.hip): the
+// level tables and decisions stay on the device between the per-level calls;
+// the caller runs the collectives (all-gather of the moment partials,
+// all-reduce of the counts) in between, stream-ordered, with no host sync.
+struct KdxState {
+    bool valid = false;
+    int n_levels = 0, d = 0;
+    std::vector<int> sizes, first, ntab;
+    std::vector<int32_t> cur;
+    std::vector<size_t> off, off_d;
+    int total = 0;
+    char* tables = nullptr;      // device: per level slot_of | axis | newlab | bounds | boundary
+    double* trace = nullptr;     // device: 13 doubles per split
+    double* bbox = nullptr;      // device: combined bbox (2d) + non-finite count
+    double* mom = nullptr;       // device: combined moments of the current level
+};
+
+// Exchange state of a sharded train between pd_route2 and pd_pack2 (shard.hip).
+struct RouteState {
+    bool valid = false;
+    int64_t n = 0;
+    int n_ranks = 0;
+    unsigned tiles = 0;
+    uint64_t* mask = nullptr;    // device u64[n]: destination ranks of each point
+    uint64_t* off = nullptr;     // device: dest-major exclusive scan of the per-tile counts
+};
+
 struct Ctx {
     int device = 0;
     Arena arena;
@@ -133,10 +160,13 @@ struct Ctx {
     bool border_roots = false;   // border sweep's single-root fast path (tuning)
     int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow
     int dense_prune = 1;         // dense count pass: projection-window tiles only (2: per-band runs)
-    int variant = 5;             // PD_OPT_SWEEP_VARIANT: batched count + border, row-wise link
+    int variant = 13;            // PD_OPT_SWEEP_VARIANT: persistent-lane count (bit 3; bit 0 the
+                                 // batched count2), batched border (bit 2), row-wise link
     Timings t;
     PhaseState st;
     DenseState dn;
+    KdxState kdx;
+    RouteState rt;
     hipEvent_t ev[16] = {};
 };
 
@@ -226,6 +256,33 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
               double* trace_out, double* lohi, int64_t* bad, hipStream_t s);
 void kd_moments_dd(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                    int n_sel, const int32_t* sel_host, double* out_host, hipStream_t s);
+// Sharded device-decided KD (kd.hip): begin -> per level (moments -> [caller:
+// all-gather] -> axes -> counts -> [caller: all-reduce] -> boundary) -> end.
+void kdx_begin(Ctx& ctx, int d, int n_levels, const int32_t* sizes, const int32_t* cur,
+               const int32_t* newl, hipStream_t s);
+void kdx_moments(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels, int level,
+                 double* out, hipStream_t s);
+void kdx_axes(Ctx& ctx, const double* gathered, int n_ranks, int level, hipStream_t s);
+void kdx_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
+                int level, unsigned long long* out, hipStream_t s);
+void kdx_boundary(Ctx& ctx, const unsigned long long* cnt, int level, hipStream_t s);
+void kdx_end(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels,
+             bool final_split, double* trace_out, double* lohi, int64_t* bad, hipStream_t s);
+// Sharded exchange (shard.hip): one ordered pass per side, every destination.
+void route2(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P, const double* ebox_host,
+            const int32_t* part_rank_host, const int32_t* kdlab, int n_ranks, int64_t* counts_host,
+            hipStream_t s);
+void pack2(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* kdlab, int P,
+           const int32_t* part_rank_host, const int32_t* local_index_host, uint32_t gid_base,
+           int n_ranks, void* const* coords, uint32_t* const* gid, int32_t* const* owner,
+           uint8_t* const* xr, hipStream_t s);
+void results(Ctx& ctx, int64_t nr, const uint32_t* keys, const uint8_t* core, const int32_t* owner,
+             const uint32_t* gid, const uint32_t* roots, int64_t n_roots, int64_t n_total,
+             uint32_t gid_base, int64_t n_local, int n_ranks, int me, const int64_t* src_off_host,
+             int64_t expect_remote, int32_t* labels, uint8_t* core_out, uint32_t* pairs,
+             hipStream_t s);
+void results_scatter(Ctx& ctx, const uint32_t* pairs, int64_t m, uint32_t gid_base, int64_t n,
+                     int32_t* labels, uint8_t* core, hipStream_t s);
 void route(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P, const double* ebox_host,
            const int32_t* part_rank_host, int n_ranks, uint64_t* mask, int64_t* counts_host,
            hipStream_t s);
@@ -262,6 +319,17 @@ void comm_all_gather_v(Comm* c, const void* send, void* recv, const int64_t* cou
 void comm_all_to_all_v(Comm* c, const void* send, const int64_t* send_counts, void* recv,
                        const int64_t* recv_counts, int elem, hipStream_t s);
 void comm_broadcast(Comm* c, void* buf, int64_t count, int elem, int root, hipStream_t s);
+// Field-wise all-to-all in ONE group (blocks in records; rec_bytes per field);
+// skip_self: the self blocks are already in place in recv.
+void comm_exchange(Comm* c, int nf, const void* const* send, void* const* recv,
+                   const int64_t* rec_bytes, const int64_t* send_counts, const int64_t* send_off,
+                   const int64_t* recv_counts, const int64_t* recv_off, bool skip_self,
+                   hipStream_t s);
+void comm_abort(Comm* c);
+// W > 1: one all_to_all_v and one all_gather_v with a known rank pattern,
+// verified on the device (throws on a mismatch); comms: every rank of one
+// process (init_all) or just this rank's.
+void comm_self_check(Comm* const* comms, int n);
 void halo_members(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P,
                   const double* ebox_host, int64_t* counts_host, int64_t* members_dev,
                   int64_t members_cap, hipStream_t s);

@@ -1604,6 +1604,268 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
     });
 }
 
+// ---------------------------------------------------------------- sharded device-decided KD
+// pd_kd_build split at its collectives: every rank runs the same level chain
+// on its slice, and between the passes the caller all-gathers the moment
+// partials (rank order) and all-reduces the counts on the device, so a level
+// costs no host round trip.  The partials of all ranks are added with the
+// host path's double-double fold (distributed.dd_combine: dd_add in rank
+// order from zero), then kdb_axes_kernel / kdb_boundary_kernel decide as
+// pd_kd_build does — the splits equal the host-decided sharded path's and the
+// single-device ones bit for bit.
+namespace {
+// out[k] for k < S*G: the rank-order fold of gathered[w][k] (counts: sums; dd
+// pairs: dd_add); level 0 also folds the bbox (min / max / non-finite sum).
+__global__ void kdx_combine_kernel(const double* __restrict__ g, int W, int len, int SG, int G,
+                                   int D, double* __restrict__ mom, double* __restrict__ bbox) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= len) return;
+    if (k < SG) {
+        const int r = k % G;
+        if (r == 0) {
+            double c = 0.0;
+            for (int w = 0; w < W; ++w) c = __dadd_rn(c, g[(size_t)w * len + k]);
+            mom[k] = c;
+        } else if ((r - 1) % 2 == 0) {
+            DD a{0.0, 0.0};
+            for (int w = 0; w < W; ++w)
+                a = dd_add(a, DD{g[(size_t)w * len + k], g[(size_t)w * len + k + 1]});
+            mom[k] = a.hi;
+            mom[k + 1] = a.lo;
+        }
+        return;
+    }
+    const int b = k - SG;
+    double x = b < D ? INFINITY : (b < 2 * D ? -INFINITY : 0.0);
+    for (int w = 0; w < W; ++w) {
+        const double v = g[(size_t)w * len + k];
+        x = b < D ? fmin(x, v) : (b < 2 * D ? fmax(x, v) : __dadd_rn(x, v));
+    }
+    bbox[b] = x;
+}
+
+// An empty slice's partials: zero moments, an empty bbox.
+__global__ void kdx_empty_kernel(double* __restrict__ out, int SG, int len, int D) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= len) return;
+    const int b = k - SG;
+    out[k] = k < SG ? 0.0 : (b < D ? INFINITY : (b < 2 * D ? -INFINITY : 0.0));
+}
+
+struct KdxLv {
+    int32_t *slot, *axis, *newlab;
+    double *bounds, *boundary;
+};
+
+KdxLv kdx_level(const KdxState& k, int l) {
+    const int S = k.sizes[l];
+    KdxLv v;
+    v.slot = (int32_t*)(k.tables + k.off[l]);
+    v.axis = v.slot + k.ntab[l];
+    v.newlab = v.axis + S;
+    v.bounds = (double*)(k.tables + k.off_d[l]);
+    v.boundary = v.bounds + 7 * S;
+    return v;
+}
+
+void kdx_check(const Ctx& ctx, int level) {
+    if (!ctx.kdx.valid) throw Error(-1, "pd_kdx_*: no pd_kdx_begin on this context");
+    if (level < 0 || level >= ctx.kdx.n_levels) throw Error(-1, "pd_kdx_*: level out of range");
+}
+}  // namespace
+
+void kdx_begin(Ctx& ctx, int d, int n_levels, const int32_t* sizes, const int32_t* cur,
+               const int32_t* newl, hipStream_t s) {
+    KdxState& k = ctx.kdx;
+    k = KdxState{};
+    if (n_levels <= 0 || n_levels > 16) throw Error(-5, "pd_kdx_begin: 1..16 levels");
+    if (d < 1 || d > kMaxDim) throw Error(-5, "pd_kdx_begin: d <= 4");
+    k.n_levels = n_levels;
+    k.d = d;
+    k.sizes.assign(sizes, sizes + n_levels);
+    k.first.assign(n_levels, 0);
+    k.ntab.assign(n_levels, 1);
+    k.off.assign(n_levels + 1, 0);
+    k.off_d.assign(n_levels, 0);
+    int total = 0;
+    for (int l = 0; l < n_levels; ++l) {
+        const int S = sizes[l];
+        if (S < 1 || S > kTabLds) throw Error(-5, "pd_kdx_begin: level too wide");
+        k.first[l] = total;
+        for (int q = 0; q < S; ++q) {
+            const int L = cur[total + q], N = newl[total + q];
+            if (L < 0 || L >= kTabLds || N < 0)
+                throw Error(-5, "pd_kdx_begin: labels beyond the LDS tables");
+            k.ntab[l] = std::max(k.ntab[l], L + 1);
+        }
+        const size_t ints = (size_t)k.ntab[l] + 2 * S;
+        k.off_d[l] = k.off[l] + ((sizeof(int32_t) * ints + 7) & ~size_t(7));
+        k.off[l + 1] = k.off_d[l] + sizeof(double) * 8 * S;
+        total += S;
+    }
+    k.total = total;
+    k.cur.assign(cur, cur + total);
+    char* h = (char*)pinned(ctx, k.off[n_levels]);
+    std::memset(h, 0, k.off[n_levels]);
+    for (int l = 0; l < n_levels; ++l) {
+        int32_t* slot = (int32_t*)(h + k.off[l]);
+        const int S = sizes[l];
+        for (int q = 0; q < k.ntab[l]; ++q) slot[q] = -1;
+        for (int q = 0; q < S; ++q) {
+            slot[cur[k.first[l] + q]] = q;
+            slot[k.ntab[l] + S + q] = newl[k.first[l] + q];
+        }
+    }
+    k.tables = ctx.arena.get<char>("kdx_tables", k.off[n_levels] + 64);
+    PD_HIP(hipMemcpyAsync(k.tables, h, k.off[n_levels], hipMemcpyHostToDevice, s));
+    sync(s);   // the pinned block is reused by later calls
+    k.trace = ctx.arena.get<double>("kdx_trace", (size_t)total * kTrace);
+    k.bbox = ctx.arena.get<double>("kdx_bbox", 2 * kMaxDim + 1);
+    k.mom = ctx.arena.get<double>("kdx_mom", (size_t)kTabLds * (1 + 4 * kMaxDim));
+    k.valid = true;
+}
+
+void kdx_moments(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels, int level,
+                 double* out, hipStream_t s) {
+    kdx_check(ctx, level);
+    const KdxState& k = ctx.kdx;
+    if (d != k.d) throw Error(-1, "pd_kdx_moments: d differs from pd_kdx_begin");
+    const int S = k.sizes[level], G = 1 + 4 * d;
+    const int len = S * G + (level == 0 ? 2 * d + 1 : 0);
+    if (n == 0) {
+        hipLaunchKernelGGL(kdx_empty_kernel, dim3((len + 255) / 256), dim3(256), 0, s, out, S * G,
+                           len, d);
+        PD_HIP(hipGetLastError());
+        return;
+    }
+    if (ctx.seq_moments || !vec_ok(d, X, labels))
+        throw Error(-5, "pd_kdx_moments: d <= 4, 16-byte aligned inputs and exact sums only");
+    const int32_t* sel = k.cur.data() + k.first[level];
+    dispatch_t(dtype, [&](auto tp) {
+        using T = std::remove_pointer_t<decltype(tp)>;
+        dispatch_d(d, [&](auto Dc) {
+            constexpr int D = decltype(Dc)::value;
+            constexpr int Gc = 1 + 4 * D;
+            const T* Xt = (const T*)X;
+            const SplitTab none{nullptr, 0, nullptr, nullptr, nullptr, 0};
+            if (level == 0) {   // bbox + the root's moments, labels not read
+                run_pass_dev<T, D, false, false, 1, true>(ctx, Xt, n, labels, none,
+                                                          make_int4(sel[0], -2, -2, -2), out, s);
+                return;
+            }
+            const KdxLv p = kdx_level(k, level - 1);
+            const SplitTab sp{p.slot, k.ntab[level - 1], p.axis, p.boundary, p.newlab,
+                              k.sizes[level - 1]};
+            for (int g0 = 0; g0 < S; g0 += kGroup) {
+                const int ng = std::min(S - g0, kGroup);
+                int4 sl = make_int4(-2, -2, -2, -2);
+                for (int g = 0; g < ng; ++g) (&sl.x)[g] = sel[g0 + g];
+                dispatch_ng(ng, [&](auto NGc) {
+                    constexpr int NG = decltype(NGc)::value;
+                    if (g0 == 0)
+                        run_pass_dev<T, D, true, true, NG, false>(ctx, Xt, n, labels, sp, sl, out, s);
+                    else
+                        run_pass_dev<T, D, true, false, NG, false>(ctx, Xt, n, labels, none, sl,
+                                                                   out + (size_t)g0 * Gc, s);
+                });
+            }
+        });
+    });
+}
+
+void kdx_axes(Ctx& ctx, const double* gathered, int n_ranks, int level, hipStream_t s) {
+    kdx_check(ctx, level);
+    const KdxState& k = ctx.kdx;
+    if (n_ranks < 1) throw Error(-1, "pd_kdx_axes: n_ranks < 1");
+    const int d = k.d, S = k.sizes[level], G = 1 + 4 * d;
+    const int len = S * G + (level == 0 ? 2 * d + 1 : 0);
+    hipLaunchKernelGGL(kdx_combine_kernel, dim3((len + 255) / 256), dim3(256), 0, s, gathered,
+                       n_ranks, len, S * G, G, d, k.mom, k.bbox);
+    const KdxLv v = kdx_level(k, level);
+    hipLaunchKernelGGL(kdb_axes_kernel, dim3(1), dim3(kTabLds), 0, s, k.mom, S, d, G, v.axis,
+                       v.bounds, k.trace + (size_t)k.first[level] * kTrace);
+    PD_HIP(hipGetLastError());
+}
+
+void kdx_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
+                int level, unsigned long long* out, hipStream_t s) {
+    kdx_check(ctx, level);
+    const KdxState& k = ctx.kdx;
+    const int S = k.sizes[level];
+    PD_HIP(hipMemsetAsync(out, 0, sizeof(unsigned long long) * S * 8, s));
+    if (n == 0) return;
+    if (!vec_ok(d, X, labels)) throw Error(-5, "pd_kdx_counts: 16-byte aligned inputs only");
+    const KdxLv v = kdx_level(k, level);
+    dispatch_t(dtype, [&](auto tp) {
+        using T = std::remove_pointer_t<decltype(tp)>;
+        dispatch_d(d, [&](auto Dc) {
+            constexpr int D = decltype(Dc)::value;
+            const T* Xt = (const T*)X;
+            const unsigned nb4 = grid_for((n + 3) / 4, 2048);
+            if (S <= 4) {
+                auto go = [&](auto NSc) {
+                    constexpr int NS = decltype(NSc)::value;
+                    hipLaunchKernelGGL((counts_reg_kernel<T, D, NS>), dim3(nb4), dim3(kBlock), 0, s,
+                                       Xt, (uint64_t)n, labels, v.slot, k.ntab[level], v.axis,
+                                       v.bounds, S, out);
+                };
+                if (S == 1)
+                    go(std::integral_constant<int, 1>{});
+                else if (S == 2)
+                    go(std::integral_constant<int, 2>{});
+                else
+                    go(std::integral_constant<int, 4>{});
+            } else {
+                int rep = kRep;
+                while (rep > 1 && (size_t)rep * S * 8 * sizeof(unsigned int) > 48 * 1024) rep >>= 1;
+                hipLaunchKernelGGL((counts4_kernel<T, D>), dim3(nb4), dim3(kBlock),
+                                   sizeof(unsigned int) * rep * S * 8, s, Xt, (uint64_t)n, labels,
+                                   v.slot, k.ntab[level], v.axis, v.bounds, S, 0, rep, out);
+            }
+        });
+    });
+    PD_HIP(hipGetLastError());
+}
+
+void kdx_boundary(Ctx& ctx, const unsigned long long* cnt, int level, hipStream_t s) {
+    kdx_check(ctx, level);
+    const KdxState& k = ctx.kdx;
+    const KdxLv v = kdx_level(k, level);
+    hipLaunchKernelGGL(kdb_boundary_kernel, dim3(1), dim3(kTabLds), 0, s, cnt, k.sizes[level],
+                       v.bounds, v.boundary, k.trace + (size_t)k.first[level] * kTrace);
+    PD_HIP(hipGetLastError());
+}
+
+void kdx_end(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels,
+             bool final_split, double* trace_out, double* lohi, int64_t* bad, hipStream_t s) {
+    KdxState& k = ctx.kdx;
+    if (!k.valid) throw Error(-1, "pd_kdx_end: no pd_kdx_begin on this context");
+    if (d != k.d) throw Error(-1, "pd_kdx_end: d differs from pd_kdx_begin");
+    const int nl = k.n_levels;
+    if (final_split && n > 0) {
+        if (!vec_ok(d, X, labels)) throw Error(-5, "pd_kdx_end: 16-byte aligned inputs only");
+        const KdxLv p = kdx_level(k, nl - 1);
+        const SplitTab sp{p.slot, k.ntab[nl - 1], p.axis, p.boundary, p.newlab, k.sizes[nl - 1]};
+        dispatch_t(dtype, [&](auto tp) {
+            using T = std::remove_pointer_t<decltype(tp)>;
+            dispatch_d(d, [&](auto Dc) {
+                constexpr int D = decltype(Dc)::value;
+                run_pass_dev<T, D, true, true, 0, false>(ctx, (const T*)X, n, labels, sp,
+                                                         make_int4(-2, -2, -2, -2), nullptr, s);
+            });
+        });
+    }
+    double* h = (double*)pinned(ctx, sizeof(double) * ((size_t)k.total * kTrace + 2 * kMaxDim + 8));
+    PD_HIP(hipMemcpyAsync(h, k.trace, sizeof(double) * k.total * kTrace, hipMemcpyDeviceToHost, s));
+    PD_HIP(hipMemcpyAsync(h + (size_t)k.total * kTrace, k.bbox, sizeof(double) * (2 * d + 1),
+                          hipMemcpyDeviceToHost, s));
+    sync(s);
+    std::memcpy(trace_out, h, sizeof(double) * k.total * kTrace);
+    for (int j = 0; j < 2 * d; ++j) lohi[j] = h[(size_t)k.total * kTrace + j];
+    if (bad) *bad = (int64_t)h[(size_t)k.total * kTrace + 2 * d];
+    k.valid = false;
+}
+
 void kd_radix_hist(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                    int n_sel, const int32_t* sel, const int32_t* axis, const uint64_t* prefix,
                    int shift, int64_t* out, hipStream_t s) {

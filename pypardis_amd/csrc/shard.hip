@@ -278,6 +278,199 @@ __global__ __launch_bounds__(kBlock) void unset_check_kernel(const int32_t* __re
     if (i < n && labels[i] == kUnset) atomicOr(bad, 2u);
 }
 
+// ---- one-pass exchange (pd_route2 / pd_pack2): tiles of 4 * kBlock points;
+// lane l of wave w takes points base + 256 w + 64 q + l (q = 0..3), so a
+// tile's points are visited in ascending index order (w, q, l) and every
+// destination receives its points in ascending local index.
+constexpr int kRTile = 4 * kBlock;
+
+template <typename T, int D>
+__device__ __forceinline__ uint64_t route_mask(const T* __restrict__ X, uint64_t i,
+                                               const double* __restrict__ eb, int P,
+                                               const int32_t* __restrict__ part_rank) {
+    double v[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) v[j] = (double)X[i * D + j];
+    uint64_t m = 0;
+    for (int L = 0; L < P; ++L) {
+        const double* b = eb + (size_t)L * 2 * D;
+        bool in = true;
+#pragma unroll
+        for (int j = 0; j < D; ++j) in &= (b[j] <= v[j]) & (b[D + j] >= v[j]);
+        if (in) m |= 1ull << part_rank[L];
+    }
+    return m;
+}
+
+// Pass 1: destination mask per point, per-tile counts (dest-major:
+// cnt[r * tiles + tile]) and per-destination totals of the points that
+// destination owns (its KD partition holds them).
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void route_tile_kernel(
+    const T* __restrict__ X, uint64_t n, const double* __restrict__ ebox, int P,
+    const int32_t* __restrict__ part_rank, const int32_t* __restrict__ kdlab, int n_ranks,
+    unsigned tiles, uint64_t* __restrict__ mask, uint32_t* __restrict__ cnt,
+    unsigned long long* __restrict__ own) {
+    __shared__ unsigned int sc[kMaxRanks], so[kMaxRanks];
+    for (int k = threadIdx.x; k < n_ranks; k += kBlock) sc[k] = so[k] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kRTile + (threadIdx.x >> 6) * 256 + (threadIdx.x & 63);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t i = base + 64 * q;
+        if (i >= n) continue;
+        uint64_t m = route_mask<T, D>(X, i, ebox, P, part_rank);
+        mask[i] = m;
+        const int32_t L = kdlab[i];
+        if (L >= 0 && L < P) atomicAdd(&so[part_rank[L]], 1u);
+        while (m) {
+            const int r = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            atomicAdd(&sc[r], 1u);
+        }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < n_ranks; k += kBlock) {
+        cnt[(size_t)k * tiles + blockIdx.x] = sc[k];
+        if (so[k]) atomicAdd(own + k, (unsigned long long)so[k]);
+    }
+}
+
+// Per destination: its block's start in the dest-major scan (off[r * tiles])
+// and total, for the host.
+__global__ void route_totals_kernel(const uint64_t* __restrict__ off, unsigned tiles, int n_ranks,
+                                    unsigned long long* __restrict__ out) {
+    const int r = threadIdx.x;
+    if (r < n_ranks)
+        out[r] = (unsigned long long)(off[(size_t)(r + 1) * tiles] - off[(size_t)r * tiles]);
+}
+
+struct PackOut {
+    void* const* coords;
+    uint32_t* const* gid;
+    int32_t* const* owner;
+    uint8_t* const* xr;
+};
+
+// Pass 2: every point written to each of its destinations at (its position
+// among the tile's points for that destination) + the tile's offset.
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void pack_tile_kernel(
+    const T* __restrict__ X, uint64_t n, const uint64_t* __restrict__ mask,
+    const uint64_t* __restrict__ off, unsigned tiles, const int32_t* __restrict__ kdlab,
+    const int32_t* __restrict__ part_rank, const int32_t* __restrict__ local_index, int P,
+    int n_ranks, uint32_t gid_base, PackOut out) {
+    __shared__ unsigned int wc[kBlock / 64][kMaxRanks];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * kRTile + w * 256 + lane;
+    uint64_t m[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m[q] = base + 64 * q < n ? mask[base + 64 * q] : 0ull;
+    unsigned long long any = m[0] | m[1] | m[2] | m[3];
+    for (int o = 32; o > 0; o >>= 1) any |= (unsigned long long)__shfl_xor((long long)any, o, 64);
+    for (int r = 0; r < n_ranks; ++r) {
+        uint32_t t = 0;
+        if ((any >> r) & 1ull) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) t += (uint32_t)__popcll(__ballot((m[q] >> r) & 1ull));
+        }
+        if (lane == 0) wc[w][r] = t;
+    }
+    __syncthreads();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int r = 0; r < n_ranks; ++r) {
+        if (!((any >> r) & 1ull)) continue;   // wave-uniform
+        uint64_t pos = off[(size_t)r * tiles + blockIdx.x] - off[(size_t)r * tiles];
+        for (int u = 0; u < w; ++u) pos += wc[u][r];
+        T* co = (T*)out.coords[r];
+        uint32_t* gi = out.gid[r];
+        int32_t* ow = out.owner[r];
+        uint8_t* xr = out.xr[r];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const bool in = (m[q] >> r) & 1ull;
+            const unsigned long long b = __ballot(in);
+            if (in) {
+                const uint64_t i = base + 64 * q;
+                const uint64_t k = pos + (uint64_t)__popcll(b & lt);
+#pragma unroll
+                for (int j = 0; j < D; ++j) co[k * D + j] = X[i * D + j];
+                gi[k] = gid_base + (uint32_t)i;
+                const int32_t L = kdlab[i];
+                ow[k] = (L >= 0 && L < P && part_rank[L] == r) ? local_index[L] : -1;
+                xr[k] = __popcll(m[q]) > 1 ? 1 : 0;
+            }
+            pos += (uint64_t)__popcll(b);
+        }
+    }
+}
+
+// ---- results: labels of the owned records back to the ranks that hold the
+// points.  A record's source rank is its block of the exchange (records
+// arrive grouped by source), so the owned records of the self block are
+// written straight into this rank's outputs and the others are compacted in
+// order, block by block = destination by destination.
+__device__ __forceinline__ int32_t root_rank(const uint32_t* __restrict__ roots, uint32_t nr,
+                                             uint32_t k) {
+    if (k == kNone) return -1;
+    const uint32_t lo = lower_bound(roots, nr, k);
+    return (lo < nr && roots[lo] == k) ? (int32_t)lo : -2;
+}
+
+__global__ __launch_bounds__(kBlock) void results_self_kernel(
+    const uint32_t* __restrict__ keys, const uint8_t* __restrict__ core,
+    const int32_t* __restrict__ owner, const uint32_t* __restrict__ gid, uint64_t lo, uint64_t hi,
+    const uint32_t* __restrict__ roots, uint32_t nroots, uint32_t gid_base, uint64_t n_local,
+    int32_t* __restrict__ labels, uint8_t* __restrict__ core_out, uint32_t* __restrict__ bad) {
+    const uint64_t i = lo + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= hi || owner[i] < 0) return;
+    const int32_t lab = root_rank(roots, nroots, keys[i]);
+    const uint32_t g = gid ? gid[i] : (uint32_t)i;
+    if (lab == -2) atomicOr(bad, 4u);
+    if (g < gid_base || (uint64_t)(g - gid_base) >= n_local) {
+        atomicOr(bad, 1u);
+        return;
+    }
+    labels[g - gid_base] = lab;
+    if (core_out) core_out[g - gid_base] = core ? core[i] : 0;
+}
+
+struct IsRemoteOwned {
+    const int32_t* owner;
+    uint64_t lo, hi;
+    __device__ bool operator()(uint32_t i) const { return owner[i] >= 0 && (i < lo || i >= hi); }
+};
+
+__global__ __launch_bounds__(kBlock) void results_pack_kernel(
+    const uint32_t* __restrict__ list, const uint32_t* __restrict__ count, int64_t expect,
+    const uint32_t* __restrict__ keys, const uint8_t* __restrict__ core,
+    const uint32_t* __restrict__ gid, const uint32_t* __restrict__ roots, uint32_t nroots,
+    uint32_t* __restrict__ pairs, uint32_t* __restrict__ bad) {
+    const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t m = *count;
+    if (k == 0 && (int64_t)m != expect) atomicOr(bad, 8u);
+    if (k >= m || (int64_t)k >= expect) return;
+    const uint32_t i = list[k];
+    const int32_t lab = root_rank(roots, nroots, keys[i]);
+    if (lab == -2) atomicOr(bad, 4u);
+    pairs[2 * (size_t)k] = gid ? gid[i] : i;
+    pairs[2 * (size_t)k + 1] = (uint32_t)(lab + 1) | (core && core[i] ? 0x80000000u : 0u);
+}
+
+__global__ __launch_bounds__(kBlock) void results_scatter_kernel(
+    const uint32_t* __restrict__ pairs, uint64_t m, uint32_t gid_base, uint64_t n,
+    int32_t* __restrict__ labels, uint8_t* __restrict__ core, uint32_t* __restrict__ bad) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= m) return;
+    const uint32_t g = pairs[2 * k], v = pairs[2 * k + 1];
+    if (g < gid_base || (uint64_t)(g - gid_base) >= n) {
+        atomicOr(bad, 1u);
+        return;
+    }
+    labels[g - gid_base] = (int32_t)(v & 0x7FFFFFFFu) - 1;
+    if (core) core[g - gid_base] = (uint8_t)(v >> 31);
+}
+
 }  // namespace
 
 void route(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P, const double* ebox_host,
@@ -522,6 +715,175 @@ void scatter_results(Ctx& ctx, const uint32_t* pairs, int64_t m, uint32_t gid_ba
     if (*hb & 1) throw Error(-1, "scatter_results: global id outside this device's points");
     if (*hb & 2) throw Error(-1, "scatter_results: a point received no result (each point must "
                                  "be owned by exactly one device)");
+}
+
+// ---------------------------------------------------------------- one-pass exchange
+void route2(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P, const double* ebox_host,
+            const int32_t* part_rank_host, const int32_t* kdlab, int n_ranks, int64_t* counts_host,
+            hipStream_t s) {
+    RouteState& rt = ctx.rt;
+    rt = RouteState{};
+    if (n_ranks < 1 || n_ranks > kMaxRanks) throw Error(-1, "n_ranks must be in [1, 64]");
+    if (P < 1) throw Error(-1, "need at least one neighbourhood");
+    if (n > (int64_t)kIdMask) throw Error(-5, "n must be < 2^30 points per device");
+    for (int L = 0; L < P; ++L)
+        if (part_rank_host[L] < 0 || part_rank_host[L] >= n_ranks)
+            throw Error(-1, "part_rank out of range");
+    const size_t tb = sizeof(double) * P * 2 * d + sizeof(int32_t) * P;
+    char* h = (char*)pinned(ctx, tb + 64);
+    std::memcpy(h, ebox_host, sizeof(double) * P * 2 * d);
+    std::memcpy(h + sizeof(double) * P * 2 * d, part_rank_host, sizeof(int32_t) * P);
+    char* dt = ctx.arena.get<char>("route_tab", tb + 64);
+    PD_HIP(hipMemcpyAsync(dt, h, tb, hipMemcpyHostToDevice, s));
+    const unsigned tiles = (unsigned)std::max<int64_t>(1, (n + kRTile - 1) / kRTile);
+    const size_t nt = (size_t)tiles * n_ranks;
+    uint64_t* mask = ctx.arena.get<uint64_t>("route_mask", (size_t)n + 1);
+    uint32_t* cnt = ctx.arena.get<uint32_t>("route_tcnt", nt + 1);
+    uint64_t* off = ctx.arena.get<uint64_t>("route_toff", nt + 1);
+    unsigned long long* dres = ctx.arena.get<unsigned long long>("route_res", 2 * kMaxRanks);
+    PD_HIP(hipMemsetAsync(dres, 0, sizeof(unsigned long long) * 2 * kMaxRanks, s));
+    PD_HIP(hipMemsetAsync(cnt, 0, sizeof(uint32_t) * (nt + 1), s));
+    if (n) {
+        dispatch(dtype, d, [&](auto tp, auto Dc) {
+            using T = std::remove_pointer_t<decltype(tp)>;
+            constexpr int D = decltype(Dc)::value;
+            hipLaunchKernelGGL((route_tile_kernel<T, D>), dim3(tiles), dim3(kBlock), 0, s,
+                               (const T*)X, (uint64_t)n, (const double*)dt, P,
+                               (const int32_t*)(dt + sizeof(double) * P * 2 * d), kdlab, n_ranks,
+                               tiles, mask, cnt, dres + kMaxRanks);
+        });
+        PD_HIP(hipGetLastError());
+    }
+    size_t sb = 0;
+    PD_HIP(rocprim::exclusive_scan(nullptr, sb, cnt, off, (uint64_t)0, nt + 1,
+                                   rocprim::plus<uint64_t>(), s));
+    void* tmp = ctx.arena.get<char>("route_scan_tmp", sb);
+    PD_HIP(rocprim::exclusive_scan(tmp, sb, cnt, off, (uint64_t)0, nt + 1,
+                                   rocprim::plus<uint64_t>(), s));
+    hipLaunchKernelGGL(route_totals_kernel, dim3(1), dim3(kMaxRanks), 0, s, off, tiles, n_ranks,
+                       dres);
+    PD_HIP(hipGetLastError());
+    unsigned long long* hc =
+        (unsigned long long*)pinned(ctx, sizeof(unsigned long long) * 2 * kMaxRanks);
+    PD_HIP(hipMemcpyAsync(hc, dres, sizeof(unsigned long long) * 2 * kMaxRanks,
+                          hipMemcpyDeviceToHost, s));
+    sync(s);
+    for (int r = 0; r < n_ranks; ++r) {
+        counts_host[2 * r] = (int64_t)hc[r];
+        counts_host[2 * r + 1] = (int64_t)hc[kMaxRanks + r];
+    }
+    rt.valid = true;
+    rt.n = n;
+    rt.n_ranks = n_ranks;
+    rt.tiles = tiles;
+    rt.mask = mask;
+    rt.off = off;
+}
+
+void pack2(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* kdlab, int P,
+           const int32_t* part_rank_host, const int32_t* local_index_host, uint32_t gid_base,
+           int n_ranks, void* const* coords, uint32_t* const* gid, int32_t* const* owner,
+           uint8_t* const* xr, hipStream_t s) {
+    RouteState& rt = ctx.rt;
+    if (!rt.valid || rt.n != n || rt.n_ranks != n_ranks)
+        throw Error(-1, "pd_pack2 without a matching pd_route2 on this context");
+    if ((uint64_t)gid_base + (uint64_t)n > 0xFFFFFFFEull)
+        throw Error(-5, "global ids must stay below 2^32 - 1");
+    // tables: part_rank | local_index | 4 x n_ranks output pointers
+    const size_t ib = sizeof(int32_t) * 2 * P, pb = sizeof(void*) * 4 * n_ranks;
+    const size_t ibp = (ib + 15) & ~size_t(15);
+    char* h = (char*)pinned(ctx, ibp + pb + 64);
+    std::memcpy(h, part_rank_host, sizeof(int32_t) * P);
+    std::memcpy(h + sizeof(int32_t) * P, local_index_host, sizeof(int32_t) * P);
+    void** hp = (void**)(h + ibp);
+    for (int r = 0; r < n_ranks; ++r) {
+        hp[r] = coords[r];
+        hp[n_ranks + r] = gid[r];
+        hp[2 * n_ranks + r] = owner[r];
+        hp[3 * n_ranks + r] = xr[r];
+    }
+    char* dt = ctx.arena.get<char>("pack2_tab", ibp + pb + 64);
+    PD_HIP(hipMemcpyAsync(dt, h, ibp + pb, hipMemcpyHostToDevice, s));
+    void** dp = (void**)(dt + ibp);
+    const PackOut po{(void* const*)dp, (uint32_t* const*)(dp + n_ranks),
+                     (int32_t* const*)(dp + 2 * n_ranks), (uint8_t* const*)(dp + 3 * n_ranks)};
+    if (n) {
+        dispatch(dtype, d, [&](auto tp, auto Dc) {
+            using T = std::remove_pointer_t<decltype(tp)>;
+            constexpr int D = decltype(Dc)::value;
+            hipLaunchKernelGGL((pack_tile_kernel<T, D>), dim3(rt.tiles), dim3(kBlock), 0, s,
+                               (const T*)X, (uint64_t)n, rt.mask, rt.off, rt.tiles, kdlab,
+                               (const int32_t*)dt, (const int32_t*)dt + P, P, n_ranks, gid_base,
+                               po);
+        });
+        PD_HIP(hipGetLastError());
+    }
+    sync(s);   // the pinned tables are reused by later calls
+    rt.valid = false;
+}
+
+void results(Ctx& ctx, int64_t nr, const uint32_t* keys, const uint8_t* core, const int32_t* owner,
+             const uint32_t* gid, const uint32_t* roots, int64_t n_roots, int64_t n_total,
+             uint32_t gid_base, int64_t n_local, int n_ranks, int me, const int64_t* src_off,
+             int64_t expect_remote, int32_t* labels, uint8_t* core_out, uint32_t* pairs,
+             hipStream_t s) {
+    if (n_ranks < 1 || n_ranks > kMaxRanks || me < 0 || me >= n_ranks)
+        throw Error(-1, "bad rank / n_ranks");
+    if (nr > (int64_t)kIdMask || n_local > (int64_t)kIdMask)
+        throw Error(-5, "n must be < 2^30 points per device");
+    if (n_roots > (int64_t)0x7FFFFFFF || n_roots > n_total) throw Error(-5, "too many clusters");
+    for (int r = 0; r < n_ranks; ++r)
+        if (src_off[r + 1] < src_off[r]) throw Error(-1, "source offsets must ascend");
+    if (src_off[0] != 0 || src_off[n_ranks] != nr) throw Error(-1, "source offsets must span the records");
+    uint32_t* dbad = ctx.arena.get<uint32_t>("res_bad", 4);
+    PD_HIP(hipMemsetAsync(dbad, 0, sizeof(uint32_t), s));
+    if (n_local) {
+        hipLaunchKernelGGL(fill_i32_kernel, dim3(blocks((uint64_t)n_local)), dim3(kBlock), 0, s,
+                           labels, (uint64_t)n_local, kUnset);
+        if (core_out) PD_HIP(hipMemsetAsync(core_out, 0, (size_t)n_local, s));
+    }
+    const uint64_t lo = (uint64_t)src_off[me], hi = (uint64_t)src_off[me + 1];
+    if (hi > lo)
+        hipLaunchKernelGGL(results_self_kernel, dim3(blocks(hi - lo)), dim3(kBlock), 0, s, keys,
+                           core, owner, gid, lo, hi, roots, (uint32_t)n_roots, gid_base,
+                           (uint64_t)n_local, labels, core_out, dbad);
+    if (expect_remote > 0) {
+        uint32_t* list = ctx.arena.get<uint32_t>("res_list", (size_t)nr + 1);
+        uint32_t* dcount = ctx.arena.get<uint32_t>("res_count", 4);
+        rocprim::counting_iterator<uint32_t> it(0u);
+        size_t tb = 0;
+        IsRemoteOwned pred{owner, lo, hi};
+        PD_HIP(rocprim::select(nullptr, tb, it, list, dcount, (size_t)nr, pred, s));
+        void* tmp = ctx.arena.get<char>("res_tmp", tb);
+        PD_HIP(rocprim::select(tmp, tb, it, list, dcount, (size_t)nr, pred, s));
+        hipLaunchKernelGGL(results_pack_kernel, dim3(blocks((uint64_t)expect_remote)), dim3(kBlock),
+                           0, s, list, dcount, expect_remote, keys, core, gid, roots,
+                           (uint32_t)n_roots, pairs, dbad);
+    }
+    PD_HIP(hipGetLastError());
+}
+
+void results_scatter(Ctx& ctx, const uint32_t* pairs, int64_t m, uint32_t gid_base, int64_t n,
+                     int32_t* labels, uint8_t* core, hipStream_t s) {
+    uint32_t* dbad = ctx.arena.get<uint32_t>("res_bad", 4);
+    if (m)
+        hipLaunchKernelGGL(results_scatter_kernel, dim3(blocks((uint64_t)m)), dim3(kBlock), 0, s,
+                           pairs, (uint64_t)m, gid_base, (uint64_t)n, labels, core, dbad);
+    if (n)
+        hipLaunchKernelGGL(unset_check_kernel, dim3(blocks((uint64_t)n)), dim3(kBlock), 0, s, labels,
+                           (uint64_t)n, dbad);
+    PD_HIP(hipGetLastError());
+    uint32_t* hb = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+    PD_HIP(hipMemcpyAsync(hb, dbad, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    sync(s);
+    const uint32_t b = *hb;
+    if (b & 1) throw Error(-1, "results: a global id outside this device's points");
+    if (b & 2) throw Error(-1, "results: a point received no result (each point must be owned by "
+                               "exactly one device)");
+    if (b & 4) throw Error(-1, "results: a cluster key has no root among the roots given (roots "
+                               "must be gathered from every device)");
+    if (b & 8) throw Error(-1, "results: the owned records to return differ from the exchanged "
+                               "counts");
 }
 
 }  // namespace pd

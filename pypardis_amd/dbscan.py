@@ -190,21 +190,21 @@ class DBSCAN(object):
     otherwise), single device only.  Never changes the labels.
 
     Multi-GPU (the reference's fan-out over executors, R:dbscan/dbscan.py:
-    104-126):
-      * inside an initialised torch.distributed process group of more than
-        one rank (one process per GPU, e.g. torchrun), ``train(slice)``
-        clusters the union of every rank's slice; each rank passes its own
-        slice and gets ``labels_`` / ``core_sample_mask_`` for it (input
-        order), the global ``n_clusters_``, the same ``bounding_boxes`` /
-        ``expanded_boxes``, ``neighbors`` over its slice, and a ``result``
-        whose ``collect()`` (a collective) returns every (key, label).  Keys
-        of array input are global indices (rank offset + row).  Collectives
-        run on RCCL through libpardis (pd_comm_*) for an "nccl" group;
-      * ``n_gpus=N > 1`` without a process group: this process drives GPUs
-        0..N-1 itself (one thread per device, pd_comm_init_all), the input
-        split by index;
-      * ``n_gpus=1``: one device even inside a process group.
-    ``group``: the process group to use (default: the world group).
+    104-126) is opt-in:
+      * ``group=`` a torch.distributed process group (or ``'world'``), one
+        process per GPU (e.g. torchrun): ``train(slice)`` clusters the union
+        of every rank's slice; each rank passes its own slice and gets
+        ``labels_`` / ``core_sample_mask_`` for it (input order), the global
+        ``n_clusters_``, the same ``bounding_boxes`` / ``expanded_boxes``,
+        ``neighbors`` over its slice, and a ``result`` whose ``collect()`` (a
+        collective) returns every (key, label).  Keys of array input are
+        global indices (rank offset + row).  Collectives run on RCCL through
+        libpardis (pd_comm_*) for an "nccl" group;
+      * ``n_gpus=N > 1`` without a group: this process drives GPUs 0..N-1
+        itself (one thread per device, pd_comm_init_all), the input split by
+        index;
+      * neither: one device — also inside an initialised process group (each
+        rank clusters its own data, the reference's single-driver behaviour).
     ``device``: where the points go (default: the current CUDA device).
     """
 
@@ -231,17 +231,21 @@ class DBSCAN(object):
         self.shard = None
 
     def _process_group(self):
-        if self.group is not None:
-            return self.group
-        if self.n_gpus == 1:
+        """The process group of an opt-in sharded train: ``group=`` (a
+        torch.distributed group, or 'world'), else None — a rank of a
+        torchrun / DDP job that does not ask for it clusters its own data on
+        its own device, as the reference's ``train`` would."""
+        if self.group is None:
             return None
         import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            if self.n_gpus not in (None, dist.get_world_size()):
-                raise ValueError(f"n_gpus={self.n_gpus} inside a process group of "
-                                 f"{dist.get_world_size()} ranks")
-            return dist.group.WORLD
-        return None
+        if not (dist.is_available() and dist.is_initialized()):
+            raise ValueError("group= needs an initialised torch.distributed process group")
+        group = dist.group.WORLD if isinstance(self.group, str) and self.group == "world" \
+            else self.group
+        if self.n_gpus not in (None, dist.get_world_size(group)):
+            raise ValueError(f"n_gpus={self.n_gpus} inside a process group of "
+                             f"{dist.get_world_size(group)} ranks")
+        return group
 
     def train(self, data):
         """

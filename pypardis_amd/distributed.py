@@ -8,13 +8,17 @@ halo records are shuffled with ``partitionBy(max_partitions)``
 (R:dbscan/dbscan.py:153-165, R:dbscan/aggregator.py:9-73).  Here each rank
 holds a slice of the points in its GPU's HBM and the same steps are:
 
-  1. bbox: one all-reduce (min / max / non-finite count);
-  2. KD levels: per level one all-gather of the double-double moment partials
-     (added exactly, so the split axes and bounds equal the single-device
-     ones bit for bit) and one all-reduce of the seven-bound counts;
+  1. bbox (min / max / non-finite count): part of the first KD level's
+     gather (min_var), else one all-reduce;
+  2. KD levels (pd_kdx_*): per level one all-gather of the double-double
+     moment partials (added exactly, so the split axes and bounds equal the
+     single-device ones bit for bit) and one all-reduce of the seven-bound
+     counts, both as device tensors, the decisions on the device — no host
+     round trip until the KD trace is read at the end;
   3. routing: neighbourhood L goes to rank ``L * world // P``; every point
      travels once to each rank whose neighbourhoods' 2·eps boxes hold it
-     (pd_route / pd_pack), one all-to-all-v per field;
+     (pd_route2 / pd_pack2: one ordered pass, the self block packed in place),
+     one grouped exchange of all fields (pd_comm_exchange);
   4. phase A on each rank (pd_train_begin): grid, counts, union-find, local
      component keys; export (global id, key) of core points that also live on
      another rank;
@@ -22,10 +26,12 @@ holds a slice of the points in its GPU's HBM and the same steps are:
      (pd_merge_exports) — the RCCL label merge;
   6. phase B (pd_train_end): border attach with global keys;
   7. labels: all-gather of the cluster roots (one id per cluster), sorted, and
-     each key's rank is its label (pd_select_roots / pd_sort_u32 /
-     pd_rank_labels) — sklearn's numbering, as the single-device pd_train.
+     each key's rank is its label — sklearn's numbering, as the single-device
+     pd_train; the owned records of this rank's own block are labelled in
+     place, the others go back to their source rank as (gid, label) pairs in
+     one exchange (pd_results / pd_results_scatter).
 
-Result: each rank returns the global ids and labels of the points it owns
+Result: each rank returns the labels of its input slice, in input order
 (every point is owned by exactly one rank: the one holding its KD partition).
 
 d > 4 (the dense tile path) shares steps 1-2 (the KD boxes of the API) and
@@ -109,6 +115,40 @@ class NativeOps(object):
 
     def select_roots(self, keys, gid):
         return _native.select_roots(keys, gid, ctx=self.ctx)
+
+    # -- device-decided KD, one-pass exchange, results (pd_kdx_*, pd_route2,
+    # pd_pack2, pd_results*)
+    def kdx_begin(self, d, levels):
+        _native.kdx_begin(d, levels, self.device.index, ctx=self.ctx)
+
+    def kdx_moments(self, X, labels, level, S):
+        return _native.kdx_moments(X, labels, level, S, ctx=self.ctx)
+
+    def kdx_axes(self, gathered, n_ranks, level):
+        _native.kdx_axes(gathered, n_ranks, level, ctx=self.ctx)
+
+    def kdx_counts(self, X, labels, level, S):
+        return _native.kdx_counts(X, labels, level, S, ctx=self.ctx)
+
+    def kdx_boundary(self, counts, level):
+        _native.kdx_boundary(counts, level, ctx=self.ctx)
+
+    def kdx_end(self, X, labels, n_splits, final_split):
+        return _native.kdx_end(X, labels, n_splits, final_split, ctx=self.ctx)
+
+    def route2(self, X, ebox, part_rank, kdlab, world):
+        return _native.route2(X, ebox, part_rank, kdlab, world, ctx=self.ctx)
+
+    def pack2(self, X, kdlab, part_rank, local_index, gid_base, outs):
+        _native.pack2(X, kdlab, part_rank, local_index, gid_base, outs, ctx=self.ctx)
+
+    def results(self, keys, core, owner, gid, roots, n_total, gid_base, n_local, world, rank,
+                src_off, expect_remote):
+        return _native.results(keys, core, owner, gid, roots, n_total, gid_base, n_local, world,
+                               rank, src_off, expect_remote, self.device.index, ctx=self.ctx)
+
+    def results_scatter(self, pairs, gid_base, labels, core):
+        _native.results_scatter(pairs, gid_base, labels, core, ctx=self.ctx)
 
     def sort(self, data):
         return _native.sort_u32(data, ctx=self.ctx)
@@ -204,9 +244,10 @@ class _TorchComm(object):
         return t.to(self.device)
 
     def all_reduce(self, arr, op):
+        if op not in _TORCH_OPS:
+            raise ValueError(f"unknown reduction {op!r}")
         t = torch.as_tensor(np.ascontiguousarray(arr)).to(self.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM,
-                        group=self.group)
+        dist.all_reduce(t, op=_TORCH_OPS[op], group=self.group)
         return t.cpu().numpy()
 
     def all_reduce_t(self, t, op):
@@ -231,6 +272,38 @@ class _TorchComm(object):
         outs = [torch.empty_like(buf) for _ in range(self.world)]
         dist.all_gather(outs, buf, group=self.group)
         return torch.cat([o[:int(s)] for o, s in zip(outs, sizes)])
+
+    def all_gather_t(self, t):
+        """(world, *t.shape): every rank's tensor of one shape, rank order."""
+        x = self.to(t).contiguous()
+        outs = [torch.empty_like(x) for _ in range(self.world)]
+        dist.all_gather(outs, x, group=self.group)
+        return torch.stack(outs)
+
+    def exchange(self, sends, recvs, send_counts, recv_counts, skip_self=True):
+        """Field-wise all-to-all into `recvs` (rows grouped by source); with
+        skip_self the self blocks are already in place (pd_pack2) and the send
+        buffers hold the other ranks' blocks only."""
+        me = self.rank
+        sc = np.array(send_counts, np.int64)
+        rc = np.array(recv_counts, np.int64)
+        if skip_self:
+            sc[me] = rc[me] = 0
+        ro = np.concatenate([[0], np.cumsum(np.asarray(recv_counts, np.int64))])
+        for snd, rcv in zip(sends, recvs):
+            row = tuple(rcv.shape[1:])
+            w = int(np.prod(row)) if row else 1
+            got = torch.empty(int(rc.sum()) * w, dtype=rcv.dtype, device=self.device)
+            dist.all_to_all_single(got, self.to(snd.reshape(-1)).contiguous(),
+                                   output_split_sizes=[int(c) * w for c in rc],
+                                   input_split_sizes=[int(c) * w for c in sc], group=self.group)
+            got = got.reshape((-1,) + row)
+            k = 0
+            for r in range(self.world):
+                c = int(rc[r])
+                if c:
+                    rcv[int(ro[r]):int(ro[r]) + c] = got[k:k + c].to(rcv.device)
+                k += c
 
     def all_to_all_v(self, send, send_counts, recv_counts):
         """Rows of `send` grouped by destination -> rows grouped by source."""
@@ -271,16 +344,33 @@ class RcclComm(object):
     def to(self, t):
         return t.to(self.device)
 
+    _OPS = {"sum": _native.PD_R_SUM, "min": _native.PD_R_MIN, "max": _native.PD_R_MAX}
+
+    def _op(self, op):
+        if op not in self._OPS:
+            raise ValueError(f"unknown reduction {op!r}")
+        return self._OPS[op]
+
     def all_reduce(self, arr, op):
         t = torch.as_tensor(np.ascontiguousarray(arr)).to(self.device)
-        self.comm.all_reduce(t, _native.PD_R_MAX if op == "max" else _native.PD_R_SUM)
+        self.comm.all_reduce(t, self._op(op))
         return t.cpu().numpy()
 
     def all_reduce_t(self, t, op):
         r = self.to(t).contiguous().clone()
-        code = {"sum": _native.PD_R_SUM, "min": _native.PD_R_MIN, "max": _native.PD_R_MAX}[op]
-        self.comm.all_reduce(r, code)
+        self.comm.all_reduce(r, self._op(op))
         return r
+
+    def all_gather_t(self, t):
+        x = self.to(t).contiguous()
+        return self.comm.all_gather_v(x.reshape((1,) + tuple(x.shape)), [1] * self.world)
+
+    def exchange(self, sends, recvs, send_counts, recv_counts, skip_self=True):
+        self.comm.exchange([self.to(t) for t in sends], recvs, send_counts, recv_counts,
+                           skip_self=skip_self)
+
+    def abort(self):
+        self.comm.abort()
 
     def all_gather_np(self, arr):
         a = np.ascontiguousarray(arr)
@@ -314,69 +404,56 @@ def make_comm(group, device):
 class ShardedResult(object):
     """Per-rank output of ``train_sharded``.
 
-    :gid: global ids of the points this rank owns (ascending)
-    :labels: their DBSCAN labels (sklearn numbering over all points, -1 noise)
-    :core: their core flags
     :local_labels, local_core: labels / core flags of this rank's INPUT
-        points in input order (returned by the owners; None when
-        ``return_local`` was off)
+        points in input order (returned by the owners)
     :gid_base: global id of this rank's first input point
     :n_total: points over all ranks
     :n_clusters: number of clusters over all points
     :splits: the KD trace (identical on every rank)
     :bounding_boxes: label -> BoundingBox of each KD partition
     :boxes: (P, 2, d) expanded boxes
+    :gid, labels, core: the records this rank owns (the points of its KD
+        partitions): global ids, labels, core flags — computed on first use
+        (diagnostics; the train itself never needs them)
     """
 
     def __init__(self, **kw):
+        self._owned = kw.pop("owned", None)
+        self._cache = None
+        if "gid" in kw:   # given directly (the dense path holds every label)
+            self._cache = (kw.pop("gid"), kw.pop("labels"), kw.pop("core"))
         self.__dict__.update(kw)
 
+    def _owned_view(self):
+        if self._cache is None:
+            if self._owned is None:
+                raise AttributeError("owned records were not kept")
+            ops, keys, core, owner, gid, roots, n = self._owned
+            own = owner >= 0
+            g = gid if gid is not None else \
+                torch.arange(n, dtype=torch.int32, device=owner.device)
+            labels = ops.rank_labels(keys, roots) if n else ops.empty(0, torch.int32)
+            self._cache = (g[own], labels[own], core[own])
+        return self._cache
 
-def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitions=None,
-                  group=None, ops=None, split_method='min_var', comm=None, return_local=True):
-    """Sharded DBSCAN train over the ranks of ``group`` (default: world).
+    @property
+    def gid(self):
+        return self._owned_view()[0]
 
-    X: this rank's (n_i, d) slice (float32/float64, on this rank's GPU for
-    NativeOps); the global id of row j is sum(n_0 .. n_{i-1}) + j.
-    ``max_partitions`` defaults to the world size (one KD partition per GPU).
-    ``split_method``: 'min_var' (default) or 'rotation' (KDPartitioner's).
-    ``comm``: a collective layer (make_comm(group, device) by default: RCCL
-    through libpardis for an "nccl" group, torch.distributed otherwise).
-    """
-    if split_method not in ('min_var', 'rotation'):
-        split_method = 'min_var'   # the reference's fallback (R:dbscan/partition.py:129-130)
-    if X.dim() != 2:
-        raise ValueError("X must be an (n, d) tensor")
-    ops = ops or NativeOps(X.device)
-    comm = comm or make_comm(group, getattr(ops, "device", X.device))
-    W, rank = comm.world, comm.rank
+    @property
+    def labels(self):
+        return self._owned_view()[1]
+
+    @property
+    def core(self):
+        return self._owned_view()[2]
+
+
+def _kd_host(X, kdlab, levels, ops, comm, split_method, dense, lap):
+    """KD partition with the level decisions on the host (rotation; d > 4):
+    per level one all-gather of the moment partials and one all-reduce of the
+    counts through host memory.  -> (data_box, boxes, splits)."""
     n, d = X.shape
-    P = int(max_partitions) if max_partitions is not None else W
-    if P < 1:
-        raise ValueError("max_partitions must be >= 1")
-    if P > 64 * 1024:
-        raise ValueError("max_partitions too large")
-    metric = _native.metric_code(metric) if not isinstance(metric, int) else metric
-    stats = {}
-    clock = [time.perf_counter()]
-
-    def lap(name):   # host wall time per phase (each phase ends in a host sync)
-        now = time.perf_counter()
-        stats[name + "_ms"] = round(1e3 * (now - clock[0]), 3)
-        clock[0] = now
-
-    # ---- global ids
-    sizes = comm.all_gather_np(np.array([n], np.int64))[:, 0]
-    gid_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-    gid_base = int(gid_off[rank])
-    n_total = int(gid_off[-1])
-    if n_total >= 0xFFFFFFFF:
-        raise ValueError("the sharded train addresses points with 32-bit global ids")
-
-    # ---- bbox (R:dbscan/partition.py:135-137), fused into the first
-    # level's moments pass for min_var
-    kdlab = ops.zeros(n, torch.int32)
-    levels = _split_schedule(P)
     fused = split_method == 'min_var'
     first = None
     if n and fused and levels:
@@ -388,18 +465,10 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     # one all-reduce (max) of (-lo, hi, non-finite count): any count > 0 fails
     ext = comm.all_reduce(np.concatenate([-np.asarray(lo, np.float64),
                                           np.asarray(hi, np.float64), [float(bad)]]), "max")
-    nbad = ext[2 * d]
-    if nbad:
+    if ext[2 * d]:
         raise ValueError("Input contains NaN or infinity.")
-    if n_total == 0:
-        raise ValueError("no points on any rank")
     data_box = np.concatenate([-ext[:d], ext[d:2 * d]])
-    box = BoundingBox(k=d).union(BoundingBox(data_box[:d], data_box[d:]))
-
-    # ---- KD partition (R:dbscan/partition.py:139-183): per level one fused
-    # pass (the previous level's split + this level's moments) and one counts
-    # pass; the last split runs alone
-    boxes = {0: box}
+    boxes = {0: BoundingBox(k=d).union(BoundingBox(data_box[:d], data_box[d:]))}
     splits = []
     fp32 = X.dtype == torch.float32
     pending = None
@@ -434,54 +503,157 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
         boundary, cand = level_boundaries(cnt, bounds)
         pending = (sel, axes, boundary, new)
         apply_level(boxes, splits, level, axes, means, vars_, cnt, cand, boundary)
-    dense = d > 4
     if pending is not None and n and not dense:
         ops.split(X, kdlab, *pending)
+    return data_box, boxes, splits
+
+
+def _kd_device(X, kdlab, levels, ops, comm, dev):
+    """KD partition (min_var, exact sums) with the level decisions on the
+    device (pd_kdx_*): per level the moment partials are all-gathered and the
+    counts all-reduced as device tensors — no host round trip until the end
+    (R:dbscan/partition.py:139-183; the splits equal one device's bit for bit).
+    -> (data_box, boxes, splits); kdlab ends as the partition labels."""
+    n, d = X.shape
+    W = comm.world
+    ops.kdx_begin(d, levels)
+    for lv, level in enumerate(levels):
+        S = len(level)
+        part = ops.kdx_moments(X, kdlab, lv, S)
+        ops.kdx_axes(comm.all_gather_t(part).to(dev), W, lv)
+        cnt = ops.kdx_counts(X, kdlab, lv, S)
+        ops.kdx_boundary(comm.all_reduce_t(cnt, "sum").to(dev), lv)
+    trace, lo, hi, bad = ops.kdx_end(X, kdlab, sum(len(lv) for lv in levels), True)
+    if bad:
+        raise ValueError("Input contains NaN or infinity.")
+    data_box = np.concatenate([lo, hi])
+    boxes = {0: BoundingBox(k=d).union(BoundingBox(lo, hi))}
+    splits = []
+    k = 0
+    for level in levels:
+        t = trace[k:k + len(level)]
+        k += len(level)
+        apply_level(boxes, splits, level, t[:, 0].astype(np.int64).tolist(), t[:, 1], t[:, 2],
+                    t[:, 3:11].astype(np.int64), t[:, 11].astype(np.int64).tolist(), t[:, 12])
+    return data_box, boxes, splits
+
+
+def _exclusive(c):
+    c = np.asarray(c, np.int64)
+    return np.concatenate([[0], np.cumsum(c)]).astype(np.int64)
+
+
+def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitions=None,
+                  group=None, ops=None, split_method='min_var', comm=None, return_local=True):
+    """Sharded DBSCAN train over the ranks of ``group`` (default: world).
+
+    X: this rank's (n_i, d) slice (float32/float64, on this rank's GPU for
+    NativeOps); the global id of row j is sum(n_0 .. n_{i-1}) + j.
+    ``max_partitions`` defaults to the world size (one KD partition per GPU).
+    ``split_method``: 'min_var' (default) or 'rotation' (KDPartitioner's).
+    ``comm``: a collective layer (make_comm(group, device) by default: RCCL
+    through libpardis for an "nccl" group, torch.distributed otherwise).
+    """
+    if split_method not in ('min_var', 'rotation'):
+        split_method = 'min_var'   # the reference's fallback (R:dbscan/partition.py:129-130)
+    if X.dim() != 2:
+        raise ValueError("X must be an (n, d) tensor")
+    ops = ops or NativeOps(X.device)
+    comm = comm or make_comm(group, getattr(ops, "device", X.device))
+    W, rank = comm.world, comm.rank
+    n, d = X.shape
+    P = int(max_partitions) if max_partitions is not None else W
+    if P < 1:
+        raise ValueError("max_partitions must be >= 1")
+    if P > 64 * 1024:
+        raise ValueError("max_partitions too large")
+    metric = _native.metric_code(metric) if not isinstance(metric, int) else metric
+    dev = getattr(ops, "device", X.device)
+    stats = {}
+    clock = [time.perf_counter()]
+
+    def lap(name):   # host wall time per phase (each phase ends in a host sync)
+        now = time.perf_counter()
+        stats[name + "_ms"] = round(1e3 * (now - clock[0]), 3)
+        clock[0] = now
+
+    # ---- global ids
+    sizes = comm.all_gather_np(np.array([n], np.int64))[:, 0]
+    gid_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    gid_base = int(gid_off[rank])
+    n_total = int(gid_off[-1])
+    if n_total >= 0xFFFFFFFF:
+        raise ValueError("the sharded train addresses points with 32-bit global ids")
+    if n_total == 0:
+        raise ValueError("no points on any rank")
+
+    # ---- KD partition (R:dbscan/partition.py:135-183)
+    kdlab = ops.zeros(n, torch.int32)
+    levels = _split_schedule(P)
+    dense = d > 4
+    if split_method == 'min_var' and levels and not dense:
+        data_box, boxes, splits = _kd_device(X, kdlab, levels, ops, comm, dev)
+    else:
+        data_box, boxes, splits = _kd_host(X, kdlab, levels, ops, comm, split_method, dense, lap)
     ebox = np.stack([boxes[L].expand(2 * eps).as_array() for L in sorted(boxes)])
     lap("kd")
     if dense:
         return _train_dense(X, eps, min_samples, metric, comm, ops, gid_off, data_box,
                             dict(splits=splits, bounding_boxes=boxes, boxes=ebox), stats, lap)
 
-    # ---- route + exchange (R:dbscan/dbscan.py:114-118,136-151)
+    # ---- route + exchange (R:dbscan/dbscan.py:114-118,136-151): one ordered
+    # pass packs every destination (the self block straight into the receive
+    # buffers), one grouped exchange moves all fields
     part_rank, local_index = partition_ranks(P, W)
-    if n:
-        mask, send_counts = ops.route(X, ebox, part_rank, W)
+    if W == 1:
+        # every neighbourhood is here: the slice is the record set as it is
+        Xr, gid, owner, xr = X, None, kdlab, None
+        nr = n
+        recv_counts = np.array([n], np.int64)
+        own_counts = np.array([[n]], np.int64)   # [src, dest] owned records
+        stats["sent"] = 0
     else:
-        mask, send_counts = None, np.zeros(W, np.int64)
-    tot = int(send_counts.sum())
-    s_coords = ops.empty(tot, X.dtype, d)
-    s_gid = ops.empty(tot, torch.int32)
-    s_owner = ops.empty(tot, torch.int32)
-    s_xr = ops.empty(tot, torch.uint8)
-    off = 0
-    for dest in range(W):
-        c = int(send_counts[dest])
-        if c and n:
-            m = ops.pack(X, mask, dest, kdlab, part_rank, local_index, gid_base,
-                         (s_coords[off:off + c], s_gid[off:off + c], s_owner[off:off + c],
-                          s_xr[off:off + c]))
-            if m != c:
-                raise RuntimeError(f"pack: {m} points for rank {dest}, route said {c}")
-        off += c
-    recv_counts = comm.all_gather_np(send_counts.astype(np.int64))[:, rank].astype(np.int64)
-    dev = getattr(ops, "device", X.device)
-    Xr = comm.all_to_all_v(s_coords, send_counts, recv_counts).to(dev).reshape(-1, d)
-    gid = comm.all_to_all_v(s_gid, send_counts, recv_counts).to(dev)
-    owner = comm.all_to_all_v(s_owner, send_counts, recv_counts).to(dev)
-    xr = comm.all_to_all_v(s_xr, send_counts, recv_counts).to(dev)
-    del s_coords, s_gid, s_owner, s_xr, mask
-    nr = int(recv_counts.sum())
-    stats["sent"], stats["received"] = tot, nr
+        cnt = ops.route2(X, ebox, part_rank, kdlab, W)            # (W, 2): routed, owned
+        allc = comm.all_gather_np(cnt.astype(np.int64))           # (src, dest, 2)
+        send_counts = cnt[:, 0].astype(np.int64)
+        recv_counts = allc[:, rank, 0].astype(np.int64)
+        own_counts = allc[:, :, 1].astype(np.int64)
+        nr = int(recv_counts.sum())
+        ro = _exclusive(recv_counts)
+        Xr = ops.empty(nr, X.dtype, d)
+        gid = ops.empty(nr, torch.int32)
+        owner = ops.empty(nr, torch.int32)
+        xr = ops.empty(nr, torch.uint8)
+        ns = int(send_counts.sum() - send_counts[rank])
+        s_coords, s_gid = ops.empty(ns, X.dtype, d), ops.empty(ns, torch.int32)
+        s_owner, s_xr = ops.empty(ns, torch.int32), ops.empty(ns, torch.uint8)
+        outs, so = [], 0
+        for r in range(W):
+            c = int(send_counts[r])
+            if r == rank:
+                a = int(ro[rank])
+                outs.append((Xr[a:a + c], gid[a:a + c], owner[a:a + c], xr[a:a + c]))
+            else:
+                outs.append((s_coords[so:so + c], s_gid[so:so + c], s_owner[so:so + c],
+                             s_xr[so:so + c]))
+                so += c
+        if n:
+            ops.pack2(X, kdlab, part_rank, local_index, gid_base, outs)
+        comm.exchange([s_coords, s_gid, s_owner, s_xr], [Xr, gid, owner, xr], send_counts,
+                      recv_counts, skip_self=True)
+        del s_coords, s_gid, s_owner, s_xr, outs
+        stats["sent"] = ns
+    stats["received"] = nr
     lap("exchange")
 
     # ---- phase A on this rank's neighbourhoods
     mine = [L for L in range(P) if part_rank[L] == rank]
-    if mine:
+    if mine and nr:
         n_exp = ops.train_begin(Xr.contiguous(), eps, min_samples, metric, ebox[mine], owner,
                                 gid, xr, data_box)
         e_gid, e_key = ops.exports(n_exp)
     else:
+        n_exp = 0
         e_gid = ops.empty(0, torch.int32)
         e_key = ops.empty(0, torch.int32)
     stats["exports"] = int(e_gid.shape[0])
@@ -489,40 +661,49 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
 
     # ---- global key merge (R:dbscan/dbscan.py:153-165): one gather of the
     # (id, key) pairs, then the same O(exports) union on every rank
-    ex = comm.all_gather_var(torch.stack([e_gid, e_key], 1)).to(dev)
-    keymap = ops.merge(ex[:, 0].contiguous(), ex[:, 1].contiguous()) if ex.shape[0] else None
-    stats["exports_total"] = int(ex.shape[0])
+    keymap = None
+    if W > 1:
+        ex = comm.all_gather_var(torch.stack([e_gid, e_key], 1)).to(dev)
+        keymap = ops.merge(ex[:, 0].contiguous(), ex[:, 1].contiguous()) if ex.shape[0] else None
+        stats["exports_total"] = int(ex.shape[0])
+    else:
+        stats["exports_total"] = 0
     lap("merge")
 
-    # ---- phase B, labels
-    if mine:
+    # ---- phase B: border attach with the global keys, the cluster roots of
+    # every rank (sklearn's numbering: a key's rank among them)
+    if mine and nr:
         keys, core = ops.train_end(nr, keymap)
     else:
         keys, core = ops.empty(0, torch.int32), ops.empty(0, torch.uint8)
     roots = ops.select_roots(keys, gid) if nr else ops.empty(0, torch.int32)
-    all_roots = comm.all_gather_var(roots).to(dev).contiguous()
+    all_roots = (comm.all_gather_var(roots) if W > 1 else roots).to(dev).contiguous()
     ops.sort(all_roots)
     # one root per cluster over all ranks: only owned records carry keys
     # (shard.hip IsRoot); a duplicate would double-count a cluster
-    if all_roots.shape[0] > 1 and bool((all_roots[1:] == all_roots[:-1]).any()):
+    if W > 1 and all_roots.shape[0] > 1 and bool((all_roots[1:] == all_roots[:-1]).any()):
         raise RuntimeError("sharded train: a cluster root was selected on two ranks")
-    labels = ops.rank_labels(keys, all_roots) if nr else ops.empty(0, torch.int32)
-    own = owner >= 0
     lap("phase_b")
 
-    # ---- results back to the ranks that hold the points, in input order
-    # (the reference's result RDD, R:dbscan/dbscan.py:162-164)
-    loc_labels = loc_core = None
-    if return_local:
-        pairs, back = ops.owned_results(owner, gid, labels, core, gid_off)
-        got = comm.all_gather_np(back.astype(np.int64))[:, rank].astype(np.int64)
-        pairs_in = comm.all_to_all_v(pairs, back, got).to(dev)
-        loc_labels, loc_core = ops.scatter_results(pairs_in, gid_base, n)
-        lap("results")
-    return ShardedResult(gid=gid[own], labels=labels[own], core=core[own],
-                         local_labels=loc_labels, local_core=loc_core, gid_base=gid_base,
+    # ---- labels back to the ranks that hold the points, in input order (the
+    # reference's result RDD, R:dbscan/dbscan.py:162-164): the self block
+    # directly, the rest as (gid, label | core) pairs in one exchange
+    src_off = _exclusive(recv_counts)
+    back_send = own_counts[:, rank].copy()    # owned records of block r go back to r
+    back_recv = own_counts[rank, :].copy()    # my points each rank owns
+    back_send[rank] = back_recv[rank] = 0
+    loc_labels, loc_core, pairs = ops.results(keys, core, owner, gid, all_roots, n_total,
+                                              gid_base, n, W, rank, src_off,
+                                              int(back_send.sum()))
+    pairs_in = ops.empty(int(back_recv.sum()), torch.int32, 2)
+    if W > 1:
+        comm.exchange([pairs], [pairs_in], back_send, back_recv, skip_self=False)
+    ops.results_scatter(pairs_in, gid_base, loc_labels, loc_core)
+    lap("results")
+    return ShardedResult(local_labels=loc_labels, local_core=loc_core, gid_base=gid_base,
                          n_total=n_total, n_clusters=int(all_roots.shape[0]), splits=splits,
-                         bounding_boxes=boxes, boxes=ebox, stats=stats)
+                         bounding_boxes=boxes, boxes=ebox, stats=stats,
+                         owned=(ops, keys, core, owner, gid, all_roots, nr))
 
 
 def _train_dense(X, eps, min_samples, metric, comm, ops, gid_off, data_box, kd, stats, lap):
@@ -559,15 +740,18 @@ def _train_dense(X, eps, min_samples, metric, comm, ops, gid_off, data_box, kd, 
 
 
 def train_threads(slices, eps, min_samples, comms, ops, metric=_native.PD_EUCLIDEAN,
-                  max_partitions=None, split_method='min_var'):
+                  max_partitions=None, split_method='min_var', abort_timeout=60.0):
     """One process driving several devices: rank r = thread r runs
     ``train_sharded`` on slices[r] with comms[r] (e.g. RcclComm over
     pd_comm_init_all) and ops[r].  Returns the per-rank results in rank order;
-    the first rank error is raised (after every thread has finished)."""
+    the first rank error is raised.  A rank that fails alone aborts every
+    communicator (pd_comm_abort) so the others return instead of waiting for
+    it; the aborted communicators are dropped from the caches."""
     import threading
 
     W = len(slices)
     out, errs = [None] * W, [None] * W
+    order = []   # ranks in the order their errors happened: the first is the cause
 
     def body(r):
         try:
@@ -579,19 +763,45 @@ def train_threads(slices, eps, min_samples, comms, ops, metric=_native.PD_EUCLID
                                    split_method=split_method)
         except BaseException as e:   # noqa: B902 - re-raised below
             errs[r] = e
+            order.append(r)
 
     ts = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(W)]
     for t in ts:
         t.start()
-    for t in ts:
-        t.join()
-    for e in errs:
-        if e is not None:
-            raise e
+    # a rank that fails alone would leave the others blocked on it for ever:
+    # on the first error abort every communicator (pd_comm_abort releases the
+    # ranks waiting in RCCL), then collect the threads
+    aborted = False
+    while any(t.is_alive() for t in ts):
+        for t in ts:
+            t.join(timeout=0.05)
+        if not aborted and any(e is not None for e in errs):
+            aborted = True
+            for c in comms:
+                if hasattr(c, "abort"):
+                    c.abort()
+            _forget_comms(comms)
+            for t in ts:
+                t.join(timeout=abort_timeout)
+            break
+    if order:
+        raise errs[order[0]]
+    if any(t.is_alive() for t in ts):
+        raise RuntimeError("train_threads: ranks still running after the communicators were "
+                           "aborted")
     return out
 
 
 _device_comms = {}
+
+
+def _forget_comms(comms):
+    """Drop aborted communicators from the caches (a new call re-creates them)."""
+    ids = {id(c) for c in comms}
+    for cache in (_device_comms, _rccl_cache):
+        for k in [k for k, v in cache.items()
+                  if (id(v) in ids) or (isinstance(v, list) and any(id(x) in ids for x in v))]:
+            del cache[k]
 
 
 def device_comms(devices):

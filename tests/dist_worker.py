@@ -53,7 +53,7 @@ def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native,
                 data = [("k%06d" % (cuts[rank] + j), v) for j, v in enumerate(Xi.cpu().numpy())]
             model = dbscan.DBSCAN(eps=eps, min_samples=min_samples,
                                   metric=["euclidean", "cityblock"][metric], max_partitions=P,
-                                  device=None if native else "cpu")
+                                  device=None if native else "cpu", group="world")
             model.train(data)
             res = model.shard
             pairs = model.assignments()
@@ -170,3 +170,79 @@ def run_rccl_world1(X, eps, min_samples, P, out_dir, timeout=300):
         raise RuntimeError(f"rank exit code {p.exitcode}")
     z = np.load(os.path.join(out_dir, "rccl.npz"))
     return dict(labels=z["labels"], n_clusters=int(z["ncl"]))
+
+
+def _rehearsal_rank(rank, world, port, x_path, eps, min_samples, P, out_dir):
+    """One rank of a full-size rehearsal: gloo on the host for the
+    collectives, every rank's device stages on cuda:0, the reference API
+    (DBSCAN(group='world').train(slice)) exactly as bench.py --gpus N runs it."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    import dbscan
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        X = np.load(x_path, mmap_mode="r")
+        cuts = cut_points(len(X), world)
+        Xi = torch.from_numpy(np.ascontiguousarray(X[cuts[rank]:cuts[rank + 1]])).to("cuda:0")
+        del X
+        dist.barrier()
+        t0 = time.perf_counter()
+        m = dbscan.DBSCAN(eps=eps, min_samples=min_samples, max_partitions=P,
+                          group="world").train(Xi)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        np.savez(os.path.join(out_dir, f"h{rank}.npz"), labels=m.labels_.cpu().numpy(),
+                 core=m.core_sample_mask_.cpu().numpy(), ncl=np.int64(m.n_clusters_),
+                 lo=np.int64(cuts[rank]), seconds=np.float64(el),
+                 received=np.int64(m.shard.stats["received"]),
+                 exports=np.int64(m.shard.stats["exports_total"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_rehearsal(world, x_path, eps, min_samples, P, out_dir, timeout=900):
+    """Spawn `world` gloo ranks sharing cuda:0 over the points saved at
+    x_path; returns the assembled labels / core flags in input order."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_rehearsal_rank,
+                         args=(r, world, port, x_path, eps, min_samples, P, out_dir))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+            p.join()
+    codes = [p.exitcode for p in procs]
+    if any(c != 0 for c in codes):
+        raise RuntimeError(f"rank exit codes {codes}")
+    n = len(np.load(x_path, mmap_mode="r"))
+    labels = np.full(n, -3, np.int64)
+    core = np.zeros(n, np.uint8)
+    ncl, secs, received, exports = set(), [], 0, 0
+    for r in range(world):
+        z = np.load(os.path.join(out_dir, f"h{r}.npz"))
+        lo = int(z["lo"])
+        labels[lo:lo + len(z["labels"])] = z["labels"]
+        core[lo:lo + len(z["core"])] = z["core"]
+        ncl.add(int(z["ncl"]))
+        secs.append(float(z["seconds"]))
+        received += int(z["received"])
+        exports = max(exports, int(z["exports"]))
+    return dict(labels=labels, core=core, ncl=ncl, seconds=secs, received=received,
+                exports=exports)

@@ -30,6 +30,34 @@ class LocalComm(object):
         self.sh.barrier.wait()
         return vals
 
+    def abort(self):
+        """pd_comm_abort's role: release every rank blocked on the group."""
+        self.sh.barrier.abort()
+
+    def all_reduce_t(self, t, op):
+        vals = torch.stack(self._exchange(t.clone()))
+        return {"sum": vals.sum(0), "max": vals.max(0).values,
+                "min": vals.min(0).values}[op].to(t.dtype)
+
+    def all_gather_t(self, t):
+        return torch.stack(self._exchange(t.clone()))
+
+    def exchange(self, sends, recvs, send_counts, recv_counts, skip_self=True):
+        me = self.rank
+        sc = [int(c) for c in send_counts]
+        if skip_self:
+            sc[me] = 0
+        blocks = [list(torch.split(s, sc)) for s in sends]
+        vals = self._exchange(blocks)
+        ro = np.concatenate([[0], np.cumsum(np.asarray(recv_counts, np.int64))])
+        for f, rcv in enumerate(recvs):
+            for src in range(self.world):
+                if skip_self and src == me:
+                    continue
+                b = vals[src][f][me]
+                assert b.shape[0] == int(recv_counts[src])
+                rcv[int(ro[src]):int(ro[src]) + b.shape[0]] = b
+
     def to(self, t):
         return t.to(self.device)
 

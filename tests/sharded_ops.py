@@ -115,10 +115,122 @@ class OracleOps(object):
         xr.copy_(torch.from_numpy(many.astype(np.uint8)))
         return len(idx)
 
+    # -- device-decided KD (pd_kdx_*) restated: the same level chain, the
+    # partial / count tensors of the collectives, the 13-double trace
+    def kdx_begin(self, d, levels):
+        self.kdx = dict(d=d, levels=levels, trace=[], dec={}, bbox=None)
+
+    def kdx_moments(self, X, labels, level, S):
+        k = self.kdx
+        lv = k["levels"][level]
+        sel = [c for c, _ in lv]
+        if level > 0:
+            prev = k["levels"][level - 1]
+            axes, boundary = k["dec"][level - 1]
+            self.split(X, labels, [c for c, _ in prev], axes, boundary, [nl for _, nl in prev])
+        out = self.moments_dd(X, labels, sel).reshape(-1)
+        if level == 0:
+            lo, hi, bad = self.bbox(X) if X.shape[0] else \
+                (np.full(k["d"], np.inf), np.full(k["d"], -np.inf), 0)
+            out = np.concatenate([out, lo, hi, [float(bad)]])
+        return torch.from_numpy(np.ascontiguousarray(out, np.float64))
+
+    def kdx_axes(self, gathered, n_ranks, level):
+        from pypardis_amd.distributed import dd_combine
+        from pypardis_amd.partition import level_axes
+        k = self.kdx
+        d = k["d"]
+        S = len(k["levels"][level])
+        g = gathered.numpy().reshape(n_ranks, -1)
+        parts = g[:, :S * (1 + 4 * d)].reshape(n_ranks, S, 1 + 4 * d)
+        if level == 0:
+            b = g[:, S * (1 + 4 * d):]
+            k["bbox"] = (b[:, :d].min(0), b[:, d:2 * d].max(0), b[:, 2 * d].sum())
+        axes, means, vars_, bounds = level_axes(dd_combine(parts))
+        k["cur"] = (axes, means, vars_, bounds)
+
+    def kdx_counts(self, X, labels, level, S):
+        axes, _, _, bounds = self.kdx["cur"]
+        sel = [c for c, _ in self.kdx["levels"][level]]
+        return torch.from_numpy(self.counts(X, labels, sel, axes, bounds).reshape(-1))
+
+    def kdx_boundary(self, counts, level):
+        from pypardis_amd.partition import level_boundaries
+        k = self.kdx
+        axes, means, vars_, bounds = k["cur"]
+        cnt = counts.numpy().reshape(-1, 8)
+        boundary, cand = level_boundaries(cnt, bounds)
+        k["dec"][level] = (axes, boundary)
+        for s in range(len(axes)):
+            k["trace"].append([axes[s], means[s], vars_[s]] + [float(c) for c in cnt[s]] +
+                              [cand[s], boundary[s]])
+
+    def kdx_end(self, X, labels, n_splits, final_split):
+        k = self.kdx
+        last = len(k["levels"]) - 1
+        if final_split and X.shape[0]:
+            lv = k["levels"][last]
+            axes, boundary = k["dec"][last]
+            self.split(X, labels, [c for c, _ in lv], axes, boundary, [nl for _, nl in lv])
+        lo, hi, bad = k["bbox"]
+        trace = np.array(k["trace"], np.float64).reshape(n_splits, 13)
+        return trace, lo, hi, int(bad)
+
+    # -- one-pass exchange (pd_route2 / pd_pack2) restated
+    def route2(self, X, ebox, part_rank, kdlab, world):
+        mask, counts = self.route(X, ebox, part_rank, world)
+        self._mask = mask
+        lab = kdlab.numpy()
+        own = np.bincount(np.asarray(part_rank)[lab], minlength=world) if len(lab) else \
+            np.zeros(world, np.int64)
+        return np.stack([counts, own[:world]], 1).astype(np.int64)
+
+    def pack2(self, X, kdlab, part_rank, local_index, gid_base, outs):
+        for r, out in enumerate(outs):
+            if out[1].numel():
+                m = self.pack(X, self._mask, r, kdlab, part_rank, local_index, gid_base, out)
+                assert m == out[1].shape[0]
+
+    # -- results (pd_results / pd_results_scatter) restated
+    def results(self, keys, core, owner, gid, roots, n_total, gid_base, n_local, world, rank,
+                src_off, expect_remote):
+        kunset = -(1 << 31)
+        labels = np.full(n_local, kunset, np.int64)
+        core_out = np.zeros(n_local, np.uint8)
+        nr = keys.shape[0]
+        lab = self.rank_labels(keys, roots).numpy().astype(np.int64) if nr else \
+            np.zeros(0, np.int64)
+        g = gid.numpy().view(np.uint32).astype(np.int64) if gid is not None else np.arange(nr)
+        own = owner.numpy() >= 0
+        c = core.numpy() if nr else np.zeros(0, np.uint8)
+        lo, hi = int(src_off[rank]), int(src_off[rank + 1])
+        selfi = np.nonzero(own[lo:hi])[0] + lo
+        labels[g[selfi] - gid_base] = lab[selfi]
+        core_out[g[selfi] - gid_base] = c[selfi]
+        rem = np.nonzero(own & ((np.arange(nr) < lo) | (np.arange(nr) >= hi)))[0]
+        assert len(rem) == expect_remote, (len(rem), expect_remote)
+        v = (lab[rem] + 1) | (c[rem].astype(np.int64) << 31)
+        pairs = np.stack([g[rem], v], 1).astype(np.uint32).view(np.int32)
+        self._unset = kunset
+        return (torch.from_numpy(labels.astype(np.int32)), torch.from_numpy(core_out),
+                torch.from_numpy(np.ascontiguousarray(pairs).reshape(-1, 2)))
+
+    def results_scatter(self, pairs, gid_base, labels, core):
+        p = pairs.numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
+        lab = labels.numpy()
+        idx = p[:, 0] - gid_base
+        assert ((idx >= 0) & (idx < len(lab))).all(), "results: gid outside this rank"
+        lab[idx] = (p[:, 1] & 0x7FFFFFFF) - 1
+        core.numpy()[idx] = (p[:, 1] >> 31).astype(np.uint8)
+        assert (lab != self._unset).all(), "results: a point received no result"
+
     def train_begin(self, X, eps, min_samples, metric, ebox, owner, gid, xr, data_box):
         m = "euclidean" if metric == 0 else "cityblock"
-        self.state, self.exp = osh.phase_a(X.numpy(), eps, min_samples, ebox, owner.numpy(),
-                                           gid.numpy(), xr.numpy(), m)
+        n = X.shape[0]
+        g = gid.numpy() if gid is not None else np.arange(n, dtype=np.int32)
+        x = xr.numpy() if xr is not None else np.zeros(n, np.uint8)
+        self.state, self.exp = osh.phase_a(X.numpy(), eps, min_samples, ebox, owner.numpy(), g, x,
+                                           m)
         return len(self.exp[0])
 
     def exports(self, m):
@@ -137,7 +249,8 @@ class OracleOps(object):
 
     def select_roots(self, keys, gid):
         k = keys.numpy()
-        return torch.from_numpy(gid.numpy()[(k >= 0) & (k == gid.numpy())].copy())
+        g = gid.numpy() if gid is not None else np.arange(len(k), dtype=np.int32)
+        return torch.from_numpy(g[(k >= 0) & (k == g)].copy())
 
     def sort(self, data):
         data.copy_(torch.sort(data).values)

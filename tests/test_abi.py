@@ -44,7 +44,7 @@ def test_python_binding_covers_header():
 def test_abi_version_and_error_string(lib):
     lib.pd_abi_version.restype = ctypes.c_int32
     lib.pd_last_error.restype = ctypes.c_char_p
-    assert lib.pd_abi_version() == 2
+    assert lib.pd_abi_version() == 3
     assert isinstance(lib.pd_last_error(), bytes)
 
 

@@ -148,6 +148,34 @@ def test_train_threads_local_comm():
     assert {r.n_clusters for r in res} == {int(g["sk_labels"].max()) + 1}
 
 
+def test_train_threads_rank_failure_aborts():
+    """A rank that fails alone (here: its ops raise in phase A) must not leave
+    the other ranks waiting for it for ever: train_threads aborts the
+    communicators and raises that rank's error."""
+    import time
+
+    from local_comm import local_comms
+    from pypardis_amd.distributed import train_threads
+    from sharded_ops import OracleOps
+    import torch
+
+    class Failing(OracleOps):
+        def train_begin(self, *a, **k):
+            raise RuntimeError("injected failure on one rank")
+
+    g = load_golden("b3d_20k")
+    X = g["X"]
+    W = 3
+    cuts = [r * len(X) // W for r in range(W + 1)]
+    slices = [torch.from_numpy(np.ascontiguousarray(X[cuts[r]:cuts[r + 1]])) for r in range(W)]
+    ops = [OracleOps(), Failing(), OracleOps()]
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="injected failure"):
+        train_threads(slices, float(g["eps"]), int(g["min_samples"]), local_comms(W), ops,
+                      max_partitions=4, abort_timeout=30.0)
+    assert time.time() - t0 < 60
+
+
 def _dense_blobs(n=6000, d=8, seed=5):
     rng = np.random.default_rng(seed)
     c = rng.uniform(-4, 4, size=(6, d))

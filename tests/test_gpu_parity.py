@@ -230,7 +230,7 @@ def test_train_matches_oracle(native, case):
 
 @pytest.mark.parametrize("variant,link_mode,border_roots",
                          [(0, 5, 0), (7, 3, 1), (5, 0, 0), (7, 2, 0), (5, 4, 0), (5, 3, 0),
-                          (5, 6, 0), (0, 6, 0)])
+                          (5, 6, 0), (0, 6, 0), (13, 6, 0), (15, 3, 1), (8, 0, 0)])
 def test_sweep_variants_exact(native, variant, link_mode, border_roots):
     """PD_OPT_SWEEP_VARIANT x PD_OPT_LINK_MODE: the row-by-row and the
     batched sweep kernels, and the sampled-union + cell-verify link (3) or the
@@ -534,6 +534,15 @@ def test_rccl_comm_single_rank(native):
     np.testing.assert_array_equal(comm.all_to_all_v(w, [6], [6]).cpu().numpy(),
                                   w.cpu().numpy())
     np.testing.assert_array_equal(comm.all_gather_np(np.array([3, 4])), [[3, 4]])
+    # the W > 1 init check's pattern, fill and verify kernels (at W = 1 the
+    # self blocks carry it), the grouped field exchange and the device gather
+    comm.comm.self_check()
+    a = torch.arange(15, dtype=torch.float32, device="cuda").reshape(5, 3)
+    b = torch.arange(5, dtype=torch.int32, device="cuda")
+    ra, rb = torch.empty_like(a), torch.empty_like(b)
+    comm.exchange([a, b], [ra, rb], [5], [5], skip_self=False)
+    assert torch.equal(ra, a) and torch.equal(rb, b)
+    assert torch.equal(comm.all_gather_t(b), b[None])
     X, cfg = synth.make_config("C2", n=300_000)
     Xd = _dev(X)
     lab1, core1, _, nc1 = native.cluster(Xd, cfg["eps"], cfg["min_samples"])

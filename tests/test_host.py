@@ -133,6 +133,11 @@ def test_as_points_edge_forms_cpu():
     # (keys, X) with two points
     p = as_points((np.array([4, 5]), X[:2]), device="cpu")
     assert list(p.keys) == [4, 5] and torch.equal(p.X, torch.from_numpy(X[:2]))
+    # (keys, X) with a torch key tensor (its elements are 0-d tensors)
+    p = as_points((torch.arange(3) + 10, X), device="cpu")
+    assert list(p.keys) == [10, 11, 12] and p.keys.dtype == np.int64 and p.n == 3
+    p = as_points((torch.arange(3), torch.from_numpy(X)), device="cpu")
+    assert list(p.keys) == [0, 1, 2] and torch.equal(p.X, torch.from_numpy(X))
     # dtype from every vector: one float64 vector after many float32 ones
     recs = [(i, X[i % 3]) for i in range(100)] + [(100, np.array([0.1, 0.2]))]
     p = as_points(recs, device="cpu")

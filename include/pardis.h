@@ -86,8 +86,9 @@ enum pd_option {
                                registers, three rows swept as one list), a clear bit the
                                row-by-row kernel; bit 3 (count) the persistent-lane kernel
                                (lanes take the next record of their wave's chunk when they
-                               finish; overrides bit 0).  Default 13 (the measured best on
-                               MI355X). */
+                               finish; overrides bit 0); bit 4 (border) likewise (overrides
+                               bit 2 unless PD_OPT_BORDER_ROOTS).  Default 13 (the measured
+                               best on MI355X). */
     PD_OPT_BORDER_ROOTS = 10, /* batched border sweep: skip or stop early where the stencil's
                                 directory words hold at most one cluster root (tuning; same
                                 labels; default 0 — slower on C2) */

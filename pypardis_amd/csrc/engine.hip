@@ -2636,6 +2636,111 @@ __global__ __launch_bounds__(kBlock) void border2_kernel(
     key_out[vals[r] & kIdMask] = best;
 }
 
+// border3_kernel (PD_OPT_SWEEP_VARIANT bit 4): border2's plain sweep (the
+// smallest cluster key among the core neighbours, every row) with count3's
+// persistent lanes and fp32-chord rows: a wave owns kChunk list entries and a
+// lane that has swept all rows of its record takes the next entry.
+template <typename T, int D, int M, bool U>
+__device__ __forceinline__ void border3_wave(const T* __restrict__ Xs, const uint32_t* __restrict__ list,
+                                             uint32_t c0, uint32_t c1, const Cells& C, int L0,
+                                             double eps, double eps2, float lo, float hi,
+                                             const uint32_t* __restrict__ vals,
+                                             const uint32_t* __restrict__ par,
+                                             const uint32_t* __restrict__ gmin,
+                                             uint32_t* __restrict__ key_out) {
+    constexpr int NR = NRows<D>::v;
+    const int lane = threadIdx.x & 63;
+    float e2 = M == 0 ? (float)eps2 : (float)eps;
+    e2 = e2 * (1.0f + 1.0f / 65536.0f);
+    Count3Grid<T, D, M, U> g;
+    if constexpr (U) g.load(C.parts + L0);
+    Pred<T, D, M> pr;
+    RowGeo<D> geo;
+    uint32_t r = kNone, best = kNone, j = 0, e = 0;
+    int q = NR;
+    uint32_t next = c0;
+    bool active = true;
+    while (true) {
+        bool need = active && j >= e;
+        while (__any(need)) {
+            const bool fin = need && q >= NR;
+            if (fin && r != kNone) key_out[vals[r] & kIdMask] = best;
+            const unsigned long long b = __ballot(fin);
+            const uint32_t pos = next + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+            next += (uint32_t)__popcll(b);
+            if (fin) {
+                if (pos < c1) {
+                    r = list[pos];
+                    double a[D];
+                    load_rec<T, D>(Xs, r, a);
+                    pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
+                    if constexpr (!U) {
+                        const int L = part_of(C.part_start, C.P, r);
+                        g.load(C.parts + L);
+                    }
+                    geo = row_geo<T, D, M, U>(g, a);
+                    best = kNone;
+                    q = 0;
+                } else {
+                    r = kNone;
+                    active = false;
+                    need = false;
+                }
+                j = e = 0;
+            }
+            if (need && q < NR) {
+                uint32_t s, en;
+                row_range3<T, D, M, U>(C, g, geo, e2, q, s, en);
+                j = s;
+                e = en;
+                ++q;
+            }
+            need = active && j >= e;
+        }
+        if (!__any(active)) break;
+        if (active) {
+            uint32_t jj[4], pj[4];
+            T b[4][D];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                jj[u] = j + u;
+                const uint32_t x = jj[u] < e ? jj[u] : j;
+                load_raw<T, D>(Xs, x, b[u]);
+                pj[u] = par[x];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (jj[u] < e && pj[u] != kNone && pr(b[u])) {
+                    const uint32_t k = gmin[pj[u]];
+                    best = k < best ? k : best;
+                }
+            j += 4;
+        }
+    }
+}
+
+template <typename T, int D, int M>
+__global__ __launch_bounds__(kBlock) void border3_kernel(
+    const T* __restrict__ Xs, uint32_t NL, const uint32_t* __restrict__ list, Cells C, double eps,
+    double eps2, float lo, float hi, const uint32_t* __restrict__ vals,
+    const uint32_t* __restrict__ par, const uint32_t* __restrict__ gmin,
+    uint32_t* __restrict__ key_out) {
+    const uint32_t wv = xcd_block(blockIdx.x, gridDim.x) * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t c0l = (uint64_t)wv * kChunk;
+    if (c0l >= NL) return;
+    const uint32_t c0 = (uint32_t)c0l;
+    const uint32_t c1 = (uint32_t)(c0l + kChunk < NL ? c0l + kChunk : NL);
+    // the list ascends, so the chunk's records span [list[c0], list[c1 - 1]]
+    const uint32_t r0 = list[c0], r1 = list[c1 - 1];
+    const int L0 = part_of(C.part_start, C.P, r0);
+    if (C.part_start[L0 + 1] > r1)
+        border3_wave<T, D, M, true>(Xs, list, c0, c1, C, L0, eps, eps2, lo, hi, vals, par, gmin,
+                                    key_out);
+    else
+        border3_wave<T, D, M, false>(Xs, list, c0, c1, C, L0, eps, eps2, lo, hi, vals, par, gmin,
+                                     key_out);
+}
+
 // Single device: key_out holds each point's label (rank; kNone = noise) with
 // the core flag in bit 30 — split it into labels and the core mask.
 __global__ __launch_bounds__(kBlock) void final_label_kernel(const uint32_t* __restrict__ key,
@@ -2766,7 +2871,12 @@ void launch_border(int variant, hipStream_t s, const T* Xs, uint32_t NL, const u
                    const Cells& C, double eps, double eps2, float lo, float hi,
                    const uint32_t* vals, const uint32_t* par, const uint32_t* gmin,
                    const uint32_t* wroot, uint32_t* key_out) {
-    if (variant & 4)
+    if ((variant & 16) && !wroot) {   // persistent lanes, kChunk list entries per wave
+        const uint64_t waves = ((uint64_t)NL + kChunk - 1) / kChunk;
+        const unsigned nb = (unsigned)((waves + kBlock / 64 - 1) / (kBlock / 64));
+        hipLaunchKernelGGL((border3_kernel<T, D, M>), dim3(nb ? nb : 1), dim3(kBlock), 0, s, Xs, NL,
+                           list, C, eps, eps2, lo, hi, vals, par, gmin, key_out);
+    } else if (variant & 4)
         hipLaunchKernelGGL((border2_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
                            list, C, eps, eps2, lo, hi, vals, par, gmin, wroot, key_out);
     else

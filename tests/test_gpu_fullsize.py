@@ -119,3 +119,104 @@ def test_c4_device_sample_vs_oracle(native):
     assert m.n_clusters_ == nc
     assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), want)
     assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_w)
+
+
+# ------------------------------------------------------------ C3 (d = 64) at full size
+def _exact_neighbours(X64, Q, eps, chunk=16384):
+    """Every point within eps of each query (self included), by sklearn's exact
+    predicate: candidates from an fp64 Gram bound with a wide margin, then the
+    per-axis sum in axis order, every operation rounded (numpy elementwise),
+    `<= eps*eps` (SK:neighbors/_binary_tree.pxi.tp:1949-1958; at d > 15 the
+    reference's brute query differs only inside a 1-ulp band)."""
+    qn = (X64[Q] ** 2).sum(1)
+    cand = [[] for _ in Q]
+    for s in range(0, len(X64), chunk):
+        C = X64[s:s + chunk]
+        cn = (C ** 2).sum(1)
+        d2 = qn[:, None] + cn[None, :] - 2.0 * (X64[Q] @ C.T)
+        ok = d2 <= eps * eps * 1.001 + 1e-9 * (qn[:, None] + cn[None, :])
+        qi, ci = np.nonzero(ok)
+        for a, b in zip(qi.tolist(), (ci + s).tolist()):
+            cand[a].append(b)
+    out = []
+    eps2 = eps * eps
+    for a, q in enumerate(Q):
+        c = np.asarray(cand[a], np.int64)
+        acc = np.zeros(len(c))
+        for j in range(X64.shape[1]):
+            t = X64[c, j] - X64[q, j]
+            acc = acc + t * t
+        out.append(c[acc <= eps2])
+    return out
+
+
+def test_c3_full_1m_vs_oracle(native):
+    """The bench's C3 answer (1M x 64-D embeddings, eps 0.114028,
+    min_samples 10) against the exact predicate on a sample:
+    2,000 random points plus every core point of a random 20 % of the
+    clusters — exact neighbour counts over all 1M points (the oracle's
+    counts_capped on each candidate set, and the numpy restatement), exact
+    core flags, equal labels on every core-core edge, each sampled cluster
+    one connected component of its core points, and the border rule (the
+    smallest label among the core neighbours, -1 without one)."""
+    import oracle
+    from pypardis_amd import synth
+    X, cfg = synth.make_config("C3")
+    eps, ms = cfg["eps"], cfg["min_samples"]
+    ctx = native.context()
+    ctx.set_option(native.PD_OPT_FULL_COUNTS, 1)
+    try:
+        lab_t, core_t, cnt_t, ncl = native.cluster(torch.from_numpy(X).cuda(), eps, ms,
+                                                   want_counts=True)
+    finally:
+        ctx.set_option(native.PD_OPT_FULL_COUNTS, 0)
+    lab = lab_t.cpu().numpy().astype(np.int64)
+    core = core_t.cpu().numpy().astype(bool)
+    cnt = cnt_t.cpu().numpy().astype(np.int64)
+    assert ncl > 100 and core.sum() > 1000
+    rng = np.random.default_rng(11)
+    sample = rng.choice(len(X), 2000, replace=False)
+    chosen = rng.choice(ncl, max(1, ncl // 5), replace=False)
+    core_pts = np.nonzero(core & np.isin(lab, chosen))[0]
+    Q = np.unique(np.concatenate([sample, core_pts]))
+    X64 = X.astype(np.float64)
+    nb = _exact_neighbours(X64, Q, eps)
+    pos = {int(q): i for i, q in enumerate(Q)}
+    edges = 0
+    for i, q in enumerate(Q):
+        c = nb[i]
+        # pinned oracle on the candidate superset == the restatement == GPU
+        assert oracle.counts_capped(X64[q:q + 1], X64[c], eps, 0)[0] == len(c)
+        assert len(c) == cnt[q], (q, len(c), cnt[q])
+        assert (len(c) >= ms) == core[q], q
+        cn = c[core[c]]
+        if core[q]:
+            assert (lab[cn] == lab[q]).all(), q
+            edges += len(cn)
+        elif len(cn):
+            assert lab[q] == lab[cn].min(), q
+        else:
+            assert lab[q] == -1, q
+    # every chosen cluster's core points form one component of exact edges
+    parent = {int(p): int(p) for p in core_pts}
+
+    def find(x):
+        while parent[x] != x:
+            parent[x] = parent[parent[x]]
+            x = parent[x]
+        return x
+
+    for p in core_pts:
+        for r in nb[pos[int(p)]]:
+            r = int(r)
+            if r in parent:
+                a, b = find(int(p)), find(r)
+                if a != b:
+                    parent[max(a, b)] = min(a, b)
+    roots = {}
+    for p in core_pts:
+        roots.setdefault(int(lab[p]), set()).add(find(int(p)))
+    assert set(roots) == set(int(c) for c in chosen if (lab[core] == c).any())
+    assert all(len(r) == 1 for r in roots.values())
+    print(f"\nC3 1M: clusters={ncl} queries={len(Q)} core-queries={len(core_pts)} "
+          f"core-core edges={edges}")

@@ -217,10 +217,10 @@ def grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages):
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "frac_kind": "model: algorithmic B_nc, every candidate cell read once per record",
-            "traffic": None, "kernel": "count3_kernel", "kernel_ms": t_cnt,
+            "traffic": None, "kernel": "count4_kernel", "kernel_ms": t_cnt,
             "bytes_per_record": per, "records": rec, "cells": cells,
             "algorithmic_bytes": alg_bytes, "pmc_source": pmc_src}
-    k = (pmc or {}).get("count3_kernel") or (pmc or {}).get("count2_kernel")
+    k = (pmc or {}).get("count4_kernel") or (pmc or {}).get("count2_kernel")
     if k:
         f = pmc_fields(k)
         if "hbm_bytes" in f:

@@ -84,11 +84,10 @@ enum pd_option {
                                identical): bit 0 count, bit 1 link, bit 2 border; a set bit
                                selects the batched lane kernel (wave-uniform grid in scalar
                                registers, three rows swept as one list), a clear bit the
-                               row-by-row kernel; bit 3 (count) the persistent-lane kernel
-                               (lanes take the next record of their wave's chunk when they
-                               finish; overrides bit 0); bit 4 (border) likewise (overrides
-                               bit 2 unless PD_OPT_BORDER_ROOTS).  Default 13 (the measured
-                               best on MI355X). */
+                               row-by-row kernel; bit 3 (count) and bit 4 (border) the
+                               batched kernels with fp32-chord rows keyed off the query cell
+                               (override bits 0 / 2; bit 4 not with PD_OPT_BORDER_ROOTS).
+                               Default 29 (the measured best on MI355X). */
     PD_OPT_BORDER_ROOTS = 10, /* batched border sweep: skip or stop early where the stencil's
                                 directory words hold at most one cluster root (tuning; same
                                 labels; default 0 — slower on C2) */

@@ -28,7 +28,7 @@ PD_OPT_DENSE_PRUNE = 11
 PD_OPT_COUNT_ROTATE = 12
 PD_OPT_CENTRE_WINDOW = 13
 PD_OPT_DIR_BUDGET = 14
-SWEEP_VARIANT_DEFAULT = 13
+SWEEP_VARIANT_DEFAULT = 29
 LINK_MODE_DEFAULT = 6
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
@@ -698,7 +698,7 @@ def select_roots(keys, gid, ctx=None):
     roots = torch.empty(max(n, 1), dtype=torch.int32, device=device)
     m = np.zeros(1, np.int64)
     _check(load().pd_select_roots(ctx.ptr, keys.data_ptr() if n else None,
-                                  gid.data_ptr() if n else None, n, roots.data_ptr(),
+                                  _ptr(gid) if n else None, n, roots.data_ptr(),
                                   m.ctypes.data, _stream(device)))
     return roots[:int(m[0])]
 

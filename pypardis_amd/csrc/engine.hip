@@ -1504,29 +1504,26 @@ __global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs
     if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
 }
 
-// ------------------------------------------------------------------ persistent-lane count
-// count3_kernel (PD_OPT_SWEEP_VARIANT bit 3, the default): the same answer as
-// count2_kernel — neighbour count with the min_samples early exit, core flag,
-// the two smallest neighbours seen — reorganised for instruction issue, which
-// is what bounds the count sweep (PMC, C2: 2086 VALU instructions per 64-record
-// wave at ~5.4 ms of pure issue time for a 7 ms kernel):
-//   * lanes are persistent within a wave: each wave owns kChunk consecutive
-//     records and a lane that finishes its record (early exit or last row)
-//     takes the next one, so a wave no longer runs at the pace of its slowest
-//     lane (count2: ~30 % of lane-slots did work);
-//   * a lane walks its record's rows one at a time (centre row first); a row's
-//     candidate range costs ~60 instructions instead of ~130: the chord of the
-//     eps-ball is taken in fp32 from the in-cell fraction (distances shrunk by
-//     2^-16 relative + 2^-20 of a cell, the chord grown by 2^-16 + 2^-16 cells:
-//     a superset of the fp64 chord, so no neighbour is ever cut; the fp64 cell
-//     index itself is the one the record keys were built with), the row's key
-//     is the query cell's key plus integer offsets, rows outside the grid have
-//     an infinite distance.
-// A lane's state: its record (query point, Pred), the next row q, the current
-// candidate range [j, e) and, for a long rotated centre row, the wrapped part
-// [ws, we).
-constexpr uint32_t kChunk = 256;   // records per wave (4 per lane on average)
-
+// ------------------------------------------------------------------ cheap-row count
+// count4_kernel (PD_OPT_SWEEP_VARIANT bit 3, the default): count2_kernel's
+// lockstep sweep — three rows as one virtual list, centre batch first, the
+// rotated start in long centre rows, four candidates per round trip — with a
+// row's candidate range at about a third of the instructions.  The count
+// sweep is bound by instruction issue (PMC, C2: 3.29e9 VALU instructions in a
+// 7 ms kernel, ~5.4 ms of pure issue at one wave-instruction per CU per
+// cycle), and the fp64 chord of every row (sqrt, two floors, 64-bit key
+// arithmetic from the cell coordinates: ~130 instructions a row, nine rows)
+// was most of it.  Here, per record once: the fp64 cell index exactly as the
+// record keys were built, the in-cell fractions, the squared distances to the
+// neighbour rows; per row: the chord in fp32 from those (distances shrunk by
+// 2^-16 relative + 2^-20 of a cell, the chord grown by 2^-16 relative + 2^-16
+// of an axis-0 cell: a superset of the fp64 chord, so no neighbour is ever
+// cut), the row's key as integer offsets from the query cell's key, rows
+// outside the grid at an infinite distance.
+//   (A persistent-lane variant — a lane that finishes takes the next record
+//   of its wave's chunk — was measured and rejected: C2 count 7.0 -> 14.6 ms,
+//   8.5e9 VALU instructions: rows hold ~5-10 candidates, so the advance step
+//   ran on almost every sweep step)
 template <int D>
 struct RowGeo {
     uint64_t kc;             // key of the query cell
@@ -1645,115 +1642,8 @@ __device__ __forceinline__ void row_range3(const Cells& C, const Count3Grid<T, D
     e = e > s ? e : s;
 }
 
-template <typename T, int D, int M, bool ST, bool U>
-__device__ __forceinline__ void count3_wave(const T* __restrict__ Xs, uint32_t c0, uint32_t c1,
-                                            const Cells& C, int L0, double eps, double eps2,
-                                            float lo, float hi, uint32_t ms, int full,
-                                            uint32_t rot_min, uint8_t* __restrict__ core,
-                                            uint32_t* __restrict__ mn_out,
-                                            uint32_t* __restrict__ cnt_out,
-                                            unsigned long long* __restrict__ stats) {
-    constexpr int NR = NRows<D>::v;
-    const int lane = threadIdx.x & 63;
-    const uint32_t stop = full ? 0xFFFFFFFFu : ms;
-    // fp32 threshold of the row test: eps^2 (eps) rounded up
-    float e2 = M == 0 ? (float)eps2 : (float)eps;
-    e2 = e2 * (1.0f + 1.0f / 65536.0f);
-    Count3Grid<T, D, M, U> g;
-    if constexpr (U) g.load(C.parts + L0);
-    Pred<T, D, M> pr;
-    RowGeo<D> geo;
-    uint32_t r = kNone, cnt = 0, mn = kNone, mn2 = kNone, n_cand = 0;
-    uint32_t j = 0, e = 0, ws = 0, we = 0;
-    int q = NR;
-    uint32_t next = c0;   // wave-uniform: next record to hand out
-    bool active = true;
-    while (true) {
-        // ---- advance lanes whose range is spent: wrap, next row, or next record
-        bool need = active && (j >= e || cnt >= stop);
-        while (__any(need)) {
-            if (need && j >= e && we > ws && cnt < stop) {   // the wrapped part of the centre row
-                j = ws;
-                e = we;
-                ws = we = 0;
-                need = false;
-            }
-            const bool fin = need && (cnt >= stop || q >= NR);
-            if (fin && r != kNone) {
-                core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
-                reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, mn2);
-                if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
-            }
-            const unsigned long long b = __ballot(fin);
-            const uint32_t pos = next + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
-            next += (uint32_t)__popcll(b);
-            if (fin) {
-                if (pos < c1) {
-                    r = pos;
-                    double a[D];
-                    load_rec<T, D>(Xs, r, a);
-                    pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
-                    if constexpr (!U) {
-                        const int L = part_of(C.part_start, C.P, r);
-                        g.load(C.parts + L);
-                    }
-                    geo = row_geo<T, D, M, U>(g, a);
-                    cnt = 0;
-                    mn = mn2 = kNone;
-                    q = 0;
-                } else {
-                    r = kNone;
-                    active = false;
-                    need = false;
-                }
-                j = e = ws = we = 0;
-            }
-            if (need && q < NR) {   // the next row (new records start at the centre row)
-                uint32_t s, en;
-                row_range3<T, D, M, U>(C, g, geo, e2, q, s, en);
-                j = s;
-                e = en;
-                // a long centre row: start at record r & ~(kRotAlign - 1) when it
-                // lies in the row, and wrap (count2_kernel's rotation)
-                if (q == 0 && en - s > rot_min) {
-                    const uint32_t v = r & ~(kRotAlign - 1u);
-                    if (v > s && v < en) {
-                        j = v;
-                        ws = s;
-                        we = v;
-                    }
-                }
-                ++q;
-            }
-            need = active && (j >= e || cnt >= stop);
-        }
-        if (!__any(active)) break;
-        // ---- four candidates of the current range
-        if (active) {
-            uint32_t jj[4];
-            T b[4][D];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                jj[u] = j + u;
-                load_raw<T, D>(Xs, jj[u] < e ? jj[u] : j, b[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const bool h = jj[u] < e && pr(b[u]);
-                cnt += h ? 1u : 0u;
-                const uint32_t x = h ? jj[u] : kNone;
-                mn2 = min(mn2, max(mn, x));   // the two smallest hits
-                mn = min(mn, x);
-            }
-            if constexpr (ST) n_cand += (e - j < 4u ? e - j : 4u);
-            j += 4;
-        }
-    }
-    if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
-}
-
 template <typename T, int D, int M, bool ST>
-__global__ __launch_bounds__(kBlock) void count3_kernel(const T* __restrict__ Xs, uint32_t R,
+__global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs, uint32_t R,
                                                         Cells C, double eps, double eps2,
                                                         float lo, float hi, uint32_t ms, int full,
                                                         uint32_t rot_min,
@@ -1761,20 +1651,76 @@ __global__ __launch_bounds__(kBlock) void count3_kernel(const T* __restrict__ Xs
                                                         uint32_t* __restrict__ mn_out,
                                                         uint32_t* __restrict__ cnt_out,
                                                         unsigned long long* __restrict__ stats) {
-    const uint32_t wv = xcd_block(blockIdx.x, gridDim.x) * (kBlock / 64) + (threadIdx.x >> 6);
-    const uint64_t c0l = (uint64_t)wv * kChunk;
-    if (c0l >= R) return;
-    const uint32_t c0 = (uint32_t)c0l;
-    const uint32_t c1 = (uint32_t)(c0l + kChunk < R ? c0l + kChunk : R);
-    // one neighbourhood for the whole chunk (all but at most P - 1 chunks):
-    // grid in scalar registers
-    const int L0 = part_of(C.part_start, C.P, c0);
-    if (C.part_start[L0 + 1] >= c1)
-        count3_wave<T, D, M, ST, true>(Xs, c0, c1, C, L0, eps, eps2, lo, hi, ms, full, rot_min,
-                                       core, mn_out, cnt_out, stats);
-    else
-        count3_wave<T, D, M, ST, false>(Xs, c0, c1, C, L0, eps, eps2, lo, hi, ms, full, rot_min,
-                                        core, mn_out, cnt_out, stats);
+    constexpr int NR = NRows<D>::v;
+    constexpr int B = NR < 3 ? NR : 3, NB = NR / B;
+    const uint32_t r = rec_index();
+    if (r >= R) return;
+    double a[D];
+    load_rec<T, D>(Xs, r, a);
+    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
+    const uint32_t stop = full ? 0xFFFFFFFFu : ms;
+    float e2 = M == 0 ? (float)eps2 : (float)eps;
+    e2 = e2 * (1.0f + 1.0f / 65536.0f);
+    uint32_t cnt = 0, mn = kNone, mn2 = kNone, n_cand = 0;
+    with_part(C.part_start, C.P, r, [&](int L, auto U) {
+        Count3Grid<T, D, M, decltype(U)::value> g;
+        g.load(C.parts + L);
+        const RowGeo<D> geo = row_geo<T, D, M, decltype(U)::value>(g, a);
+        for (int bt = 0; bt < NB; ++bt) {   // batch 0: the centre batch, centre row first
+            uint32_t s0, e0, s1 = 0, e1 = 0, s2 = 0, e2r = 0;
+            row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B, s0, e0);
+            if constexpr (B > 1) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 1, s1, e1);
+            if constexpr (B > 2) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 2, s2, e2r);
+            const uint32_t l0 = e0 - s0, l01 = l0 + (e1 - s1), tot = l01 + (e2r - s2);
+            // virtual position w -> record (three rows, no dynamic indexing)
+            auto jpos = [&](uint32_t w) -> uint32_t {
+                uint32_t j = s0 + w;
+                if constexpr (B > 1) j = w >= l0 ? s1 + (w - l0) : j;
+                if constexpr (B > 2) j = w >= l01 ? s2 + (w - l01) : j;
+                return j;
+            };
+            // a long centre batch: start at record r & ~(kRotAlign - 1) when it
+            // lies in the centre row (count2_kernel's rotation) and wrap
+            uint32_t v0 = 0;
+            if (bt == 0 && tot > rot_min) {
+                const uint32_t vr = (r & ~(kRotAlign - 1u)) - s0;
+                v0 = vr < l0 ? vr : 0u;
+            }
+            auto sweep = [&](auto ROT) -> bool {
+                for (uint32_t v = 0; v < tot; v += 4) {
+                    uint32_t j[4];
+                    T b[4][D];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        uint32_t w = v + u;
+                        if constexpr (decltype(ROT)::value) {
+                            w += v0;
+                            w = w >= tot ? w - tot : w;
+                        }
+                        j[u] = jpos(w);
+                        load_raw<T, D>(Xs, v + u < tot ? j[u] : r, b[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool h = (v + u < tot) && pr(b[u]);
+                        cnt += h ? 1u : 0u;
+                        const uint32_t x = h ? j[u] : kNone;
+                        mn2 = min(mn2, max(mn, x));   // the two smallest hits
+                        mn = min(mn, x);
+                    }
+                    if constexpr (ST) n_cand += (tot - v < 4u ? tot - v : 4u);
+                    if (cnt >= stop) return true;
+                }
+                return false;
+            };
+            const bool stopped = __any(v0 != 0) ? sweep(std::true_type{}) : sweep(std::false_type{});
+            if (stopped) return;
+        }
+    });
+    core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
+    reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, mn2);
+    if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
+    if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
 }
 
 // ------------------------------------------------------------------ link mode 3
@@ -2636,109 +2582,59 @@ __global__ __launch_bounds__(kBlock) void border2_kernel(
     key_out[vals[r] & kIdMask] = best;
 }
 
-// border3_kernel (PD_OPT_SWEEP_VARIANT bit 4): border2's plain sweep (the
-// smallest cluster key among the core neighbours, every row) with count3's
-// persistent lanes and fp32-chord rows: a wave owns kChunk list entries and a
-// lane that has swept all rows of its record takes the next entry.
-template <typename T, int D, int M, bool U>
-__device__ __forceinline__ void border3_wave(const T* __restrict__ Xs, const uint32_t* __restrict__ list,
-                                             uint32_t c0, uint32_t c1, const Cells& C, int L0,
-                                             double eps, double eps2, float lo, float hi,
-                                             const uint32_t* __restrict__ vals,
-                                             const uint32_t* __restrict__ par,
-                                             const uint32_t* __restrict__ gmin,
-                                             uint32_t* __restrict__ key_out) {
-    constexpr int NR = NRows<D>::v;
-    const int lane = threadIdx.x & 63;
-    float e2 = M == 0 ? (float)eps2 : (float)eps;
-    e2 = e2 * (1.0f + 1.0f / 65536.0f);
-    Count3Grid<T, D, M, U> g;
-    if constexpr (U) g.load(C.parts + L0);
-    Pred<T, D, M> pr;
-    RowGeo<D> geo;
-    uint32_t r = kNone, best = kNone, j = 0, e = 0;
-    int q = NR;
-    uint32_t next = c0;
-    bool active = true;
-    while (true) {
-        bool need = active && j >= e;
-        while (__any(need)) {
-            const bool fin = need && q >= NR;
-            if (fin && r != kNone) key_out[vals[r] & kIdMask] = best;
-            const unsigned long long b = __ballot(fin);
-            const uint32_t pos = next + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
-            next += (uint32_t)__popcll(b);
-            if (fin) {
-                if (pos < c1) {
-                    r = list[pos];
-                    double a[D];
-                    load_rec<T, D>(Xs, r, a);
-                    pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
-                    if constexpr (!U) {
-                        const int L = part_of(C.part_start, C.P, r);
-                        g.load(C.parts + L);
-                    }
-                    geo = row_geo<T, D, M, U>(g, a);
-                    best = kNone;
-                    q = 0;
-                } else {
-                    r = kNone;
-                    active = false;
-                    need = false;
-                }
-                j = e = 0;
-            }
-            if (need && q < NR) {
-                uint32_t s, en;
-                row_range3<T, D, M, U>(C, g, geo, e2, q, s, en);
-                j = s;
-                e = en;
-                ++q;
-            }
-            need = active && j >= e;
-        }
-        if (!__any(active)) break;
-        if (active) {
-            uint32_t jj[4], pj[4];
-            T b[4][D];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                jj[u] = j + u;
-                const uint32_t x = jj[u] < e ? jj[u] : j;
-                load_raw<T, D>(Xs, x, b[u]);
-                pj[u] = par[x];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (jj[u] < e && pj[u] != kNone && pr(b[u])) {
-                    const uint32_t k = gmin[pj[u]];
-                    best = k < best ? k : best;
-                }
-            j += 4;
-        }
-    }
-}
-
+// border4_kernel (PD_OPT_SWEEP_VARIANT bit 4, the default): border2's plain
+// sweep (the smallest cluster key among the core neighbours, every row) with
+// count4's cheap rows.
 template <typename T, int D, int M>
-__global__ __launch_bounds__(kBlock) void border3_kernel(
+__global__ __launch_bounds__(kBlock) void border4_kernel(
     const T* __restrict__ Xs, uint32_t NL, const uint32_t* __restrict__ list, Cells C, double eps,
     double eps2, float lo, float hi, const uint32_t* __restrict__ vals,
     const uint32_t* __restrict__ par, const uint32_t* __restrict__ gmin,
     uint32_t* __restrict__ key_out) {
-    const uint32_t wv = xcd_block(blockIdx.x, gridDim.x) * (kBlock / 64) + (threadIdx.x >> 6);
-    const uint64_t c0l = (uint64_t)wv * kChunk;
-    if (c0l >= NL) return;
-    const uint32_t c0 = (uint32_t)c0l;
-    const uint32_t c1 = (uint32_t)(c0l + kChunk < NL ? c0l + kChunk : NL);
-    // the list ascends, so the chunk's records span [list[c0], list[c1 - 1]]
-    const uint32_t r0 = list[c0], r1 = list[c1 - 1];
-    const int L0 = part_of(C.part_start, C.P, r0);
-    if (C.part_start[L0 + 1] > r1)
-        border3_wave<T, D, M, true>(Xs, list, c0, c1, C, L0, eps, eps2, lo, hi, vals, par, gmin,
-                                    key_out);
-    else
-        border3_wave<T, D, M, false>(Xs, list, c0, c1, C, L0, eps, eps2, lo, hi, vals, par, gmin,
-                                     key_out);
+    constexpr int NR = NRows<D>::v;
+    constexpr int B = NR < 3 ? NR : 3, NB = NR / B;
+    const uint32_t i = rec_index();
+    if (i >= NL) return;
+    const uint32_t r = list[i];   // owner, non-core records with a neighbour, ascending
+    double a[D];
+    load_rec<T, D>(Xs, r, a);
+    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
+    float e2 = M == 0 ? (float)eps2 : (float)eps;
+    e2 = e2 * (1.0f + 1.0f / 65536.0f);
+    uint32_t best = kNone;
+    with_part(C.part_start, C.P, r, [&](int L, auto U) {
+        Count3Grid<T, D, M, decltype(U)::value> g;
+        g.load(C.parts + L);
+        const RowGeo<D> geo = row_geo<T, D, M, decltype(U)::value>(g, a);
+        for (int bt = 0; bt < NB; ++bt) {
+            uint32_t s0, e0, s1 = 0, e1 = 0, s2 = 0, e2r = 0;
+            row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B, s0, e0);
+            if constexpr (B > 1) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 1, s1, e1);
+            if constexpr (B > 2) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 2, s2, e2r);
+            const uint32_t l0 = e0 - s0, l01 = l0 + (e1 - s1), tot = l01 + (e2r - s2);
+            for (uint32_t v = 0; v < tot; v += 4) {
+                uint32_t j[4], pj[4];
+                T b[4][D];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t w = v + u;
+                    uint32_t jj = s0 + w;
+                    if constexpr (B > 1) jj = w >= l0 ? s1 + (w - l0) : jj;
+                    if constexpr (B > 2) jj = w >= l01 ? s2 + (w - l01) : jj;
+                    j[u] = w < tot ? jj : r;
+                    load_raw<T, D>(Xs, j[u], b[u]);
+                    pj[u] = par[j[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (v + u < tot && pj[u] != kNone && pr(b[u])) {
+                        const uint32_t k = gmin[pj[u]];
+                        best = k < best ? k : best;
+                    }
+            }
+        }
+    });
+    key_out[vals[r] & kIdMask] = best;
 }
 
 // Single device: key_out holds each point's label (rank; kNone = noise) with
@@ -2841,12 +2737,10 @@ template <typename T, int D, int M, bool ST>
 void launch_count(int variant, hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double eps,
                   double eps2, float lo, float hi, uint32_t ms, int full, uint32_t rot_min,
                   uint8_t* core, uint32_t* mn, uint32_t* cnt, unsigned long long* st) {
-    if (variant & 8) {   // persistent lanes, kChunk records per wave
-        const uint64_t waves = ((uint64_t)R + kChunk - 1) / kChunk;
-        const unsigned nb = (unsigned)((waves + kBlock / 64 - 1) / (kBlock / 64));
-        hipLaunchKernelGGL((count3_kernel<T, D, M, ST>), dim3(nb ? nb : 1), dim3(kBlock), 0, s, Xs,
-                           R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
-    } else if (variant & 1)
+    if (variant & 8)   // cheap rows
+        hipLaunchKernelGGL((count4_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
+                           C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
+    else if (variant & 1)
         hipLaunchKernelGGL((count2_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
                            C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
     else
@@ -2871,12 +2765,10 @@ void launch_border(int variant, hipStream_t s, const T* Xs, uint32_t NL, const u
                    const Cells& C, double eps, double eps2, float lo, float hi,
                    const uint32_t* vals, const uint32_t* par, const uint32_t* gmin,
                    const uint32_t* wroot, uint32_t* key_out) {
-    if ((variant & 16) && !wroot) {   // persistent lanes, kChunk list entries per wave
-        const uint64_t waves = ((uint64_t)NL + kChunk - 1) / kChunk;
-        const unsigned nb = (unsigned)((waves + kBlock / 64 - 1) / (kBlock / 64));
-        hipLaunchKernelGGL((border3_kernel<T, D, M>), dim3(nb ? nb : 1), dim3(kBlock), 0, s, Xs, NL,
+    if ((variant & 16) && !wroot)   // cheap rows
+        hipLaunchKernelGGL((border4_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
                            list, C, eps, eps2, lo, hi, vals, par, gmin, key_out);
-    } else if (variant & 4)
+    else if (variant & 4)
         hipLaunchKernelGGL((border2_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
                            list, C, eps, eps2, lo, hi, vals, par, gmin, wroot, key_out);
     else

@@ -18,7 +18,7 @@ if [ "${PMC:-1}" = "1" ]; then
   python - <<'PY'
 import json
 s = json.load(open("gpurun_out/pmc_quick_summary.json"))
-for k in ("count3_kernel", "count2_kernel", "border2_kernel", "window_uf_kernel", "gather_kernel"):
+for k in ("count4_kernel", "count2_kernel", "border4_kernel", "border2_kernel", "window_uf_kernel", "gather_kernel"):
     if k in s:
         v = s[k]
         print(k, {c: round(v[c] / 1e6, 2) for c in v if c.startswith("SQ_")}, "(1e6)")

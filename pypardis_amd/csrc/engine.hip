@@ -255,6 +255,32 @@ struct Pred {
         for (int j = 0; j < D; ++j) bb[j] = (double)b[j];
         return within<D, M>(a, bb, eps, eps2);
     }
+    // Branch-free screen: in = decided inside, maybe = needs exact(); fp64
+    // inputs are always "maybe".
+    __device__ __forceinline__ void screen(const T (&b)[D], bool& in, bool& maybe) const {
+        if constexpr (std::is_same<T, float>::value) {
+            float d = 0.0f;
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const float t = ar[j] - b[j];
+                if constexpr (M == 0)
+                    d = __builtin_fmaf(t, t, d);
+                else
+                    d += fabsf(t);
+            }
+            in = d <= lo;
+            maybe = !in & (d <= hi);
+        } else {
+            in = false;
+            maybe = true;
+        }
+    }
+    __device__ __forceinline__ bool exact(const T (&b)[D]) const {
+        double bb[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) bb[j] = (double)b[j];
+        return within<D, M>(a, bb, eps, eps2);
+    }
 };
 
 template <typename T, int D, int M>
@@ -1672,12 +1698,14 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
             if constexpr (B > 1) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 1, s1, e1);
             if constexpr (B > 2) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 2, s2, e2r);
             const uint32_t l0 = e0 - s0, l01 = l0 + (e1 - s1), tot = l01 + (e2r - s2);
-            // virtual position w -> record (three rows, no dynamic indexing)
+            // virtual position w -> record w + off (three rows, no dynamic
+            // indexing; unsigned wrap-around makes the offsets exact)
+            const uint32_t o1 = s1 - l0, o2 = s2 - l01;
             auto jpos = [&](uint32_t w) -> uint32_t {
-                uint32_t j = s0 + w;
-                if constexpr (B > 1) j = w >= l0 ? s1 + (w - l0) : j;
-                if constexpr (B > 2) j = w >= l01 ? s2 + (w - l01) : j;
-                return j;
+                uint32_t o = s0;
+                if constexpr (B > 1) o = w >= l0 ? o1 : o;
+                if constexpr (B > 2) o = w >= l01 ? o2 : o;
+                return w + o;
             };
             // a long centre batch: start at record r & ~(kRotAlign - 1) when it
             // lies in the centre row (count2_kernel's rotation) and wrap
@@ -1700,11 +1728,25 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
                         j[u] = jpos(w);
                         load_raw<T, D>(Xs, v + u < tot ? j[u] : r, b[u]);
                     }
+                    // screen all four without branches; the exact fp64 test
+                    // only when some lane of the wave has a pair in the band
+                    bool h[4], mb[4];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        const bool h = (v + u < tot) && pr(b[u]);
-                        cnt += h ? 1u : 0u;
-                        const uint32_t x = h ? j[u] : kNone;
+                        pr.screen(b[u], h[u], mb[u]);
+                        const bool ok = v + u < tot;
+                        h[u] &= ok;
+                        mb[u] &= ok;
+                    }
+                    if (__any(mb[0] | mb[1] | mb[2] | mb[3])) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (mb[u]) h[u] = pr.exact(b[u]);
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        cnt += h[u] ? 1u : 0u;
+                        const uint32_t x = h[u] ? j[u] : kNone;
                         mn2 = min(mn2, max(mn, x));   // the two smallest hits
                         mn = min(mn, x);
                     }
@@ -2612,22 +2654,36 @@ __global__ __launch_bounds__(kBlock) void border4_kernel(
             if constexpr (B > 1) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 1, s1, e1);
             if constexpr (B > 2) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 2, s2, e2r);
             const uint32_t l0 = e0 - s0, l01 = l0 + (e1 - s1), tot = l01 + (e2r - s2);
+            const uint32_t o1 = s1 - l0, o2 = s2 - l01;
             for (uint32_t v = 0; v < tot; v += 4) {
                 uint32_t j[4], pj[4];
                 T b[4][D];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const uint32_t w = v + u;
-                    uint32_t jj = s0 + w;
-                    if constexpr (B > 1) jj = w >= l0 ? s1 + (w - l0) : jj;
-                    if constexpr (B > 2) jj = w >= l01 ? s2 + (w - l01) : jj;
-                    j[u] = w < tot ? jj : r;
+                    uint32_t o = s0;
+                    if constexpr (B > 1) o = w >= l0 ? o1 : o;
+                    if constexpr (B > 2) o = w >= l01 ? o2 : o;
+                    j[u] = w < tot ? w + o : r;
                     load_raw<T, D>(Xs, j[u], b[u]);
                     pj[u] = par[j[u]];
                 }
+                bool h[4], mb[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    pr.screen(b[u], h[u], mb[u]);
+                    const bool ok = (v + u < tot) & (pj[u] != kNone);
+                    h[u] &= ok;
+                    mb[u] &= ok;
+                }
+                if (__any(mb[0] | mb[1] | mb[2] | mb[3])) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (mb[u]) h[u] = pr.exact(b[u]);
+                }
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    if (v + u < tot && pj[u] != kNone && pr(b[u])) {
+                    if (h[u]) {
                         const uint32_t k = gmin[pj[u]];
                         best = k < best ? k : best;
                     }

@@ -108,7 +108,11 @@ enum pd_option {
     PD_OPT_DIR_BUDGET = 14    /* bytes the bbox-sized eps-grid directory may take (20 B per 64
                                 cells); beyond it every cell grows by a common factor until it
                                 fits (exact at any width >= eps; more candidates per record).
-                                Default 32 GiB (PD_T_GRID_GROW reports the factor) */
+                                Default 32 GiB (PD_T_GRID_GROW reports the factor) */,
+    PD_OPT_LABEL_BUCKETS = 15 /* single device: the labels reach input order through two
+                                coalesced passes (pairs bucketed by point id, then scattered
+                                inside L2-sized buckets) instead of one scattered write per
+                                record (default 1; same labels with 0) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -1254,7 +1254,7 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
         const uint32_t pt = v & kIdMask;
         if (core_out && !core_bit) core_out[pt] = fl & 1;
         if (cnt_out) cnt_out[pt] = cnt_rec[r];
-        if (fl & 1) key_out[pt] = gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u);
+        if ((fl & 1) && key_out) key_out[pt] = gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u);
     }
     // border candidates (owner record, not core, has a neighbour) per tile;
     // border_list_kernel lists them in order after a scan of the counts
@@ -1698,14 +1698,12 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
             if constexpr (B > 1) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 1, s1, e1);
             if constexpr (B > 2) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 2, s2, e2r);
             const uint32_t l0 = e0 - s0, l01 = l0 + (e1 - s1), tot = l01 + (e2r - s2);
-            // virtual position w -> record w + off (three rows, no dynamic
-            // indexing; unsigned wrap-around makes the offsets exact)
-            const uint32_t o1 = s1 - l0, o2 = s2 - l01;
+            // virtual position w -> record (three rows, no dynamic indexing)
             auto jpos = [&](uint32_t w) -> uint32_t {
-                uint32_t o = s0;
-                if constexpr (B > 1) o = w >= l0 ? o1 : o;
-                if constexpr (B > 2) o = w >= l01 ? o2 : o;
-                return w + o;
+                uint32_t j = s0 + w;
+                if constexpr (B > 1) j = w >= l0 ? s1 + (w - l0) : j;
+                if constexpr (B > 2) j = w >= l01 ? s2 + (w - l01) : j;
+                return j;
             };
             // a long centre batch: start at record r & ~(kRotAlign - 1) when it
             // lies in the centre row (count2_kernel's rotation) and wrap
@@ -1728,25 +1726,11 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
                         j[u] = jpos(w);
                         load_raw<T, D>(Xs, v + u < tot ? j[u] : r, b[u]);
                     }
-                    // screen all four without branches; the exact fp64 test
-                    // only when some lane of the wave has a pair in the band
-                    bool h[4], mb[4];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        pr.screen(b[u], h[u], mb[u]);
-                        const bool ok = v + u < tot;
-                        h[u] &= ok;
-                        mb[u] &= ok;
-                    }
-                    if (__any(mb[0] | mb[1] | mb[2] | mb[3])) {
-#pragma unroll
-                        for (int u = 0; u < 4; ++u)
-                            if (mb[u]) h[u] = pr.exact(b[u]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        cnt += h[u] ? 1u : 0u;
-                        const uint32_t x = h[u] ? j[u] : kNone;
+                        const bool h = (v + u < tot) && pr(b[u]);
+                        cnt += h ? 1u : 0u;
+                        const uint32_t x = h ? j[u] : kNone;
                         mn2 = min(mn2, max(mn, x));   // the two smallest hits
                         mn = min(mn, x);
                     }
@@ -2632,7 +2616,7 @@ __global__ __launch_bounds__(kBlock) void border4_kernel(
     const T* __restrict__ Xs, uint32_t NL, const uint32_t* __restrict__ list, Cells C, double eps,
     double eps2, float lo, float hi, const uint32_t* __restrict__ vals,
     const uint32_t* __restrict__ par, const uint32_t* __restrict__ gmin,
-    uint32_t* __restrict__ key_out) {
+    uint32_t* __restrict__ key_out, uint32_t* __restrict__ rec_out) {
     constexpr int NR = NRows<D>::v;
     constexpr int B = NR < 3 ? NR : 3, NB = NR / B;
     const uint32_t i = rec_index();
@@ -2690,7 +2674,87 @@ __global__ __launch_bounds__(kBlock) void border4_kernel(
             }
         }
     });
-    key_out[vals[r] & kIdMask] = best;
+    // rec_out: by record (the bucketed label pass moves it to the point)
+    if (rec_out)
+        rec_out[r] = best;
+    else
+        key_out[vals[r] & kIdMask] = best;
+}
+
+// ---- labels into input order in two coalesced passes (single device).  The
+// owner records sit in key order, their points in input order: a permutation
+// whose direct scatter (owner_kernel: one 4-B write per record, anywhere in
+// n) moved 28 GB for C4's 1e9 records.  Here label_bucket_kernel partitions
+// the (point, key) pairs of a 64K-record tile by the point's high bits
+// (buckets of 2^kLabBits points, one global reservation per tile and
+// bucket, ~8 pairs per run), and label_scatter_kernel writes each bucket's
+// keys into its 512 KB of key_out from blocks of one XCD, so the random
+// writes combine in that XCD's L2.
+constexpr int kLabBits = 17;
+constexpr uint32_t kLabTile = 65536;
+
+__device__ __forceinline__ bool label_pair(uint32_t r, const uint32_t* __restrict__ vals,
+                                           const uint8_t* __restrict__ core,
+                                           const uint32_t* __restrict__ par,
+                                           const uint32_t* __restrict__ gmin,
+                                           const uint32_t* __restrict__ keyrec, uint32_t& pt,
+                                           uint32_t& key) {
+    const uint32_t v = vals[r];
+    if (!(v & kOwnerBit)) return false;
+    pt = v & kIdMask;
+    const uint8_t fl = core[r];
+    if (fl & 1) {
+        key = gmin[par[r]] | kKeyCoreBit;
+        return true;
+    }
+    if ((fl & 3) != 2) return false;   // noise: key_out keeps kNone
+    key = keyrec[r];
+    return key != kNone;
+}
+
+__global__ __launch_bounds__(kBlock) void label_bucket_kernel(
+    uint32_t R, const uint32_t* __restrict__ vals, const uint8_t* __restrict__ core,
+    const uint32_t* __restrict__ par, const uint32_t* __restrict__ gmin,
+    const uint32_t* __restrict__ keyrec, int nbk, uint32_t* __restrict__ bcnt,
+    uint2* __restrict__ pairs) {
+    extern __shared__ uint32_t lab_sh[];
+    uint32_t* cnt = lab_sh;          // per bucket: pairs of this tile
+    uint32_t* run = lab_sh + nbk;    // then: the next free slot
+    for (int k = threadIdx.x; k < nbk; k += kBlock) cnt[k] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kLabTile;
+    const uint64_t t1 = t0 + kLabTile < R ? t0 + kLabTile : R;
+    for (uint64_t r = t0 + threadIdx.x; r < t1; r += kBlock) {
+        uint32_t pt, key;
+        if (label_pair((uint32_t)r, vals, core, par, gmin, keyrec, pt, key))
+            atomicAdd(&cnt[pt >> kLabBits], 1u);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nbk; k += kBlock) run[k] = cnt[k] ? atomicAdd(bcnt + k, cnt[k]) : 0u;
+    __syncthreads();
+    for (uint64_t r = t0 + threadIdx.x; r < t1; r += kBlock) {
+        uint32_t pt, key;
+        if (label_pair((uint32_t)r, vals, core, par, gmin, keyrec, pt, key)) {
+            const uint32_t b = pt >> kLabBits;
+            const uint32_t pos = atomicAdd(&run[b], 1u);
+            pairs[((uint64_t)b << kLabBits) + pos] = make_uint2(pt, key);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void label_scatter_kernel(const uint2* __restrict__ pairs,
+                                                               const uint32_t* __restrict__ bcnt,
+                                                               int nbk, unsigned bpb,
+                                                               uint32_t* __restrict__ key_out) {
+    const unsigned lb = xcd_block(blockIdx.x, gridDim.x);   // a bucket's blocks share an XCD
+    const unsigned b = lb / bpb, part = lb % bpb;
+    if ((int)b >= nbk) return;
+    const uint32_t c = bcnt[b];
+    const uint2* p = pairs + ((uint64_t)b << kLabBits);
+    for (uint32_t k = part * kBlock + threadIdx.x; k < c; k += bpb * kBlock) {
+        const uint2 q = p[k];
+        key_out[q.x] = q.y;
+    }
 }
 
 // Single device: key_out holds each point's label (rank; kNone = noise) with
@@ -2820,10 +2884,10 @@ template <typename T, int D, int M>
 void launch_border(int variant, hipStream_t s, const T* Xs, uint32_t NL, const uint32_t* list,
                    const Cells& C, double eps, double eps2, float lo, float hi,
                    const uint32_t* vals, const uint32_t* par, const uint32_t* gmin,
-                   const uint32_t* wroot, uint32_t* key_out) {
+                   const uint32_t* wroot, uint32_t* key_out, uint32_t* rec_out = nullptr) {
     if ((variant & 16) && !wroot)   // cheap rows
         hipLaunchKernelGGL((border4_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
-                           list, C, eps, eps2, lo, hi, vals, par, gmin, key_out);
+                           list, C, eps, eps2, lo, hi, vals, par, gmin, key_out, rec_out);
     else if (variant & 4)
         hipLaunchKernelGGL((border2_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
                            list, C, eps, eps2, lo, hi, vals, par, gmin, wroot, key_out);
@@ -3282,20 +3346,41 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     const int core_bit = a.phase == 2 ? 0 : 1;
     PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
     if (a.core && !core_bit) PD_HIP(hipMemsetAsync(a.core, 0, n, s));
+    // single device, no counts wanted, the cheap-row border: labels reach
+    // input order through the bucketed pair passes instead of owner_kernel's
+    // scatter (ctx.label_buckets, PD_OPT_LABEL_BUCKETS)
+    const bool bucketed = a.phase != 2 && core_bit && !a.counts && ctx.label_buckets &&
+                          (ctx.variant & 16) && !st.wroot && n > 0;
     if (R) {
         uint32_t* blist = ctx.arena.get<uint32_t>("border_list", R);
         const unsigned tiles = blocks(R);
         uint32_t* tcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)tiles + 1);
         uint64_t* toff = ctx.arena.get<uint64_t>("tile_off", (size_t)tiles + 1);
+        // bucketed: owner_kernel only tallies the border candidates (no key_out)
         hipLaunchKernelGGL(owner_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core, par, gmin,
-                           st.cnt_rec, core_bit, key_out, a.core, a.counts, tcnt);
+                           st.cnt_rec, core_bit, bucketed ? nullptr : key_out, a.core, a.counts,
+                           tcnt);
         const uint32_t NB = (uint32_t)tile_offsets(ctx, tcnt, tiles, toff, s, true);
         if (NB)
             hipLaunchKernelGGL(border_list_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core,
                                toff, blist);
+        uint32_t* keyrec = bucketed ? ctx.arena.get<uint32_t>("key_rec", R) : nullptr;
         if (NB)
             launch_border<T, D, M>(ctx.variant, s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par,
-                                   gmin, st.wroot, key_out);
+                                   gmin, st.wroot, key_out, keyrec);
+        if (bucketed) {
+            const int nbk = (int)((n + (1ull << kLabBits) - 1) >> kLabBits);
+            uint32_t* bcnt = ctx.arena.get<uint32_t>("lab_bcnt", (size_t)nbk);
+            uint2* pairs = ctx.arena.get<uint2>("lab_pairs", (size_t)nbk << kLabBits);
+            PD_HIP(hipMemsetAsync(bcnt, 0, sizeof(uint32_t) * nbk, s));
+            const unsigned ltiles = (unsigned)(((uint64_t)R + kLabTile - 1) / kLabTile);
+            hipLaunchKernelGGL(label_bucket_kernel, dim3(ltiles), dim3(kBlock),
+                               sizeof(uint32_t) * 2 * nbk, s, R, vals, core, par, gmin, keyrec, nbk,
+                               bcnt, pairs);
+            const unsigned bpb = (1u << kLabBits) / (kBlock * 8);
+            hipLaunchKernelGGL(label_scatter_kernel, dim3((unsigned)nbk * bpb), dim3(kBlock), 0, s,
+                               pairs, bcnt, nbk, bpb, key_out);
+        }
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 9 (phase 2: 1)

@@ -936,3 +936,28 @@ def test_train_many_partitions_fallbacks(native, P):
     assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)
     assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_o)
     assert m.n_clusters_ == nc_o and len(m.bounding_boxes) == P
+
+
+@pytest.mark.parametrize("cfg,n", [("C2", 2_000_000), ("C4", 3_000_000), ("C1", 500_000)])
+def test_label_buckets_equal_direct_scatter(native, cfg, n):
+    """PD_OPT_LABEL_BUCKETS (default on): the labels reach input order through
+    the bucketed (point, key) pair passes instead of one scattered write per
+    owner record — identical labels and core flags, several buckets of 2^17
+    points, partial last bucket, noise and border points included."""
+    from pypardis_amd import DBSCAN, synth
+    X, c = synth.make_config(cfg, n=n, device="cuda" if cfg == "C4" else "cpu")
+    Xd = X if torch.is_tensor(X) else _dev(X)
+    ctx = native.context()
+    outs = []
+    for on in (1, 0):
+        ctx.set_option(native.PD_OPT_LABEL_BUCKETS, on)
+        try:
+            m = DBSCAN(eps=c["eps"], min_samples=c["min_samples"],
+                       max_partitions=c.get("max_partitions") or 1).train(Xd)
+        finally:
+            ctx.set_option(native.PD_OPT_LABEL_BUCKETS, 1)
+        outs.append((m.labels_.clone(), m.core_sample_mask_.clone(), m.n_clusters_))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
+    lab = outs[0][0]
+    assert bool((lab == -1).any()) and bool((lab >= 0).any())

@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--count-rotate", type=int, default=None,
                     help="PD_OPT_COUNT_ROTATE override (0 = count sweeps always start at the row)")
     ap.add_argument("--jump-rounds", type=int, default=None, help="PD_OPT_JUMP_ROUNDS override")
+    ap.add_argument("--label-buckets", type=int, default=None,
+                    help="PD_OPT_LABEL_BUCKETS override (0: one scattered label write per record)")
     ap.add_argument("--centre-window", type=int, default=None,
                     help="PD_OPT_CENTRE_WINDOW override (link window length)")
     ap.add_argument("--rehearse", action="store_true",
@@ -381,7 +383,8 @@ def main():
                      (_native.PD_OPT_COUNT_ROTATE, args.count_rotate),
                      (_native.PD_OPT_LINK_MODE, args.link_mode),
                      (_native.PD_OPT_JUMP_ROUNDS, args.jump_rounds),
-                     (_native.PD_OPT_DIR_BUDGET, args.dir_budget)):
+                     (_native.PD_OPT_DIR_BUDGET, args.dir_budget),
+                     (_native.PD_OPT_LABEL_BUCKETS, args.label_buckets)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None
@@ -455,7 +458,8 @@ def main():
     if rank == 0:
         t_cnt = float(np.mean(count_ms))
         stages = {k: round(v / args.steps, 3) for k, v in stage_sum.items()
-                  if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records")
+                  if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records",
+                               "count_deferred")
                   and not k.startswith("s_")}
         if not stages.get("count_kernel"):
             stages.pop("count_kernel", None)   # dense path only

@@ -127,6 +127,8 @@ enum pd_timing_slot {
                                   directory budget made the cells grow) */
     PD_T_COUNT_KERNEL,         /* dense path: ms of the count pass's tile kernel alone
                                   (PD_T_COUNT includes its projection sorts) */
+    PD_T_COUNT_DEFERRED,       /* grid path, split count (PD_OPT_SWEEP_VARIANT bit 5): records
+                                  swept beyond the centre batch */
     PD_T_NSLOTS
 };
 

@@ -1245,11 +1245,15 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
                                                        uint32_t* __restrict__ key_out,
                                                        uint8_t* __restrict__ core_out,
                                                        uint32_t* __restrict__ cnt_out,
-                                                       uint32_t* __restrict__ tile_cnt) {
+                                                       uint32_t* __restrict__ tile_cnt,
+                                                       uint2* __restrict__ recs) {
     const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t v = r < R ? vals[r] : 0u;
     const bool own = r < R && (v & kOwnerBit);
     const uint8_t fl = own ? core[r] : 0;
+    if (recs && r < R)   // bucketed labels: the pair in record order, coalesced
+        recs[r] = make_uint2(own ? v & kIdMask : kNone,
+                             (fl & 1) ? gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u) : kNone);
     if (own) {
         const uint32_t pt = v & kIdMask;
         if (core_out && !core_bit) core_out[pt] = fl & 1;
@@ -1668,7 +1672,12 @@ __device__ __forceinline__ void row_range3(const Cells& C, const Count3Grid<T, D
     e = e > s ? e : s;
 }
 
-template <typename T, int D, int M, bool ST>
+// PH 0: every batch.  PH 1 (split, d >= 3): the centre batch only; a record
+// that has not reached min_samples saves its state (count, two smallest
+// neighbours) and is listed; PH 2 runs the other batches for the listed
+// records only, so the waves that sweep the outer rows are full of records
+// that need them instead of waiting on one lane in sixteen.
+template <typename T, int D, int M, bool ST, int PH>
 __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs, uint32_t R,
                                                         Cells C, double eps, double eps2,
                                                         float lo, float hi, uint32_t ms, int full,
@@ -1676,11 +1685,19 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
                                                         uint8_t* __restrict__ core,
                                                         uint32_t* __restrict__ mn_out,
                                                         uint32_t* __restrict__ cnt_out,
-                                                        unsigned long long* __restrict__ stats) {
+                                                        unsigned long long* __restrict__ stats,
+                                                        uint32_t* __restrict__ list,
+                                                        uint32_t* __restrict__ list_count,
+                                                        uint32_t* __restrict__ cstate) {
     constexpr int NR = NRows<D>::v;
     constexpr int B = NR < 3 ? NR : 3, NB = NR / B;
-    const uint32_t r = rec_index();
-    if (r >= R) return;
+    constexpr int BT0 = PH == 2 ? 1 : 0, BT1 = PH == 1 ? 1 : NB;
+    const uint32_t i = rec_index();
+    const bool live = PH == 2 ? i < *list_count : i < R;
+    bool defer = false;
+    uint32_t r = i;
+    if (live) {
+    if constexpr (PH == 2) r = list[i];
     double a[D];
     load_rec<T, D>(Xs, r, a);
     const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
@@ -1688,11 +1705,18 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
     float e2 = M == 0 ? (float)eps2 : (float)eps;
     e2 = e2 * (1.0f + 1.0f / 65536.0f);
     uint32_t cnt = 0, mn = kNone, mn2 = kNone, n_cand = 0;
+    if constexpr (PH == 2) {
+        cnt = cstate[r];
+        const uint2 m = reinterpret_cast<const uint2*>(mn_out)[r];
+        mn = m.x;
+        mn2 = m.y;
+    }
+    bool done = false;
     with_part(C.part_start, C.P, r, [&](int L, auto U) {
         Count3Grid<T, D, M, decltype(U)::value> g;
         g.load(C.parts + L);
         const RowGeo<D> geo = row_geo<T, D, M, decltype(U)::value>(g, a);
-        for (int bt = 0; bt < NB; ++bt) {   // batch 0: the centre batch, centre row first
+        for (int bt = BT0; bt < BT1; ++bt) {   // batch 0: the centre batch, centre row first
             uint32_t s0, e0, s1 = 0, e1 = 0, s2 = 0, e2r = 0;
             row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B, s0, e0);
             if constexpr (B > 1) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 1, s1, e1);
@@ -1740,13 +1764,23 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
                 return false;
             };
             const bool stopped = __any(v0 != 0) ? sweep(std::true_type{}) : sweep(std::false_type{});
-            if (stopped) return;
+            if (stopped) {
+                done = true;
+                return;
+            }
         }
     });
-    core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
     reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, mn2);
-    if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
+    if (PH == 1 && NB > 1 && !done) {
+        defer = true;
+        cstate[r] = cnt;
+    } else {
+        core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
+        if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
+    }
     if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
+    }
+    if constexpr (PH == 1) wave_append(list, list_count, defer, r);   // every lane of the wave
 }
 
 // ------------------------------------------------------------------ link mode 3
@@ -2674,9 +2708,9 @@ __global__ __launch_bounds__(kBlock) void border4_kernel(
             }
         }
     });
-    // rec_out: by record (the bucketed label pass moves it to the point)
+    // rec_out: by record, into the pairs of the bucketed label pass
     if (rec_out)
-        rec_out[r] = best;
+        rec_out[2 * (size_t)r] = best;   // the key half of the record's (point, key) pair
     else
         key_out[vals[r] & kIdMask] = best;
 }
@@ -2691,53 +2725,34 @@ __global__ __launch_bounds__(kBlock) void border4_kernel(
 // keys into its 512 KB of key_out from blocks of one XCD, so the random
 // writes combine in that XCD's L2.
 constexpr int kLabBits = 17;
-constexpr uint32_t kLabTile = 65536;
 
-__device__ __forceinline__ bool label_pair(uint32_t r, const uint32_t* __restrict__ vals,
-                                           const uint8_t* __restrict__ core,
-                                           const uint32_t* __restrict__ par,
-                                           const uint32_t* __restrict__ gmin,
-                                           const uint32_t* __restrict__ keyrec, uint32_t& pt,
-                                           uint32_t& key) {
-    const uint32_t v = vals[r];
-    if (!(v & kOwnerBit)) return false;
-    pt = v & kIdMask;
-    const uint8_t fl = core[r];
-    if (fl & 1) {
-        key = gmin[par[r]] | kKeyCoreBit;
-        return true;
-    }
-    if ((fl & 3) != 2) return false;   // noise: key_out keeps kNone
-    key = keyrec[r];
-    return key != kNone;
-}
-
-__global__ __launch_bounds__(kBlock) void label_bucket_kernel(
-    uint32_t R, const uint32_t* __restrict__ vals, const uint8_t* __restrict__ core,
-    const uint32_t* __restrict__ par, const uint32_t* __restrict__ gmin,
-    const uint32_t* __restrict__ keyrec, int nbk, uint32_t* __restrict__ bcnt,
-    uint2* __restrict__ pairs) {
+// (point, key) pairs in record order: pairs[r] = (owner record ? its point :
+// kNone, core: the cluster key | kKeyCoreBit; else kNone — the border sweep
+// fills in its key afterwards).  Written by owner_kernel in bucketed mode.
+__global__ __launch_bounds__(kBlock) void label_bucket_kernel(uint32_t R,
+                                                              const uint2* __restrict__ recs,
+                                                              uint32_t tile, int nbk,
+                                                              uint32_t* __restrict__ bcnt,
+                                                              uint2* __restrict__ pairs) {
     extern __shared__ uint32_t lab_sh[];
     uint32_t* cnt = lab_sh;          // per bucket: pairs of this tile
     uint32_t* run = lab_sh + nbk;    // then: the next free slot
     for (int k = threadIdx.x; k < nbk; k += kBlock) cnt[k] = 0;
     __syncthreads();
-    const uint64_t t0 = (uint64_t)blockIdx.x * kLabTile;
-    const uint64_t t1 = t0 + kLabTile < R ? t0 + kLabTile : R;
+    const uint64_t t0 = (uint64_t)blockIdx.x * tile;
+    const uint64_t t1 = t0 + tile < R ? t0 + tile : R;
     for (uint64_t r = t0 + threadIdx.x; r < t1; r += kBlock) {
-        uint32_t pt, key;
-        if (label_pair((uint32_t)r, vals, core, par, gmin, keyrec, pt, key))
-            atomicAdd(&cnt[pt >> kLabBits], 1u);
+        const uint2 q = recs[r];
+        if (q.x != kNone && q.y != kNone) atomicAdd(&cnt[q.x >> kLabBits], 1u);
     }
     __syncthreads();
     for (int k = threadIdx.x; k < nbk; k += kBlock) run[k] = cnt[k] ? atomicAdd(bcnt + k, cnt[k]) : 0u;
     __syncthreads();
     for (uint64_t r = t0 + threadIdx.x; r < t1; r += kBlock) {
-        uint32_t pt, key;
-        if (label_pair((uint32_t)r, vals, core, par, gmin, keyrec, pt, key)) {
-            const uint32_t b = pt >> kLabBits;
-            const uint32_t pos = atomicAdd(&run[b], 1u);
-            pairs[((uint64_t)b << kLabBits) + pos] = make_uint2(pt, key);
+        const uint2 q = recs[r];
+        if (q.x != kNone && q.y != kNone) {
+            const uint32_t b = q.x >> kLabBits;
+            pairs[((uint64_t)b << kLabBits) + atomicAdd(&run[b], 1u)] = q;
         }
     }
 }
@@ -2853,13 +2868,37 @@ void cell_roots(Ctx& ctx, hipStream_t s, uint32_t R, const uint32_t* cstart, con
 // Launch helpers for the three neighbour sweeps: bit k of `variant`
 // (PD_OPT_SWEEP_VARIANT) selects the batched lane kernel for sweep k (0
 // count, 1 link, 2 border) instead of the row-by-row one.
+// count4's centre-batch split (PD_OPT_SWEEP_VARIANT bit 5): deferred-record
+// list, its count and the saved counts.
+struct CountSplit {
+    Ctx* ctx;
+    uint32_t* list;
+    uint32_t* count;
+    uint32_t* state;
+    uint32_t deferred;
+};
+
 template <typename T, int D, int M, bool ST>
 void launch_count(int variant, hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double eps,
                   double eps2, float lo, float hi, uint32_t ms, int full, uint32_t rot_min,
-                  uint8_t* core, uint32_t* mn, uint32_t* cnt, unsigned long long* st) {
-    if (variant & 8)   // cheap rows
-        hipLaunchKernelGGL((count4_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
-                           C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
+                  uint8_t* core, uint32_t* mn, uint32_t* cnt, unsigned long long* st,
+                  CountSplit* split = nullptr) {
+    if ((variant & 40) == 40 && NRows<D>::v > 3 && split) {   // cheap rows, centre batch split
+        hipLaunchKernelGGL((count4_kernel<T, D, M, ST, 1>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs,
+                           R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st,
+                           split->list, split->count, split->state);
+        uint32_t* h = (uint32_t*)pinned(*split->ctx, sizeof(uint32_t));
+        PD_HIP(hipMemcpyAsync(h, split->count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        sync(s);
+        split->deferred = *h;
+        if (*h)
+            hipLaunchKernelGGL((count4_kernel<T, D, M, ST, 2>), dim3(blocks(*h)), dim3(kBlock), 0, s,
+                               Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st,
+                               split->list, split->count, split->state);
+    } else if (variant & 8)   // cheap rows
+        hipLaunchKernelGGL((count4_kernel<T, D, M, ST, 0>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs,
+                           R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st, nullptr,
+                           nullptr, nullptr);
     else if (variant & 1)
         hipLaunchKernelGGL((count2_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
                            C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
@@ -3080,18 +3119,24 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     }
     const int mode = ctx.link_mode;
     if (R) {
+        CountSplit split{&ctx, nullptr, nullptr, nullptr, 0};
+        if ((ctx.variant & 40) == 40 && NRows<D>::v > 3) {
+            split.list = ctx.arena.get<uint32_t>("count_defer", R);
+            split.count = ctx.arena.get<uint32_t>("count_defer_n", 4);
+            split.state = ctx.arena.get<uint32_t>("count_state", R);
+            PD_HIP(hipMemsetAsync(split.count, 0, sizeof(uint32_t), s));
+        }
         if (sst)
             launch_count<T, D, M, true>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
                                         (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
                                         ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu,
-                                        core,
-                                        mn, cnt_rec, sst);
+                                        core, mn, cnt_rec, sst, &split);
         else
             launch_count<T, D, M, false>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
                                          (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
-                                        ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu,
-                                        core,
-                                         mn, cnt_rec, sst);
+                                         ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu,
+                                         core, mn, cnt_rec, sst, &split);
+        ctx.t.count_deferred = split.deferred;
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 5
@@ -3356,27 +3401,32 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         const unsigned tiles = blocks(R);
         uint32_t* tcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)tiles + 1);
         uint64_t* toff = ctx.arena.get<uint64_t>("tile_off", (size_t)tiles + 1);
-        // bucketed: owner_kernel only tallies the border candidates (no key_out)
+        // bucketed: owner_kernel writes the (point, key) pairs in record order
+        // instead of scattering key_out; the border sweep fills in its keys
+        uint2* recs = bucketed ? ctx.arena.get<uint2>("lab_recs", R) : nullptr;
         hipLaunchKernelGGL(owner_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core, par, gmin,
                            st.cnt_rec, core_bit, bucketed ? nullptr : key_out, a.core, a.counts,
-                           tcnt);
+                           tcnt, recs);
         const uint32_t NB = (uint32_t)tile_offsets(ctx, tcnt, tiles, toff, s, true);
         if (NB)
             hipLaunchKernelGGL(border_list_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core,
                                toff, blist);
-        uint32_t* keyrec = bucketed ? ctx.arena.get<uint32_t>("key_rec", R) : nullptr;
         if (NB)
             launch_border<T, D, M>(ctx.variant, s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par,
-                                   gmin, st.wroot, key_out, keyrec);
+                                   gmin, st.wroot, key_out, recs ? (uint32_t*)recs + 1 : nullptr);
         if (bucketed) {
             const int nbk = (int)((n + (1ull << kLabBits) - 1) >> kLabBits);
             uint32_t* bcnt = ctx.arena.get<uint32_t>("lab_bcnt", (size_t)nbk);
             uint2* pairs = ctx.arena.get<uint2>("lab_pairs", (size_t)nbk << kLabBits);
             PD_HIP(hipMemsetAsync(bcnt, 0, sizeof(uint32_t) * nbk, s));
-            const unsigned ltiles = (unsigned)(((uint64_t)R + kLabTile - 1) / kLabTile);
+            // ~16 pairs per bucket and tile (128-B runs), >= 4096 records a tile
+            uint64_t tile = std::max<uint64_t>(4096, 16ull * (uint64_t)nbk);
+            tile = std::min<uint64_t>(tile, 1ull << 20);
+            tile = (tile + 1023) & ~1023ull;
+            const unsigned ltiles = (unsigned)(((uint64_t)R + tile - 1) / tile);
             hipLaunchKernelGGL(label_bucket_kernel, dim3(ltiles), dim3(kBlock),
-                               sizeof(uint32_t) * 2 * nbk, s, R, vals, core, par, gmin, keyrec, nbk,
-                               bcnt, pairs);
+                               sizeof(uint32_t) * 2 * nbk, s, R, recs, (uint32_t)tile, nbk, bcnt,
+                               pairs);
             const unsigned bpb = (1u << kLabBits) / (kBlock * 8);
             hipLaunchKernelGGL(label_scatter_kernel, dim3((unsigned)nbk * bpb), dim3(kBlock), 0, s,
                                pairs, bcnt, nbk, bpb, key_out);

@@ -52,6 +52,7 @@ struct Timings {
     int64_t sweep[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     double grid_grow = 1.0;      // cell width / eps (PD_OPT_DIR_BUDGET)
     float count_kernel = 0;      // dense path: the count pass's tile kernel alone (ms)
+    int64_t count_deferred = 0;  // count4 split: records swept beyond the centre batch
 };
 
 // Device state carried from phase A (local clustering) to phase B (border

@@ -458,8 +458,7 @@ def main():
     if rank == 0:
         t_cnt = float(np.mean(count_ms))
         stages = {k: round(v / args.steps, 3) for k, v in stage_sum.items()
-                  if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records",
-                               "count_deferred")
+                  if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records")
                   and not k.startswith("s_")}
         if not stages.get("count_kernel"):
             stages.pop("count_kernel", None)   # dense path only

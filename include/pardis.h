@@ -112,7 +112,9 @@ enum pd_option {
     PD_OPT_LABEL_BUCKETS = 15 /* single device: the labels reach input order through two
                                 coalesced passes (pairs bucketed by point id, then scattered
                                 inside L2-sized buckets) instead of one scattered write per
-                                record (default 1; same labels with 0) */
+                                record: 1 on, 0 off, -1 (default) from 2^28 points on, where
+                                it is faster (C4 1e9: border 42 -> 38 ms; C2 1e8: slower).
+                                Same labels either way */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */
@@ -127,8 +129,6 @@ enum pd_timing_slot {
                                   directory budget made the cells grow) */
     PD_T_COUNT_KERNEL,         /* dense path: ms of the count pass's tile kernel alone
                                   (PD_T_COUNT includes its projection sorts) */
-    PD_T_COUNT_DEFERRED,       /* grid path, split count (PD_OPT_SWEEP_VARIANT bit 5): records
-                                  swept beyond the centre batch */
     PD_T_NSLOTS
 };
 

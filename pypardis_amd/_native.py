@@ -35,7 +35,7 @@ TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "ro
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
                 "s_count_cand", "s_link_cand", "s_link_hit", "s_link_core", "s_link_same",
                 "s_link_find_same", "s_link_unions", "s_verify_pairs", "grid_grow",
-                "count_kernel", "count_deferred"]
+                "count_kernel"]
 
 # every symbol include/pardis.h declares (tests/test_abi.py checks the .so)
 EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",

@@ -150,7 +150,7 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         } else if (option == PD_OPT_BORDER_ROOTS)
             ctx->c.border_roots = value != 0;
         else if (option == PD_OPT_SWEEP_VARIANT) {
-            if (value < 0 || value > 63) throw Error(PD_EINVAL, "sweep variant is a 6-bit mask");
+            if (value < 0 || value > 31) throw Error(PD_EINVAL, "sweep variant is a 5-bit mask");
             ctx->c.variant = (int)value;
         } else if (option == PD_OPT_COUNT_ROTATE) {
             if (value < 0 || value > 0x7FFFFFFF) throw Error(PD_EINVAL, "count rotate must be >= 0");
@@ -165,7 +165,7 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             if (value < 1 || value > 16) throw Error(PD_EINVAL, "xsub must be in [1, 16]");
             ctx->c.xsub = (int)value;
         } else if (option == PD_OPT_LABEL_BUCKETS) {
-            ctx->c.label_buckets = value != 0;
+            ctx->c.label_buckets = value < 0 ? -1 : (value ? 1 : 0);
         }
         else
             throw Error(PD_EINVAL, "unknown option");
@@ -185,7 +185,7 @@ int32_t pd_ctx_timings(pd_ctx* ctx, double* out, int32_t n) {
                                        (double)t.sweep[2], (double)t.sweep[3],
                                        (double)t.sweep[4], (double)t.sweep[5],
                                        (double)t.sweep[6], (double)t.sweep[7], t.grid_grow,
-                                       (double)t.count_kernel, (double)t.count_deferred};
+                                       (double)t.count_kernel};
         for (int i = 0; i < n && i < PD_T_NSLOTS; ++i) out[i] = v[i];
     });
 }

@@ -1672,12 +1672,7 @@ __device__ __forceinline__ void row_range3(const Cells& C, const Count3Grid<T, D
     e = e > s ? e : s;
 }
 
-// PH 0: every batch.  PH 1 (split, d >= 3): the centre batch only; a record
-// that has not reached min_samples saves its state (count, two smallest
-// neighbours) and is listed; PH 2 runs the other batches for the listed
-// records only, so the waves that sweep the outer rows are full of records
-// that need them instead of waiting on one lane in sixteen.
-template <typename T, int D, int M, bool ST, int PH>
+template <typename T, int D, int M, bool ST>
 __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs, uint32_t R,
                                                         Cells C, double eps, double eps2,
                                                         float lo, float hi, uint32_t ms, int full,
@@ -1685,19 +1680,11 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
                                                         uint8_t* __restrict__ core,
                                                         uint32_t* __restrict__ mn_out,
                                                         uint32_t* __restrict__ cnt_out,
-                                                        unsigned long long* __restrict__ stats,
-                                                        uint32_t* __restrict__ list,
-                                                        uint32_t* __restrict__ list_count,
-                                                        uint32_t* __restrict__ cstate) {
+                                                        unsigned long long* __restrict__ stats) {
     constexpr int NR = NRows<D>::v;
     constexpr int B = NR < 3 ? NR : 3, NB = NR / B;
-    constexpr int BT0 = PH == 2 ? 1 : 0, BT1 = PH == 1 ? 1 : NB;
-    const uint32_t i = rec_index();
-    const bool live = PH == 2 ? i < *list_count : i < R;
-    bool defer = false;
-    uint32_t r = i;
-    if (live) {
-    if constexpr (PH == 2) r = list[i];
+    const uint32_t r = rec_index();
+    if (r >= R) return;
     double a[D];
     load_rec<T, D>(Xs, r, a);
     const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
@@ -1705,18 +1692,11 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
     float e2 = M == 0 ? (float)eps2 : (float)eps;
     e2 = e2 * (1.0f + 1.0f / 65536.0f);
     uint32_t cnt = 0, mn = kNone, mn2 = kNone, n_cand = 0;
-    if constexpr (PH == 2) {
-        cnt = cstate[r];
-        const uint2 m = reinterpret_cast<const uint2*>(mn_out)[r];
-        mn = m.x;
-        mn2 = m.y;
-    }
-    bool done = false;
     with_part(C.part_start, C.P, r, [&](int L, auto U) {
         Count3Grid<T, D, M, decltype(U)::value> g;
         g.load(C.parts + L);
         const RowGeo<D> geo = row_geo<T, D, M, decltype(U)::value>(g, a);
-        for (int bt = BT0; bt < BT1; ++bt) {   // batch 0: the centre batch, centre row first
+        for (int bt = 0; bt < NB; ++bt) {   // batch 0: the centre batch, centre row first
             uint32_t s0, e0, s1 = 0, e1 = 0, s2 = 0, e2r = 0;
             row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B, s0, e0);
             if constexpr (B > 1) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 1, s1, e1);
@@ -1764,23 +1744,13 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
                 return false;
             };
             const bool stopped = __any(v0 != 0) ? sweep(std::true_type{}) : sweep(std::false_type{});
-            if (stopped) {
-                done = true;
-                return;
-            }
+            if (stopped) return;
         }
     });
+    core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
     reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, mn2);
-    if (PH == 1 && NB > 1 && !done) {
-        defer = true;
-        cstate[r] = cnt;
-    } else {
-        core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
-        if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
-    }
+    if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
     if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
-    }
-    if constexpr (PH == 1) wave_append(list, list_count, defer, r);   // every lane of the wave
 }
 
 // ------------------------------------------------------------------ link mode 3
@@ -2868,37 +2838,13 @@ void cell_roots(Ctx& ctx, hipStream_t s, uint32_t R, const uint32_t* cstart, con
 // Launch helpers for the three neighbour sweeps: bit k of `variant`
 // (PD_OPT_SWEEP_VARIANT) selects the batched lane kernel for sweep k (0
 // count, 1 link, 2 border) instead of the row-by-row one.
-// count4's centre-batch split (PD_OPT_SWEEP_VARIANT bit 5): deferred-record
-// list, its count and the saved counts.
-struct CountSplit {
-    Ctx* ctx;
-    uint32_t* list;
-    uint32_t* count;
-    uint32_t* state;
-    uint32_t deferred;
-};
-
 template <typename T, int D, int M, bool ST>
 void launch_count(int variant, hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double eps,
                   double eps2, float lo, float hi, uint32_t ms, int full, uint32_t rot_min,
-                  uint8_t* core, uint32_t* mn, uint32_t* cnt, unsigned long long* st,
-                  CountSplit* split = nullptr) {
-    if ((variant & 40) == 40 && NRows<D>::v > 3 && split) {   // cheap rows, centre batch split
-        hipLaunchKernelGGL((count4_kernel<T, D, M, ST, 1>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs,
-                           R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st,
-                           split->list, split->count, split->state);
-        uint32_t* h = (uint32_t*)pinned(*split->ctx, sizeof(uint32_t));
-        PD_HIP(hipMemcpyAsync(h, split->count, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        sync(s);
-        split->deferred = *h;
-        if (*h)
-            hipLaunchKernelGGL((count4_kernel<T, D, M, ST, 2>), dim3(blocks(*h)), dim3(kBlock), 0, s,
-                               Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st,
-                               split->list, split->count, split->state);
-    } else if (variant & 8)   // cheap rows
-        hipLaunchKernelGGL((count4_kernel<T, D, M, ST, 0>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs,
-                           R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st, nullptr,
-                           nullptr, nullptr);
+                  uint8_t* core, uint32_t* mn, uint32_t* cnt, unsigned long long* st) {
+    if (variant & 8)   // cheap rows
+        hipLaunchKernelGGL((count4_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs,
+                           R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
     else if (variant & 1)
         hipLaunchKernelGGL((count2_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
                            C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
@@ -3119,24 +3065,16 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     }
     const int mode = ctx.link_mode;
     if (R) {
-        CountSplit split{&ctx, nullptr, nullptr, nullptr, 0};
-        if ((ctx.variant & 40) == 40 && NRows<D>::v > 3) {
-            split.list = ctx.arena.get<uint32_t>("count_defer", R);
-            split.count = ctx.arena.get<uint32_t>("count_defer_n", 4);
-            split.state = ctx.arena.get<uint32_t>("count_state", R);
-            PD_HIP(hipMemsetAsync(split.count, 0, sizeof(uint32_t), s));
-        }
         if (sst)
             launch_count<T, D, M, true>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
                                         (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
                                         ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu,
-                                        core, mn, cnt_rec, sst, &split);
+                                        core, mn, cnt_rec, sst);
         else
             launch_count<T, D, M, false>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
                                          (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
                                          ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu,
-                                         core, mn, cnt_rec, sst, &split);
-        ctx.t.count_deferred = split.deferred;
+                                         core, mn, cnt_rec, sst);
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 5
@@ -3394,7 +3332,8 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     // single device, no counts wanted, the cheap-row border: labels reach
     // input order through the bucketed pair passes instead of owner_kernel's
     // scatter (ctx.label_buckets, PD_OPT_LABEL_BUCKETS)
-    const bool bucketed = a.phase != 2 && core_bit && !a.counts && ctx.label_buckets &&
+    const bool want_buckets = ctx.label_buckets > 0 || (ctx.label_buckets < 0 && n >= (1ull << 28));
+    const bool bucketed = a.phase != 2 && core_bit && !a.counts && want_buckets &&
                           (ctx.variant & 16) && !st.wroot && n > 0;
     if (R) {
         uint32_t* blist = ctx.arena.get<uint32_t>("border_list", R);

@@ -52,7 +52,6 @@ struct Timings {
     int64_t sweep[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     double grid_grow = 1.0;      // cell width / eps (PD_OPT_DIR_BUDGET)
     float count_kernel = 0;      // dense path: the count pass's tile kernel alone (ms)
-    int64_t count_deferred = 0;  // count4 split: records swept beyond the centre batch
 };
 
 // Device state carried from phase A (local clustering) to phase B (border
@@ -161,7 +160,8 @@ struct Ctx {
     bool border_roots = false;   // border sweep's single-root fast path (tuning)
     int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow
     int dense_prune = 1;         // dense count pass: projection-window tiles only (2: per-band runs)
-    bool label_buckets = true;   // labels to input order by bucketed pair passes (PD_OPT_LABEL_BUCKETS)
+    int label_buckets = -1;      // labels to input order by bucketed pair passes (PD_OPT_LABEL_BUCKETS;
+                                 // -1: from 2^28 points on, where they beat the direct scatter)
     int variant = 29;            // PD_OPT_SWEEP_VARIANT: cheap-row count (bit 3; bit 0 the batched
                                  // count2), cheap-row border (bit 4; bit 2 the batched border2),
                                  // row-wise link

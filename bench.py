@@ -83,6 +83,8 @@ def parse():
     ap.add_argument("--count-rotate", type=int, default=None,
                     help="PD_OPT_COUNT_ROTATE override (0 = count sweeps always start at the row)")
     ap.add_argument("--jump-rounds", type=int, default=None, help="PD_OPT_JUMP_ROUNDS override")
+    ap.add_argument("--sort-payload", type=int, default=None,
+                    help="PD_OPT_SORT_PAYLOAD override (1: coordinates ride the sort)")
     ap.add_argument("--label-buckets", type=int, default=None,
                     help="PD_OPT_LABEL_BUCKETS override (0: one scattered label write per record)")
     ap.add_argument("--centre-window", type=int, default=None,
@@ -384,7 +386,8 @@ def main():
                      (_native.PD_OPT_LINK_MODE, args.link_mode),
                      (_native.PD_OPT_JUMP_ROUNDS, args.jump_rounds),
                      (_native.PD_OPT_DIR_BUDGET, args.dir_budget),
-                     (_native.PD_OPT_LABEL_BUCKETS, args.label_buckets)):
+                     (_native.PD_OPT_LABEL_BUCKETS, args.label_buckets),
+                     (_native.PD_OPT_SORT_PAYLOAD, args.sort_payload)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None

@@ -114,7 +114,10 @@ enum pd_option {
                                 inside L2-sized buckets) instead of one scattered write per
                                 record: 1 on, 0 off, -1 (default) from 2^28 points on, where
                                 it is faster (C4 1e9: border 42 -> 38 ms; C2 1e8: slower).
-                                Same labels either way */
+                                Same labels either way */,
+    PD_OPT_SORT_PAYLOAD = 16  /* fp32 3-D: the halo records carry their coordinates through the
+                                radix sort (16-B values) instead of a gather after it
+                                (default 0 — see DESIGN.md §6 for the measured A/B) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -29,6 +29,7 @@ PD_OPT_COUNT_ROTATE = 12
 PD_OPT_CENTRE_WINDOW = 13
 PD_OPT_DIR_BUDGET = 14
 PD_OPT_LABEL_BUCKETS = 15
+PD_OPT_SORT_PAYLOAD = 16
 SWEEP_VARIANT_DEFAULT = 29
 LINK_MODE_DEFAULT = 6
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",

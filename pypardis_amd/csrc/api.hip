@@ -164,6 +164,8 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         } else if (option == PD_OPT_XSUB) {
             if (value < 1 || value > 16) throw Error(PD_EINVAL, "xsub must be in [1, 16]");
             ctx->c.xsub = (int)value;
+        } else if (option == PD_OPT_SORT_PAYLOAD) {
+            ctx->c.sort_payload = value != 0;
         } else if (option == PD_OPT_LABEL_BUCKETS) {
             ctx->c.label_buckets = value < 0 ? -1 : (value ? 1 : 0);
         }

@@ -658,7 +658,7 @@ template <typename T, int D, typename K, bool MASK>
 __global__ __launch_bounds__(kBlock) void halo_write_kernel(
     const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
     const int32_t* __restrict__ owner, KdTree tree, const uint64_t* __restrict__ tile_off,
-    K* __restrict__ keys, uint32_t* __restrict__ vals) {
+    K* __restrict__ keys, uint32_t* __restrict__ vals, float4* __restrict__ pay) {
     uint64_t idx[4];
     T v[4][D];
     unsigned long long m[4];
@@ -720,7 +720,15 @@ __global__ __launch_bounds__(kBlock) void halo_write_kernel(
                 mm &= mm - 1;
                 const K key = key_of<T, D, K>(v[q], kg[L]);
                 keys[o] = key;
-                vals[o] = tag | (own == L ? kOwnerBit : 0u);
+                const uint32_t vb = tag | (own == L ? kOwnerBit : 0u);
+                if constexpr (std::is_same<T, float>::value && D == 3) {
+                    if (pay) {   // the sort carries the coordinates (PD_OPT_SORT_PAYLOAD)
+                        pay[o] = make_float4(v[q][0], v[q][1], v[q][2], __uint_as_float(vb));
+                        ++o;
+                        continue;
+                    }
+                }
+                vals[o] = vb;
                 ++o;
             } while (mm);
         } else {
@@ -730,7 +738,15 @@ __global__ __launch_bounds__(kBlock) void halo_write_kernel(
                 K key;
                 halo_record<T, D, K>(v[q], g, key);
                 keys[o] = key;
-                vals[o] = tag | (own == L ? kOwnerBit : 0u);
+                const uint32_t vb = tag | (own == L ? kOwnerBit : 0u);
+                if constexpr (std::is_same<T, float>::value && D == 3) {
+                    if (pay) {
+                        pay[o] = make_float4(v[q][0], v[q][1], v[q][2], __uint_as_float(vb));
+                        ++o;
+                        continue;
+                    }
+                }
+                vals[o] = vb;
                 ++o;
             }
         }
@@ -753,6 +769,20 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const T* __restrict__ X,
 #pragma unroll
         for (int j = 0; j < S; ++j) Xs[r * S + j] = j < D ? X[i * D + j] : T(0);
     }
+    wave_append(dup_list, dup_count, r < R && (v & kDupBit), (uint32_t)r);
+}
+
+// PD_OPT_SORT_PAYLOAD: the sorted (x, y, z, vals) payload is Xs as it is
+// (3-D records padded to 4, the 4th word unread as a coordinate); vals and
+// the duplicate list come out of its 4th word.
+__global__ __launch_bounds__(kBlock) void payload_vals_kernel(const float4* __restrict__ pay,
+                                                              uint64_t R,
+                                                              uint32_t* __restrict__ vals,
+                                                              uint32_t* __restrict__ dup_list,
+                                                              uint32_t* __restrict__ dup_count) {
+    const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t v = r < R ? __float_as_uint(pay[r].w) : 0u;
+    if (r < R) vals[r] = v;
     wave_append(dup_list, dup_count, r < R && (v & kDupBit), (uint32_t)r);
 }
 
@@ -2980,17 +3010,31 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         tree.ax_new = (const int32_t*)dt + nslot;
         tree.bound = (const double*)(dt + db);
     }
+    // PD_OPT_SORT_PAYLOAD (fp32, 3-D): the records carry their coordinates
+    // through the sort (16-B values) instead of a gather after it
+    const bool payload = ctx.sort_payload && std::is_same<T, float>::value && D == 3;
+    float4* pay = payload ? ctx.arena.get<float4>("pay", R) : nullptr;
     if (P <= 64)
         hipLaunchKernelGGL((halo_write_kernel<T, D, K, true>), dim3(htiles), dim3(kBlock), 0, s, X,
-                           n, parts, P, a.owner, tree, toff, keys, vals);
+                           n, parts, P, a.owner, tree, toff, keys, vals, pay);
     else
         hipLaunchKernelGGL((halo_write_kernel<T, D, K, false>), dim3(htiles), dim3(kBlock), 0, s,
-                           X, n, parts, P, a.owner, tree, toff, keys, vals);
+                           X, n, parts, P, a.owner, tree, toff, keys, vals, pay);
     PD_HIP(hipGetLastError());
     tm.mark();   // 1
 
     // ---- shuffle by neighbourhood == sort by (neighbourhood, cell) key
-    {
+    if (payload) {
+        float4* pay2 = ctx.arena.get<float4>("pay2", R);
+        rocprim::double_buffer<K> kb(keys, keys2);
+        rocprim::double_buffer<float4> vb(pay, pay2);
+        size_t tb = 0;
+        PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
+        void* tmp = ctx.arena.get<char>("sort_tmp", tb);
+        PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
+        keys = kb.current();
+        pay = vb.current();
+    } else {
         rocprim::double_buffer<K> kb(keys, keys2);
         rocprim::double_buffer<uint32_t> vb(vals, vals2);
         size_t tb = 0;
@@ -3001,12 +3045,16 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         vals = vb.current();
     }
     tm.mark();   // 2
-    T* Xs = ctx.arena.get<T>("Xs", (size_t)R * Stride<D>::v);
+    T* Xs = payload ? reinterpret_cast<T*>(pay) : ctx.arena.get<T>("Xs", (size_t)R * Stride<D>::v);
     uint32_t* dup_list = ctx.arena.get<uint32_t>("dup_list", R);
     uint32_t* lcount = ctx.arena.get<uint32_t>("list_counts", 8);   // dup, roots, core, border
     PD_HIP(hipMemsetAsync(lcount, 0, sizeof(uint32_t) * 8, s));
-    hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X, (uint64_t)R,
-                       vals, Xs, dup_list, lcount);
+    if (payload)
+        hipLaunchKernelGGL(payload_vals_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, pay, (uint64_t)R,
+                           vals, dup_list, lcount);
+    else
+        hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X,
+                           (uint64_t)R, vals, Xs, dup_list, lcount);
     tm.mark();   // 3
 
     // ---- cell directory

@@ -160,6 +160,7 @@ struct Ctx {
     bool border_roots = false;   // border sweep's single-root fast path (tuning)
     int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow
     int dense_prune = 1;         // dense count pass: projection-window tiles only (2: per-band runs)
+    bool sort_payload = false;   // fp32 3-D: coordinates ride the sort (PD_OPT_SORT_PAYLOAD)
     int label_buckets = -1;      // labels to input order by bucketed pair passes (PD_OPT_LABEL_BUCKETS;
                                  // -1: from 2^28 points on, where they beat the direct scatter)
     int variant = 29;            // PD_OPT_SWEEP_VARIANT: cheap-row count (bit 3; bit 0 the batched

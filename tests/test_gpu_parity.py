@@ -961,3 +961,31 @@ def test_label_buckets_equal_direct_scatter(native, cfg, n):
     assert outs[0][2] == outs[1][2]
     lab = outs[0][0]
     assert bool((lab == -1).any()) and bool((lab >= 0).any())
+
+
+def test_sort_payload_equals_gather(native):
+    """PD_OPT_SORT_PAYLOAD (fp32 3-D): coordinates carried through the radix
+    sort instead of gathered after it — identical labels and core flags,
+    several neighbourhoods (duplicate halo records), and the exact labels of
+    the oracle on a golden."""
+    from pypardis_amd import DBSCAN, synth
+    ctx = native.context()
+    X, c = synth.make_config("C2", n=1_500_000)
+    outs = []
+    for on in (1, 0):
+        ctx.set_option(native.PD_OPT_SORT_PAYLOAD, on)
+        try:
+            m = DBSCAN(eps=c["eps"], min_samples=c["min_samples"], max_partitions=8).train(_dev(X))
+        finally:
+            ctx.set_option(native.PD_OPT_SORT_PAYLOAD, 0)
+        outs.append((m.labels_.clone(), m.core_sample_mask_.clone(), m.n_clusters_))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    g = load_golden("b3d_20k")
+    ctx.set_option(native.PD_OPT_SORT_PAYLOAD, 1)
+    try:
+        m = DBSCAN(eps=float(g["eps"]), min_samples=int(g["min_samples"]),
+                   max_partitions=4).train(_dev(g["X"].astype(np.float32)))
+    finally:
+        ctx.set_option(native.PD_OPT_SORT_PAYLOAD, 0)
+    lab_o = oracle.dbscan(g["X"].astype(np.float32), float(g["eps"]), int(g["min_samples"]))[0]
+    assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)

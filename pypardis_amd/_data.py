@@ -113,6 +113,10 @@ def as_points(data, device=None):
         recs = list(recs)
     if not recs:
         raise ValueError("no points")
+    got = _unzip_native(recs)
+    if got is not None:
+        X, k = got
+        return PointSet(_to_tensor(X, dev), _dense_or(k))
     # unzip of the (key, vector) records: itemgetter maps (an order of
     # magnitude faster than zip(*recs)), one concatenate for equal-length
     # vectors
@@ -132,7 +136,40 @@ def as_points(data, device=None):
     # a mixed list already promotes); anything else becomes float64
     if X.dtype not in (np.float32, np.float64):
         X = X.astype(np.float64)
-    k = _keys(keys)
+    return PointSet(_to_tensor(X, dev), _dense_or(_keys(keys)))
+
+
+def _dense_or(k):
+    """None for the keys 0..n-1 (the implicit key array), else k."""
     if k.dtype == np.int64 and len(k) and k[0] == 0 and np.array_equal(k, np.arange(len(k))):
-        k = None
-    return PointSet(_to_tensor(X, dev), k)
+        return None
+    return k
+
+
+def _unzip_native(recs):
+    """(X, keys) from csrc/ingest.cpp's one-pass unzip, or None when the
+    extension is not built or the records are not uniform (key, 1-D vector)
+    pairs — the numpy path below then handles (or rejects) them."""
+    try:
+        from . import _ingest
+    except ImportError:
+        return None
+    try:
+        v0 = recs[0][1]
+        if np.ndim(v0) != 1:
+            return None
+        d = len(v0)
+        if d < 1:
+            return None
+        n = len(recs)
+        K = np.empty(n, dtype=np.int64)
+        f64 = 0 if getattr(v0, "dtype", None) == np.float32 else 1
+        X = np.empty((n, d), dtype=np.float64 if f64 else np.float32)
+        st = _ingest.unzip(recs, X, K, d, f64)
+        if st == 2:   # a non-float32 vector: the set is float64
+            X = np.empty((n, d), dtype=np.float64)
+            st = _ingest.unzip(recs, X, K, d, 1)
+    except (TypeError, ValueError, IndexError):
+        return None
+    keys = K if st & 1 else _keys(list(map(itemgetter(0), recs)))
+    return X, keys

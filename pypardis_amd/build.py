@@ -54,6 +54,24 @@ def _compile(src):
     return obj, None
 
 
+INGEST_SRC = os.path.join(CSRC, "ingest.cpp")
+INGEST = os.path.join(HERE, "_ingest.so")
+
+
+def build_ingest(force=False):
+    """The host-side (key, vector) record unzip (csrc/ingest.cpp), a CPython
+    extension built with the system g++ against this interpreter's headers."""
+    if not force and _mtime(INGEST) >= _mtime(INGEST_SRC):
+        return INGEST
+    import sysconfig
+    cmd = ["g++", "-O2", "-shared", "-fPIC", "-std=c++17", "-Wall",
+           f"-I{sysconfig.get_paths()['include']}", INGEST_SRC, "-o", INGEST]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"ingest build failed:\n{r.stdout}\n{r.stderr}")
+    return INGEST
+
+
 def build(force=False, verbose=True):
     os.makedirs(OBJ, exist_ok=True)
     srcs = sources()
@@ -67,6 +85,7 @@ def build(force=False, verbose=True):
     if errs:
         raise RuntimeError("libpardis build failed:\n" + "\n".join(errs))
     objs = [o for o, _ in results]
+    build_ingest(force)
     if force or _mtime(LIB) < max(_mtime(o) for o in objs):
         # librccl.so.1 (pd_comm_*): under torch the process already holds
         # torch's RCCL (same soname), so one RCCL serves both

@@ -149,6 +149,44 @@ def test_as_points_edge_forms_cpu():
         as_points([], device="cpu")
 
 
+def test_native_ingest_matches_numpy_unzip(monkeypatch):
+    """csrc/ingest.cpp's one-pass unzip gives the same X (values and dtype)
+    and keys as the numpy path, for every record form it accepts."""
+    from pypardis_amd import _data
+    from pypardis_amd.build import build_ingest
+    build_ingest()
+    from pypardis_amd import _ingest  # noqa: F401  (must import once built)
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(50, 3)).astype(np.float32)
+    X64 = X.astype(np.float64) + 1e-9
+    forms = [
+        [(i, X[i]) for i in range(50)],
+        [(49 - i, X[i]) for i in range(50)],
+        [(i, X64[i]) for i in range(50)],
+        [(i, X[i] if i % 3 else X64[i]) for i in range(50)],
+        [(f"k{i}", list(map(float, X64[i]))) for i in range(50)],
+        [[i, X[i].astype(np.float16)] for i in range(50)],
+        [(i, np.asarray(X.T)[:, i]) for i in range(50)],          # strided rows
+        [(2 ** 65 + i, X[i]) for i in range(50)],                  # non-int64 keys
+        [(i, [1, 2, 3]) for i in range(50)],
+    ]
+    for recs in forms:
+        got = _data._unzip_native(recs)
+        assert got is not None
+        monkeypatch.setattr(_data, "_unzip_native", lambda r: None)
+        want = _data.as_points(recs, device="cpu")
+        monkeypatch.undo()
+        gx, gk = got
+        assert gx.dtype == want.X.numpy().dtype
+        assert np.array_equal(gx, want.X.numpy())
+        wk = want.key_array()
+        assert list(_data._dense_or(gk) if _data._dense_or(gk) is not None
+                    else np.arange(50)) == list(wk)
+    # ragged / scalar vectors are left to the numpy path
+    assert _data._unzip_native([(0, [1.0, 2.0]), (1, [1.0])]) is None
+    assert _data._unzip_native([(0, 1.0), (1, 2.0)]) is None
+
+
 def test_map_cluster_id():
     """R:dbscan/dbscan.py:37-53: first label of the group, '*' stripped; noise
     or unmapped labels give -1; a broadcast wrapper or a plain dict."""

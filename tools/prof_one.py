@@ -5,8 +5,11 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
-from pypardis_amd import DBSCAN, synth
+from pypardis_amd import DBSCAN, _native, synth
 
+if "PROF_SORT_PAYLOAD" in os.environ:   # A/B: coordinates ride the radix sort
+    _native.context(0).set_option(_native.PD_OPT_SORT_PAYLOAD,
+                                  int(os.environ["PROF_SORT_PAYLOAD"]))
 n = int(os.environ.get("PROF_N", "100000000"))
 name = os.environ.get("PROF_CFG", "C2")
 X, cfg = synth.make_config(name, n=n, device="cuda" if name == "C4" else "cpu")

@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--jump-rounds", type=int, default=None, help="PD_OPT_JUMP_ROUNDS override")
     ap.add_argument("--sort-payload", type=int, default=None,
                     help="PD_OPT_SORT_PAYLOAD override (1: coordinates ride the sort)")
+    ap.add_argument("--dir-paged", type=int, default=None,
+                    help="PD_OPT_DIR_PAGED override (1 paged, 0 flat, -1 auto)")
     ap.add_argument("--label-buckets", type=int, default=None,
                     help="PD_OPT_LABEL_BUCKETS override (0: one scattered label write per record)")
     ap.add_argument("--centre-window", type=int, default=None,
@@ -387,7 +389,8 @@ def main():
                      (_native.PD_OPT_JUMP_ROUNDS, args.jump_rounds),
                      (_native.PD_OPT_DIR_BUDGET, args.dir_budget),
                      (_native.PD_OPT_LABEL_BUCKETS, args.label_buckets),
-                     (_native.PD_OPT_SORT_PAYLOAD, args.sort_payload)):
+                     (_native.PD_OPT_SORT_PAYLOAD, args.sort_payload),
+                     (_native.PD_OPT_DIR_PAGED, args.dir_paged)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None
@@ -412,6 +415,7 @@ def main():
     stage_sum = {}
     count_ms = []
     rec = cells = 0
+    directory = None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -425,6 +429,8 @@ def main():
         # grid: the count stage is the count2 launch)
         count_ms.append(t["count_kernel"] if t.get("count_kernel", 0) > 0 else t["count"])
         rec, cells, gcells = int(t["records"]), int(t["cells_n"]), int(t["grid_cells"])
+        directory = {"paged": bool(t["dir_paged"]), "words": int(t["dir_words"]),
+                     "key_bits": int(t["key_bits"])}
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -461,7 +467,8 @@ def main():
     if rank == 0:
         t_cnt = float(np.mean(count_ms))
         stages = {k: round(v / args.steps, 3) for k, v in stage_sum.items()
-                  if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records")
+                  if k not in ("records", "cells_n", "grid_cells", "key_bits", "core_records",
+                               "dir_paged", "dir_words")
                   and not k.startswith("s_")}
         if not stages.get("count_kernel"):
             stages.pop("count_kernel", None)   # dense path only
@@ -508,6 +515,7 @@ def main():
             "n_clusters": ncl,
             "shard_stats": shard_stats,
             "sweep_stats": sweep,
+            "directory": directory if d <= 4 else None,
         }
         line = json.dumps(out)
         print(line, flush=True)

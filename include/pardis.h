@@ -105,9 +105,10 @@ enum pd_option {
                                 mode 6 takes 4 when cells hold <= 4 records on average, else 16
                                 (modes 3/5: 16).  A heuristic either way: the cell verify proves
                                 or tests every edge, so labels are the same */,
-    PD_OPT_DIR_BUDGET = 14    /* bytes the bbox-sized eps-grid directory may take (20 B per 64
-                                cells); beyond it every cell grows by a common factor until it
-                                fits (exact at any width >= eps; more candidates per record).
+    PD_OPT_DIR_BUDGET = 14    /* bytes the eps-grid directory may take (flat: 20 B per 64 cells;
+                                paged: 16 B per 4096 cells + 40 B per point); beyond it every cell
+                                grows by a common factor until it fits (exact at any width >= eps;
+                                more candidates per record).
                                 Default 32 GiB (PD_T_GRID_GROW reports the factor) */,
     PD_OPT_LABEL_BUCKETS = 15 /* single device: the labels reach input order through two
                                 coalesced passes (pairs bucketed by point id, then scattered
@@ -117,7 +118,13 @@ enum pd_option {
                                 Same labels either way */,
     PD_OPT_SORT_PAYLOAD = 16  /* fp32 3-D: the halo records carry their coordinates through the
                                 radix sort (16-B values) instead of a gather after it
-                                (default 0 — see DESIGN.md §6 for the measured A/B) */
+                                (default 0 — see DESIGN.md §6 for the measured A/B) */,
+    PD_OPT_DIR_PAGED = 17     /* eps-grid directory layout: 1 paged (pages of 4096 cells hold a
+                                mask of their occupied 64-cell words; only occupied words are
+                                stored: memory and build time follow the occupied cells, not the
+                                extent), 0 flat (one word per 64 cells of the bounding box), -1
+                                (default) paged when the grid has more words than points or the
+                                flat one would pass PD_OPT_DIR_BUDGET.  Same results either way */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */
@@ -132,6 +139,8 @@ enum pd_timing_slot {
                                   directory budget made the cells grow) */
     PD_T_COUNT_KERNEL,         /* dense path: ms of the count pass's tile kernel alone
                                   (PD_T_COUNT includes its projection sorts) */
+    PD_T_DIR_PAGED,            /* 1 if the last grid train used the paged directory */
+    PD_T_DIR_WORDS,            /* directory words it allocated (paged: occupied + 1) */
     PD_T_NSLOTS
 };
 

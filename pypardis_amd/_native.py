@@ -30,13 +30,14 @@ PD_OPT_CENTRE_WINDOW = 13
 PD_OPT_DIR_BUDGET = 14
 PD_OPT_LABEL_BUCKETS = 15
 PD_OPT_SORT_PAYLOAD = 16
+PD_OPT_DIR_PAGED = 17
 SWEEP_VARIANT_DEFAULT = 29
 LINK_MODE_DEFAULT = 6
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
                 "s_count_cand", "s_link_cand", "s_link_hit", "s_link_core", "s_link_same",
                 "s_link_find_same", "s_link_unions", "s_verify_pairs", "grid_grow",
-                "count_kernel"]
+                "count_kernel", "dir_paged", "dir_words"]
 
 # every symbol include/pardis.h declares (tests/test_abi.py checks the .so)
 EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",

@@ -168,6 +168,8 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.sort_payload = value != 0;
         } else if (option == PD_OPT_LABEL_BUCKETS) {
             ctx->c.label_buckets = value < 0 ? -1 : (value ? 1 : 0);
+        } else if (option == PD_OPT_DIR_PAGED) {
+            ctx->c.dir_paged = value < 0 ? -1 : (value ? 1 : 0);
         }
         else
             throw Error(PD_EINVAL, "unknown option");
@@ -187,7 +189,8 @@ int32_t pd_ctx_timings(pd_ctx* ctx, double* out, int32_t n) {
                                        (double)t.sweep[2], (double)t.sweep[3],
                                        (double)t.sweep[4], (double)t.sweep[5],
                                        (double)t.sweep[6], (double)t.sweep[7], t.grid_grow,
-                                       (double)t.count_kernel};
+                                       (double)t.count_kernel, (double)t.dir_paged,
+                                       (double)t.dir_words};
         for (int i = 0; i < n && i < PD_T_NSLOTS; ++i) out[i] = v[i];
     });
 }

@@ -367,6 +367,7 @@ struct Cells {
     int P;
     const uint4* dir;
     const uint32_t* cstart;
+    const uint4* pages;   // paged directory (null: flat, dir[k >> 6]); see dir_word
 };
 
 template <int D>
@@ -474,6 +475,53 @@ __device__ __forceinline__ uint32_t dir_rank(const uint4& w, uint64_t k) {
     return w.z + (uint32_t)__popcll(m);
 }
 
+// Paged directory (PD_OPT_DIR_PAGED; automatic when the grid has more
+// directory words than points).  Keys are grouped in pages of 64 words (4096
+// cells); pages[p] = {occupancy mask of the page's 64 words (x, y), number of
+// occupied words before the page (z)}, and only the occupied words are
+// stored, in key order, followed by a terminal word {0, 0, ncells}.  The word
+// of key k is one page load and one word load; an empty word reads as the
+// next occupied word with its bits cleared — the same prefix rank — so
+// dir_rank and every sweep are unchanged.  Memory: 16 B per page + 16 B per
+// occupied word, instead of 16 B per word of the bounding box.
+__device__ __forceinline__ uint64_t page_slot(const uint4& pg, uint64_t wid, bool& occ) {
+    const uint64_t m = ((uint64_t)pg.y << 32) | (uint64_t)pg.x;
+    const uint32_t b = (uint32_t)(wid & 63);
+    occ = (m >> b) & 1ull;
+    const uint64_t below = b ? (m & ((~0ull) >> (64 - b))) : 0ull;
+    return (uint64_t)pg.z + (uint64_t)__popcll(below);
+}
+
+// Directory word of key k (either layout).
+__device__ __forceinline__ uint4 dir_word(const Cells& C, uint64_t k) {
+    if (!C.pages) return C.dir[k >> 6];
+    bool occ;
+    const uint64_t s = page_slot(C.pages[k >> 12], k >> 6, occ);
+    uint4 w = C.dir[s];
+    if (!occ) {
+        w.x = 0u;
+        w.y = 0u;
+    }
+    return w;
+}
+
+// Word slot of an occupied cell key (flat: k >> 6).
+__device__ __forceinline__ uint64_t word_slot(const uint4* __restrict__ pages, uint64_t k) {
+    if (!pages) return k >> 6;
+    bool occ;
+    return page_slot(pages[k >> 12], k >> 6, occ);
+}
+
+// Word root (wroot: per directory word slot) of key k's word; kNone for an
+// empty word.
+__device__ __forceinline__ uint32_t word_root_at(const Cells& C, const uint32_t* __restrict__ wroot,
+                                                 uint64_t k) {
+    if (!C.pages) return wroot[k >> 6];
+    bool occ;
+    const uint64_t s = page_slot(C.pages[k >> 12], k >> 6, occ);
+    return occ ? wroot[s] : kNone;
+}
+
 template <int D, int M>
 __device__ __forceinline__ void row_ranges(const Cells& C, const double (&a)[D], int L, double eps,
                                            uint32_t (&s)[NRows<D>::v],
@@ -490,8 +538,8 @@ __device__ __forceinline__ void row_ranges(const Cells& C, const double (&a)[D],
         uint4 w0[B], w1[B];
 #pragma unroll
         for (int b = 0; b < B; ++b) {
-            w0[b] = C.dir[k0[b] >> 6];
-            w1[b] = C.dir[k1[b] >> 6];
+            w0[b] = dir_word(C, k0[b]);
+            w1[b] = dir_word(C, k1[b]);
         }
         uint32_t i0[B], i1[B];
 #pragma unroll
@@ -867,14 +915,16 @@ __global__ __launch_bounds__(kBlock) void cell_write_kernel(const K* __restrict_
 // the wave (Hillis-Steele; equal words at distance o imply equal words in
 // between) leaves each word's bits in its last lane, which adds them with
 // one atomicOr (a word can continue into the neighbouring waves).
-template <typename K>
+// SH = 6: the paged directory's page masks (one bit per occupied word of
+// the page; the units are then words, k >> 6).
+template <typename K, int SH>
 __global__ __launch_bounds__(kBlock) void dir_bits_kernel(const K* __restrict__ keys,
                                                           const uint32_t* __restrict__ cstart,
                                                           const uint32_t* __restrict__ ncells,
                                                           uint4* __restrict__ dir) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     const bool in = c < *ncells;
-    const uint64_t k = in ? (uint64_t)keys[cstart[c]] : ~0ull;
+    const uint64_t k = in ? ((uint64_t)keys[cstart[c]] >> SH) : ~0ull;
     const uint64_t word = k >> 6;
     unsigned long long v = in ? (1ull << (k & 63)) : 0ull;
     const int lane = threadIdx.x & 63;
@@ -887,6 +937,50 @@ __global__ __launch_bounds__(kBlock) void dir_bits_kernel(const K* __restrict__ 
     const uint64_t wn = (uint64_t)__shfl_down((long long)word, 1, 64);
     const bool last = lane == 63 || wn != word;
     if (in && last) atomicOr(reinterpret_cast<unsigned long long*>(dir + word), v);
+}
+
+// Paged directory, the occupied words (pages already hold their masks and
+// word prefixes): each word is written whole, by the lane of its first cell —
+// bits = a segmented suffix OR of the word's cells across the wave (a word
+// whose cells run past the wave's last lane continues with a serial walk of
+// at most 63 cells), z = that cell's index (the occupied cells before the
+// word).  The last cell also writes the terminal word {0, 0, ncells}.
+template <typename K>
+__global__ __launch_bounds__(kBlock) void word_write_kernel(const K* __restrict__ keys,
+                                                            const uint32_t* __restrict__ cstart,
+                                                            const uint32_t* __restrict__ ncells,
+                                                            const uint4* __restrict__ pages,
+                                                            uint4* __restrict__ words) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t nc = *ncells;
+    const bool in = c < nc;
+    const uint64_t k = in ? (uint64_t)keys[cstart[c]] : ~0ull;
+    const uint64_t word = k >> 6;
+    unsigned long long v = in ? (1ull << (k & 63)) : 0ull;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t wo = (uint64_t)__shfl_down((long long)word, o, 64);
+        const unsigned long long vo = (unsigned long long)__shfl_down((long long)v, o, 64);
+        if (lane + o < 64 && wo == word) v |= vo;
+    }
+    const uint64_t wp = (uint64_t)__shfl_up((long long)word, 1, 64);
+    const uint64_t w63 = (uint64_t)__shfl((long long)word, 63, 64);
+    if (!in) return;
+    bool first = c == 0;
+    if (!first) first = lane ? wp != word : ((uint64_t)keys[cstart[c - 1]] >> 6) != word;
+    bool occ;
+    const uint64_t slot = page_slot(pages[word >> 6], word, occ);
+    if (first) {
+        if (w63 == word)   // the word continues past this wave
+            for (uint32_t c2 = c - (uint32_t)lane + 64; c2 < nc; ++c2) {
+                const uint64_t k2 = (uint64_t)keys[cstart[c2]];
+                if ((k2 >> 6) != word) break;
+                v |= 1ull << (k2 & 63);
+            }
+        words[slot] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), c, 0u);
+    }
+    if (c == nc - 1) words[slot + 1] = make_uint4(0u, 0u, nc, 0u);
 }
 
 // Directory ranks dir[w].z = occupied cells in words < w: per-tile popcount
@@ -1451,8 +1545,8 @@ __device__ __forceinline__ uint32_t batch_list(const Cells& C, const QueryCell<D
     uint4 w0[B], w1[B];
 #pragma unroll
     for (int b = 0; b < B; ++b) {
-        w0[b] = C.dir[k0[b] >> 6];
-        w1[b] = C.dir[k1[b] >> 6];
+        w0[b] = dir_word(C, k0[b]);
+        w1[b] = dir_word(C, k1[b]);
     }
     uint32_t i0[B], i1[B];
 #pragma unroll
@@ -1695,7 +1789,7 @@ __device__ __forceinline__ void row_range3(const Cells& C, const Count3Grid<T, D
     const uint64_t rb = R.kc + (uint64_t)koff;
     const uint64_t k0 = ok ? rb + (uint64_t)(int64_t)dx0 : R.kc;
     const uint64_t k1 = ok ? rb + (uint64_t)(int64_t)(dx1 + 1) : R.kc;
-    const uint4 w0 = C.dir[k0 >> 6], w1 = C.dir[k1 >> 6];
+    const uint4 w0 = dir_word(C, k0), w1 = dir_word(C, k1);
     const uint32_t i0 = dir_rank(w0, k0), i1 = dir_rank(w1, k1);
     s = C.cstart[i0];
     e = C.cstart[i1];
@@ -1813,8 +1907,8 @@ __global__ __launch_bounds__(kBlock) void centre_link_kernel(const T* __restrict
     const QueryCell<D> Q = query_cell<D>(C.parts + L, a);
     uint64_t k0, k1;
     const bool ok = row_keys<D, M>(Q, a, eps, NRows<D>::v / 2, k0, k1);
-    const uint32_t s0 = C.cstart[dir_rank(C.dir[k0 >> 6], k0)];
-    const uint32_t e0 = C.cstart[dir_rank(C.dir[k1 >> 6], k1)];
+    const uint32_t s0 = C.cstart[dir_rank(dir_word(C, k0), k0)];
+    const uint32_t e0 = C.cstart[dir_rank(dir_word(C, k1), k1)];
     const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
     Linker<false> lk{par, uf_find_l1(par, r), {}};
     uint32_t j = s0 > r + 1 ? s0 : r + 1;
@@ -2149,7 +2243,7 @@ __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
     const uint32_t* __restrict__ cstart, const uint32_t* __restrict__ ncells,
     const K* __restrict__ keys, uint32_t* __restrict__ par, uint32_t* __restrict__ croot,
     uint32_t* __restrict__ wroot, uint32_t* __restrict__ mid, uint32_t* __restrict__ nmid,
-    uint32_t* __restrict__ big, uint32_t* __restrict__ nbig) {
+    uint32_t* __restrict__ big, uint32_t* __restrict__ nbig, const uint4* __restrict__ pages) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const uint32_t nc = *ncells;
@@ -2159,7 +2253,7 @@ __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
     if (c < nc) {
         s = cstart[c];
         sz = cstart[c + 1] - s;
-        word = (uint64_t)keys[s] >> 6;
+        word = word_slot(pages, (uint64_t)keys[s]);
     }
     // the larger cells' roots join their words in the mid / big kernels
     wave_append(mid, nmid, sz > kMidCell && sz <= kWordBig, c);
@@ -2182,7 +2276,8 @@ template <typename K>
 __global__ __launch_bounds__(kBlock) void mid_cell_word_root_kernel(
     const uint32_t* __restrict__ cstart, const K* __restrict__ keys,
     const uint32_t* __restrict__ mid, const uint32_t* __restrict__ nmid,
-    uint32_t* __restrict__ par, uint32_t* __restrict__ croot, uint32_t* __restrict__ wroot) {
+    uint32_t* __restrict__ par, uint32_t* __restrict__ croot, uint32_t* __restrict__ wroot,
+    const uint4* __restrict__ pages) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nm = *nmid;
     const uint32_t nw = gridDim.x * (kBlock / 64);
@@ -2195,7 +2290,7 @@ __global__ __launch_bounds__(kBlock) void mid_cell_word_root_kernel(
         for (int o = 32; o > 0; o >>= 1) v = root_merge(v, (uint32_t)__shfl_xor((int)v, o, 64));
         if (lane == 0) {
             croot[c] = v;
-            word_merge(wroot, (uint64_t)keys[s] >> 6, v);
+            word_merge(wroot, word_slot(pages, (uint64_t)keys[s]), v);
         }
     }
 }
@@ -2204,7 +2299,8 @@ template <typename K>
 __global__ __launch_bounds__(kBlock) void big_cell_word_root_kernel(
     const uint32_t* __restrict__ cstart, const K* __restrict__ keys,
     const uint32_t* __restrict__ big, const uint32_t* __restrict__ nbig,
-    uint32_t* __restrict__ par, uint32_t* __restrict__ croot, uint32_t* __restrict__ wroot) {
+    uint32_t* __restrict__ par, uint32_t* __restrict__ croot, uint32_t* __restrict__ wroot,
+    const uint4* __restrict__ pages) {
     __shared__ uint32_t part[kBlock / 64];
     const uint32_t nb = *nbig;
     for (uint32_t i = blockIdx.x; i < nb; i += gridDim.x) {
@@ -2221,7 +2317,7 @@ __global__ __launch_bounds__(kBlock) void big_cell_word_root_kernel(
 #pragma unroll
             for (int k = 0; k < kBlock / 64; ++k) w = root_merge(w, part[k]);
             croot[c] = w;
-            word_merge(wroot, (uint64_t)keys[cstart[c]] >> 6, w);
+            word_merge(wroot, word_slot(pages, (uint64_t)keys[cstart[c]]), w);
         }
         __syncthreads();
     }
@@ -2376,8 +2472,8 @@ __global__ __launch_bounds__(kBlock) void verify_screen_kernel(
         uint32_t wa[NF], wb[NF];
 #pragma unroll
         for (int f = 0; f < NF; ++f) {
-            wa[f] = wroot[fr.k0[f] >> 6];
-            wb[f] = wroot[(fr.k1[f] - 1) >> 6];
+            wa[f] = word_root_at(C, wroot, fr.k0[f]);
+            wb[f] = word_root_at(C, wroot, fr.k1[f] - 1);
         }
 #pragma unroll
         for (int f = 0; f < NF; ++f)
@@ -2445,8 +2541,8 @@ __global__ __launch_bounds__(kBlock) void cell_verify_kernel(
     uint32_t wa[NF], wb[NF];
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
-        wa[f] = wroot[fr.k0[f] >> 6];
-        wb[f] = wroot[(fr.k1[f] - 1) >> 6];
+        wa[f] = word_root_at(C, wroot, fr.k0[f]);
+        wb[f] = word_root_at(C, wroot, fr.k1[f] - 1);
     }
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
@@ -2454,8 +2550,8 @@ __global__ __launch_bounds__(kBlock) void cell_verify_kernel(
         // the row's words hold no root but ours: nothing to test
         if (rc != kMixed && (wa[f] == kNone || wa[f] == rc) && (wb[f] == kNone || wb[f] == rc))
             continue;
-        const uint32_t i0 = dir_rank(C.dir[fr.k0[f] >> 6], fr.k0[f]);
-        const uint32_t i1 = dir_rank(C.dir[fr.k1[f] >> 6], fr.k1[f]);
+        const uint32_t i0 = dir_rank(dir_word(C, fr.k0[f]), fr.k0[f]);
+        const uint32_t i1 = dir_rank(dir_word(C, fr.k1[f]), fr.k1[f]);
         for (uint32_t c2 = i0 > c + 1 ? i0 : c + 1; c2 < i1; ++c2) {
             const uint32_t r2 = croot[c2];
             if (r2 == kNone || (r2 == rc && rc != kMixed)) continue;
@@ -2582,7 +2678,7 @@ __global__ __launch_bounds__(kBlock) void border2_kernel(
             for (int q = 0; q < NR; ++q) {
                 uint64_t k0, k1;
                 if (!row_keys<D, M>(Q, a, eps, q, k0, k1)) continue;
-                const uint32_t w2[2] = {wroot[k0 >> 6], wroot[(k1 - 1) >> 6]};
+                const uint32_t w2[2] = {word_root_at(C, wroot, k0), word_root_at(C, wroot, k1 - 1)};
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const uint32_t w = w2[h];
@@ -3061,9 +3157,6 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     uint32_t* part_start = ctx.arena.get<uint32_t>("part_start", P + 1);
     hipLaunchKernelGGL((part_start_kernel<K>), dim3((P + 1 + 63) / 64), dim3(64), 0, s, keys,
                        (uint64_t)R, parts, P, part_start);
-    const uint64_t W = (Gtot >> 6) + 2;
-    uint4* dir = ctx.arena.get<uint4>("dir", W);
-    PD_HIP(hipMemsetAsync(dir, 0, sizeof(uint4) * W, s));
     uint32_t* cstart = ctx.arena.get<uint32_t>("cstart", (size_t)R + 1);
     uint32_t* dncells = ctx.arena.get<uint32_t>("ncells", 4);
     if (R) {
@@ -3075,24 +3168,54 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         tile_offsets(ctx, ccnt, ctiles, coff, s, false);
         hipLaunchKernelGGL((cell_write_kernel<K>), dim3(ctiles), dim3(kBlock), 0, s, keys,
                            (uint64_t)R, coff, cstart, dncells);
-        hipLaunchKernelGGL((dir_bits_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s, keys, cstart,
-                           dncells, dir);
     } else {
         PD_HIP(hipMemsetAsync(cstart, 0, sizeof(uint32_t), s));
         PD_HIP(hipMemsetAsync(dncells, 0, sizeof(uint32_t), s));
     }
-    {
-        const unsigned wtiles = (unsigned)std::max<uint64_t>(1, (W + 4 * kBlock - 1) / (4 * kBlock));
+    // per-tile popcount prefix over a uint4 array's (x, y) bits into .z
+    auto prefix_words = [&](uint4* d, uint64_t nw, bool read_total) -> uint64_t {
+        const unsigned wtiles = (unsigned)std::max<uint64_t>(1, (nw + 4 * kBlock - 1) / (4 * kBlock));
         uint32_t* wcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)wtiles + 1);
         uint64_t* woff = ctx.arena.get<uint64_t>("tile_off", (size_t)wtiles + 1);
-        hipLaunchKernelGGL(dir_tile_kernel, dim3(wtiles), dim3(kBlock), 0, s, dir, W, wcnt);
-        tile_offsets(ctx, wcnt, wtiles, woff, s, false);
-        hipLaunchKernelGGL(dir_write_kernel, dim3(wtiles), dim3(kBlock), 0, s, dir, W, woff);
+        hipLaunchKernelGGL(dir_tile_kernel, dim3(wtiles), dim3(kBlock), 0, s, d, nw, wcnt);
+        const uint64_t tot = tile_offsets(ctx, wcnt, wtiles, woff, s, read_total);
+        hipLaunchKernelGGL(dir_write_kernel, dim3(wtiles), dim3(kBlock), 0, s, d, nw, woff);
+        return tot;
+    };
+    uint64_t W;            // directory words (flat: the whole grid; paged: occupied + terminal)
+    uint4* dir;
+    uint4* pages = nullptr;
+    if (!a.dir_paged) {
+        W = (Gtot >> 6) + 2;
+        dir = ctx.arena.get<uint4>("dir", W);
+        PD_HIP(hipMemsetAsync(dir, 0, sizeof(uint4) * W, s));
+        if (R)
+            hipLaunchKernelGGL((dir_bits_kernel<K, 0>), dim3(blocks(R)), dim3(kBlock), 0, s, keys,
+                               cstart, dncells, dir);
+        prefix_words(dir, W, false);
+    } else {
+        // pages: word masks, then the occupied words before each page (the
+        // total sizes the word array: one sync); then the words themselves
+        const uint64_t NP = (Gtot >> 12) + 2;
+        pages = ctx.arena.get<uint4>("dir_pages", NP);
+        PD_HIP(hipMemsetAsync(pages, 0, sizeof(uint4) * NP, s));
+        if (R)
+            hipLaunchKernelGGL((dir_bits_kernel<K, 6>), dim3(blocks(R)), dim3(kBlock), 0, s, keys,
+                               cstart, dncells, pages);
+        const uint64_t nw = prefix_words(pages, NP, true);
+        W = nw + 1;
+        dir = ctx.arena.get<uint4>("dir", W);
+        if (R)
+            hipLaunchKernelGGL((word_write_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s, keys,
+                               cstart, dncells, pages, dir);
+        else
+            PD_HIP(hipMemsetAsync(dir, 0, sizeof(uint4), s));
     }
+    ctx.t.dir_words = (int64_t)W;
     PD_HIP(hipGetLastError());
     tm.mark();   // 4
 
-    Cells C{parts, part_start, P, dir, cstart};
+    Cells C{parts, part_start, P, dir, cstart, pages};
     const double eps = a.eps, eps2 = a.eps * a.eps;
     // fp32 screening band (see Pred): thresholds rounded outward
     float slo = -1.0f, shi = INFINITY;
@@ -3200,11 +3323,12 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
             PD_HIP(hipMemsetAsync(nbig, 0, 2 * sizeof(uint32_t), s));
             PD_HIP(hipMemsetAsync(wroot, 0xFF, sizeof(uint32_t) * W, s));
             hipLaunchKernelGGL((cell_word_root_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                               cstart, dncells, keys, par, croot, wroot, mid, nbig + 1, big, nbig);
+                               cstart, dncells, keys, par, croot, wroot, mid, nbig + 1, big, nbig,
+                               pages);
             hipLaunchKernelGGL((mid_cell_word_root_kernel<K>), dim3(2048), dim3(kBlock), 0, s,
-                               cstart, keys, mid, nbig + 1, par, croot, wroot);
+                               cstart, keys, mid, nbig + 1, par, croot, wroot, pages);
             hipLaunchKernelGGL((big_cell_word_root_kernel<K>), dim3(1024), dim3(kBlock), 0, s,
-                               cstart, keys, big, nbig, par, croot, wroot);
+                               cstart, keys, big, nbig, par, croot, wroot, pages);
         } else {
             cell_roots(ctx, s, R, cstart, dncells, par, croot);
             hipLaunchKernelGGL(word_root_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, W, croot,
@@ -3325,6 +3449,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     st.parts = parts;
     st.part_start = part_start;
     st.dir = dir;
+    st.pages = pages;
     st.cstart = cstart;
     st.vals = vals;
     st.core = core;
@@ -3363,7 +3488,8 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     const uint8_t* core = st.core;
     const uint32_t* par = st.par;
     uint32_t* gmin = st.gmin;
-    const Cells C{(const PartGrid*)st.parts, st.part_start, st.P, (const uint4*)st.dir, st.cstart};
+    const Cells C{(const PartGrid*)st.parts, st.part_start, st.P, (const uint4*)st.dir, st.cstart,
+                  (const uint4*)st.pages};
     const double eps = st.eps, eps2 = st.eps * st.eps;
     const float slo = st.slo, shi = st.shi;
     if (a.phase == 2) {
@@ -3628,10 +3754,12 @@ void train(Ctx& ctx, TrainArgs& a) {
         }
         return;
     }
-    // per-neighbourhood grids.  Cells are eps (eps/xsub along axis 0) wide;
-    // when the bbox-sized directory (20 B per 64 cells: occupancy word +
-    // word root) would pass the budget (PD_OPT_DIR_BUDGET, default 32 GiB),
-    // every cell grows by a common factor k >= 1 until it fits.  Any width >=
+    // per-neighbourhood grids.  Cells are eps (eps/xsub along axis 0) wide.
+    // The directory is flat (20 B per 64 cells of the bounding box:
+    // occupancy word + word root) or paged (16 B per 4096 cells + the
+    // occupied words; PD_OPT_DIR_PAGED, automatic for sparse grids); when its
+    // extent-dependent part would pass the budget (PD_OPT_DIR_BUDGET, default
+    // 32 GiB), every cell grows by a common factor k >= 1 until it fits.  Any width >=
     // eps is exact: the sweeps derive their candidate ranges from the cell
     // geometry (chords along axis 0, rows +-1 beyond it) and the cell verify
     // covers +-xsub axis-0 cells of width >= eps/xsub; wider cells only add
@@ -3641,6 +3769,7 @@ void train(Ctx& ctx, TrainArgs& a) {
     uint64_t G = 0;
     const long double budget = (long double)ctx.dir_budget;
     double grow = 1.0;
+    bool paged = false;
     for (int attempt = 0;; ++attempt) {
         const double cw = a.eps * (1.0 + 1.0 / 1048576.0) * grow;
         G = 0;
@@ -3696,7 +3825,14 @@ void train(Ctx& ctx, TrainArgs& a) {
             }
             G += (uint64_t)cells;
         }
-        const long double dir_bytes = too_big ? 1e30L : gsum / 64.0L * 20.0L;
+        // the extent-dependent bytes: flat, 20 B per 64 cells of the grid;
+        // paged, 16 B per 4096 cells (its occupied words, 20 B each, follow
+        // the data like the records do, not the extent)
+        const long double words = gsum / 64.0L;
+        paged = ctx.dir_paged > 0 ||
+                (ctx.dir_paged < 0 && (words > (long double)a.n || words * 20.0L > budget));
+        const long double dir_bytes =
+            too_big ? 1e30L : (paged ? gsum / 4096.0L * 16.0L : words * 20.0L);
         if (dir_bytes <= budget) break;
         if (attempt >= 64 || !std::isfinite(grow * 2.0))
             throw Error(-5, "eps-grid directory does not fit the budget at any cell size");
@@ -3706,6 +3842,8 @@ void train(Ctx& ctx, TrainArgs& a) {
         grow *= std::max(k, 1.25);
     }
     ctx.t.grid_grow = grow;
+    ctx.t.dir_paged = paged ? 1 : 0;
+    a.dir_paged = paged;
     int key_bits = 1;
     while (key_bits < 64 && ((G - (G ? 1 : 0)) >> key_bits)) ++key_bits;
     if (a.dtype == 0) {

@@ -51,6 +51,8 @@ struct Timings {
     // cell pairs tested record by record (link mode 3)
     int64_t sweep[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     double grid_grow = 1.0;      // cell width / eps (PD_OPT_DIR_BUDGET)
+    int64_t dir_words = 0;       // directory words allocated (paged: occupied + 1)
+    int dir_paged = 0;           // the last train's directory layout
     float count_kernel = 0;      // dense path: the count pass's tile kernel alone (ms)
 };
 
@@ -71,6 +73,7 @@ struct PhaseState {
     void* parts = nullptr;
     uint32_t* part_start = nullptr;
     void* dir = nullptr;
+    void* pages = nullptr;       // paged directory (null: flat)
     uint32_t* cstart = nullptr;
     uint32_t* vals = nullptr;
     uint8_t* core = nullptr;
@@ -159,6 +162,8 @@ struct Ctx {
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
     bool border_roots = false;   // border sweep's single-root fast path (tuning)
     int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow
+    int dir_paged = -1;          // PD_OPT_DIR_PAGED: 1 paged, 0 flat, -1 paged when the grid has
+                                 // more directory words than points
     int dense_prune = 1;         // dense count pass: projection-window tiles only (2: per-band runs)
     bool sort_payload = false;   // fp32 3-D: coordinates ride the sort (PD_OPT_SORT_PAYLOAD)
     int label_buckets = -1;      // labels to input order by bucketed pair passes (PD_OPT_LABEL_BUCKETS;
@@ -211,6 +216,7 @@ struct TrainArgs {
     const double* tree_bound = nullptr;
     const int32_t* tree_new = nullptr;
     int64_t n_exports = 0;            // out (phase 1)
+    bool dir_paged = false;           // internal: directory layout of this train
 };
 
 void train(Ctx& ctx, TrainArgs& a);

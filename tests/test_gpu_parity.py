@@ -847,6 +847,69 @@ def test_grid_growth_is_exact(native, name, budget):
     assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), g["sk_labels"])
 
 
+@pytest.mark.parametrize("name", ["b2d_20k", "b3d_20k", "c0", "lattice_900", "c0_p5_cityblock",
+                                  "neg_3k", "dup_1d", "c0_p3"])
+def test_dir_layouts_equal(native, name):
+    """The paged directory (occupied words only) and the flat one give
+    sklearn's counts, core flags and labels on the goldens — pd_cluster and
+    the partitioned train — with both layouts forced."""
+    from pypardis_amd import DBSCAN
+    g = load_golden(name)
+    ctx = native.context()
+    P = int(g["max_partitions"])
+    for layout in (1, 0):
+        ctx.set_option(native.PD_OPT_DIR_PAGED, layout)
+        try:
+            lab, core, ncl, cnt = _cluster(native, g["X"], float(g["eps"]),
+                                           int(g["min_samples"]), _metric(g), full=True)
+            t = ctx.timings()
+            m = DBSCAN(eps=float(g["eps"]), min_samples=int(g["min_samples"]), metric=_metric(g),
+                       max_partitions=P if P > 0 else None).train(_dev(g["X"]))
+        finally:
+            ctx.set_option(native.PD_OPT_DIR_PAGED, -1)
+        assert t["dir_paged"] == layout
+        assert np.array_equal(cnt, g["sk_counts"])
+        assert np.array_equal(core, g["sk_core"])
+        assert np.array_equal(lab, g["sk_labels"]) and ncl == int(g["sk_labels"].max()) + 1
+        assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), g["sk_labels"])
+
+
+@pytest.mark.parametrize("cfg,n", [("C4", 4_000_000), ("C2", 1_000_000), ("C1", 300_000)])
+def test_dir_paged_equals_flat_synth(native, cfg, n):
+    """Paged == flat directory on the bench distributions (C4's globe-wide
+    noise and dense cities: words spanning waves, empty pages between
+    occupied ones), labels and core flags bit-identical, and the oracle's on
+    a 300k C4 sample with the paged layout."""
+    from pypardis_amd import DBSCAN, synth
+    X, c = synth.make_config(cfg, n=n, device="cuda" if cfg == "C4" else "cpu")
+    Xd = X if torch.is_tensor(X) else _dev(X)
+    ctx = native.context()
+    outs = []
+    for layout in (1, 0):
+        ctx.set_option(native.PD_OPT_DIR_PAGED, layout)
+        try:
+            m = DBSCAN(eps=c["eps"], min_samples=c["min_samples"],
+                       max_partitions=c.get("max_partitions") or 1).train(Xd)
+            words = ctx.timings()["dir_words"]
+        finally:
+            ctx.set_option(native.PD_OPT_DIR_PAGED, -1)
+        outs.append((m.labels_.clone(), m.core_sample_mask_.clone(), m.n_clusters_, words))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
+    assert outs[0][3] <= outs[1][3]   # occupied words only
+    if cfg == "C4":
+        Xs = Xd[:300_000].cpu().numpy()
+        lab_o, core_o, _, nc_o = oracle.dbscan(Xs, c["eps"], c["min_samples"])
+        ctx.set_option(native.PD_OPT_DIR_PAGED, 1)
+        try:
+            m = DBSCAN(eps=c["eps"], min_samples=c["min_samples"], max_partitions=8).train(
+                _dev(Xs))
+        finally:
+            ctx.set_option(native.PD_OPT_DIR_PAGED, -1)
+        assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)
+        assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_o)
+
+
 @pytest.mark.parametrize("d", [2, 3, 4])
 def test_globe_sized_extent(native, d):
     """Clusters 1e7 eps apart on every axis (a bbox-sized directory of 1e14 -

@@ -826,11 +826,14 @@ def test_dense_sharded_process_group_native(native, tmp_path):
 def test_grid_growth_is_exact(native, name, budget):
     """Cells wider than eps (the directory budget forces them to grow) give
     sklearn's counts, core flags and labels — through pd_cluster and through
-    the partitioned train (halo, merge, border)."""
+    the partitioned train (halo, merge, border).  The flat directory is
+    forced: the paged one's budget only bounds its extent-dependent pages,
+    which these small grids never fill."""
     from pypardis_amd import DBSCAN
     g = load_golden(name)
     ctx = native.context()
     ctx.set_option(native.PD_OPT_DIR_BUDGET, budget)
+    ctx.set_option(native.PD_OPT_DIR_PAGED, 0)
     try:
         lab, core, ncl, cnt = _cluster(native, g["X"], float(g["eps"]), int(g["min_samples"]),
                                        _metric(g), full=True)
@@ -840,6 +843,7 @@ def test_grid_growth_is_exact(native, name, budget):
                    max_partitions=P if P > 0 else None).train(_dev(g["X"]))
     finally:
         ctx.set_option(native.PD_OPT_DIR_BUDGET, 32 << 30)
+        ctx.set_option(native.PD_OPT_DIR_PAGED, -1)
     assert grow > 1.5, grow
     assert np.array_equal(cnt, g["sk_counts"])
     assert np.array_equal(core, g["sk_core"])

@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--jump-rounds", type=int, default=None, help="PD_OPT_JUMP_ROUNDS override")
     ap.add_argument("--sort-payload", type=int, default=None,
                     help="PD_OPT_SORT_PAYLOAD override (1: coordinates ride the sort)")
+    ap.add_argument("--dense-screen", type=int, default=None,
+                    help="PD_OPT_DENSE_SCREEN override (1 e4m3, 0 bf16 hi.hi)")
     ap.add_argument("--dir-paged", type=int, default=None,
                     help="PD_OPT_DIR_PAGED override (1 paged, 0 flat, -1 auto)")
     ap.add_argument("--label-buckets", type=int, default=None,
@@ -390,7 +392,8 @@ def main():
                      (_native.PD_OPT_DIR_BUDGET, args.dir_budget),
                      (_native.PD_OPT_LABEL_BUCKETS, args.label_buckets),
                      (_native.PD_OPT_SORT_PAYLOAD, args.sort_payload),
-                     (_native.PD_OPT_DIR_PAGED, args.dir_paged)):
+                     (_native.PD_OPT_DIR_PAGED, args.dir_paged),
+                     (_native.PD_OPT_DENSE_SCREEN, args.dense_screen)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None

@@ -124,7 +124,11 @@ enum pd_option {
                                 stored: memory and build time follow the occupied cells, not the
                                 extent), 0 flat (one word per 64 cells of the bounding box), -1
                                 (default) paged when the grid has more words than points or the
-                                flat one would pass PD_OPT_DIR_BUDGET.  Same results either way */
+                                flat one would pass PD_OPT_DIR_BUDGET.  Same results either way */,
+    PD_OPT_DENSE_SCREEN = 18  /* d > 4 count pass: the tile screen that decides which tiles
+                                compute the exact-banded split-bf16 product.  1 (default): e4m3
+                                Gram tiles on v_mfma_f32_32x32x64_f8f6f4 (half the staged bytes,
+                                twice the MFMA rate); 0: bf16 hi.hi.  Same counts either way */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

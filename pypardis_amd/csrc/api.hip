@@ -170,6 +170,9 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.label_buckets = value < 0 ? -1 : (value ? 1 : 0);
         } else if (option == PD_OPT_DIR_PAGED) {
             ctx->c.dir_paged = value < 0 ? -1 : (value ? 1 : 0);
+        } else if (option == PD_OPT_DENSE_SCREEN) {
+            if (value < 0 || value > 1) throw Error(PD_EINVAL, "dense screen is 0 or 1");
+            ctx->c.dense_screen = (int)value;
         }
         else
             throw Error(PD_EINVAL, "unknown option");

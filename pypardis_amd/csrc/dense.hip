@@ -51,6 +51,7 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));   // 32 e4m3 values
 
 enum { kCount = 0, kLink = 1, kBorder = 2 };
 constexpr int kTile = 64;                 // points per wave tile (2 MFMA tiles of 32)
@@ -63,6 +64,25 @@ constexpr float kBandC = 1.0f / 8192.0f;  // error band c (see header)
 // tiles that can hold one fetch the lo fragments and finish the split
 // product; C3 pairs lie ~100 eps^2 apart, so most tiles stop at the screen.
 constexpr float kScreenC = 1.0f / 128.0f;
+// e4m3 screen (PD_OPT_DENSE_SCREEN = 1, the default for the count pass):
+// v_mfma_f32_32x32x64_f8f6f4 on coordinates scaled by 2^8 (|v| <= 256 <=
+// 448) and rounded to OCP e4m3 (round-to-nearest-even, subnormals kept:
+// tools/fp8x64_probe.hip).  Per coordinate |q - x| <= 2^-4 |x| + 2^-18 (the
+// subnormal spacing 2^-9 over the 2^8 scale, halved), so with a = 2^-18
+// sqrt(d_pad): |<qx,qy> - <x,y>| <= (2^-3 + 2^-8)|x||y| + 1.125 a (|x| + |y|)
+// + a^2; products of e4m3 values are exact and the fp32 accumulation of <= 128
+// of them adds <= 2^-17 |qx||qy|.  d2 is therefore within (2^-3 + 2^-8 +
+// 2^-17) s + 4.5 a sqrt(max|x|^2) + 2 a^2 of the truth; the band below, c8 =
+// 2^-3 + 2^-7, keeps 0.004 s of slack for the fp32 epilogue.  A tile where no
+// pair passes it holds no neighbour; the others compute the split-bf16
+// product from scratch (hi and lo from global memory).  Half the staged bytes
+// of the hi.hi screen, and one 32x32x64 MFMA (64 cycles) per 64 dims where the
+// bf16 screen issues four 32x32x16 (32 cycles each).  At C3's distances the
+// same tiles pass (clustered pairs lie within 0.05 of each other, the rest
+// beyond 0.88 in d2; the band adds 0.27).
+constexpr float kScreen8C = 1.0f / 8.0f + 1.0f / 128.0f;
+constexpr float kF8Scale = 256.0f;        // coordinates -> e4m3 range
+constexpr float kF8Acc = kF8Scale * kF8Scale;
 constexpr float kPadNorm = 1.0e30f;       // norm of padding rows: never a neighbour
 
 inline unsigned nblocks(uint64_t n, unsigned per = kBlock) {
@@ -75,6 +95,9 @@ inline uint32_t pad_rows(uint32_t m) { return (m + 2 * kTile - 1) / (2 * kTile) 
 struct FragSet {
     const bf16x8* hi;
     const bf16x8* lo;
+    const i32x8* f8;       // e4m3 fragments (count pass screen) or null: row group g,
+                           // k8-step s (64 dims) is 64 lanes x 32 bytes, lane 32h + r holding
+                           // dims 64s + 32h .. +31 of row 32g + r
     const float* norm;     // [rows_pad]
     const float* nmax;     // max norm over the valid rows (device scalar)
     const uint32_t* idx;   // row -> point id (null: identity)
@@ -123,6 +146,40 @@ __global__ __launch_bounds__(kBlock) void prep_kernel(const T* __restrict__ X, i
     const uint64_t o = ((uint64_t)(r >> 5) * KS + s) * 64 + 32 * h + (r & 31);
     Fh[o] = vh;
     Fl[o] = vl;
+}
+
+// One thread per (row, k8-step, lane half): 32 dims -> e4m3 (scaled by 2^8).
+// The k order inside a lane is the same for both MFMA operands (a Gram tile),
+// so any consistent (h, j) -> k map computes the same products.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void prep8_kernel(const T* __restrict__ X, int d,
+                                                       const uint32_t* __restrict__ idx, uint32_t m,
+                                                       uint32_t rows_pad, int KS8,
+                                                       const double* __restrict__ center,
+                                                       double scale, i32x8* __restrict__ F8) {
+    const uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= (uint64_t)rows_pad * KS8 * 2) return;
+    const int h = (int)(t & 1);
+    const int s = (int)((t >> 1) % KS8);
+    const uint32_t r = (uint32_t)((t >> 1) / KS8);
+    const uint32_t p = r < m ? (idx ? idx[r] : r) : 0u;
+    i32x8 v;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        float f[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = 64 * s + 32 * h + 4 * w + q;
+            // the bf16 path's fp32 value, then the exact power-of-two scale
+            f[q] = (r < m && k < d)
+                       ? (float)(((double)X[(uint64_t)p * d + k] - center[k]) * scale) * kF8Scale
+                       : 0.0f;
+        }
+        int x = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+        x = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], x, true);
+        v[w] = x;
+    }
+    F8[((uint64_t)(r >> 5) * KS8 + s) * 64 + 32 * h + (r & 31)] = v;
 }
 
 // |v|^2 of the scaled fp32 coordinates (the values the fragments split).
@@ -180,6 +237,7 @@ struct TileArgs {
     double win;
     unsigned long long* tiles;  // [2]: wave tiles computed, of which refined past the
                                 // count screen (null: not counted)
+    float f8_a;                 // e4m3 screen: 2^-18 sqrt(d_pad), the subnormal term
     // sharded train: this device computes the I rows of the chunks
     // (kShardChunk rows each) c with c % shard_world == shard_rank
     uint32_t shard_rank, shard_world;
@@ -258,21 +316,32 @@ struct TileLds {
     bf16x8 lo[LO ? 2 : 1][LO ? 2 : 1][LO ? KS : 1][LO ? 64 : 1];
     float nta[2][kTile];       // -ta_j = -(1+c)|x_j|^2 / 2
 };
+// e4m3 screen: the staged tile is the e4m3 fragments only (4 KiB per 64 rows
+// of up to 64 dims)
+template <int KS8>
+struct TileLds8 {
+    i32x8 f8[2][2][KS8][64];   // [buffer][row group][k8-step][lane]
+    float nta[2][kTile];
+};
 
 // QT: 32-query groups per wave (B operand tiles held in registers).  QT = 4
 // doubles the MFMA work per streamed byte (each staged tile feeds 2 x 4 x 3 x
 // KS MFMAs per wave) at one wave per SIMD.
-template <typename T, int MODE, int KS, int QT>
-__global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu((KS >= 8 || QT > 2) ? 1 : 2))) void tile_kernel(TileArgs<T> A) {
+constexpr int kF8Waves = 3;   // e4m3 count pass: waves per SIMD (no bf16 query fragments held)
+template <typename T, int MODE, int KS, int QT, bool F8>
+__global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu((KS >= 8 || QT > 2) ? 1 : (F8 ? kF8Waves : 2)))) void tile_kernel(TileArgs<T> A) {
     constexpr int TB = tile_threads(KS, MODE);
     constexpr int QW = 32 * QT;                  // query rows per wave
+    constexpr int KS8 = (KS + 3) / 4;            // e4m3 k-steps of 64 dims
+    static_assert(!F8 || MODE == kCount, "the e4m3 screen is the count pass's");
     // every mode screens with hi.hi and reads lo from global memory for the
     // tiles it keeps (link / border too: their core x core and border x core
     // pairs are as far apart as the count pass's); LO = true would stage lo
     constexpr bool LO = false;
-    constexpr int NC = (LO ? 2 : 1) * 2 * KS * 64;   // 16-byte chunks per staged tile
+    // 16-byte chunks per staged tile (e4m3: two per lane fragment)
+    constexpr int NC = F8 ? 2 * KS8 * 64 * 2 : (LO ? 2 : 1) * 2 * KS * 64;
     constexpr int NCH = (NC + TB - 1) / TB;      // per thread
-    __shared__ TileLds<KS, LO> S;
+    __shared__ std::conditional_t<F8, TileLds8<KS8>, TileLds<KS, LO>> S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // block -> query rows.  Pruned count: bands are dealt round-robin to the
     // 8 XCDs (dispatch puts block id b on XCD b % 8), a band's blocks kept
@@ -297,17 +366,29 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
     const int col = lane & 31, h = lane >> 5;
     const float nJmax = *A.J.nmax;
     // the wave's 32 QT query points: B operand fragments, kept in registers
-    bf16x8 bh[QT][KS], bl[QT][KS];
+    // (e4m3 screen: the bf16 query fragments are re-read for the few kept
+    // tiles instead of held, 64 registers fewer)
+    bf16x8 bh[F8 ? 1 : QT][F8 ? 1 : KS], bl[F8 ? 1 : QT][F8 ? 1 : KS];
+    i32x8 bq8[F8 ? QT : 1][F8 ? KS8 : 1];
     uint32_t iq[QT];
     float ai[QT], bi[QT], bc[QT];
     bool ok[QT];
+    // e4m3 screen's absolute term (subnormals), over max |x_j|^2 for both rows
+    const float a8 = A.f8_a;
+    const float abs8 = 4.5f * a8 * __builtin_sqrtf(nJmax) * 1.001f + 2.0f * a8 * a8;
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
+        if constexpr (!F8) {
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const uint64_t o = ((uint64_t)((wave_ok ? i0 : 0) / 32 + t) * KS + s) * 64 + lane;
-            bh[t][s] = A.I.hi[o];
-            bl[t][s] = A.I.lo[o];
+            for (int s = 0; s < KS; ++s) {
+                const uint64_t o = ((uint64_t)((wave_ok ? i0 : 0) / 32 + t) * KS + s) * 64 + lane;
+                bh[t][s] = A.I.hi[o];
+                bl[t][s] = A.I.lo[o];
+            }
+        } else {
+#pragma unroll
+            for (int s = 0; s < KS8; ++s)
+                bq8[t][s] = A.I.f8[((uint64_t)((wave_ok ? i0 : 0) / 32 + t) * KS8 + s) * 64 + lane];
         }
         iq[t] = i0 + 32 * t + col;
         ok[t] = wave_ok && iq[t] < A.I.m;
@@ -318,6 +399,9 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
         // widened by max |x_j|^2
         bc[t] = ((1.0f - kScreenC) * nI - A.ehi) * 0.5f -
                 (0.5f * (kScreenC + kBandC)) * 1.001f * nJmax;
+        if constexpr (F8)   // in the e4m3 accumulator's units (x 2^16, exact)
+            bc[t] = kF8Acc * (((1.0f - kScreen8C) * nI - A.ehi - abs8) * 0.5f -
+                              (0.5f * (kScreen8C + kBandC)) * 1.001f * nJmax);
     }
     uint32_t cnt[QT], best[QT];
 #pragma unroll
@@ -455,10 +539,16 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
         for (int q = 0; q < NCH; ++q) {
             const int c = threadIdx.x + q * TB;        // [0, 2 * 2 * KS * 64)
             if (NC % TB != 0 && c >= NC) break;
-            const int half = c / (2 * KS * 64);            // 0 hi, 1 lo
-            const int w = c % (2 * KS * 64);               // (row group, k-step, lane)
-            const uint64_t o = (uint64_t)(j0 / 32) * KS * 64 + w;
-            st.v[q] = (LO && half) ? A.J.lo[o] : A.J.hi[o];
+            if constexpr (F8) {   // the tile's e4m3 fragments are contiguous
+                const bf16x8* src = reinterpret_cast<const bf16x8*>(A.J.f8) +
+                                    (uint64_t)(j0 / 32) * KS8 * 64 * 2;
+                st.v[q] = src[c];
+            } else {
+                const int half = c / (2 * KS * 64);            // 0 hi, 1 lo
+                const int w = c % (2 * KS * 64);               // (row group, k-step, lane)
+                const uint64_t o = (uint64_t)(j0 / 32) * KS * 64 + w;
+                st.v[q] = (LO && half) ? A.J.lo[o] : A.J.hi[o];
+            }
         }
         if (threadIdx.x < kTile) st.n = A.J.norm[j0 + threadIdx.x];
     };
@@ -467,12 +557,18 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
         for (int q = 0; q < NCH; ++q) {
             const int c = threadIdx.x + q * TB;
             if (NC % TB != 0 && c >= NC) break;
-            const int half = c / (2 * KS * 64);
-            const int w = c % (2 * KS * 64);
-            bf16x8* dst = (LO && half) ? &S.lo[LO ? buf : 0][0][0][0] : &S.hi[buf][0][0][0];
-            dst[w] = st.v[q];
+            if constexpr (F8) {
+                reinterpret_cast<bf16x8*>(&S.f8[buf][0][0][0])[c] = st.v[q];
+            } else {
+                const int half = c / (2 * KS * 64);
+                const int w = c % (2 * KS * 64);
+                bf16x8* dst = (LO && half) ? &S.lo[LO ? buf : 0][0][0][0] : &S.hi[buf][0][0][0];
+                dst[w] = st.v[q];
+            }
         }
-        if (threadIdx.x < kTile) S.nta[buf][threadIdx.x] = -((1.0f + kBandC) * 0.5f) * st.n;
+        // (e4m3 screen: in the x 2^16 units of its products, exact)
+        if (threadIdx.x < kTile)
+            S.nta[buf][threadIdx.x] = -((1.0f + kBandC) * 0.5f) * st.n * (F8 ? kF8Acc : 1.0f);
     };
     // cursors: current tile (in LDS buf), next (in `ready`), the one after
     uint32_t sg = 0, j0 = seg_lo[0];
@@ -495,18 +591,26 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
         if (compute) {
             ++ntiles;
             // C operand: -ta of the tile's rows, element 4q + e = row 32u + 8q + 4h + e
-            f32x16 nt[2];
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
+            // (read where it is used: the e4m3 screen re-reads it for a kept tile
+            // rather than holding 32 registers across the screen)
+            auto nt_of = [&](int u) {
+                f32x16 v16;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const float4 v =
                         *reinterpret_cast<const float4*>(&S.nta[buf][32 * u + 8 * q + 4 * h]);
-                    nt[u][4 * q + 0] = v.x;
-                    nt[u][4 * q + 1] = v.y;
-                    nt[u][4 * q + 2] = v.z;
-                    nt[u][4 * q + 3] = v.w;
+                    v16[4 * q + 0] = v.x;
+                    v16[4 * q + 1] = v.y;
+                    v16[4 * q + 2] = v.z;
+                    v16[4 * q + 3] = v.w;
                 }
+                return v16;
+            };
+            f32x16 nt[2];
+            if constexpr (!F8) {
+                nt[0] = nt_of(0);
+                nt[1] = nt_of(1);
+            }
             f32x16 acc[2][QT];
             bool refine = true;
             if constexpr (LO) {
@@ -529,6 +633,63 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
                             acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[u], bh[t][s],
                                                                                 acc[u][t], 0, 0, 0);
                         }
+                }
+            } else if constexpr (F8) {
+                // count pass, e4m3 screen (kScreen8C, in the x 2^16 units of
+                // the e4m3 products); a kept tile recomputes the split-bf16
+                // product from scratch, hi and lo from global memory
+#pragma unroll
+                for (int s = 0; s < KS8; ++s) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const i32x8 a8 = S.f8[buf][u][s][lane];
+#pragma unroll
+                        for (int t = 0; t < QT; ++t)
+                            acc[u][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                                a8, bq8[t][s], s == 0 ? nt_of(u) : acc[u][t], 0, 0, 0, 0, 0, 0);
+                    }
+                }
+                bool mb = false;
+#pragma unroll
+                for (int t = 0; t < QT; ++t) {
+                    float m0 = fmaxf(acc[0][t][0], acc[1][t][0]);
+#pragma unroll
+                    for (int r = 1; r < 16; ++r) m0 = fmaxf(fmaxf(m0, acc[0][t][r]), acc[1][t][r]);
+                    mb |= m0 >= bc[t];
+                }
+                refine = __any(mb);
+                nrefined += refine ? 1u : 0u;
+                if (refine) {
+                    const uint32_t iw = (wave_ok ? i0 : 0) / 32;
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) nt[u] = nt_of(u) * (1.0f / kF8Acc);   // exact
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) {
+                        bf16x8 ah[2], al[2], qh[QT], ql[QT];
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            const uint64_t o = ((uint64_t)(j0 / 32 + u) * KS + s) * 64 + lane;
+                            ah[u] = A.J.hi[o];
+                            al[u] = A.J.lo[o];
+                        }
+#pragma unroll
+                        for (int t = 0; t < QT; ++t) {
+                            const uint64_t o = ((uint64_t)(iw + t) * KS + s) * 64 + lane;
+                            qh[t] = A.I.hi[o];
+                            ql[t] = A.I.lo[o];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 2; ++u)
+#pragma unroll
+                            for (int t = 0; t < QT; ++t) {
+                                acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                    ah[u], qh[t], s == 0 ? nt[u] : acc[u][t], 0, 0, 0);
+                                acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                    ah[u], ql[t], acc[u][t], 0, 0, 0);
+                                acc[u][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                    al[u], qh[t], acc[u][t], 0, 0, 0);
+                            }
+                    }
                 }
             } else {
                 // count pass: the hi.hi screen (kScreenC), then the rest of the
@@ -894,6 +1055,7 @@ struct Geometry {
     double scale = 1.0;
     float elo = 0, ehi = 0;
     bool mfma = false;
+    bool f8 = false;       // also build the e4m3 fragments (count pass screen)
 };
 
 template <typename T>
@@ -903,10 +1065,18 @@ FragSet make_frags(Ctx& ctx, const std::string& tag, const T* X, int d, const ui
     FragSet F;
     F.m = m;
     F.idx = idx;
+    F.f8 = nullptr;
     if (!G.mfma) {
         F.hi = F.lo = nullptr;
         F.norm = F.nmax = nullptr;
         return F;
+    }
+    if (G.f8) {
+        const int KS8 = (G.KS + 3) / 4;
+        i32x8* f8 = ctx.arena.get<i32x8>(tag + "_f8", (size_t)(rp / 32) * KS8 * 64);
+        hipLaunchKernelGGL(prep8_kernel<T>, dim3(nblocks((uint64_t)rp * KS8 * 2)), dim3(kBlock), 0,
+                           s, X, d, idx, m, rp, KS8, G.center, G.scale, f8);
+        F.f8 = f8;
     }
     const size_t nfrag = (size_t)(rp / 32) * G.KS * 64;
     bf16x8* hi = ctx.arena.get<bf16x8>(tag + "_hi", nfrag);
@@ -939,7 +1109,14 @@ void run_tiles(const TileArgs<T>& A, const Geometry& G, int metric, hipStream_t 
             // pruned count: 8 x ceil(bands / 8) x blocks per band (tile_kernel)
             const unsigned grid = A.p3 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (TB / 64 * 32 * QT))
                                        : nblocks(waves, TB / 64);
-            hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT>), dim3(grid), dim3(TB), 0, s, A);
+            if constexpr (MODE == kCount) {
+                if (A.I.f8 && A.J.f8) {
+                    hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT, true>), dim3(grid), dim3(TB), 0,
+                                       s, A);
+                    return;
+                }
+            }
+            hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT, false>), dim3(grid), dim3(TB), 0, s, A);
         };
         switch (G.KS) {
             case 1: launch(std::integral_constant<int, 1>{}); break;
@@ -1041,8 +1218,10 @@ void count_stage(Ctx& ctx, TrainArgs& a, int rank, int world) {
         std::memcpy(h, hc.data(), sizeof(double) * d);
         PD_HIP(hipMemcpyAsync(ds.center, h, sizeof(double) * d, hipMemcpyHostToDevice, s));
     }
-    const Geometry G = geometry_of(ds);
+    Geometry G = geometry_of(ds);
+    G.f8 = G.mfma && ctx.dense_screen == 1;   // the count pass's e4m3 screen
     TileArgs<T> A = base_args<T>(ds);
+    A.f8_a = (float)std::ldexp(std::sqrt(64.0 * ((ds.KS + 3) / 4)), -18);
 
     uint32_t* cnt = ctx.arena.get<uint32_t>("dn_cnt", n);
     unsigned long long* dtiles = nullptr;

@@ -863,16 +863,19 @@ __global__ void part_start_kernel(const K* __restrict__ keys, uint64_t R,
 // cstart[cell] = record.
 template <typename K>
 __device__ __forceinline__ uint32_t cell_starts4(const K* __restrict__ keys, uint64_t R,
-                                                 uint64_t r0, uint32_t (&st)[4]) {
+                                                 uint64_t r0, uint32_t (&st)[4],
+                                                 uint64_t (&kv)[4]) {
     uint32_t c = 0;
     uint64_t prev = r0 > 0 && r0 < R ? (uint64_t)keys[r0 - 1] : ~0ull;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint64_t r = r0 + q;
         st[q] = 0;
+        kv[q] = 0;
         if (r < R) {
             const uint64_t k = (uint64_t)keys[r];
             st[q] = (r == 0 || k != prev) ? 1u : 0u;
+            kv[q] = k;
             prev = k;
         }
         c += st[q];
@@ -884,8 +887,9 @@ template <typename K>
 __global__ __launch_bounds__(kBlock) void cell_tile_kernel(const K* __restrict__ keys, uint64_t R,
                                                            uint32_t* __restrict__ tile_cnt) {
     uint32_t st[4];
+    uint64_t kv[4];
     const uint64_t r0 = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
-    const uint32_t t = block_sum_u32(cell_starts4<K>(keys, R, r0, st));
+    const uint32_t t = block_sum_u32(cell_starts4<K>(keys, R, r0, st, kv));
     if (threadIdx.x == 0) tile_cnt[blockIdx.x] = t;
 }
 
@@ -893,15 +897,20 @@ template <typename K>
 __global__ __launch_bounds__(kBlock) void cell_write_kernel(const K* __restrict__ keys, uint64_t R,
                                                             const uint64_t* __restrict__ tile_off,
                                                             uint32_t* __restrict__ cstart,
+                                                            K* __restrict__ ckeys,
                                                             uint32_t* __restrict__ ncells) {
     uint32_t st[4];
+    uint64_t kv[4];
     const uint64_t r0 = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
     uint32_t btot;
-    const uint32_t c = cell_starts4<K>(keys, R, r0, st);
+    const uint32_t c = cell_starts4<K>(keys, R, r0, st, kv);
     uint32_t cid = (uint32_t)tile_off[blockIdx.x] + block_excl_scan(c, btot);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        if (st[q]) cstart[cid] = (uint32_t)(r0 + q);
+        if (st[q]) {
+            cstart[cid] = (uint32_t)(r0 + q);
+            ckeys[cid] = (K)kv[q];   // the cell's key, dense: the directory passes read it in order
+        }
         cid += st[q];
         if (r0 + q == R - 1) {
             cstart[cid] = (uint32_t)R;
@@ -918,13 +927,12 @@ __global__ __launch_bounds__(kBlock) void cell_write_kernel(const K* __restrict_
 // SH = 6: the paged directory's page masks (one bit per occupied word of
 // the page; the units are then words, k >> 6).
 template <typename K, int SH>
-__global__ __launch_bounds__(kBlock) void dir_bits_kernel(const K* __restrict__ keys,
-                                                          const uint32_t* __restrict__ cstart,
+__global__ __launch_bounds__(kBlock) void dir_bits_kernel(const K* __restrict__ ckeys,
                                                           const uint32_t* __restrict__ ncells,
                                                           uint4* __restrict__ dir) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     const bool in = c < *ncells;
-    const uint64_t k = in ? ((uint64_t)keys[cstart[c]] >> SH) : ~0ull;
+    const uint64_t k = in ? ((uint64_t)ckeys[c] >> SH) : ~0ull;
     const uint64_t word = k >> 6;
     unsigned long long v = in ? (1ull << (k & 63)) : 0ull;
     const int lane = threadIdx.x & 63;
@@ -946,15 +954,14 @@ __global__ __launch_bounds__(kBlock) void dir_bits_kernel(const K* __restrict__ 
 // at most 63 cells), z = that cell's index (the occupied cells before the
 // word).  The last cell also writes the terminal word {0, 0, ncells}.
 template <typename K>
-__global__ __launch_bounds__(kBlock) void word_write_kernel(const K* __restrict__ keys,
-                                                            const uint32_t* __restrict__ cstart,
+__global__ __launch_bounds__(kBlock) void word_write_kernel(const K* __restrict__ ckeys,
                                                             const uint32_t* __restrict__ ncells,
                                                             const uint4* __restrict__ pages,
                                                             uint4* __restrict__ words) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t nc = *ncells;
     const bool in = c < nc;
-    const uint64_t k = in ? (uint64_t)keys[cstart[c]] : ~0ull;
+    const uint64_t k = in ? (uint64_t)ckeys[c] : ~0ull;
     const uint64_t word = k >> 6;
     unsigned long long v = in ? (1ull << (k & 63)) : 0ull;
     const int lane = threadIdx.x & 63;
@@ -968,13 +975,13 @@ __global__ __launch_bounds__(kBlock) void word_write_kernel(const K* __restrict_
     const uint64_t w63 = (uint64_t)__shfl((long long)word, 63, 64);
     if (!in) return;
     bool first = c == 0;
-    if (!first) first = lane ? wp != word : ((uint64_t)keys[cstart[c - 1]] >> 6) != word;
+    if (!first) first = lane ? wp != word : ((uint64_t)ckeys[c - 1] >> 6) != word;
     bool occ;
     const uint64_t slot = page_slot(pages[word >> 6], word, occ);
     if (first) {
         if (w63 == word)   // the word continues past this wave
             for (uint32_t c2 = c - (uint32_t)lane + 64; c2 < nc; ++c2) {
-                const uint64_t k2 = (uint64_t)keys[cstart[c2]];
+                const uint64_t k2 = (uint64_t)ckeys[c2];
                 if ((k2 >> 6) != word) break;
                 v |= 1ull << (k2 & 63);
             }
@@ -2241,7 +2248,7 @@ constexpr uint32_t kMidCell = 16, kWordBig = 1024;
 template <typename K>
 __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
     const uint32_t* __restrict__ cstart, const uint32_t* __restrict__ ncells,
-    const K* __restrict__ keys, uint32_t* __restrict__ par, uint32_t* __restrict__ croot,
+    const K* __restrict__ ckeys, uint32_t* __restrict__ par, uint32_t* __restrict__ croot,
     uint32_t* __restrict__ wroot, uint32_t* __restrict__ mid, uint32_t* __restrict__ nmid,
     uint32_t* __restrict__ big, uint32_t* __restrict__ nbig, const uint4* __restrict__ pages) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
@@ -2253,7 +2260,7 @@ __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
     if (c < nc) {
         s = cstart[c];
         sz = cstart[c + 1] - s;
-        word = word_slot(pages, (uint64_t)keys[s]);
+        word = word_slot(pages, (uint64_t)ckeys[c]);
     }
     // the larger cells' roots join their words in the mid / big kernels
     wave_append(mid, nmid, sz > kMidCell && sz <= kWordBig, c);
@@ -2274,7 +2281,7 @@ __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
 
 template <typename K>
 __global__ __launch_bounds__(kBlock) void mid_cell_word_root_kernel(
-    const uint32_t* __restrict__ cstart, const K* __restrict__ keys,
+    const uint32_t* __restrict__ cstart, const K* __restrict__ ckeys,
     const uint32_t* __restrict__ mid, const uint32_t* __restrict__ nmid,
     uint32_t* __restrict__ par, uint32_t* __restrict__ croot, uint32_t* __restrict__ wroot,
     const uint4* __restrict__ pages) {
@@ -2290,14 +2297,14 @@ __global__ __launch_bounds__(kBlock) void mid_cell_word_root_kernel(
         for (int o = 32; o > 0; o >>= 1) v = root_merge(v, (uint32_t)__shfl_xor((int)v, o, 64));
         if (lane == 0) {
             croot[c] = v;
-            word_merge(wroot, word_slot(pages, (uint64_t)keys[s]), v);
+            word_merge(wroot, word_slot(pages, (uint64_t)ckeys[c]), v);
         }
     }
 }
 
 template <typename K>
 __global__ __launch_bounds__(kBlock) void big_cell_word_root_kernel(
-    const uint32_t* __restrict__ cstart, const K* __restrict__ keys,
+    const uint32_t* __restrict__ cstart, const K* __restrict__ ckeys,
     const uint32_t* __restrict__ big, const uint32_t* __restrict__ nbig,
     uint32_t* __restrict__ par, uint32_t* __restrict__ croot, uint32_t* __restrict__ wroot,
     const uint4* __restrict__ pages) {
@@ -2317,7 +2324,7 @@ __global__ __launch_bounds__(kBlock) void big_cell_word_root_kernel(
 #pragma unroll
             for (int k = 0; k < kBlock / 64; ++k) w = root_merge(w, part[k]);
             croot[c] = w;
-            word_merge(wroot, word_slot(pages, (uint64_t)keys[cstart[c]]), w);
+            word_merge(wroot, word_slot(pages, (uint64_t)ckeys[c]), w);
         }
         __syncthreads();
     }
@@ -3158,6 +3165,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     hipLaunchKernelGGL((part_start_kernel<K>), dim3((P + 1 + 63) / 64), dim3(64), 0, s, keys,
                        (uint64_t)R, parts, P, part_start);
     uint32_t* cstart = ctx.arena.get<uint32_t>("cstart", (size_t)R + 1);
+    K* ckeys = ctx.arena.get<K>("cell_keys", (size_t)R + 1);   // key of each occupied cell
     uint32_t* dncells = ctx.arena.get<uint32_t>("ncells", 4);
     if (R) {
         const unsigned ctiles = (unsigned)((R + 4 * kBlock - 1) / (4 * kBlock));
@@ -3167,7 +3175,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
                            (uint64_t)R, ccnt);
         tile_offsets(ctx, ccnt, ctiles, coff, s, false);
         hipLaunchKernelGGL((cell_write_kernel<K>), dim3(ctiles), dim3(kBlock), 0, s, keys,
-                           (uint64_t)R, coff, cstart, dncells);
+                           (uint64_t)R, coff, cstart, ckeys, dncells);
     } else {
         PD_HIP(hipMemsetAsync(cstart, 0, sizeof(uint32_t), s));
         PD_HIP(hipMemsetAsync(dncells, 0, sizeof(uint32_t), s));
@@ -3190,8 +3198,8 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         dir = ctx.arena.get<uint4>("dir", W);
         PD_HIP(hipMemsetAsync(dir, 0, sizeof(uint4) * W, s));
         if (R)
-            hipLaunchKernelGGL((dir_bits_kernel<K, 0>), dim3(blocks(R)), dim3(kBlock), 0, s, keys,
-                               cstart, dncells, dir);
+            hipLaunchKernelGGL((dir_bits_kernel<K, 0>), dim3(blocks(R)), dim3(kBlock), 0, s, ckeys,
+                               dncells, dir);
         prefix_words(dir, W, false);
     } else {
         // pages: word masks, then the occupied words before each page (the
@@ -3200,14 +3208,14 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         pages = ctx.arena.get<uint4>("dir_pages", NP);
         PD_HIP(hipMemsetAsync(pages, 0, sizeof(uint4) * NP, s));
         if (R)
-            hipLaunchKernelGGL((dir_bits_kernel<K, 6>), dim3(blocks(R)), dim3(kBlock), 0, s, keys,
-                               cstart, dncells, pages);
+            hipLaunchKernelGGL((dir_bits_kernel<K, 6>), dim3(blocks(R)), dim3(kBlock), 0, s, ckeys,
+                               dncells, pages);
         const uint64_t nw = prefix_words(pages, NP, true);
         W = nw + 1;
         dir = ctx.arena.get<uint4>("dir", W);
         if (R)
-            hipLaunchKernelGGL((word_write_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s, keys,
-                               cstart, dncells, pages, dir);
+            hipLaunchKernelGGL((word_write_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s, ckeys,
+                               dncells, pages, dir);
         else
             PD_HIP(hipMemsetAsync(dir, 0, sizeof(uint4), s));
     }
@@ -3323,12 +3331,12 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
             PD_HIP(hipMemsetAsync(nbig, 0, 2 * sizeof(uint32_t), s));
             PD_HIP(hipMemsetAsync(wroot, 0xFF, sizeof(uint32_t) * W, s));
             hipLaunchKernelGGL((cell_word_root_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                               cstart, dncells, keys, par, croot, wroot, mid, nbig + 1, big, nbig,
+                               cstart, dncells, ckeys, par, croot, wroot, mid, nbig + 1, big, nbig,
                                pages);
             hipLaunchKernelGGL((mid_cell_word_root_kernel<K>), dim3(2048), dim3(kBlock), 0, s,
-                               cstart, keys, mid, nbig + 1, par, croot, wroot, pages);
+                               cstart, ckeys, mid, nbig + 1, par, croot, wroot, pages);
             hipLaunchKernelGGL((big_cell_word_root_kernel<K>), dim3(1024), dim3(kBlock), 0, s,
-                               cstart, keys, big, nbig, par, croot, wroot, pages);
+                               cstart, ckeys, big, nbig, par, croot, wroot, pages);
         } else {
             cell_roots(ctx, s, R, cstart, dncells, par, croot);
             hipLaunchKernelGGL(word_root_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, W, croot,

@@ -656,6 +656,54 @@ def test_dense_prune_full_size(native, n, eps):
         assert int(core0.sum()) > 0
 
 
+def _subnormal_heavy():
+    """16-D points whose coordinates mostly fall in e4m3's subnormal range
+    after scaling (a few far outliers set the scale), with pairs near eps."""
+    rng = np.random.default_rng(77)
+    X = rng.normal(scale=1e-5, size=(6000, 16)).astype(np.float32)
+    X[:3000] += np.float32(3e-5)
+    X[-4:] = np.sign(rng.normal(size=(4, 16))).astype(np.float32)   # scale ~ 1
+    return X
+
+
+@pytest.mark.parametrize("case", ["c3_30k", "d5_blobs", "d100_f64", "subnormal", "ties", "c3_1m"])
+def test_dense_screens_equal(native, case):
+    """The count pass's e4m3 screen (PD_OPT_DENSE_SCREEN = 1, default) and the
+    bf16 hi.hi screen decide the same counts: bit-identical counts, core flags
+    and labels, and the oracle's where it runs (the e4m3 rounding bound is
+    checked here on coordinates in e4m3's subnormal range and on exact ties)."""
+    from pypardis_amd import synth
+    if case == "subnormal":
+        X, eps, ms = _subnormal_heavy(), 3e-5, 6
+    elif case == "ties":
+        g = np.arange(6, dtype=np.float32) * np.float32(0.05)
+        X = np.stack(np.meshgrid(*([g] * 6), indexing="ij"), -1).reshape(-1, 6).astype(np.float32)
+        eps, ms = float(np.float32(0.05)), 7
+    elif case == "c3_1m":
+        X, eps, ms = synth.make_config("C3", n=1_000_000)[0], 0.114028, 10
+    else:
+        c = next(c for c in DENSE if c[0] == case)
+        X, eps, ms = np.ascontiguousarray(c[1]()), c[2], c[3]
+    ctx = native.context()
+    outs = []
+    for screen in (1, 0):
+        ctx.set_option(native.PD_OPT_DENSE_SCREEN, screen)
+        try:
+            outs.append(_cluster(native, X, eps, ms, full=True))
+        finally:
+            ctx.set_option(native.PD_OPT_DENSE_SCREEN, 1)
+    (lab1, core1, ncl1, cnt1), (lab0, core0, ncl0, cnt0) = outs
+    assert np.array_equal(cnt1, cnt0)
+    assert np.array_equal(core1, core0)
+    assert np.array_equal(lab1, lab0) and ncl1 == ncl0
+    if len(X) <= 60_000:
+        lab_o, core_o, cnt_o, nc_o = oracle.dbscan(X, eps, ms)
+        assert np.array_equal(cnt1, cnt_o)
+        assert np.array_equal(lab1, lab_o) and ncl1 == nc_o
+    if case == "subnormal":
+        assert 0 < int(core1.sum()) < len(X)
+
+
 def test_dense_edge_cases(native):
     from pypardis_amd import DBSCAN
     X = np.full((300, 16), 0.25, np.float32)   # identical points

@@ -55,6 +55,7 @@ sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md; no sparsity)
+MFMA_FP8_PEAK_TFLOPS = 5000.0    # dense e4m3 (32x32x64 f8f6f4: 2x bf16 per clock)
 BASELINE_METRIC = "points clustered/sec (whole node), 100M 3-D pts, 1/2/4/8 GPUs; % HBM roofline"
 LINK_KERNELS = ("init_kernel", "flatten_kernel", "window_link_kernel", "window_uf_kernel",
                 "centre_link_kernel", "link_kernel", "link2_kernel", "cell_root_kernel",
@@ -268,32 +269,47 @@ def grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages):
     return roof, stage
 
 
-def dense_roofline(n, d, t_cnt, cells, pmc, pmc_src, refined=None):
+def dense_roofline(n, d, t_cnt, cells, pmc, pmc_src, refined=None, screen=1):
     # dense tiles (dense.hip): the count pass's Gram tiles, 2 d flops per pair
     # over the 64 x 64 wave tiles it computes (the engine reports them in
-    # cells_n; the projection window prunes the rest of the n^2 pairs); the
-    # MFMA executes the hi.hi screen on every tile (d padded to 16 ks) and the
-    # two remaining split-bf16 products on the tiles the screen keeps
-    # (grid_cells)
+    # cells_n; the projection window prunes the rest of the n^2 pairs).  The
+    # MFMA executes the screen on every tile — e4m3 32x32x64 (d padded to 64,
+    # at the fp8 rate; screen 1, the default) or bf16 hi.hi (d padded to 16
+    # ks) — and the split-bf16 product on the tiles the screen keeps
+    # (grid_cells): from scratch after the e4m3 screen (three products), the
+    # two remaining ones after the hi.hi screen.  `frac` prices the
+    # algorithmic flops at the bf16 peak (the exact product's dtype; the
+    # fp8-peak fraction is beside it); `mfma_utilisation` is the MFMA pipe
+    # time those executed flops take at their dtype's peak over the kernel time
     ks = 1 if d <= 16 else 2 if d <= 32 else 4 if d <= 64 else 8
+    ks8 = (ks + 3) // 4
     n_pad = -(-n // 64) * 64
     tiles = cells if cells > 0 else (n_pad // 64) ** 2
     refined = tiles if refined is None else refined
     alg = 2.0 * d * 64 * 64 * tiles
-    exe = 2.0 * 64 * 64 * 16 * ks * (tiles + 2 * refined)
+    if screen == 1:
+        exe8 = 2.0 * 64 * 64 * 64 * ks8 * tiles
+        exe16 = 2.0 * 64 * 64 * 16 * ks * 3 * refined
+    else:
+        exe8 = 0.0
+        exe16 = 2.0 * 64 * 64 * 16 * ks * (tiles + 2 * refined)
     if not t_cnt > 0:   # no kernel time recorded (never expected): no rate, no crash
         t_cnt = 1e30
     achieved = alg / (t_cnt * 1e-3) / 1e12
+    pipe_s = exe8 / (MFMA_FP8_PEAK_TFLOPS * 1e12) + exe16 / (MFMA_BF16_PEAK_TFLOPS * 1e12)
     roof = {"bound": "mfma", "achieved": achieved, "peak": MFMA_BF16_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": achieved / MFMA_BF16_PEAK_TFLOPS,
-            "frac_kind": "algorithmic: 2 d flops per computed pair", "traffic": None,
+            "frac_kind": "algorithmic: 2 d flops per computed pair, at the bf16 peak",
+            "frac_fp8_peak": achieved / MFMA_FP8_PEAK_TFLOPS,
+            "screen": "e4m3 32x32x64" if screen == 1 else "bf16 hi.hi",
+            "traffic": None,
             "kernel": "tile_kernel (count pass)", "kernel_ms": t_cnt,
-            "algorithmic_flops": alg, "mfma_executed_flops": exe,
+            "algorithmic_flops": alg, "mfma_executed_flops_fp8": exe8,
+            "mfma_executed_flops_bf16": exe16,
             "wave_tiles": tiles, "refined_tiles": refined,
             "tiles_all_pairs": (n_pad // 64) ** 2,
             "tile_fraction": tiles / (n_pad // 64) ** 2,
-            "mfma_executed_tflops": exe / (t_cnt * 1e-3) / 1e12,
-            "mfma_utilisation": exe / (t_cnt * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFLOPS,
+            "mfma_utilisation": pipe_s / (t_cnt * 1e-3),
             "pmc_source": pmc_src}
     k = (pmc or {}).get("tile_kernel_m0")
     if k:
@@ -483,7 +499,8 @@ def main():
             roof, stage_roof = grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages)
             dtype = f"{'f32' if Xd.dtype == torch.float32 else 'f64'} coords, f64 predicate"
         else:
-            roof = dense_roofline(n, d, t_cnt, cells, pmc, pmc_src, refined=gcells)
+            roof = dense_roofline(n, d, t_cnt, cells, pmc, pmc_src, refined=gcells,
+                                  screen=1 if args.dense_screen is None else args.dense_screen)
             dtype = "bf16 hi.hi screen, split-bf16 x3 where it keeps a pair (fp32 accumulate), f64 recheck"
         if args.config == "C2" and n == cfgd["n"]:
             metric = BASELINE_METRIC

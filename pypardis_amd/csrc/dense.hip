@@ -328,8 +328,9 @@ struct TileLds8 {
 // doubles the MFMA work per streamed byte (each staged tile feeds 2 x 4 x 3 x
 // KS MFMAs per wave) at one wave per SIMD.
 constexpr int kF8Waves = 3;   // e4m3 count pass: waves per SIMD (no bf16 query fragments held)
+constexpr int kF8QT = 2;      // e4m3 count pass: query tiles (of 32) per wave
 template <typename T, int MODE, int KS, int QT, bool F8>
-__global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu((KS >= 8 || QT > 2) ? 1 : (F8 ? kF8Waves : 2)))) void tile_kernel(TileArgs<T> A) {
+__global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu(F8 ? (KS >= 8 ? 1 : kF8Waves) : ((KS >= 8 || QT > 2) ? 1 : 2)))) void tile_kernel(TileArgs<T> A) {
     constexpr int TB = tile_threads(KS, MODE);
     constexpr int QW = 32 * QT;                  // query rows per wave
     constexpr int KS8 = (KS + 3) / 4;            // e4m3 k-steps of 64 dims
@@ -1111,8 +1112,12 @@ void run_tiles(const TileArgs<T>& A, const Geometry& G, int metric, hipStream_t 
                                        : nblocks(waves, TB / 64);
             if constexpr (MODE == kCount) {
                 if (A.I.f8 && A.J.f8) {
-                    hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT, true>), dim3(grid), dim3(TB), 0,
-                                       s, A);
+                    constexpr int QT8 = KS <= 4 ? kF8QT : 2;
+                    const unsigned grid8 =
+                        A.p3 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (TB / 64 * 32 * QT8))
+                             : nblocks((A.I.m + 32 * QT8 - 1) / (32 * QT8), TB / 64);
+                    hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true>), dim3(grid8), dim3(TB),
+                                       0, s, A);
                     return;
                 }
             }

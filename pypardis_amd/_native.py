@@ -15,7 +15,7 @@ import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpardis.so")
+LIB_PATH = os.environ.get("PYPARDIS_LIB") or os.path.join(HERE, "libpardis.so")   # (override: A/B builds)
 
 PD_F32, PD_F64 = 0, 1
 PD_EUCLIDEAN, PD_CITYBLOCK = 0, 1

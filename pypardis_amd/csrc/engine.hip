@@ -1786,7 +1786,11 @@ __device__ __forceinline__ void row_range3(const Cells& C, const Count3Grid<T, D
     const bool ok = d2 <= e2;
     float w;
     if constexpr (M == 0)
-        w = __builtin_sqrtf(fmaxf(e2 - d2, 0.0f));
+        // the raw v_sqrt_f32 (<= 1 ulp; the chord is widened by 2^-16 relative
+        // below) instead of the correctly rounded sequence (~20 instructions a
+        // row).  It may flush a denormal input to 0; the floor at sqrt(FLT_MIN)
+        // keeps w >= the true root then (a superset of the chord either way)
+        w = fmaxf(__builtin_amdgcn_sqrtf(fmaxf(e2 - d2, 0.0f)), 1.0842022e-19f);
     else
         w = fmaxf(e2 - d2, 0.0f);
     const float wc = w * g.wsc + g.wsl;
@@ -2828,11 +2832,12 @@ __global__ __launch_bounds__(kBlock) void border4_kernel(
 // keys into its 512 KB of key_out from blocks of one XCD, so the random
 // writes combine in that XCD's L2.
 constexpr int kLabBits = 17;
+constexpr int kLabBlock = 1024;   // label_bucket_kernel threads: 16 waves share one tile's histogram
 
 // (point, key) pairs in record order: pairs[r] = (owner record ? its point :
 // kNone, core: the cluster key | kKeyCoreBit; else kNone — the border sweep
 // fills in its key afterwards).  Written by owner_kernel in bucketed mode.
-__global__ __launch_bounds__(kBlock) void label_bucket_kernel(uint32_t R,
+__global__ __launch_bounds__(kLabBlock) void label_bucket_kernel(uint32_t R,
                                                               const uint2* __restrict__ recs,
                                                               uint32_t tile, int nbk,
                                                               uint32_t* __restrict__ bcnt,
@@ -2840,18 +2845,19 @@ __global__ __launch_bounds__(kBlock) void label_bucket_kernel(uint32_t R,
     extern __shared__ uint32_t lab_sh[];
     uint32_t* cnt = lab_sh;          // per bucket: pairs of this tile
     uint32_t* run = lab_sh + nbk;    // then: the next free slot
-    for (int k = threadIdx.x; k < nbk; k += kBlock) cnt[k] = 0;
+    for (int k = threadIdx.x; k < nbk; k += kLabBlock) cnt[k] = 0;
     __syncthreads();
     const uint64_t t0 = (uint64_t)blockIdx.x * tile;
     const uint64_t t1 = t0 + tile < R ? t0 + tile : R;
-    for (uint64_t r = t0 + threadIdx.x; r < t1; r += kBlock) {
+    for (uint64_t r = t0 + threadIdx.x; r < t1; r += kLabBlock) {
         const uint2 q = recs[r];
         if (q.x != kNone && q.y != kNone) atomicAdd(&cnt[q.x >> kLabBits], 1u);
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < nbk; k += kBlock) run[k] = cnt[k] ? atomicAdd(bcnt + k, cnt[k]) : 0u;
+    for (int k = threadIdx.x; k < nbk; k += kLabBlock)
+        run[k] = cnt[k] ? atomicAdd(bcnt + k, cnt[k]) : 0u;
     __syncthreads();
-    for (uint64_t r = t0 + threadIdx.x; r < t1; r += kBlock) {
+    for (uint64_t r = t0 + threadIdx.x; r < t1; r += kLabBlock) {
         const uint2 q = recs[r];
         if (q.x != kNone && q.y != kNone) {
             const uint32_t b = q.x >> kLabBits;
@@ -3545,7 +3551,7 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
             tile = std::min<uint64_t>(tile, 1ull << 20);
             tile = (tile + 1023) & ~1023ull;
             const unsigned ltiles = (unsigned)(((uint64_t)R + tile - 1) / tile);
-            hipLaunchKernelGGL(label_bucket_kernel, dim3(ltiles), dim3(kBlock),
+            hipLaunchKernelGGL(label_bucket_kernel, dim3(ltiles), dim3(kLabBlock),
                                sizeof(uint32_t) * 2 * nbk, s, R, recs, (uint32_t)tile, nbk, bcnt,
                                pairs);
             const unsigned bpb = (1u << kLabBits) / (kBlock * 8);

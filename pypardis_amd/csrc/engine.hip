@@ -1366,6 +1366,8 @@ __global__ __launch_bounds__(kBlock) void remap_kernel(uint32_t R, const uint8_t
 // ids < 2^30): the core flag rides in bit 30 of the key instead of a byte
 // scattered to core_out — the label pass writes the core mask coalesced.
 constexpr uint32_t kKeyCoreBit = 0x40000000u;
+constexpr int kOwnPer = 4;                    // owner_kernel / border_list_kernel records per thread
+constexpr uint32_t kOwnTile = kBlock * kOwnPer;
 
 __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_t* __restrict__ vals,
                                                        const uint8_t* __restrict__ core,
@@ -1378,22 +1380,30 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
                                                        uint32_t* __restrict__ cnt_out,
                                                        uint32_t* __restrict__ tile_cnt,
                                                        uint2* __restrict__ recs) {
-    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t v = r < R ? vals[r] : 0u;
-    const bool own = r < R && (v & kOwnerBit);
-    const uint8_t fl = own ? core[r] : 0;
-    if (recs && r < R)   // bucketed labels: the pair in record order, coalesced
-        recs[r] = make_uint2(own ? v & kIdMask : kNone,
-                             (fl & 1) ? gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u) : kNone);
-    if (own) {
-        const uint32_t pt = v & kIdMask;
-        if (core_out && !core_bit) core_out[pt] = fl & 1;
-        if (cnt_out) cnt_out[pt] = cnt_rec[r];
-        if ((fl & 1) && key_out) key_out[pt] = gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u);
+    // kOwnPer consecutive records per thread (a tile of kOwnTile records per
+    // block: a quarter of the workgroups of one record per thread, which
+    // dominated these light passes over C4's 1e9 records)
+    uint32_t nb = 0;
+#pragma unroll
+    for (int q = 0; q < kOwnPer; ++q) {
+        const uint32_t r = (blockIdx.x * kBlock + threadIdx.x) * kOwnPer + q;
+        const uint32_t v = r < R ? vals[r] : 0u;
+        const bool own = r < R && (v & kOwnerBit);
+        const uint8_t fl = own ? core[r] : 0;
+        if (recs && r < R)   // bucketed labels: the pair in record order, coalesced
+            recs[r] = make_uint2(own ? v & kIdMask : kNone,
+                                 (fl & 1) ? gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u) : kNone);
+        if (own) {
+            const uint32_t pt = v & kIdMask;
+            if (core_out && !core_bit) core_out[pt] = fl & 1;
+            if (cnt_out) cnt_out[pt] = cnt_rec[r];
+            if ((fl & 1) && key_out) key_out[pt] = gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u);
+        }
+        nb += own && (fl & 3) == 2 ? 1u : 0u;
     }
     // border candidates (owner record, not core, has a neighbour) per tile;
     // border_list_kernel lists them in order after a scan of the counts
-    const uint32_t c = block_sum_u32(own && (fl & 3) == 2 ? 1u : 0u);
+    const uint32_t c = block_sum_u32(nb);
     if (threadIdx.x == 0) tile_cnt[blockIdx.x] = c;
 }
 
@@ -1402,12 +1412,24 @@ __global__ __launch_bounds__(kBlock) void border_list_kernel(uint32_t R,
                                                              const uint8_t* __restrict__ core,
                                                              const uint64_t* __restrict__ tile_off,
                                                              uint32_t* __restrict__ blist) {
-    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    const bool cand = r < R && (vals[r] & kOwnerBit) && (core[r] & 3) == 2;
+    // the owner_kernel tiling: kOwnPer consecutive records per thread, so the
+    // list stays in ascending record order
+    bool cand[kOwnPer];
+    uint32_t nc = 0;
+    const uint32_t r0 = (blockIdx.x * kBlock + threadIdx.x) * kOwnPer;
+#pragma unroll
+    for (int q = 0; q < kOwnPer; ++q) {
+        const uint32_t r = r0 + q;
+        cand[q] = r < R && (vals[r] & kOwnerBit) && (core[r] & 3) == 2;
+        nc += cand[q] ? 1u : 0u;
+    }
     uint32_t btot;
-    const uint32_t off = block_excl_scan(cand ? 1u : 0u, btot);
+    uint32_t off = block_excl_scan(nc, btot);
     if (btot == 0) return;
-    if (cand) blist[tile_off[blockIdx.x] + off] = r;
+    const uint64_t base = tile_off[blockIdx.x];
+#pragma unroll
+    for (int q = 0; q < kOwnPer; ++q)
+        if (cand[q]) blist[base + off++] = r0 + q;
 }
 
 struct IsCore {
@@ -2826,49 +2848,79 @@ __global__ __launch_bounds__(kBlock) void border4_kernel(
 // owner records sit in key order, their points in input order: a permutation
 // whose direct scatter (owner_kernel: one 4-B write per record, anywhere in
 // n) moved 28 GB for C4's 1e9 records.  Here label_bucket_kernel partitions
-// the (point, key) pairs of a 64K-record tile by the point's high bits
-// (buckets of 2^kLabBits points, one global reservation per tile and
-// bucket, ~8 pairs per run), and label_scatter_kernel writes each bucket's
-// keys into its 512 KB of key_out from blocks of one XCD, so the random
-// writes combine in that XCD's L2.
-constexpr int kLabBits = 17;
-constexpr int kLabBlock = 1024;   // label_bucket_kernel threads: 16 waves share one tile's histogram
+// the (point, key) pairs of a tile by the point's high bits (buckets of
+// 2^kLabBits points): the tile is counting-sorted by bucket in LDS and each
+// bucket's run is written out by consecutive threads (whole lines, one
+// global reservation per tile and bucket, ~15 pairs per run); then
+// label_scatter_kernel writes each bucket's keys into its 4 MB of key_out
+// from blocks of one XCD, so the random writes combine in that XCD's L2.
+// (Round 3, first form: 2^17-point buckets and pairs written straight from
+// an LDS atomic slot — partial lines; C4 label_bucket 12.2 ms.)
+constexpr int kLabBlock = 1024;                 // threads per label_bucket tile
+constexpr int kLabPer = 15;                     // pairs per thread
+constexpr int kLabTile = kLabBlock * kLabPer;   // 15360 pairs (120 KiB staged)
+constexpr int kLabMaxBk = 2048;                 // buckets (2 per thread in the scan)
 
 // (point, key) pairs in record order: pairs[r] = (owner record ? its point :
 // kNone, core: the cluster key | kKeyCoreBit; else kNone — the border sweep
 // fills in its key afterwards).  Written by owner_kernel in bucketed mode.
 __global__ __launch_bounds__(kLabBlock) void label_bucket_kernel(uint32_t R,
-                                                              const uint2* __restrict__ recs,
-                                                              uint32_t tile, int nbk,
-                                                              uint32_t* __restrict__ bcnt,
-                                                              uint2* __restrict__ pairs) {
-    extern __shared__ uint32_t lab_sh[];
-    uint32_t* cnt = lab_sh;          // per bucket: pairs of this tile
-    uint32_t* run = lab_sh + nbk;    // then: the next free slot
-    for (int k = threadIdx.x; k < nbk; k += kLabBlock) cnt[k] = 0;
+                                                                 const uint2* __restrict__ recs,
+                                                                 int kLabBits, int nbk,
+                                                                 uint32_t* __restrict__ bcnt,
+                                                                 uint2* __restrict__ pairs) {
+    __shared__ uint2 stage[kLabTile];
+    __shared__ uint32_t cnt[kLabMaxBk], off[kLabMaxBk], gbase[kLabMaxBk];
+    const int tid = threadIdx.x;
+    for (int k = tid; k < kLabMaxBk; k += kLabBlock) cnt[k] = 0;
     __syncthreads();
-    const uint64_t t0 = (uint64_t)blockIdx.x * tile;
-    const uint64_t t1 = t0 + tile < R ? t0 + tile : R;
-    for (uint64_t r = t0 + threadIdx.x; r < t1; r += kLabBlock) {
-        const uint2 q = recs[r];
-        if (q.x != kNone && q.y != kNone) atomicAdd(&cnt[q.x >> kLabBits], 1u);
+    const uint64_t t0 = (uint64_t)blockIdx.x * kLabTile;
+    uint2 q[kLabPer];
+    uint32_t lr[kLabPer];
+#pragma unroll
+    for (int i = 0; i < kLabPer; ++i) {
+        const uint64_t r = t0 + (uint64_t)i * kLabBlock + tid;
+        q[i] = make_uint2(kNone, kNone);
+        if (r < R) {   // streamed once: non-temporal
+            const unsigned long long w =
+                __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(recs + r));
+            q[i] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < kLabPer; ++i) {
+        const bool ok = q[i].x != kNone && q[i].y != kNone;
+        lr[i] = ok ? atomicAdd(&cnt[q[i].x >> kLabBits], 1u) : 0u;
+        if (!ok) q[i].x = kNone;
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < nbk; k += kLabBlock)
-        run[k] = cnt[k] ? atomicAdd(bcnt + k, cnt[k]) : 0u;
+    uint32_t total;
+    const int k0 = 2 * tid, k1 = 2 * tid + 1;   // two buckets per thread
+    const uint32_t c0 = k0 < nbk ? cnt[k0] : 0u, c1 = k1 < nbk ? cnt[k1] : 0u;
+    const uint32_t ex = block_excl_scan<kLabBlock>(c0 + c1, total);
+    if (k0 < nbk) {
+        off[k0] = ex;
+        gbase[k0] = c0 ? atomicAdd(bcnt + k0, c0) : 0u;
+    }
+    if (k1 < nbk) {
+        off[k1] = ex + c0;
+        gbase[k1] = c1 ? atomicAdd(bcnt + k1, c1) : 0u;
+    }
     __syncthreads();
-    for (uint64_t r = t0 + threadIdx.x; r < t1; r += kLabBlock) {
-        const uint2 q = recs[r];
-        if (q.x != kNone && q.y != kNone) {
-            const uint32_t b = q.x >> kLabBits;
-            pairs[((uint64_t)b << kLabBits) + atomicAdd(&run[b], 1u)] = q;
-        }
+#pragma unroll
+    for (int i = 0; i < kLabPer; ++i)
+        if (q[i].x != kNone) stage[off[q[i].x >> kLabBits] + lr[i]] = q[i];
+    __syncthreads();
+    for (uint32_t p = tid; p < total; p += kLabBlock) {
+        const uint2 v = stage[p];
+        const uint32_t b = v.x >> kLabBits;
+        pairs[((uint64_t)b << kLabBits) + gbase[b] + (p - off[b])] = v;
     }
 }
 
 __global__ __launch_bounds__(kBlock) void label_scatter_kernel(const uint2* __restrict__ pairs,
                                                                const uint32_t* __restrict__ bcnt,
-                                                               int nbk, unsigned bpb,
+                                                               int kLabBits, int nbk, unsigned bpb,
                                                                uint32_t* __restrict__ key_out) {
     const unsigned lb = xcd_block(blockIdx.x, gridDim.x);   // a bucket's blocks share an XCD
     const unsigned b = lb / bpb, part = lb % bpb;
@@ -2876,8 +2928,10 @@ __global__ __launch_bounds__(kBlock) void label_scatter_kernel(const uint2* __re
     const uint32_t c = bcnt[b];
     const uint2* p = pairs + ((uint64_t)b << kLabBits);
     for (uint32_t k = part * kBlock + threadIdx.x; k < c; k += bpb * kBlock) {
-        const uint2 q = p[k];
-        key_out[q.x] = q.y;
+        // streamed: non-temporal, the L2 is kept for key_out
+        const unsigned long long w =
+            __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p + k));
+        key_out[(uint32_t)w] = (uint32_t)(w >> 32);
     }
 }
 
@@ -3525,7 +3579,7 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
                           (ctx.variant & 16) && !st.wroot && n > 0;
     if (R) {
         uint32_t* blist = ctx.arena.get<uint32_t>("border_list", R);
-        const unsigned tiles = blocks(R);
+        const unsigned tiles = (unsigned)(((uint64_t)R + kOwnTile - 1) / kOwnTile);
         uint32_t* tcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)tiles + 1);
         uint64_t* toff = ctx.arena.get<uint64_t>("tile_off", (size_t)tiles + 1);
         // bucketed: owner_kernel writes the (point, key) pairs in record order
@@ -3542,21 +3596,21 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
             launch_border<T, D, M>(ctx.variant, s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par,
                                    gmin, st.wroot, key_out, recs ? (uint32_t*)recs + 1 : nullptr);
         if (bucketed) {
+            // buckets of 2^19 points: a bucket's 2 MB of key_out stays in one
+            // XCD's 4 MB L2 (C4 border: 2^20 29.2, 2^19 27.9, 2^18 29.5 ms)
+            int kLabBits = 19;
+            while (((n + (1ull << kLabBits) - 1) >> kLabBits) > (uint64_t)kLabMaxBk) ++kLabBits;
             const int nbk = (int)((n + (1ull << kLabBits) - 1) >> kLabBits);
+            if (nbk > kLabMaxBk) throw Error(-5, "label buckets: too many points");
             uint32_t* bcnt = ctx.arena.get<uint32_t>("lab_bcnt", (size_t)nbk);
             uint2* pairs = ctx.arena.get<uint2>("lab_pairs", (size_t)nbk << kLabBits);
             PD_HIP(hipMemsetAsync(bcnt, 0, sizeof(uint32_t) * nbk, s));
-            // ~16 pairs per bucket and tile (128-B runs), >= 4096 records a tile
-            uint64_t tile = std::max<uint64_t>(4096, 16ull * (uint64_t)nbk);
-            tile = std::min<uint64_t>(tile, 1ull << 20);
-            tile = (tile + 1023) & ~1023ull;
-            const unsigned ltiles = (unsigned)(((uint64_t)R + tile - 1) / tile);
-            hipLaunchKernelGGL(label_bucket_kernel, dim3(ltiles), dim3(kLabBlock),
-                               sizeof(uint32_t) * 2 * nbk, s, R, recs, (uint32_t)tile, nbk, bcnt,
-                               pairs);
+            const unsigned ltiles = (unsigned)(((uint64_t)R + kLabTile - 1) / kLabTile);
+            hipLaunchKernelGGL(label_bucket_kernel, dim3(ltiles), dim3(kLabBlock), 0, s, R, recs,
+                               kLabBits, nbk, bcnt, pairs);
             const unsigned bpb = (1u << kLabBits) / (kBlock * 8);
             hipLaunchKernelGGL(label_scatter_kernel, dim3((unsigned)nbk * bpb), dim3(kBlock), 0, s,
-                               pairs, bcnt, nbk, bpb, key_out);
+                               pairs, bcnt, kLabBits, nbk, bpb, key_out);
         }
     }
     PD_HIP(hipGetLastError());

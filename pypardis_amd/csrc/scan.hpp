@@ -6,10 +6,11 @@
 
 namespace pd {
 
-// Block-wide exclusive scan of one u32 per thread (kBlock threads); returns
+// Block-wide exclusive scan of one u32 per thread (NT threads); returns
 // the thread's exclusive prefix within the block and the block total.
+template <int NT = kBlock>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t& total) {
-    __shared__ uint32_t wsum[kBlock / 64];
+    __shared__ uint32_t wsum[NT / 64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t x = v;
 #pragma unroll
@@ -21,7 +22,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t& total)
     __syncthreads();
     uint32_t before = 0, tot = 0;
 #pragma unroll
-    for (int u = 0; u < kBlock / 64; ++u) {
+    for (int u = 0; u < NT / 64; ++u) {
         before += u < w ? wsum[u] : 0u;
         tot += wsum[u];
     }

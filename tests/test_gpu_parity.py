@@ -1057,7 +1057,7 @@ def test_train_many_partitions_fallbacks(native, P):
 def test_label_buckets_equal_direct_scatter(native, cfg, n):
     """PD_OPT_LABEL_BUCKETS (default on): the labels reach input order through
     the bucketed (point, key) pair passes instead of one scattered write per
-    owner record — identical labels and core flags, several buckets of 2^17
+    owner record — identical labels and core flags, several buckets of 2^20
     points, partial last bucket, noise and border points included."""
     from pypardis_amd import DBSCAN, synth
     X, c = synth.make_config(cfg, n=n, device="cuda" if cfg == "C4" else "cpu")

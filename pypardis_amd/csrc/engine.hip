@@ -1098,23 +1098,29 @@ done:
 // The count pass keeps the two smallest neighbours it saw (mn2[r]): the
 // parent is the smaller of them that is core and below r — two candidates
 // leave about half the trees of one (tools/init_forest_study.py).
+constexpr int kSubTiles = 4;   // init_kernel / roots_kernel: record tiles per block
 __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t R, const uint8_t* __restrict__ core,
                                                       const uint32_t* __restrict__ mn,
                                                       int use_mn, uint32_t* __restrict__ par) {
-    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R) return;
-    uint32_t p = kNone;
-    if (core[r] & 1) {
-        p = r;
-        if (use_mn) {
-            const uint2 m = reinterpret_cast<const uint2*>(mn)[r];
-            if (m.x < r && (core[m.x] & 1))
-                p = m.x;
-            else if (m.y < r && (core[m.y] & 1))
-                p = m.y;
+    // kSubTiles record tiles of kBlock per block (fewer workgroups for the
+    // light per-record passes over 1e9 records)
+#pragma unroll
+    for (int q = 0; q < kSubTiles; ++q) {
+        const uint32_t r = (blockIdx.x * kSubTiles + q) * kBlock + threadIdx.x;
+        if (r >= R) return;
+        uint32_t p = kNone;
+        if (core[r] & 1) {
+            p = r;
+            if (use_mn) {
+                const uint2 m = reinterpret_cast<const uint2*>(mn)[r];
+                if (m.x < r && (core[m.x] & 1))
+                    p = m.x;
+                else if (m.y < r && (core[m.y] & 1))
+                    p = m.y;
+            }
         }
+        par[r] = p;
     }
-    par[r] = p;
 }
 
 // Core-core edges (j > r only; the predicate is symmetric) → union-find.
@@ -1251,27 +1257,31 @@ __global__ __launch_bounds__(kBlock) void roots_kernel(uint32_t R, const uint32_
                                                        uint32_t* __restrict__ gmin,
                                                        uint32_t* __restrict__ root_list,
                                                        uint32_t* __restrict__ counts, int stats) {
-    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t x0 = r < R ? par[r] : kNone;
-    const bool core = x0 != kNone;
-    uint32_t root = 0;
-    if (core) {
-        uint32_t x = x0;
-        while (true) {
-            const uint32_t p = par[x];
-            if (p == x) break;
-            x = p;
+    uint32_t ncore = 0;
+    for (int q = 0; q < kSubTiles; ++q) {   // kSubTiles record tiles of kBlock per block
+        const uint32_t r = (blockIdx.x * kSubTiles + q) * kBlock + threadIdx.x;
+        const uint32_t x0 = r < R ? par[r] : kNone;
+        const bool core = x0 != kNone;
+        uint32_t root = 0;
+        if (core) {
+            uint32_t x = x0;
+            while (true) {
+                const uint32_t p = par[x];
+                if (p == x) break;
+                x = p;
+            }
+            if (x != x0) par[r] = x;
+            root = x;
         }
-        if (x != x0) par[r] = x;
-        root = x;
+        uint32_t pt = core ? (vals[r] & kIdMask) : kNone;
+        if (core && gid) pt = gid[pt];
+        wave_atomic_min(gmin, core, root, pt);
+        // roots are rare (one per component): a wave-aggregated append is cheap
+        if (root_list) wave_append(root_list, counts, core && root == r, r);
+        ncore += core ? 1u : 0u;
     }
-    uint32_t pt = core ? (vals[r] & kIdMask) : kNone;
-    if (core && gid) pt = gid[pt];
-    wave_atomic_min(gmin, core, root, pt);
-    // roots are rare (one per component): a wave-aggregated append is cheap
-    if (root_list) wave_append(root_list, counts, core && root == r, r);
     if (stats) {   // core records (sweep statistics): one atomic per block
-        const uint32_t c = block_sum_u32(core ? 1u : 0u);
+        const uint32_t c = block_sum_u32(ncore);
         if (threadIdx.x == 0 && c) atomicAdd(counts + 1, c);
     }
 }
@@ -2996,6 +3006,10 @@ struct EvTimer {
 };
 
 inline unsigned blocks(uint64_t n) { return n ? (unsigned)((n + kBlock - 1) / kBlock) : 1u; }
+// blocks of kSubTiles record tiles (init_kernel, roots_kernel)
+inline unsigned sub_blocks(uint64_t n) {
+    return n ? (unsigned)((n + (uint64_t)kBlock * kSubTiles - 1) / ((uint64_t)kBlock * kSubTiles)) : 1u;
+}
 
 // Exclusive scan of `tiles` per-tile counts into u64 offsets (off[tiles] =
 // total); with `read_total` the total is copied back (syncs) and returned.
@@ -3321,7 +3335,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     uint32_t* par = ctx.arena.get<uint32_t>("parent", R);
     if (R && (mode == 3 || mode == 4 || mode == 5 || mode == 6)) {
         // forest from the count pass's smallest neighbour (links across rows)
-        hipLaunchKernelGGL(init_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, mn, 1, par);
+        hipLaunchKernelGGL(init_kernel, dim3(sub_blocks(R)), dim3(kBlock), 0, s, R, core, mn, 1, par);
         if (mode != 6)
             hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
         if (mode == 6) {
@@ -3425,7 +3439,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         hipLaunchKernelGGL((pair_kernel<T, D, M>), dim3(std::min(blocks(pcap), 4096u)), dim3(kBlock), 0, s, Xs, plist,
                            pcount, pcap, cstart, croot, eps, eps2, slo, shi, par);
     } else if (R) {
-        hipLaunchKernelGGL(init_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, mn,
+        hipLaunchKernelGGL(init_kernel, dim3(sub_blocks(R)), dim3(kBlock), 0, s, R, core, mn,
                            mode == 0 ? 1 : 0, par);
         {
             if (mode == 0)
@@ -3463,7 +3477,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         // ranked here (labels); sharded: keys stay global ids (merge first)
         uint32_t* root_list = a.phase == 0 ? ctx.arena.get<uint32_t>("root_list", R) : nullptr;
         PD_HIP(hipMemsetAsync(gmin, 0xFF, sizeof(uint32_t) * R, s));
-        hipLaunchKernelGGL(roots_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, vals, a.gid, par,
+        hipLaunchKernelGGL(roots_kernel, dim3(sub_blocks(R)), dim3(kBlock), 0, s, R, vals, a.gid, par,
                            gmin, root_list, lcount + 1, ctx.sweep_stats ? 1 : 0);
         uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t) * 4);
         PD_HIP(hipMemcpyAsync(h, lcount + 1, sizeof(uint32_t) * 2, hipMemcpyDeviceToHost, s));

@@ -1384,6 +1384,7 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
                                                        const uint32_t* __restrict__ par,
                                                        const uint32_t* __restrict__ gmin,
                                                        const uint32_t* __restrict__ cnt_rec,
+                                                       const uint2* __restrict__ mn,
                                                        int core_bit,
                                                        uint32_t* __restrict__ key_out,
                                                        uint8_t* __restrict__ core_out,
@@ -1400,16 +1401,28 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
         const uint32_t v = r < R ? vals[r] : 0u;
         const bool own = r < R && (v & kOwnerBit);
         const uint8_t fl = own ? core[r] : 0;
+        // the record's key: core -> its component's; a border record with a
+        // single neighbour (bit 2) -> that neighbour's if it is core (the
+        // border sweep's smallest core key, over one candidate); else none
+        uint32_t key = kNone;
+        if (fl & 1) {
+            key = gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u);
+        } else if ((fl & 7) == 6 && mn) {
+            const uint2 m = mn[r];
+            const uint32_t j = m.x == r ? m.y : m.x;
+            const uint32_t pj = par[j];
+            key = pj != kNone ? gmin[pj] : kNone;
+        }
         if (recs && r < R)   // bucketed labels: the pair in record order, coalesced
-            recs[r] = make_uint2(own ? v & kIdMask : kNone,
-                                 (fl & 1) ? gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u) : kNone);
+            recs[r] = make_uint2(own ? v & kIdMask : kNone, key);
         if (own) {
             const uint32_t pt = v & kIdMask;
             if (core_out && !core_bit) core_out[pt] = fl & 1;
             if (cnt_out) cnt_out[pt] = cnt_rec[r];
-            if ((fl & 1) && key_out) key_out[pt] = gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u);
+            if (key != kNone && key_out) key_out[pt] = key;
         }
-        nb += own && (fl & 3) == 2 ? 1u : 0u;
+        // the rest of the border candidates go to the sweep
+        nb += own && (fl & 3) == 2 && !((fl & 4) && mn) ? 1u : 0u;
     }
     // border candidates (owner record, not core, has a neighbour) per tile;
     // border_list_kernel lists them in order after a scan of the counts
@@ -1420,6 +1433,7 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
 __global__ __launch_bounds__(kBlock) void border_list_kernel(uint32_t R,
                                                              const uint32_t* __restrict__ vals,
                                                              const uint8_t* __restrict__ core,
+                                                             int single_done,
                                                              const uint64_t* __restrict__ tile_off,
                                                              uint32_t* __restrict__ blist) {
     // the owner_kernel tiling: kOwnPer consecutive records per thread, so the
@@ -1430,7 +1444,8 @@ __global__ __launch_bounds__(kBlock) void border_list_kernel(uint32_t R,
 #pragma unroll
     for (int q = 0; q < kOwnPer; ++q) {
         const uint32_t r = r0 + q;
-        cand[q] = r < R && (vals[r] & kOwnerBit) && (core[r] & 3) == 2;
+        const uint8_t fl = r < R ? core[r] : 0;
+        cand[q] = r < R && (vals[r] & kOwnerBit) && (fl & 3) == 2 && !(single_done && (fl & 4));
         nc += cand[q] ? 1u : 0u;
     }
     uint32_t btot;
@@ -1914,7 +1929,10 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
             if (stopped) return;
         }
     });
-    core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
+    // bit 2: exactly one neighbour besides the record itself (no early exit
+    // below min_samples, so the sweep saw it, and it is the other of the two
+    // smallest hits): owner_kernel attaches such a border record directly
+    core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0) | (cnt == 2 ? 4 : 0);
     reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, mn2);
     if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
     if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
@@ -3538,6 +3556,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     st.par = par;
     st.gmin = gmin;
     st.cnt_rec = cnt_rec;
+    st.mn = mn;
     st.wroot = wroot_final;
     st.n_exports = 0;
     if (a.phase == 1 && R && a.xr) {
@@ -3599,13 +3618,19 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         // bucketed: owner_kernel writes the (point, key) pairs in record order
         // instead of scattering key_out; the border sweep fills in its keys
         uint2* recs = bucketed ? ctx.arena.get<uint2>("lab_recs", R) : nullptr;
+        // count4 (variant bit 3) flags records with exactly one neighbour
+        // besides themselves (core bit 2): owner_kernel attaches those border
+        // records from the count pass's two smallest hits, the sweep takes
+        // the rest
+        const bool single = (ctx.variant & 8) && st.mn;
         hipLaunchKernelGGL(owner_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core, par, gmin,
-                           st.cnt_rec, core_bit, bucketed ? nullptr : key_out, a.core, a.counts,
+                           st.cnt_rec, single ? (const uint2*)st.mn : nullptr, core_bit,
+                           bucketed ? nullptr : key_out, a.core, a.counts,
                            tcnt, recs);
         const uint32_t NB = (uint32_t)tile_offsets(ctx, tcnt, tiles, toff, s, true);
         if (NB)
             hipLaunchKernelGGL(border_list_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core,
-                               toff, blist);
+                               single ? 1 : 0, toff, blist);
         if (NB)
             launch_border<T, D, M>(ctx.variant, s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par,
                                    gmin, st.wroot, key_out, recs ? (uint32_t*)recs + 1 : nullptr);

@@ -80,6 +80,7 @@ struct PhaseState {
     uint32_t* par = nullptr;
     uint32_t* gmin = nullptr;
     uint32_t* cnt_rec = nullptr;
+    uint32_t* mn = nullptr;      // per record: the two smallest neighbours the count sweep saw
     uint32_t* wroot = nullptr;   // directory-word roots of the final forest (border fast path)
     uint32_t* exp_gid = nullptr;
     uint32_t* exp_key = nullptr;

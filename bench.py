@@ -11,6 +11,11 @@
   python bench.py [--gpus N --steps K --warmup W] [--config C2|C1|C3|C4]
                   [--points N] [--no-cpu] [--no-host]
 
+`python bench.py --gpus N` (N > 1) outside a torchrun environment starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py <same args>`
+as a CHILD process (this process never imports torch or touches a GPU, and
+never execs) and exits with its status; rank 0's JSON line is the line.
+
 For N > 1 (torch.distributed.run, one rank per GPU) the same points are split
 by index over the ranks and each rank calls DBSCAN(...).train(its slice) in
 the process group: the sharded train over RCCL through libpardis's pd_comm_*
@@ -356,9 +361,36 @@ def host_legs(DBSCAN, eps, ms, P, Xh):
     return out
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """One process per GPU for `--gpus n` without torchrun around us: the
+    rank processes come from torch.distributed.run started as a child (no
+    exec; this process has not imported torch), each with WORLD_SIZE / RANK /
+    LOCAL_RANK set, so they run main()'s rank path.  Returns the child's exit
+    status (rank 0 prints the JSON line to the stdout we share)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"[bench] launching {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env, cwd=HERE)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in os.environ and args.gpus not in (1, world):
+        print(f"[bench] --gpus {args.gpus} inside a torchrun job of {world} ranks: "
+              f"the job's {world} ranks are measured", file=sys.stderr, flush=True)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -381,6 +413,10 @@ def main():
 
     if args.rehearse:
         local_rank = 0
+    if world > 1 and local_rank >= torch.cuda.device_count():
+        raise SystemExit(f"[bench] rank {rank}: local rank {local_rank} but "
+                         f"{torch.cuda.device_count()} GPU(s) visible (--rehearse runs every "
+                         f"rank on cuda:0 over gloo)")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
@@ -477,6 +513,21 @@ def main():
     value = n * args.steps / el
     ncl = m.n_clusters_
     shard_stats = m.shard.stats if m.shard is not None else None
+    rccl_ranks = None
+    if world > 1:
+        # the slowest rank's per-phase times, and the rank count RCCL itself
+        # reports for the communicator the train ran on (0: gloo rehearsal)
+        allst = [None] * world
+        dist.all_gather_object(allst, (el, shard_stats))
+        slow = max(range(world), key=lambda r: allst[r][0])
+        shard_stats = dict(allst[slow][1] or {}, rank=slow,
+                           rank_seconds=[round(a[0], 4) for a in allst])
+        if not args.rehearse:
+            from pypardis_amd import distributed
+            comm = distributed.make_comm(dist.group.WORLD, dev)
+            rccl_ranks = comm.comm.size()[0] if hasattr(comm, "comm") else 0
+        else:
+            rccl_ranks = 0
     del m
 
     host = None
@@ -501,7 +552,9 @@ def main():
         else:
             roof = dense_roofline(n, d, t_cnt, cells, pmc, pmc_src, refined=gcells,
                                   screen=1 if args.dense_screen is None else args.dense_screen)
-            dtype = "bf16 hi.hi screen, split-bf16 x3 where it keeps a pair (fp32 accumulate), f64 recheck"
+            dtype = ("e4m3 screen (32x32x64 f8f6f4)" if args.dense_screen in (None, 1)
+                     else "bf16 hi.hi screen") + \
+                ", split-bf16 x3 where it keeps a pair (fp32 accumulate), f64 recheck"
         if args.config == "C2" and n == cfgd["n"]:
             metric = BASELINE_METRIC
         else:
@@ -513,6 +566,7 @@ def main():
             "value": value,
             "unit": "points/s",
             "n_gpus": world,
+            "rccl_ranks": rccl_ranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_step,
@@ -526,7 +580,9 @@ def main():
                        "n_points": n, "d": d, "eps": eps, "min_samples": ms,
                        "max_partitions": P,
                        "input": f"{str(Xd.dtype).replace('torch.', '')} device-resident",
-                       "parallelism": f"kd-sharded{world}" if world > 1 else "single"},
+                       "parallelism": f"kd-sharded{world}" if world > 1 else "single",
+                       "transport": (("gloo rehearsal, every rank on cuda:0" if args.rehearse
+                                      else "RCCL (pd_comm)") if world > 1 else None)},
             "roofline": roof,
             "stage_roofline": stage_roof,
             "cpu_baseline": cpu,

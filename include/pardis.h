@@ -145,6 +145,8 @@ enum pd_timing_slot {
                                   (PD_T_COUNT includes its projection sorts) */
     PD_T_DIR_PAGED,            /* 1 if the last grid train used the paged directory */
     PD_T_DIR_WORDS,            /* directory words it allocated (paged: occupied + 1) */
+    PD_T_S_COUNT_BATCHES,      /* count sweep (PD_OPT_SWEEP_STATS): wave batches swept */
+    PD_T_S_COUNT_STAGED,       /*   of which read their candidates from LDS (bit 5) */
     PD_T_NSLOTS
 };
 
@@ -492,6 +494,10 @@ int32_t pd_comm_all_to_all_v(pd_comm* comm, const void* send, const int64_t* sen
                              void* stream);
 int32_t pd_comm_broadcast(pd_comm* comm, void* buf, int64_t count, int32_t elem, int32_t root,
                           void* stream);
+/* ncclCommCount / ncclCommUserRank: the rank count and this rank as RCCL
+ * reports them (the executor count of the reference's fan-out,
+ * R:dbscan/dbscan.py:116-126; bench.py's rccl_ranks). */
+int32_t pd_comm_size(pd_comm* comm, int32_t* n_ranks, int32_t* rank);
 /* n_fields buffers exchanged in ONE group (the halo-record fields of the
  * partitionBy shuffle): block r of field f = rec_bytes[f] * counts[r] bytes at
  * rec_bytes[f] * offsets[r] (send grouped by destination, recv by source;

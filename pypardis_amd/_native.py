@@ -38,7 +38,7 @@ TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "ro
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
                 "s_count_cand", "s_link_cand", "s_link_hit", "s_link_core", "s_link_same",
                 "s_link_find_same", "s_link_unions", "s_verify_pairs", "grid_grow",
-                "count_kernel", "dir_paged", "dir_words"]
+                "count_kernel", "dir_paged", "dir_words", "s_count_batches", "s_count_staged"]
 
 # every symbol include/pardis.h declares (tests/test_abi.py checks the .so)
 EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
@@ -53,7 +53,7 @@ EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
            "pd_dense_finish", "pd_kd_build", "pd_train_tree", "pd_kdx_begin", "pd_kdx_moments",
            "pd_kdx_axes", "pd_kdx_counts", "pd_kdx_boundary", "pd_kdx_end", "pd_route2",
            "pd_pack2", "pd_results", "pd_results_scatter", "pd_comm_exchange", "pd_comm_abort",
-           "pd_comm_self_check"]
+           "pd_comm_self_check", "pd_comm_size"]
 
 
 class PardisError(RuntimeError):
@@ -141,6 +141,7 @@ def load():
             "pd_comm_exchange": ([P, I32, P, P, P, P, P, P, P, I32, P], I32),
             "pd_comm_abort": ([P], I32),
             "pd_comm_self_check": ([P], I32),
+            "pd_comm_size": ([P, P, P], I32),
         }
         for name, (args, res) in sig.items():
             f = getattr(lib, name)
@@ -934,3 +935,9 @@ class Comm:
         _check(load().pd_comm_broadcast(self.ptr, t.data_ptr(), t.numel(), self._elem(t),
                                         int(root), _stream(self.device)))
         return t
+
+    def size(self):
+        """(n_ranks, rank) as RCCL reports them (ncclCommCount / ncclCommUserRank)."""
+        n, r = ctypes.c_int32(0), ctypes.c_int32(-1)
+        _check(load().pd_comm_size(self.ptr, ctypes.byref(n), ctypes.byref(r)))
+        return int(n.value), int(r.value)

@@ -193,7 +193,8 @@ int32_t pd_ctx_timings(pd_ctx* ctx, double* out, int32_t n) {
                                        (double)t.sweep[4], (double)t.sweep[5],
                                        (double)t.sweep[6], (double)t.sweep[7], t.grid_grow,
                                        (double)t.count_kernel, (double)t.dir_paged,
-                                       (double)t.dir_words};
+                                       (double)t.dir_words, (double)t.sweep[8],
+                                       (double)t.sweep[9]};
         for (int i = 0; i < n && i < PD_T_NSLOTS; ++i) out[i] = v[i];
     });
 }
@@ -830,6 +831,16 @@ int32_t pd_comm_abort(pd_comm* comm) {
 
 int32_t pd_comm_self_check(pd_comm* comm) {
     return comm_guard(comm, [&] { comm_self_check(&comm->c, 1); });
+}
+
+int32_t pd_comm_size(pd_comm* comm, int32_t* n_ranks, int32_t* rank) {
+    return comm_guard(comm, [&] {
+        if (!n_ranks || !rank) throw Error(PD_EINVAL, "null argument");
+        int n = 0, r = 0;
+        comm_size(comm->c, &n, &r);
+        *n_ranks = n;
+        *rank = r;
+    });
 }
 
 int32_t pd_comm_broadcast(pd_comm* comm, void* buf, int64_t count, int32_t elem, int32_t root,

@@ -134,6 +134,17 @@ void comm_destroy(Comm* c) {
 
 int comm_device(const Comm* c) { return c->device; }
 
+// Rank count and this rank as RCCL itself reports them (not the values the
+// communicator was created with): the bench line's rccl_ranks.
+void comm_size(const Comm* c, int* n_ranks, int* rank) {
+    if (!c->nc) throw Error(-4, "communicator was aborted");
+    int n = 0, r = -1;
+    check(ncclCommCount(c->nc, &n), "ncclCommCount");
+    check(ncclCommUserRank(c->nc, &r), "ncclCommUserRank");
+    *n_ranks = n;
+    *rank = r;
+}
+
 void comm_all_reduce(Comm* c, const void* send, void* recv, int64_t count, int elem, int op,
                      hipStream_t s) {
     if (count <= 0) return;
@@ -355,13 +366,38 @@ void comm_self_check(Comm* const* comms, int n) {
                                comms[i]->rank, b[i].bad);
             PD_HIP(hipGetLastError());
         }
+        // every rank learns every rank's verdict (max of the flags), so a
+        // check that fails on some ranks fails on all of them: none returns a
+        // communicator its peers have destroyed
+        std::vector<uint32_t> local(n, 0), any(n, 0);
         for (int i = 0; i < n; ++i) {
             PD_HIP(hipSetDevice(comms[i]->device));
-            uint32_t hb = 0;
-            PD_HIP(hipMemcpyAsync(&hb, b[i].bad, sizeof(uint32_t), hipMemcpyDeviceToHost, b[i].s));
+            PD_HIP(hipMemcpyAsync(&local[i], b[i].bad, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                  b[i].s));
+        }
+        if (W > 1) {
+            check(ncclGroupStart(), "ncclGroupStart");
+            for (int i = 0; i < n; ++i) {
+                PD_HIP(hipSetDevice(comms[i]->device));
+                check(ncclAllReduce(b[i].bad, b[i].bad, 1, ncclUint32, ncclMax, comms[i]->nc,
+                                    b[i].s),
+                      "ncclAllReduce");
+            }
+            check(ncclGroupEnd(), "ncclGroupEnd");
+        }
+        for (int i = 0; i < n; ++i) {
+            PD_HIP(hipSetDevice(comms[i]->device));
+            PD_HIP(hipMemcpyAsync(&any[i], b[i].bad, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                  b[i].s));
             PD_HIP(hipStreamSynchronize(b[i].s));
+        }
+        for (int i = 0; i < n; ++i) {
+            const uint32_t hb = local[i] ? local[i] : any[i];
             if (hb)
-                throw Error(-4, "RCCL self check failed on rank " + std::to_string(comms[i]->rank) +
+                throw Error(-4, std::string("RCCL self check failed ") +
+                                    (local[i] ? "on rank " + std::to_string(comms[i]->rank)
+                                              : "on another rank (seen from rank " +
+                                                    std::to_string(comms[i]->rank) + ")") +
                                     " of " + std::to_string(W) + ((hb & 1) ? ": all_to_all_v" : "") +
                                     ((hb & 2) ? ": all_gather_v" : "") +
                                     " delivered wrong data (PD_COMM_SELF_CHECK=0 skips this check)");

@@ -1938,6 +1938,220 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
     if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
 }
 
+// ------------------------------------------------------------------ staged count
+// count5_kernel (PD_OPT_SWEEP_VARIANT bit 5, the default for fp32 2-D / 3-D /
+// 4-D): count4_kernel with each batch's candidates read from LDS.  PMC of
+// count4 (C2): 89 vector-memory instructions per 64-record wave, ~65 of them
+// candidate gathers, the texture addresser busy ~0.73 of the kernel and the
+// VALU ~0.44 of its issue rate: the sweep is bound by the vector-memory path
+// (addresses and round-trip latency), not by DRAM.  A wave's 64 records are
+// cell-sorted (~28 cells of one grid row for C2), so each row slot of a
+// batch covers one short, contiguous record window for the whole wave — the
+// union of the lanes' chord ranges, ~75 records per row.  When the three
+// windows of a batch fit the wave's LDS slice (kStageRecs records), the wave
+// copies them with coalesced 16-B loads (a few instructions for ~220
+// records) and every lane sweeps its own ranges out of LDS; otherwise (a wave
+// spanning grid rows, dense cells, a wave spanning neighbourhoods) it sweeps
+// from global memory exactly as count4.  Candidate order, early exit and
+// outputs are count4's (a batch staged or not visits the same positions in
+// the same order), so counts, core flags and the two smallest hits are
+// identical (`test_sweep_variants_exact`).
+extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
+extern "C" __device__ uint32_t __ockl_wfred_max_u32(uint32_t);
+
+// Order this wave's LDS writes before its lanes' reads of other lanes' data
+// (one wave: no workgroup barrier; waves of a block run different batch counts).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int kStageBytes = 5120;   // per wave: 320 3-D records (20 KiB per block)
+
+template <int S>
+struct StageVec {
+    using type = typename std::conditional<S == 4, float4, float2>::type;
+};
+
+template <typename T, int D, int M, bool ST>
+__global__ __launch_bounds__(kBlock) void count5_kernel(const T* __restrict__ Xs, uint32_t R,
+                                                        Cells C, double eps, double eps2,
+                                                        float lo, float hi, uint32_t ms, int full,
+                                                        uint32_t rot_min,
+                                                        uint8_t* __restrict__ core,
+                                                        uint32_t* __restrict__ mn_out,
+                                                        uint32_t* __restrict__ cnt_out,
+                                                        unsigned long long* __restrict__ stats) {
+    static_assert(std::is_same<T, float>::value, "fp32 records only");
+    constexpr int NR = NRows<D>::v;
+    constexpr int B = NR < 3 ? NR : 3, NB = NR / B;
+    constexpr int S = Stride<D>::v;
+    static_assert(S == 2 || S == 4, "2-D, 3-D or 4-D records");
+    using V = typename StageVec<S>::type;
+    constexpr uint32_t CAP = kStageBytes / sizeof(V);
+    __shared__ V stage[kBlock / 64][CAP];
+    if (R == 0) return;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t r0 = rec_index();
+    const bool live = r0 < R;
+    // no lane leaves early: the window reductions below need the whole wave
+    // (a tail lane mirrors the last record and is done from the start)
+    const uint32_t r = live ? r0 : R - 1;
+    double a[D];
+    load_rec<T, D>(Xs, r, a);
+    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
+    const uint32_t stop = full ? 0xFFFFFFFFu : ms;
+    float e2 = M == 0 ? (float)eps2 : (float)eps;
+    e2 = e2 * (1.0f + 1.0f / 65536.0f);
+    uint32_t cnt = 0, mn = kNone, mn2 = kNone, n_cand = 0, n_staged = 0, n_batches = 0;
+    bool done = !live;
+    const V* __restrict__ Xv = reinterpret_cast<const V*>(Xs);
+    with_part(C.part_start, C.P, r, [&](int L, auto U) {
+        Count3Grid<T, D, M, decltype(U)::value> g;
+        g.load(C.parts + L);
+        const RowGeo<D> geo = row_geo<T, D, M, decltype(U)::value>(g, a);
+        for (int bt = 0; bt < NB; ++bt) {   // batch 0: the centre batch, centre row first
+            uint32_t s0 = 0, e0 = 0, s1 = 0, e1 = 0, s2 = 0, e2r = 0;
+            if (!done) {
+                row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B, s0, e0);
+                if constexpr (B > 1) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 1, s1, e1);
+                if constexpr (B > 2) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 2, s2, e2r);
+            }
+            const uint32_t l0 = e0 - s0, l01 = l0 + (e1 - s1), tot = l01 + (e2r - s2);
+            // the wave's window per row slot: [min s, max e) over the lanes
+            // with a non-empty range (uniform; the whole wave is active here)
+            bool staged = false;
+            uint32_t io0 = 0, io1 = 0, io2 = 0;   // per-slot position -> LDS slot offsets
+            if constexpr (decltype(U)::value) {
+                const uint32_t lo0 = __ockl_wfred_min_u32(e0 > s0 ? s0 : kNone);
+                const uint32_t hi0 = __ockl_wfred_max_u32(e0 > s0 ? e0 : 0u);
+                uint32_t lo1 = 0, hi1 = 0, lo2 = 0, hi2 = 0;
+                if constexpr (B > 1) {
+                    lo1 = __ockl_wfred_min_u32(e1 > s1 ? s1 : kNone);
+                    hi1 = __ockl_wfred_max_u32(e1 > s1 ? e1 : 0u);
+                }
+                if constexpr (B > 2) {
+                    lo2 = __ockl_wfred_min_u32(e2r > s2 ? s2 : kNone);
+                    hi2 = __ockl_wfred_max_u32(e2r > s2 ? e2r : 0u);
+                }
+                const uint32_t q1 = hi0 > lo0 ? hi0 - lo0 : 0u;
+                const uint32_t q2 = q1 + (hi1 > lo1 ? hi1 - lo1 : 0u);
+                const uint32_t total = q2 + (hi2 > lo2 ? hi2 - lo2 : 0u);
+                staged = total <= CAP;
+                if (staged && total) {
+                    for (uint32_t i = (uint32_t)lane; i < total; i += 64) {
+                        const uint32_t rec = i < q1 ? lo0 + i : (i < q2 ? lo1 + (i - q1) : lo2 + (i - q2));
+                        stage[wv][i] = Xv[rec];
+                    }
+                    wave_lds_sync();
+                }
+                io0 = s0 - lo0;
+                io1 = q1 + (s1 - lo1) - l0;
+                io2 = q2 + (s2 - lo2) - l01;
+                if constexpr (ST) {
+                    n_batches += 1;
+                    n_staged += staged ? 1 : 0;
+                }
+            }
+            if (staged) {
+                for (uint32_t v = 0; v < tot && !done; v += 4) {
+                    uint32_t j[4];
+                    T b[4][D];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t w = v + u;
+                        uint32_t jj = s0 + w, ii = io0 + w;
+                        if constexpr (B > 1) {
+                            jj = w >= l0 ? s1 + (w - l0) : jj;
+                            ii = w >= l0 ? io1 + w : ii;
+                        }
+                        if constexpr (B > 2) {
+                            jj = w >= l01 ? s2 + (w - l01) : jj;
+                            ii = w >= l01 ? io2 + w : ii;
+                        }
+                        j[u] = jj;
+                        const V x = stage[wv][w < tot ? ii : 0u];
+                        b[u][0] = x.x;
+                        b[u][1] = x.y;
+                        if constexpr (D >= 3) b[u][2] = x.z;
+                        if constexpr (D == 4) b[u][3] = x.w;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool h = (v + u < tot) && pr(b[u]);
+                        cnt += h ? 1u : 0u;
+                        const uint32_t x = h ? j[u] : kNone;
+                        mn2 = min(mn2, max(mn, x));   // the two smallest hits
+                        mn = min(mn, x);
+                    }
+                    if constexpr (ST) n_cand += (tot - v < 4u ? tot - v : 4u);
+                    if (cnt >= stop) done = true;
+                }
+            } else {
+                auto jpos = [&](uint32_t w) -> uint32_t {
+                    uint32_t j = s0 + w;
+                    if constexpr (B > 1) j = w >= l0 ? s1 + (w - l0) : j;
+                    if constexpr (B > 2) j = w >= l01 ? s2 + (w - l01) : j;
+                    return j;
+                };
+                uint32_t v0 = 0;
+                if (bt == 0 && tot > rot_min) {
+                    const uint32_t vr = (r & ~(kRotAlign - 1u)) - s0;
+                    v0 = vr < l0 ? vr : 0u;
+                }
+                auto sweep = [&](auto ROT) {
+                    for (uint32_t v = 0; v < tot && !done; v += 4) {
+                        uint32_t j[4];
+                        T b[4][D];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            uint32_t w = v + u;
+                            if constexpr (decltype(ROT)::value) {
+                                w += v0;
+                                w = w >= tot ? w - tot : w;
+                            }
+                            j[u] = jpos(w);
+                            load_raw<T, D>(Xs, v + u < tot ? j[u] : r, b[u]);
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const bool h = (v + u < tot) && pr(b[u]);
+                            cnt += h ? 1u : 0u;
+                            const uint32_t x = h ? j[u] : kNone;
+                            mn2 = min(mn2, max(mn, x));
+                            mn = min(mn, x);
+                        }
+                        if constexpr (ST) n_cand += (tot - v < 4u ? tot - v : 4u);
+                        if (cnt >= stop) done = true;
+                    }
+                };
+                if (__any(v0 != 0))
+                    sweep(std::true_type{});
+                else
+                    sweep(std::false_type{});
+            }
+            if (__all(done)) break;
+            if constexpr (decltype(U)::value) {
+                // every lane's reads of this batch's window are issued before
+                // the next batch's copy overwrites it
+                if (staged) wave_lds_sync();
+            }
+        }
+    });
+    if constexpr (ST) {
+        if (live) atomicAdd(stats + 0, (unsigned long long)n_cand);
+        if (lane == 0) {
+            atomicAdd(stats + 8, (unsigned long long)n_batches);
+            atomicAdd(stats + 9, (unsigned long long)n_staged);
+        }
+    }
+    if (!live) return;
+    core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0) | (cnt == 2 ? 4 : 0);
+    reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, mn2);
+    if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
+}
+
 // ------------------------------------------------------------------ link mode 3
 // (1) on the forest of the count pass's smallest neighbours (init_kernel),
 // union over the centre row only (each core record with the core records of
@@ -3067,6 +3281,14 @@ template <typename T, int D, int M, bool ST>
 void launch_count(int variant, hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double eps,
                   double eps2, float lo, float hi, uint32_t ms, int full, uint32_t rot_min,
                   uint8_t* core, uint32_t* mn, uint32_t* cnt, unsigned long long* st) {
+    constexpr bool kStageable = std::is_same<T, float>::value && (D >= 2 && D <= 4);
+    if constexpr (kStageable) {
+        if ((variant & 40) == 40) {   // cheap rows + LDS-staged windows
+            hipLaunchKernelGGL((count5_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                               Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
+            return;
+        }
+    }
     if (variant & 8)   // cheap rows
         hipLaunchKernelGGL((count4_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs,
                            R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
@@ -3331,8 +3553,8 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     uint32_t* cnt_rec = a.counts ? ctx.arena.get<uint32_t>("cnt_rec", R) : nullptr;
     unsigned long long* sst = nullptr;
     if (ctx.sweep_stats) {
-        sst = ctx.arena.get<unsigned long long>("sweep_stats", 8);
-        PD_HIP(hipMemsetAsync(sst, 0, sizeof(unsigned long long) * 8, s));
+        sst = ctx.arena.get<unsigned long long>("sweep_stats", 10);
+        PD_HIP(hipMemsetAsync(sst, 0, sizeof(unsigned long long) * 10, s));
     }
     const int mode = ctx.link_mode;
     if (R) {
@@ -3679,11 +3901,11 @@ void finish(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         sync(s);
         ctx.t.cells_n = *hnc;
         if (ctx.sweep_stats && ctx.st.R) {
-            unsigned long long* hs = (unsigned long long*)pinned(ctx, 8 * sizeof(unsigned long long));
-            PD_HIP(hipMemcpyAsync(hs, ctx.arena.get<unsigned long long>("sweep_stats", 8),
-                                  8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+            unsigned long long* hs = (unsigned long long*)pinned(ctx, 10 * sizeof(unsigned long long));
+            PD_HIP(hipMemcpyAsync(hs, ctx.arena.get<unsigned long long>("sweep_stats", 10),
+                                  10 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
             sync(s);
-            for (int k = 0; k < 8; ++k) ctx.t.sweep[k] = (int64_t)hs[k];
+            for (int k = 0; k < 10; ++k) ctx.t.sweep[k] = (int64_t)hs[k];
         }
         ctx.t.grid_cells = (int64_t)ctx.st.G;
         ctx.t.key_bits = ctx.st.key_bits;

@@ -49,7 +49,7 @@ struct Timings {
     // PD_OPT_SWEEP_STATS: count candidates; link candidates, predicate hits,
     // core hits, hits already under the root, finds that met the root, unions;
     // cell pairs tested record by record (link mode 3)
-    int64_t sweep[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int64_t sweep[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     double grid_grow = 1.0;      // cell width / eps (PD_OPT_DIR_BUDGET)
     int64_t dir_words = 0;       // directory words allocated (paged: occupied + 1)
     int dir_paged = 0;           // the last train's directory layout
@@ -324,6 +324,7 @@ void comm_init_all(int n, const int32_t* devices, Comm** out);
 void comm_destroy(Comm* c);
 void comm_unique_id(uint8_t* id);
 int comm_device(const Comm* c);
+void comm_size(const Comm* c, int* n_ranks, int* rank);
 void comm_all_reduce(Comm* c, const void* send, void* recv, int64_t count, int elem, int op,
                      hipStream_t s);
 void comm_all_gather_v(Comm* c, const void* send, void* recv, const int64_t* counts, int elem,

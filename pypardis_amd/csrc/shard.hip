@@ -449,7 +449,12 @@ __global__ __launch_bounds__(kBlock) void results_pack_kernel(
     const uint32_t k = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t m = *count;
     if (k == 0 && (int64_t)m != expect) atomicOr(bad, 8u);
-    if (k >= m || (int64_t)k >= expect) return;
+    if ((int64_t)k >= expect) return;
+    if (k >= m) {   // short: the slots the peers expect carry an invalid id, so the
+        pairs[2 * (size_t)k] = kNone;   // receivers fail in results_scatter too
+        pairs[2 * (size_t)k + 1] = 0u;
+        return;
+    }
     const uint32_t i = list[k];
     const int32_t lab = root_rank(roots, nroots, keys[i]);
     if (lab == -2) atomicOr(bad, 4u);
@@ -877,7 +882,8 @@ void results_scatter(Ctx& ctx, const uint32_t* pairs, int64_t m, uint32_t gid_ba
     PD_HIP(hipMemcpyAsync(hb, dbad, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     sync(s);
     const uint32_t b = *hb;
-    if (b & 1) throw Error(-1, "results: a global id outside this device's points");
+    if (b & 1) throw Error(-1, "results: a global id outside this device's points (or a sender's "
+                               "owned records differed from the exchanged counts)");
     if (b & 2) throw Error(-1, "results: a point received no result (each point must be owned by "
                                "exactly one device)");
     if (b & 4) throw Error(-1, "results: a cluster key has no root among the roots given (roots "

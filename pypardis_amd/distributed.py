@@ -427,7 +427,8 @@ class ShardedResult(object):
     def _owned_view(self):
         if self._cache is None:
             if self._owned is None:
-                raise AttributeError("owned records were not kept")
+                raise AttributeError("owned records were not kept "
+                                     "(train_sharded(..., keep_owned=True))")
             ops, keys, core, owner, gid, roots, n = self._owned
             own = owner >= 0
             g = gid if gid is not None else \
@@ -538,13 +539,28 @@ def _kd_device(X, kdlab, levels, ops, comm, dev):
     return data_box, boxes, splits
 
 
+_KD_TAB = 256   # kd.hip kTabLds: labels / splits per level of the device KD tables
+
+
+def device_kd_ok(levels, split_method, dense):
+    """The device-decided KD (pd_kdx_*) applies: min_var, d <= 4, and a
+    schedule whose levels fit its LDS tables (every level <= 256 splits,
+    every split label < 256, i.e. max_partitions <= 512).  Decided from the
+    schedule alone, so every rank decides the same (inputs are made 16-byte
+    aligned before the KD)."""
+    if split_method != 'min_var' or dense or not levels:
+        return False
+    return all(len(lv) <= _KD_TAB and all(c < _KD_TAB for c, _ in lv) for lv in levels)
+
+
 def _exclusive(c):
     c = np.asarray(c, np.int64)
     return np.concatenate([[0], np.cumsum(c)]).astype(np.int64)
 
 
 def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitions=None,
-                  group=None, ops=None, split_method='min_var', comm=None, return_local=True):
+                  group=None, ops=None, split_method='min_var', comm=None, return_local=True,
+                  keep_owned=False):
     """Sharded DBSCAN train over the ranks of ``group`` (default: world).
 
     X: this rank's (n_i, d) slice (float32/float64, on this rank's GPU for
@@ -553,6 +569,11 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     ``split_method``: 'min_var' (default) or 'rotation' (KDPartitioner's).
     ``comm``: a collective layer (make_comm(group, device) by default: RCCL
     through libpardis for an "nccl" group, torch.distributed otherwise).
+    ``return_local``: return the labels of this rank's input points (the
+    results exchange); False skips it (``local_labels`` is None) and keeps
+    the owned records instead.  ``keep_owned``: keep the records this rank
+    owns (``gid`` / ``labels`` / ``core`` of the result, ~13 B of HBM per
+    received record while the result lives); off by default.
     """
     if split_method not in ('min_var', 'rotation'):
         split_method = 'min_var'   # the reference's fallback (R:dbscan/partition.py:129-130)
@@ -569,6 +590,11 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
         raise ValueError("max_partitions too large")
     metric = _native.metric_code(metric) if not isinstance(metric, int) else metric
     dev = getattr(ops, "device", X.device)
+    keep_owned = keep_owned or not return_local
+    if n and X.is_cuda and X.data_ptr() % 16:
+        # a view at an odd offset (e.g. X_full[a:b] of fp32 3-D): the fused
+        # KD and record kernels read 16-B vectors; one copy realigns it
+        X = X.clone()
     stats = {}
     clock = [time.perf_counter()]
 
@@ -591,7 +617,7 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     kdlab = ops.zeros(n, torch.int32)
     levels = _split_schedule(P)
     dense = d > 4
-    if split_method == 'min_var' and levels and not dense:
+    if device_kd_ok(levels, split_method, dense):
         data_box, boxes, splits = _kd_device(X, kdlab, levels, ops, comm, dev)
     else:
         data_box, boxes, splits = _kd_host(X, kdlab, levels, ops, comm, split_method, dense, lap)
@@ -685,6 +711,13 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
         raise RuntimeError("sharded train: a cluster root was selected on two ranks")
     lap("phase_b")
 
+    owned = (ops, keys, core, owner, gid, all_roots, nr) if keep_owned else None
+    common = dict(gid_base=gid_base, n_total=n_total, n_clusters=int(all_roots.shape[0]),
+                  splits=splits, bounding_boxes=boxes, boxes=ebox, stats=stats, owned=owned)
+    if not return_local:
+        lap("results")
+        return ShardedResult(local_labels=None, local_core=None, **common)
+
     # ---- labels back to the ranks that hold the points, in input order (the
     # reference's result RDD, R:dbscan/dbscan.py:162-164): the self block
     # directly, the rest as (gid, label | core) pairs in one exchange
@@ -700,10 +733,7 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
         comm.exchange([pairs], [pairs_in], back_send, back_recv, skip_self=False)
     ops.results_scatter(pairs_in, gid_base, loc_labels, loc_core)
     lap("results")
-    return ShardedResult(local_labels=loc_labels, local_core=loc_core, gid_base=gid_base,
-                         n_total=n_total, n_clusters=int(all_roots.shape[0]), splits=splits,
-                         bounding_boxes=boxes, boxes=ebox, stats=stats,
-                         owned=(ops, keys, core, owner, gid, all_roots, nr))
+    return ShardedResult(local_labels=loc_labels, local_core=loc_core, **common)
 
 
 def _train_dense(X, eps, min_samples, metric, comm, ops, gid_off, data_box, kd, stats, lap):
@@ -740,7 +770,8 @@ def _train_dense(X, eps, min_samples, metric, comm, ops, gid_off, data_box, kd, 
 
 
 def train_threads(slices, eps, min_samples, comms, ops, metric=_native.PD_EUCLIDEAN,
-                  max_partitions=None, split_method='min_var', abort_timeout=60.0):
+                  max_partitions=None, split_method='min_var', abort_timeout=60.0,
+                  keep_owned=False):
     """One process driving several devices: rank r = thread r runs
     ``train_sharded`` on slices[r] with comms[r] (e.g. RcclComm over
     pd_comm_init_all) and ops[r].  Returns the per-rank results in rank order;
@@ -760,7 +791,7 @@ def train_threads(slices, eps, min_samples, comms, ops, metric=_native.PD_EUCLID
                 torch.cuda.set_device(torch.device(dev))
             out[r] = train_sharded(slices[r], eps, min_samples, metric=metric,
                                    max_partitions=max_partitions, ops=ops[r], comm=comms[r],
-                                   split_method=split_method)
+                                   split_method=split_method, keep_owned=keep_owned)
         except BaseException as e:   # noqa: B902 - re-raised below
             errs[r] = e
             order.append(r)

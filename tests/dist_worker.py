@@ -53,7 +53,8 @@ def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native,
                 data = [("k%06d" % (cuts[rank] + j), v) for j, v in enumerate(Xi.cpu().numpy())]
             model = dbscan.DBSCAN(eps=eps, min_samples=min_samples,
                                   metric=["euclidean", "cityblock"][metric], max_partitions=P,
-                                  device=None if native else "cpu", group="world")
+                                  device=None if native else "cpu", group="world",
+                                  keep_shard_records=True)
             model.train(data)
             res = model.shard
             pairs = model.assignments()
@@ -66,7 +67,7 @@ def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native,
             loc = model.labels_.cpu().numpy(), model.core_sample_mask_.cpu().numpy()
         else:
             res = train_sharded(Xi, eps, min_samples, metric=metric, max_partitions=P, ops=ops,
-                                split_method=split_method)
+                                split_method=split_method, keep_owned=True)
             loc = res.local_labels.cpu().numpy(), res.local_core.cpu().numpy()
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), gid=res.gid.cpu().numpy(),
                  labels=res.labels.cpu().numpy(), core=res.core.cpu().numpy(),

@@ -209,3 +209,42 @@ def test_sharded_dense_equals_sklearn(tmp_path, case, world, api):
     kd = oracle.kd_partition(X, P, sums="exact")
     for sp in out["splits"]:
         np.testing.assert_array_equal(sp, np.array(kd["splits"], np.float64))
+
+
+def test_device_kd_applicability_from_schedule():
+    """The device-decided KD needs levels that fit its 256-entry tables; the
+    decision comes from the schedule alone, so every rank takes the same path
+    (P = 1000 used to raise PD_EUNSUPPORTED on the sharded path)."""
+    from pypardis_amd.distributed import device_kd_ok
+    from pypardis_amd.partition import _split_schedule
+    assert device_kd_ok(_split_schedule(8), 'min_var', False)
+    assert device_kd_ok(_split_schedule(512), 'min_var', False)
+    assert not device_kd_ok(_split_schedule(1000), 'min_var', False)
+    assert not device_kd_ok(_split_schedule(8), 'rotation', False)
+    assert not device_kd_ok(_split_schedule(8), 'min_var', True)
+    assert not device_kd_ok(_split_schedule(1), 'min_var', False)
+
+
+def test_sharded_result_keeps_owned_records_only_on_request():
+    """train_sharded frees the per-record arrays unless keep_owned (ADVICE
+    r03); return_local=False returns no local labels and keeps them."""
+    from local_comm import local_comms
+    from pypardis_amd.distributed import train_threads
+    from sharded_ops import OracleOps
+    import torch
+    g = load_golden("b3d_20k")
+    X = g["X"]
+    W = 2
+    cuts = [r * len(X) // W for r in range(W + 1)]
+    slices = [torch.from_numpy(np.ascontiguousarray(X[cuts[r]:cuts[r + 1]])) for r in range(W)]
+    res = train_threads(slices, float(g["eps"]), int(g["min_samples"]), local_comms(W),
+                        [OracleOps() for _ in range(W)], max_partitions=4)
+    with pytest.raises(AttributeError, match="keep_owned"):
+        res[0].gid
+    res = train_threads(slices, float(g["eps"]), int(g["min_samples"]), local_comms(W),
+                        [OracleOps() for _ in range(W)], max_partitions=4, keep_owned=True)
+    gid = np.concatenate([r.gid.numpy() for r in res])
+    lab = np.concatenate([r.labels.numpy() for r in res])
+    order = np.argsort(gid)
+    np.testing.assert_array_equal(gid[order], np.arange(len(X)))
+    np.testing.assert_array_equal(lab[order], g["sk_labels"])

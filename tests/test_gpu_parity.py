@@ -231,7 +231,7 @@ def test_train_matches_oracle(native, case):
 @pytest.mark.parametrize("variant,link_mode,border_roots",
                          [(0, 5, 0), (7, 3, 1), (5, 0, 0), (7, 2, 0), (5, 4, 0), (5, 3, 0),
                           (5, 6, 0), (0, 6, 0), (13, 6, 0), (15, 3, 1), (8, 0, 0), (29, 6, 0),
-                          (24, 3, 0)])
+                          (24, 3, 0), (61, 6, 0), (40, 0, 0), (45, 3, 1)])
 def test_sweep_variants_exact(native, variant, link_mode, border_roots):
     """PD_OPT_SWEEP_VARIANT x PD_OPT_LINK_MODE: the row-by-row and the
     batched sweep kernels, and the sampled-union + cell-verify link (3) or the
@@ -538,6 +538,7 @@ def test_rccl_comm_single_rank(native):
     # the W > 1 init check's pattern, fill and verify kernels (at W = 1 the
     # self blocks carry it), the grouped field exchange and the device gather
     comm.comm.self_check()
+    assert comm.comm.size() == (1, 0)       # as RCCL reports it (bench.py's rccl_ranks)
     a = torch.arange(15, dtype=torch.float32, device="cuda").reshape(5, 3)
     b = torch.arange(5, dtype=torch.int32, device="cuda")
     ra, rb = torch.empty_like(a), torch.empty_like(b)
@@ -553,6 +554,27 @@ def test_rccl_comm_single_rank(native):
     assert res[0].n_clusters == nc1
     np.testing.assert_array_equal(res[0].local_labels.cpu().numpy(), lab1.cpu().numpy())
     np.testing.assert_array_equal(res[0].local_core.cpu().numpy(), core1.cpu().numpy())
+
+
+def test_sharded_unaligned_view_and_wide_schedule(native):
+    """a slice that is a view at a 12-byte offset (fp32 3-D
+    X_full[1:]) and max_partitions = 1000 (KD levels wider than the device
+    tables: the host-decided KD) both train on a 1-rank RCCL communicator and
+    equal pd_cluster."""
+    from pypardis_amd import distributed, synth
+    comm = distributed.device_comms([0])[0]
+    X, cfg = synth.make_config("C2", n=200_001)
+    Xfull = _dev(X)
+    view = Xfull[1:]
+    assert view.data_ptr() % 16 != 0
+    want, core_w, _, nc = native.cluster(view.contiguous(), cfg["eps"], cfg["min_samples"])
+    for P in (8, 1000):
+        res = distributed.train_threads([view], cfg["eps"], cfg["min_samples"], [comm],
+                                        [distributed.NativeOps(torch.device("cuda", 0))],
+                                        max_partitions=P)
+        assert res[0].n_clusters == nc, P
+        np.testing.assert_array_equal(res[0].local_labels.cpu().numpy(), want.cpu().numpy())
+        np.testing.assert_array_equal(res[0].local_core.cpu().numpy(), core_w.cpu().numpy())
 
 
 def test_rccl_process_group_single_rank(native, tmp_path):

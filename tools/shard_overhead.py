@@ -1,17 +1,19 @@
 """Sharded-train overhead on one GPU: DBSCAN(group=WORLD).train on a 1-rank
-"nccl" (RCCL) group vs the single-device train, C2 (--points), with the
-per-phase host laps of distributed.train_sharded.  Diagnostic only."""
+"nccl" (RCCL) group vs the single-device train, on a config's points
+(--config C2|C4, --points: the per-rank share at 8 GPUs is 12.5M of C2 or
+125M of C4), with the per-phase times of distributed.train_sharded.
+Diagnostic only."""
 import argparse
 import json
 import os
-import time
-
 import sys
+import time
 
 import torch
 import torch.distributed as dist
 
 ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="C2")
 ap.add_argument("--points", type=int, default=100_000_000)
 ap.add_argument("--steps", type=int, default=3)
 args = ap.parse_args()
@@ -22,18 +24,28 @@ dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cu
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pypardis_amd import DBSCAN, synth  # noqa: E402
 
-X, cfg = synth.make_config("C2", n=args.points)
-Xd = torch.from_numpy(X).cuda()
-out = {}
+dev = torch.device("cuda", 0)
+X, cfg = synth.make_config(args.config, n=args.points,
+                           device=dev if args.config == "C4" else "cpu")
+Xd = X if torch.is_tensor(X) else torch.from_numpy(X).to(dev)
+del X
+P = cfg.get("max_partitions") or 8
+out = {"config": args.config, "points": int(Xd.shape[0])}
 for name, kw in (("single", dict(n_gpus=1)), ("sharded_w1", dict(group=dist.group.WORLD))):
-    m = DBSCAN(eps=cfg["eps"], min_samples=cfg["min_samples"], max_partitions=8, **kw).train(Xd)
+    m = DBSCAN(eps=cfg["eps"], min_samples=cfg["min_samples"], max_partitions=P, **kw).train(Xd)
     torch.cuda.synchronize()
+    stats = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        m = DBSCAN(eps=cfg["eps"], min_samples=cfg["min_samples"], max_partitions=8, **kw).train(Xd)
+        m = DBSCAN(eps=cfg["eps"], min_samples=cfg["min_samples"], max_partitions=P,
+                   **kw).train(Xd)
+        if m.shard is not None:
+            stats.append(m.shard.stats)
     torch.cuda.synchronize()
     out[name] = {"ms": 1e3 * (time.perf_counter() - t0) / args.steps,
-                 "stats": getattr(m.shard, "stats", None) if m.shard is not None else None,
+                 "stats": stats[-1] if stats else None,
                  "n_clusters": m.n_clusters_}
-print(json.dumps(out))
+    del m
+out["ratio"] = out["sharded_w1"]["ms"] / out["single"]["ms"]
+print(json.dumps(out), flush=True)
 dist.destroy_process_group()

@@ -86,7 +86,9 @@ enum pd_option {
                                registers, three rows swept as one list), a clear bit the
                                row-by-row kernel; bit 3 (count) and bit 4 (border) the
                                batched kernels with fp32-chord rows keyed off the query cell
-                               (override bits 0 / 2; bit 4 not with PD_OPT_BORDER_ROOTS).
+                               (override bits 0 / 2; bit 4 not with PD_OPT_BORDER_ROOTS);
+                               bit 5 with bit 3: the count sweep reads each batch's
+                               candidate windows from LDS (fp32, 2-4 D).
                                Default 29 (the measured best on MI355X). */
     PD_OPT_BORDER_ROOTS = 10, /* batched border sweep: skip or stop early where the stencil's
                                 directory words hold at most one cluster root (tuning; same

@@ -150,7 +150,7 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         } else if (option == PD_OPT_BORDER_ROOTS)
             ctx->c.border_roots = value != 0;
         else if (option == PD_OPT_SWEEP_VARIANT) {
-            if (value < 0 || value > 31) throw Error(PD_EINVAL, "sweep variant is a 5-bit mask");
+            if (value < 0 || value > 63) throw Error(PD_EINVAL, "sweep variant is a 6-bit mask");
             ctx->c.variant = (int)value;
         } else if (option == PD_OPT_COUNT_ROTATE) {
             if (value < 0 || value > 0x7FFFFFFF) throw Error(PD_EINVAL, "count rotate must be >= 0");

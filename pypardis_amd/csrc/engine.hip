@@ -1716,12 +1716,14 @@ __global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs
 // count4_kernel (PD_OPT_SWEEP_VARIANT bit 3, the default): count2_kernel's
 // lockstep sweep — three rows as one virtual list, centre batch first, the
 // rotated start in long centre rows, four candidates per round trip — with a
-// row's candidate range at about a third of the instructions.  The count
-// sweep is bound by instruction issue (PMC, C2: 3.29e9 VALU instructions in a
-// 7 ms kernel, ~5.4 ms of pure issue at one wave-instruction per CU per
-// cycle), and the fp64 chord of every row (sqrt, two floors, 64-bit key
-// arithmetic from the cell coordinates: ~130 instructions a row, nine rows)
-// was most of it.  Here, per record once: the fp64 cell index exactly as the
+// row's candidate range at about a third of the instructions.  count2 spent
+// 3.29e9 VALU instructions per C2 launch (PMC), and the fp64 chord of every
+// row (sqrt, two floors, 64-bit key arithmetic from the cell coordinates:
+// ~130 instructions a row, nine rows) was most of them.  (At the guide's
+// issue rate — a wave64 VALU instruction takes 2 cycles on a SIMD-32, so 2
+// wave-instructions per CU per cycle — count4's 2.66e9 are 0.44 of the issue
+// budget of its 4.87 ms: the sweep is bound by the vector-memory path, see
+// count5_kernel.)  Here, per record once: the fp64 cell index exactly as the
 // record keys were built, the in-cell fractions, the squared distances to the
 // neighbour rows; per row: the chord in fp32 from those (distances shrunk by
 // 2^-16 relative + 2^-20 of a cell, the chord grown by 2^-16 relative + 2^-16

@@ -514,17 +514,32 @@ def _kd_device(X, kdlab, levels, ops, comm, dev):
     device (pd_kdx_*): per level the moment partials are all-gathered and the
     counts all-reduced as device tensors — no host round trip until the end
     (R:dbscan/partition.py:139-183; the splits equal one device's bit for bit).
-    -> (data_box, boxes, splits); kdlab ends as the partition labels."""
+    The slice sizes ride level 0's gather as one more fp64 column (exact below
+    2^53) and are read back with the KD trace: no collective or host sync of
+    their own.  -> (data_box, boxes, splits, sizes); kdlab ends as the
+    partition labels."""
     n, d = X.shape
     W = comm.world
     ops.kdx_begin(d, levels)
+    sizes_dev = None
     for lv, level in enumerate(levels):
         S = len(level)
         part = ops.kdx_moments(X, kdlab, lv, S)
-        ops.kdx_axes(comm.all_gather_t(part).to(dev), W, lv)
+        if lv == 0:
+            L = part.shape[0]
+            ext = torch.empty(L + 1, dtype=part.dtype, device=part.device)
+            ext[:L] = part
+            ext[L] = float(n)
+            g = comm.all_gather_t(ext).to(dev)
+            sizes_dev = g[:, L].clone()
+            ops.kdx_axes(g[:, :L].contiguous(), W, lv)
+        else:
+            ops.kdx_axes(comm.all_gather_t(part).to(dev), W, lv)
         cnt = ops.kdx_counts(X, kdlab, lv, S)
         ops.kdx_boundary(comm.all_reduce_t(cnt, "sum").to(dev), lv)
     trace, lo, hi, bad = ops.kdx_end(X, kdlab, sum(len(lv) for lv in levels), True)
+    # the KD trace read above synchronised the stream: this copy waits on nothing
+    sizes = sizes_dev.cpu().numpy().astype(np.int64)
     if bad:
         raise ValueError("Input contains NaN or infinity.")
     data_box = np.concatenate([lo, hi])
@@ -536,7 +551,7 @@ def _kd_device(X, kdlab, levels, ops, comm, dev):
         k += len(level)
         apply_level(boxes, splits, level, t[:, 0].astype(np.int64).tolist(), t[:, 1], t[:, 2],
                     t[:, 3:11].astype(np.int64), t[:, 11].astype(np.int64).tolist(), t[:, 12])
-    return data_box, boxes, splits
+    return data_box, boxes, splits, sizes
 
 
 _KD_TAB = 256   # kd.hip kTabLds: labels / splits per level of the device KD tables
@@ -551,6 +566,42 @@ def device_kd_ok(levels, split_method, dense):
     if split_method != 'min_var' or dense or not levels:
         return False
     return all(len(lv) <= _KD_TAB and all(c < _KD_TAB for c, _ in lv) for lv in levels)
+
+
+class _PhaseClock(object):
+    """Per-phase times of the sharded train (``stats['<phase>_ms']``) without
+    host syncs of its own: on a GPU, events recorded on the current stream at
+    each phase boundary and read once, when the train has already synchronised
+    at its end; on the host (gloo / CPU stand-ins), wall time."""
+
+    def __init__(self, device, stats):
+        self.stats = stats
+        self.cuda = torch.device(device).type == "cuda"
+        self.marks = []
+        self.t0 = self._mark()
+
+    def _mark(self):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def __call__(self, name):
+        self.marks.append((name, self._mark()))
+
+    def finish(self):
+        prev = self.t0
+        if self.cuda and self.marks:
+            self.marks[-1][1].synchronize()
+        total = 0.0
+        for name, m in self.marks:
+            ms = prev.elapsed_time(m) if self.cuda else 1e3 * (m - prev)
+            self.stats[name + "_ms"] = round(ms, 3)
+            total += ms
+            prev = m
+        self.stats["total_ms"] = round(total, 3)
+        self.marks = []
 
 
 def _exclusive(c):
@@ -596,15 +647,18 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
         # KD and record kernels read 16-B vectors; one copy realigns it
         X = X.clone()
     stats = {}
-    clock = [time.perf_counter()]
+    lap = _PhaseClock(dev, stats)
 
-    def lap(name):   # host wall time per phase (each phase ends in a host sync)
-        now = time.perf_counter()
-        stats[name + "_ms"] = round(1e3 * (now - clock[0]), 3)
-        clock[0] = now
-
-    # ---- global ids
-    sizes = comm.all_gather_np(np.array([n], np.int64))[:, 0]
+    # ---- KD partition (R:dbscan/partition.py:135-183); the global ids (rank
+    # offset + row) from the slice sizes gathered with it
+    kdlab = ops.zeros(n, torch.int32)
+    levels = _split_schedule(P)
+    dense = d > 4
+    if device_kd_ok(levels, split_method, dense):
+        data_box, boxes, splits, sizes = _kd_device(X, kdlab, levels, ops, comm, dev)
+    else:
+        sizes = comm.all_gather_np(np.array([n], np.int64))[:, 0]
+        data_box, boxes, splits = _kd_host(X, kdlab, levels, ops, comm, split_method, dense, lap)
     gid_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
     gid_base = int(gid_off[rank])
     n_total = int(gid_off[-1])
@@ -612,15 +666,6 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
         raise ValueError("the sharded train addresses points with 32-bit global ids")
     if n_total == 0:
         raise ValueError("no points on any rank")
-
-    # ---- KD partition (R:dbscan/partition.py:135-183)
-    kdlab = ops.zeros(n, torch.int32)
-    levels = _split_schedule(P)
-    dense = d > 4
-    if device_kd_ok(levels, split_method, dense):
-        data_box, boxes, splits = _kd_device(X, kdlab, levels, ops, comm, dev)
-    else:
-        data_box, boxes, splits = _kd_host(X, kdlab, levels, ops, comm, split_method, dense, lap)
     ebox = np.stack([boxes[L].expand(2 * eps).as_array() for L in sorted(boxes)])
     lap("kd")
     if dense:
@@ -716,6 +761,7 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
                   splits=splits, bounding_boxes=boxes, boxes=ebox, stats=stats, owned=owned)
     if not return_local:
         lap("results")
+        lap.finish()
         return ShardedResult(local_labels=None, local_core=None, **common)
 
     # ---- labels back to the ranks that hold the points, in input order (the
@@ -733,6 +779,7 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
         comm.exchange([pairs], [pairs_in], back_send, back_recv, skip_self=False)
     ops.results_scatter(pairs_in, gid_base, loc_labels, loc_core)
     lap("results")
+    lap.finish()
     return ShardedResult(local_labels=loc_labels, local_core=loc_core, **common)
 
 
@@ -761,6 +808,7 @@ def _train_dense(X, eps, min_samples, metric, comm, ops, gid_off, data_box, kd, 
     best = comm.all_reduce_t(best, "min").to(dev)
     labels, core, ncl = ops.dense_finish(best, n_total)
     lap("border")
+    lap.finish()
     lo = int(gid_off[rank])
     loc_labels, loc_core = labels[lo:lo + n], core[lo:lo + n]
     gid = torch.arange(lo, lo + n, dtype=torch.int32, device=dev)

@@ -1,14 +1,15 @@
 #!/bin/bash
 # Round-4 development call.  Steps (each with its own time limit, stop at the
 # first failure):
-#   TESTS   pytest node ids / files to run first ("" = none)
+#   TESTS   pytest node ids / files to run first ("" = none); KEXPR: their -k expression
 #   AB      space-separated sweep variants for C2 bench A/B (e.g. "29 61")
 #   PMCV    a sweep variant for one PMC pass set (SQ + TA + TCP + fetch) on C2
 #   FLOOR=1 the sharded floor (tools/gpu_floor.sh without its tests)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp; mkdir -p gpurun_out
 if [ -n "${TESTS:-}" ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-      -m gpu $TESTS > gpurun_out/r4_pytest.log 2>&1
+  KARGS=(); [ -n "${KEXPR:-}" ] && KARGS=(-k "$KEXPR")
+  timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest -x -v --timeout ${PER_TEST:-300} --timeout-method thread \
+      -m gpu "${KARGS[@]}" $TESTS > gpurun_out/r4_pytest.log 2>&1
   rc=$?; grep -E "PASS|FAIL|Error|passed|failed" gpurun_out/r4_pytest.log | tail -25
   [ $rc -eq 0 ] || exit $rc
 fi

@@ -22,7 +22,7 @@ os.environ.setdefault("MASTER_PORT", "29533")
 torch.cuda.set_device(0)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from pypardis_amd import DBSCAN, synth  # noqa: E402
+from pypardis_amd import DBSCAN, _native, synth  # noqa: E402
 
 dev = torch.device("cuda", 0)
 X, cfg = synth.make_config(args.config, n=args.points,
@@ -42,8 +42,16 @@ for name, kw in (("single", dict(n_gpus=1)), ("sharded_w1", dict(group=dist.grou
         if m.shard is not None:
             stats.append(m.shard.stats)
     torch.cuda.synchronize()
-    out[name] = {"ms": 1e3 * (time.perf_counter() - t0) / args.steps,
-                 "stats": stats[-1] if stats else None,
+    ms = 1e3 * (time.perf_counter() - t0) / args.steps
+    ctx = _native.context(0)   # one more, with the engine's per-stage events
+    ctx.set_option(_native.PD_OPT_TIMING, 1)
+    DBSCAN(eps=cfg["eps"], min_samples=cfg["min_samples"], max_partitions=P, **kw).train(Xd)
+    torch.cuda.synchronize()
+    ctx.set_option(_native.PD_OPT_TIMING, 0)
+    stages = {k: round(v, 3) for k, v in ctx.timings().items()
+              if v and k in ("halo", "sort", "gather", "cells", "count", "link", "merge", "roots",
+                             "border", "label", "total")}
+    out[name] = {"ms": ms, "stats": stats[-1] if stats else None, "stages": stages,
                  "n_clusters": m.n_clusters_}
     del m
 out["ratio"] = out["sharded_w1"]["ms"] / out["single"]["ms"]

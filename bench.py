@@ -327,6 +327,30 @@ def dense_roofline(n, d, t_cnt, cells, pmc, pmc_src, refined=None, screen=1):
     return roof
 
 
+def train_roofline(pmc, pmc_src, ms_step):
+    """The whole train's measured HBM bytes (every kernel's per-launch bytes
+    from the PMC summary x its launches per train) over the step time: the
+    step's own fraction of the 8 TB/s peak, beside the one-kernel roofline."""
+    if not pmc or "_meta" not in pmc or not ms_step:
+        return None
+    tot, per = 0.0, {}
+    for k, v in pmc.items():
+        if k.startswith("_") or "hbm_bytes_per_launch" not in v:
+            continue
+        b = v["hbm_bytes_per_launch"] * v.get("dispatches_per_train", 0.0)
+        if b > 0:
+            per[k] = b
+            tot += b
+    if tot <= 0:
+        return None
+    top = dict(sorted(per.items(), key=lambda kv: -kv[1])[:8])
+    return {"bytes_per_train": tot, "achieved_gbs": tot / (ms_step * 1e-3) / 1e9,
+            "peak": HBM_PEAK_GBS, "frac": tot / (ms_step * 1e-3) / (HBM_PEAK_GBS * 1e9),
+            "kind": "measured: sum over every kernel of (2*FETCH_SIZE + WRITE_SIZE) x launches "
+                    "per train, over ms_per_step",
+            "top_kernels_bytes": top, "pmc_source": pmc_src}
+
+
 def host_legs(DBSCAN, eps, ms, P, Xh):
     """The same train from host memory: a numpy array (H2D inside the step),
     and a list of (key, vector) records — the reference's RDD element form
@@ -584,6 +608,7 @@ def main():
                        "transport": (("gloo rehearsal, every rank on cuda:0" if args.rehearse
                                       else "RCCL (pd_comm)") if world > 1 else None)},
             "roofline": roof,
+            "train_roofline": train_roofline(pmc, pmc_src, ms_step) if world == 1 else None,
             "stage_roofline": stage_roof,
             "cpu_baseline": cpu,
             "host_input": host,

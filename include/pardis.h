@@ -130,7 +130,11 @@ enum pd_option {
     PD_OPT_DENSE_SCREEN = 18  /* d > 4 count pass: the tile screen that decides which tiles
                                 compute the exact-banded split-bf16 product.  1 (default): e4m3
                                 Gram tiles on v_mfma_f32_32x32x64_f8f6f4 (half the staged bytes,
-                                twice the MFMA rate); 0: bf16 hi.hi.  Same counts either way */
+                                twice the MFMA rate); 0: bf16 hi.hi.  Same counts either way */,
+    PD_OPT_SHARD_CORE_BIT = 19 /* pd_train_end: 1 = the caller guarantees every global id is
+                                < 2^31, so the core flags ride bit 31 of the keys and reach
+                                core_out by one coalesced pass instead of a byte scattered per
+                                owner record (default 0; same outputs) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -173,6 +173,8 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         } else if (option == PD_OPT_DENSE_SCREEN) {
             if (value < 0 || value > 1) throw Error(PD_EINVAL, "dense screen is 0 or 1");
             ctx->c.dense_screen = (int)value;
+        } else if (option == PD_OPT_SHARD_CORE_BIT) {
+            ctx->c.shard_core_bit = value != 0;
         }
         else
             throw Error(PD_EINVAL, "unknown option");

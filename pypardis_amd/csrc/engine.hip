@@ -1372,9 +1372,10 @@ __global__ __launch_bounds__(kBlock) void remap_kernel(uint32_t R, const uint8_t
 }
 
 // Owner records: publish core flag / count, and the cluster key of core
-// points (their component's smallest core point).  core_bit (single device,
-// ids < 2^30): the core flag rides in bit 30 of the key instead of a byte
-// scattered to core_out — the label pass writes the core mask coalesced.
+// points (their component's smallest core point).  core_mask (single device,
+// ids < 2^30: bit 30; sharded phase B with global ids < 2^31: bit 31): the
+// core flag rides in the key instead of a byte scattered to core_out — the
+// label pass (split_core_kernel) writes the core mask coalesced.
 constexpr uint32_t kKeyCoreBit = 0x40000000u;
 constexpr int kOwnPer = 4;                    // owner_kernel / border_list_kernel records per thread
 constexpr uint32_t kOwnTile = kBlock * kOwnPer;
@@ -1385,7 +1386,7 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
                                                        const uint32_t* __restrict__ gmin,
                                                        const uint32_t* __restrict__ cnt_rec,
                                                        const uint2* __restrict__ mn,
-                                                       int core_bit,
+                                                       uint32_t core_mask,
                                                        uint32_t* __restrict__ key_out,
                                                        uint8_t* __restrict__ core_out,
                                                        uint32_t* __restrict__ cnt_out,
@@ -1406,7 +1407,7 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
         // border sweep's smallest core key, over one candidate); else none
         uint32_t key = kNone;
         if (fl & 1) {
-            key = gmin[par[r]] | (core_bit ? kKeyCoreBit : 0u);
+            key = gmin[par[r]] | core_mask;
         } else if ((fl & 7) == 6 && mn) {
             const uint2 m = mn[r];
             const uint32_t j = m.x == r ? m.y : m.x;
@@ -1417,7 +1418,7 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
             recs[r] = make_uint2(own ? v & kIdMask : kNone, key);
         if (own) {
             const uint32_t pt = v & kIdMask;
-            if (core_out && !core_bit) core_out[pt] = fl & 1;
+            if (core_out && !core_mask) core_out[pt] = fl & 1;
             if (cnt_out) cnt_out[pt] = cnt_rec[r];
             if (key != kNone && key_out) key_out[pt] = key;
         }
@@ -3191,6 +3192,19 @@ __global__ __launch_bounds__(kBlock) void final_label_kernel(const uint32_t* __r
     if (core_out) core_out[i] = (k != kNone && (k & kKeyCoreBit)) ? 1 : 0;
 }
 
+// Sharded phase B: the core flag out of bit `mask` of each key into a byte,
+// both coalesced (kNone stays: a noise point).
+__global__ __launch_bounds__(kBlock) void split_core_kernel(uint32_t* __restrict__ key, uint64_t n,
+                                                            uint32_t mask,
+                                                            uint8_t* __restrict__ core) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = key[i];
+    const bool c = k != kNone && (k & mask);
+    if (core) core[i] = c ? 1 : 0;
+    if (c) key[i] = k & ~mask;
+}
+
 // Keys may carry kKeyCoreBit (owner_kernel core_bit mode): strip it.
 __device__ __forceinline__ uint32_t key_id(uint32_t k, int core_bit) {
     return (core_bit && k != kNone) ? (k & ~kKeyCoreBit) : k;
@@ -3824,10 +3838,14 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
                                a.map_ids, a.map_keys, (uint32_t)a.n_map, gmin);
     }
     uint32_t* key_out = a.phase == 2 ? a.keys_out : ctx.arena.get<uint32_t>("key_out", n);
-    // single device: core flags travel in the keys (ids < 2^30); sharded: global ids
+    // core flags travel in the keys: single device bit 30 (ids < 2^30);
+    // sharded (global ids) bit 31 when the caller vouches for ids < 2^31
+    // (PD_OPT_SHARD_CORE_BIT), else a byte scattered per owner record
+    const uint32_t core_mask =
+        a.phase == 2 ? (ctx.shard_core_bit ? 0x80000000u : 0u) : kKeyCoreBit;
     const int core_bit = a.phase == 2 ? 0 : 1;
     PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
-    if (a.core && !core_bit) PD_HIP(hipMemsetAsync(a.core, 0, n, s));
+    if (a.core && !core_mask) PD_HIP(hipMemsetAsync(a.core, 0, n, s));
     // single device, no counts wanted, the cheap-row border: labels reach
     // input order through the bucketed pair passes instead of owner_kernel's
     // scatter (ctx.label_buckets, PD_OPT_LABEL_BUCKETS)
@@ -3848,7 +3866,7 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         // the rest
         const bool single = (ctx.variant & 8) && st.mn;
         hipLaunchKernelGGL(owner_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core, par, gmin,
-                           st.cnt_rec, single ? (const uint2*)st.mn : nullptr, core_bit,
+                           st.cnt_rec, single ? (const uint2*)st.mn : nullptr, core_mask,
                            bucketed ? nullptr : key_out, a.core, a.counts,
                            tcnt, recs);
         const uint32_t NB = (uint32_t)tile_offsets(ctx, tcnt, tiles, toff, s, true);
@@ -3879,6 +3897,10 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     PD_HIP(hipGetLastError());
     tm.mark();   // 9 (phase 2: 1)
     if (a.phase == 2) {
+        if (core_mask && n)
+            hipLaunchKernelGGL(split_core_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key_out, n,
+                               core_mask, a.core);
+        PD_HIP(hipGetLastError());
         tm.mark();
         return;
     }

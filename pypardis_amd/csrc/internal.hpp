@@ -166,6 +166,7 @@ struct Ctx {
     int dir_paged = -1;          // PD_OPT_DIR_PAGED: 1 paged, 0 flat, -1 paged when the grid has
                                  // more directory words than points
     int dense_prune = 1;         // dense count pass: projection-window tiles only (2: per-band runs)
+    bool shard_core_bit = false; // PD_OPT_SHARD_CORE_BIT: sharded phase B keys carry the core flag
     int dense_screen = 1;        // dense count pass screen: 1 e4m3 (32x32x64), 0 bf16 hi.hi
     bool sort_payload = false;   // fp32 3-D: coordinates ride the sort (PD_OPT_SORT_PAYLOAD)
     int label_buckets = -1;      // labels to input order by bucketed pair passes (PD_OPT_LABEL_BUCKETS;

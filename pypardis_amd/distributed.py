@@ -110,7 +110,10 @@ class NativeOps(object):
     def merge(self, gid, key):
         return _native.merge_exports(gid, key, ctx=self.ctx)
 
-    def train_end(self, n, keymap):
+    def train_end(self, n, keymap, n_total=None):
+        # global ids below 2^31: the core flags ride the keys' top bit
+        self.ctx.set_option(_native.PD_OPT_SHARD_CORE_BIT,
+                            1 if n_total is not None and n_total < (1 << 31) else 0)
         return _native.train_end(n, keymap, self.device, ctx=self.ctx)
 
     def select_roots(self, keys, gid):
@@ -601,6 +604,9 @@ class _PhaseClock(object):
             total += ms
             prev = m
         self.stats["total_ms"] = round(total, 3)
+        if "phase_b_roots_ms" in self.stats:
+            self.stats["phase_b_ms"] = round(self.stats["phase_b_border_ms"] +
+                                             self.stats["phase_b_roots_ms"], 3)
         self.marks = []
 
 
@@ -744,9 +750,10 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     # ---- phase B: border attach with the global keys, the cluster roots of
     # every rank (sklearn's numbering: a key's rank among them)
     if mine and nr:
-        keys, core = ops.train_end(nr, keymap)
+        keys, core = ops.train_end(nr, keymap, n_total)
     else:
         keys, core = ops.empty(0, torch.int32), ops.empty(0, torch.uint8)
+    lap("phase_b_border")
     roots = ops.select_roots(keys, gid) if nr else ops.empty(0, torch.int32)
     all_roots = (comm.all_gather_var(roots) if W > 1 else roots).to(dev).contiguous()
     ops.sort(all_roots)
@@ -754,7 +761,7 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     # (shard.hip IsRoot); a duplicate would double-count a cluster
     if W > 1 and all_roots.shape[0] > 1 and bool((all_roots[1:] == all_roots[:-1]).any()):
         raise RuntimeError("sharded train: a cluster root was selected on two ranks")
-    lap("phase_b")
+    lap("phase_b_roots")
 
     owned = (ops, keys, core, owner, gid, all_roots, nr) if keep_owned else None
     common = dict(gid_base=gid_base, n_total=n_total, n_clusters=int(all_roots.shape[0]),

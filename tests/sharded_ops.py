@@ -242,7 +242,7 @@ class OracleOps(object):
         return (torch.from_numpy(ids.astype(np.uint32).view(np.int32)),
                 torch.from_numpy(keys.astype(np.uint32).view(np.int32)))
 
-    def train_end(self, n, keymap):
+    def train_end(self, n, keymap, n_total=None):
         km = None if keymap is None else tuple(t.numpy().view(np.uint32) for t in keymap)
         keys, core = osh.phase_b(self.state, km)
         return torch.from_numpy(keys.astype(np.int32)), torch.from_numpy(core)

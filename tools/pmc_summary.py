@@ -28,6 +28,9 @@ def short(name):
     return name[:60]
 
 
+REPS = int(os.environ.get("PROF_REPS", "2"))   # trains per profiled run (tools/prof_one.py)
+
+
 def main(dirs):
     acc = defaultdict(lambda: defaultdict(list))
     for d in dirs:
@@ -51,7 +54,13 @@ def main(dirs):
             o[c] = sum(per.values()) / max(1, len(per))
         if "FETCH_SIZE" in o or "WRITE_SIZE" in o:
             o["hbm_bytes_per_launch"] = (2 * o.get("FETCH_SIZE", 0.0) + o.get("WRITE_SIZE", 0.0)) * 1024
+        # dispatches of this kernel name per profiled train (the FETCH_SIZE
+        # pass: every counter pass runs the same trains)
+        disp = {dd for dd, _ in cs.get("FETCH_SIZE", next(iter(cs.values())))}
+        o["dispatches_per_train"] = len(disp) / REPS
         out[k] = o
+    out["_meta"] = {"trains": REPS, "note": "counter values: mean per dispatch; "
+                    "dispatches_per_train: launches of this kernel name in one train"}
     json.dump(out, sys.stdout, indent=1, sort_keys=True)
 
 

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
+#include "compact.hpp"
 #include "internal.hpp"
 
 namespace pd {
@@ -452,22 +453,40 @@ __device__ __forceinline__ int32_t root_rank(const RootIndex& R, uint32_t k) {
     return (lo < hi && R.roots[lo] == k) ? (int32_t)lo : -2;
 }
 
+// kResPer records per thread (coalesced rounds of kBlock), their root
+// lookups interleaved: four independent two-table-read chains per lane in
+// flight instead of one (the lookups are L2 latency, not bandwidth)
+constexpr int kResPer = 4;
 __global__ __launch_bounds__(kBlock) void results_self_kernel(
     const uint32_t* __restrict__ keys, const uint8_t* __restrict__ core,
     const int32_t* __restrict__ owner, const uint32_t* __restrict__ gid, uint64_t lo, uint64_t hi,
     RootIndex RI, uint32_t gid_base, uint64_t n_local,
     int32_t* __restrict__ labels, uint8_t* __restrict__ core_out, uint32_t* __restrict__ bad) {
-    const uint64_t i = lo + (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= hi || owner[i] < 0) return;
-    const int32_t lab = root_rank(RI, keys[i]);
-    const uint32_t g = gid ? gid[i] : (uint32_t)i;
-    if (lab == -2) atomicOr(bad, 4u);
-    if (g < gid_base || (uint64_t)(g - gid_base) >= n_local) {
-        atomicOr(bad, 1u);
-        return;
+    const uint64_t i0 = lo + (uint64_t)blockIdx.x * kBlock * kResPer + threadIdx.x;
+    uint32_t k[kResPer];
+    bool ok[kResPer];
+#pragma unroll
+    for (int q = 0; q < kResPer; ++q) {
+        const uint64_t i = i0 + (uint64_t)q * kBlock;
+        ok[q] = i < hi && owner[i] >= 0;
+        k[q] = ok[q] ? keys[i] : kNone;
     }
-    labels[g - gid_base] = lab;
-    if (core_out) core_out[g - gid_base] = core ? core[i] : 0;
+    int32_t lab[kResPer];
+#pragma unroll
+    for (int q = 0; q < kResPer; ++q) lab[q] = root_rank(RI, k[q]);
+#pragma unroll
+    for (int q = 0; q < kResPer; ++q) {
+        if (!ok[q]) continue;
+        const uint64_t i = i0 + (uint64_t)q * kBlock;
+        const uint32_t g = gid ? gid[i] : (uint32_t)i;
+        if (lab[q] == -2) atomicOr(bad, 4u);
+        if (g < gid_base || (uint64_t)(g - gid_base) >= n_local) {
+            atomicOr(bad, 1u);
+            continue;
+        }
+        labels[g - gid_base] = lab[q];
+        if (core_out) core_out[g - gid_base] = core ? core[i] : 0;
+    }
 }
 
 struct IsRemoteOwned {
@@ -562,18 +581,8 @@ int64_t pack(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const uint64_
     PD_HIP(hipMemcpyAsync(dt, h, tb, hipMemcpyHostToDevice, s));
     uint32_t* list = ctx.arena.get<uint32_t>("pack_list", n + 1);
     uint32_t* dcount = ctx.arena.get<uint32_t>("pack_count", 4);
-    {
-        rocprim::counting_iterator<uint32_t> it(0u);
-        size_t tmp_b = 0;
-        HasBit pred{mask, dest};
-        PD_HIP(rocprim::select(nullptr, tmp_b, it, list, dcount, (size_t)n, pred, s));
-        void* tmp = ctx.arena.get<char>("pack_tmp", tmp_b);
-        PD_HIP(rocprim::select(tmp, tmp_b, it, list, dcount, (size_t)n, pred, s));
-    }
-    uint32_t* hm = (uint32_t*)pinned(ctx, sizeof(uint32_t));
-    PD_HIP(hipMemcpyAsync(hm, dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    sync(s);
-    const uint32_t m = *hm;
+    const uint32_t m =
+        (uint32_t)compact_ordered(ctx, "pack_cmp", (uint64_t)n, HasBit{mask, dest}, list, dcount, s);
     if ((int64_t)m > cap) throw Error(-1, "pack: output buffers too small");
     if (m) {
         dispatch(dtype, d, [&](auto tp, auto Dc) {
@@ -638,19 +647,8 @@ int64_t select_roots(Ctx& ctx, const uint32_t* keys, const uint32_t* gid, int64_
                      hipStream_t s) {
     if (n > (int64_t)kIdMask) throw Error(-5, "n must be < 2^30 points per device");
     uint32_t* dcount = ctx.arena.get<uint32_t>("roots_count", 4);
-    PD_HIP(hipMemsetAsync(dcount, 0, sizeof(uint32_t), s));
-    if (n) {
-        rocprim::counting_iterator<uint32_t> it(0u);
-        size_t tb = 0;
-        IsRoot pred{keys, gid};
-        PD_HIP(rocprim::select(nullptr, tb, it, out, dcount, (size_t)n, pred, s));
-        void* tmp = ctx.arena.get<char>("roots_tmp", tb);
-        PD_HIP(rocprim::select(tmp, tb, it, out, dcount, (size_t)n, pred, s));
-    }
-    uint32_t* hm = (uint32_t*)pinned(ctx, sizeof(uint32_t));
-    PD_HIP(hipMemcpyAsync(hm, dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    sync(s);
-    const uint32_t m = *hm;
+    const uint32_t m =
+        (uint32_t)compact_ordered(ctx, "roots_cmp", (uint64_t)n, IsRoot{keys, gid}, out, dcount, s);
     if (m && gid) {
         hipLaunchKernelGGL(map_gid_kernel, dim3(blocks(m)), dim3(kBlock), 0, s, out, m, gid);
         PD_HIP(hipGetLastError());
@@ -891,18 +889,17 @@ void results(Ctx& ctx, int64_t nr, const uint32_t* keys, const uint8_t* core, co
                        roots, (uint32_t)n_roots, sh, ridx);
     const RootIndex RI{roots, ridx, (uint32_t)n_roots, sh};
     if (hi > lo)
-        hipLaunchKernelGGL(results_self_kernel, dim3(blocks(hi - lo)), dim3(kBlock), 0, s, keys,
+        hipLaunchKernelGGL(results_self_kernel,
+                           dim3((unsigned)((hi - lo + (uint64_t)kBlock * kResPer - 1) /
+                                           ((uint64_t)kBlock * kResPer))),
+                           dim3(kBlock), 0, s, keys,
                            core, owner, gid, lo, hi, RI, gid_base,
                            (uint64_t)n_local, labels, core_out, dbad);
     if (expect_remote > 0) {
         uint32_t* list = ctx.arena.get<uint32_t>("res_list", (size_t)nr + 1);
         uint32_t* dcount = ctx.arena.get<uint32_t>("res_count", 4);
-        rocprim::counting_iterator<uint32_t> it(0u);
-        size_t tb = 0;
-        IsRemoteOwned pred{owner, lo, hi};
-        PD_HIP(rocprim::select(nullptr, tb, it, list, dcount, (size_t)nr, pred, s));
-        void* tmp = ctx.arena.get<char>("res_tmp", tb);
-        PD_HIP(rocprim::select(tmp, tb, it, list, dcount, (size_t)nr, pred, s));
+        compact_ordered(ctx, "res_cmp", (uint64_t)nr, IsRemoteOwned{owner, lo, hi}, list, dcount, s,
+                        false);
         hipLaunchKernelGGL(results_pack_kernel, dim3(blocks((uint64_t)expect_remote)), dim3(kBlock),
                            0, s, list, dcount, expect_remote, keys, core, gid, RI, pairs, dbad);
     }

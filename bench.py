@@ -99,6 +99,8 @@ def parse():
                     help="PD_OPT_LABEL_BUCKETS override (0: one scattered label write per record)")
     ap.add_argument("--centre-window", type=int, default=None,
                     help="PD_OPT_CENTRE_WINDOW override (link window length)")
+    ap.add_argument("--border-lists", type=int, default=None,
+                    help="PD_OPT_BORDER_LISTS override (0: border points by a second sweep)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
@@ -469,7 +471,8 @@ def main():
                      (_native.PD_OPT_LABEL_BUCKETS, args.label_buckets),
                      (_native.PD_OPT_SORT_PAYLOAD, args.sort_payload),
                      (_native.PD_OPT_DIR_PAGED, args.dir_paged),
-                     (_native.PD_OPT_DENSE_SCREEN, args.dense_screen)):
+                     (_native.PD_OPT_DENSE_SCREEN, args.dense_screen),
+                     (_native.PD_OPT_BORDER_LISTS, args.border_lists)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None

@@ -88,7 +88,9 @@ enum pd_option {
                                batched kernels with fp32-chord rows keyed off the query cell
                                (override bits 0 / 2; bit 4 not with PD_OPT_BORDER_ROOTS);
                                bit 5 with bit 3: the count sweep reads each batch's
-                               candidate windows from LDS (fp32, 2-4 D).
+                               candidate windows from LDS (fp32, 2-4 D); bit 6 with bit 3
+                               / bit 7 with bit 4: the count / border kernel compiled for
+                               8 waves per SIMD (at most 64 VGPRs).
                                Default 29 (the measured best on MI355X). */
     PD_OPT_BORDER_ROOTS = 10, /* batched border sweep: skip or stop early where the stencil's
                                 directory words hold at most one cluster root (tuning; same
@@ -134,7 +136,13 @@ enum pd_option {
     PD_OPT_SHARD_CORE_BIT = 19 /* pd_train_end: 1 = the caller guarantees every global id is
                                 < 2^31, so the core flags ride bit 31 of the keys and reach
                                 core_out by one coalesced pass instead of a byte scattered per
-                                owner record (default 0; same outputs) */
+                                owner record (default 0; same outputs) */,
+    PD_OPT_BORDER_LISTS = 20  /* grid path, min_samples <= 33: the count sweep keeps the
+                                neighbours of every record that ends non-core (at most
+                                min_samples - 1) and the owner pass attaches a border point
+                                from that list instead of a second sweep over its candidates
+                                (default 0, measured: C2 count +0.8 ms for border -0.9 ms,
+                                C4 count +6.7 ms for no border gain; same labels either way) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

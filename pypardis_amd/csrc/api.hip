@@ -150,7 +150,7 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         } else if (option == PD_OPT_BORDER_ROOTS)
             ctx->c.border_roots = value != 0;
         else if (option == PD_OPT_SWEEP_VARIANT) {
-            if (value < 0 || value > 63) throw Error(PD_EINVAL, "sweep variant is a 6-bit mask");
+            if (value < 0 || value > 255) throw Error(PD_EINVAL, "sweep variant is an 8-bit mask");
             ctx->c.variant = (int)value;
         } else if (option == PD_OPT_COUNT_ROTATE) {
             if (value < 0 || value > 0x7FFFFFFF) throw Error(PD_EINVAL, "count rotate must be >= 0");
@@ -175,6 +175,8 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.dense_screen = (int)value;
         } else if (option == PD_OPT_SHARD_CORE_BIT) {
             ctx->c.shard_core_bit = value != 0;
+        } else if (option == PD_OPT_BORDER_LISTS) {
+            ctx->c.border_lists = value != 0;
         }
         else
             throw Error(PD_EINVAL, "unknown option");

@@ -41,6 +41,7 @@
 #include <cstring>
 #include <vector>
 
+#include "compact.hpp"
 #include "internal.hpp"
 #include "scan.hpp"
 #include "stream.hpp"
@@ -1386,6 +1387,8 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
                                                        const uint32_t* __restrict__ gmin,
                                                        const uint32_t* __restrict__ cnt_rec,
                                                        const uint2* __restrict__ mn,
+                                                       const uint32_t* __restrict__ blist,
+                                                       const uint32_t* __restrict__ boff,
                                                        uint32_t core_mask,
                                                        uint32_t* __restrict__ key_out,
                                                        uint8_t* __restrict__ core_out,
@@ -1403,11 +1406,23 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
         const bool own = r < R && (v & kOwnerBit);
         const uint8_t fl = own ? core[r] : 0;
         // the record's key: core -> its component's; a border record with a
-        // single neighbour (bit 2) -> that neighbour's if it is core (the
-        // border sweep's smallest core key, over one candidate); else none
+        // list of its neighbours (count sweep) -> the smallest key among the
+        // core ones, a border record with a single neighbour (bit 2) -> that
+        // neighbour's if it is core (the border sweep's smallest core key,
+        // over one candidate); else none
         uint32_t key = kNone;
+        bool listed = false;
         if (fl & 1) {
             key = gmin[par[r]] | core_mask;
+        } else if ((fl & 3) == 2 && blist && boff[r] != kNone) {
+            listed = true;
+            const uint32_t o = boff[r], len = blist[o];
+            for (uint32_t k = 0; k < len; ++k) {
+                const uint32_t j = blist[o + 1 + k];
+                const uint32_t pj = j < R ? par[j] : kNone;
+                const uint32_t kk = pj != kNone ? gmin[pj] : kNone;
+                key = kk < key ? kk : key;
+            }
         } else if ((fl & 7) == 6 && mn) {
             const uint2 m = mn[r];
             const uint32_t j = m.x == r ? m.y : m.x;
@@ -1423,7 +1438,7 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
             if (key != kNone && key_out) key_out[pt] = key;
         }
         // the rest of the border candidates go to the sweep
-        nb += own && (fl & 3) == 2 && !((fl & 4) && mn) ? 1u : 0u;
+        nb += own && (fl & 3) == 2 && !listed && !((fl & 4) && mn) ? 1u : 0u;
     }
     // border candidates (owner record, not core, has a neighbour) per tile;
     // border_list_kernel lists them in order after a scan of the counts
@@ -1435,6 +1450,7 @@ __global__ __launch_bounds__(kBlock) void border_list_kernel(uint32_t R,
                                                              const uint32_t* __restrict__ vals,
                                                              const uint8_t* __restrict__ core,
                                                              int single_done,
+                                                             const uint32_t* __restrict__ boff,
                                                              const uint64_t* __restrict__ tile_off,
                                                              uint32_t* __restrict__ blist) {
     // the owner_kernel tiling: kOwnPer consecutive records per thread, so the
@@ -1446,7 +1462,11 @@ __global__ __launch_bounds__(kBlock) void border_list_kernel(uint32_t R,
     for (int q = 0; q < kOwnPer; ++q) {
         const uint32_t r = r0 + q;
         const uint8_t fl = r < R ? core[r] : 0;
-        cand[q] = r < R && (vals[r] & kOwnerBit) && (fl & 3) == 2 && !(single_done && (fl & 4));
+        // (owner_kernel's rule: listed records and, without a list, single-
+        // neighbour records are attached there)
+        const bool listed = boff && r < R && (fl & 3) == 2 && boff[r] != kNone;
+        cand[q] = r < R && (vals[r] & kOwnerBit) && (fl & 3) == 2 && !listed &&
+                  !(single_done && (fl & 4));
         nc += cand[q] ? 1u : 0u;
     }
     uint32_t btot;
@@ -1857,19 +1877,56 @@ __device__ __forceinline__ void row_range3(const Cells& C, const Count3Grid<T, D
     e = e > s ? e : s;
 }
 
-template <typename T, int D, int M, bool ST>
-__global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs, uint32_t R,
+// Border lists (PD_OPT_BORDER_LISTS, min_samples <= kListMax + 1 = 33): a record
+// that ends the sweep non-core has met every neighbour it has (no early exit
+// below min_samples), at most min_samples - 1 of them.  The sweep keeps its
+// hits in LDS as it goes (slot = hits so far, lane fastest: conflict-free)
+// and, at the end, a non-core record with a neighbour besides itself writes
+// them to a compact list — [len, hits...] at BorderLists::off[r], one
+// wave-aggregated reservation per wave.  The owner pass then attaches such a
+// border record from its list (the smallest key among its core neighbours:
+// one gather per hit) instead of a second sweep over every candidate; a
+// record whose list did not fit (cap) gets kNone and is swept as before.
+constexpr int kListMax = 32;
+
+// The list buffer is cut into kListStripes stripes, each with its own
+// reservation counter (stripe = block id mod kListStripes): one counter for
+// every wave of the grid serialised ~1.6e6 same-address atomics on C2.
+constexpr uint32_t kListStripes = 256;
+
+struct BorderLists {
+    uint32_t* list;    // [kListStripes * cap]: per listed record len, then len hit records
+    uint32_t* off;     // [R]: list offset of a non-core record with a neighbour, or kNone
+    uint32_t* count;   // [kListStripes]: entries reserved so far in each stripe
+    uint32_t cap;      // entries per stripe
+};
+
+// WPE: the minimum waves per SIMD the register allocation must allow (1: no
+// constraint; 8: at most 64 VGPRs — PD_OPT_SWEEP_VARIANT bit 6)
+template <typename T, int D, int M, bool ST, bool LST, int WPE = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void count4_kernel(const T* __restrict__ Xs, uint32_t R,
                                                         Cells C, double eps, double eps2,
                                                         float lo, float hi, uint32_t ms, int full,
                                                         uint32_t rot_min,
                                                         uint8_t* __restrict__ core,
                                                         uint32_t* __restrict__ mn_out,
                                                         uint32_t* __restrict__ cnt_out,
-                                                        unsigned long long* __restrict__ stats) {
+                                                        unsigned long long* __restrict__ stats,
+                                                        BorderLists BL) {
     constexpr int NR = NRows<D>::v;
     constexpr int B = NR < 3 ? NR : 3, NB = NR / B;
-    const uint32_t r = rec_index();
-    if (r >= R) return;
+    // LST: min_samples - 1 hit slots per lane (dynamic LDS, lane fastest)
+    // (not named L: the neighbourhood index of with_part's body is)
+    extern __shared__ uint32_t s_list_dyn[];
+    const uint32_t n_slots = ms > 1 ? ms - 1 : 1;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t* s_hit = s_list_dyn + (size_t)wv * n_slots * 64 + lane;
+    (void)s_hit;
+    const uint32_t r0 = rec_index();
+    // with lists the whole wave stays to the end (the reservation scans it)
+    if (!LST && r0 >= R) return;
+    const bool live = r0 < R;
+    const uint32_t r = live ? r0 : R - 1;
     double a[D];
     load_rec<T, D>(Xs, r, a);
     const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
@@ -1918,6 +1975,9 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const bool h = (v + u < tot) && pr(b[u]);
+                        if constexpr (LST) {
+                            if (h && cnt < n_slots) s_hit[cnt * 64] = j[u];
+                        }
                         cnt += h ? 1u : 0u;
                         const uint32_t x = h ? j[u] : kNone;
                         mn2 = min(mn2, max(mn, x));   // the two smallest hits
@@ -1932,6 +1992,33 @@ __global__ __launch_bounds__(kBlock) void count4_kernel(const T* __restrict__ Xs
             if (stopped) return;
         }
     });
+    if constexpr (LST) {
+        // non-core with a neighbour besides itself: its hits (self included)
+        // go to the compact list; the whole wave is active here
+        const bool want = live && cnt >= 2 && cnt < ms;
+        const uint32_t need = want ? cnt + 1u : 0u;
+        uint32_t incl = need;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t wtot = (uint32_t)__shfl((int)incl, 63, 64);
+        const uint32_t stripe = blockIdx.x % kListStripes;
+        uint32_t base = 0;
+        if (lane == 0 && wtot) base = atomicAdd(BL.count + stripe, wtot);
+        base = (uint32_t)__shfl((int)base, 0, 64) + (incl - need);
+        if (want) {
+            const bool fits = (uint64_t)base + need <= (uint64_t)BL.cap;
+            const uint32_t o = stripe * BL.cap + base;
+            BL.off[r] = fits ? o : kNone;
+            if (fits) {
+                BL.list[o] = cnt;
+                for (uint32_t k = 0; k < cnt; ++k) BL.list[o + 1 + k] = s_hit[k * 64];
+            }
+        }
+        if (!live) return;
+    }
     // bit 2: exactly one neighbour besides the record itself (no early exit
     // below min_samples, so the sweep saw it, and it is the other of the two
     // smallest hits): owner_kernel attaches such a border record directly
@@ -3019,8 +3106,8 @@ __global__ __launch_bounds__(kBlock) void border2_kernel(
 // border4_kernel (PD_OPT_SWEEP_VARIANT bit 4, the default): border2's plain
 // sweep (the smallest cluster key among the core neighbours, every row) with
 // count4's cheap rows.
-template <typename T, int D, int M>
-__global__ __launch_bounds__(kBlock) void border4_kernel(
+template <typename T, int D, int M, int WPE = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void border4_kernel(
     const T* __restrict__ Xs, uint32_t NL, const uint32_t* __restrict__ list, Cells C, double eps,
     double eps2, float lo, float hi, const uint32_t* __restrict__ vals,
     const uint32_t* __restrict__ par, const uint32_t* __restrict__ gmin,
@@ -3293,10 +3380,18 @@ void cell_roots(Ctx& ctx, hipStream_t s, uint32_t R, const uint32_t* cstart, con
 // Launch helpers for the three neighbour sweeps: bit k of `variant`
 // (PD_OPT_SWEEP_VARIANT) selects the batched lane kernel for sweep k (0
 // count, 1 link, 2 border) instead of the row-by-row one.
+// Whether the count sweep records border lists (count4 only, min_samples <=
+// kListMax + 1, PD_OPT_BORDER_LISTS).
+inline bool border_lists_on(const Ctx& ctx, uint32_t ms) {
+    return ctx.border_lists && (ctx.variant & 8) && (ctx.variant & 40) != 40 &&
+           ms <= (uint32_t)kListMax + 1u;
+}
+
 template <typename T, int D, int M, bool ST>
 void launch_count(int variant, hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double eps,
                   double eps2, float lo, float hi, uint32_t ms, int full, uint32_t rot_min,
-                  uint8_t* core, uint32_t* mn, uint32_t* cnt, unsigned long long* st) {
+                  uint8_t* core, uint32_t* mn, uint32_t* cnt, unsigned long long* st,
+                  const BorderLists* bl = nullptr) {
     constexpr bool kStageable = std::is_same<T, float>::value && (D >= 2 && D <= 4);
     if constexpr (kStageable) {
         if ((variant & 40) == 40) {   // cheap rows + LDS-staged windows
@@ -3305,9 +3400,29 @@ void launch_count(int variant, hipStream_t s, const T* Xs, uint32_t R, const Cel
             return;
         }
     }
-    if (variant & 8)   // cheap rows
-        hipLaunchKernelGGL((count4_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs,
-                           R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
+    if ((variant & 8) && bl)   // cheap rows, border lists (min_samples - 1 LDS slots per lane)
+        hipLaunchKernelGGL((count4_kernel<T, D, M, ST, true>), dim3(blocks(R)), dim3(kBlock),
+                           (size_t)kBlock * (ms > 1 ? ms - 1 : 1) * sizeof(uint32_t), s,
+                           Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st, *bl);
+    else if constexpr (!ST) {
+        if ((variant & 72) == 72)   // cheap rows, registers for 8 waves per SIMD
+            hipLaunchKernelGGL((count4_kernel<T, D, M, false, false, 8>), dim3(blocks(R)),
+                               dim3(kBlock), 0, s, Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min,
+                               core, mn, cnt, st, BorderLists{nullptr, nullptr, nullptr, 0u});
+        else if (variant & 8)
+            hipLaunchKernelGGL((count4_kernel<T, D, M, false, false>), dim3(blocks(R)),
+                               dim3(kBlock), 0, s, Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min,
+                               core, mn, cnt, st, BorderLists{nullptr, nullptr, nullptr, 0u});
+        else if (variant & 1)
+            hipLaunchKernelGGL((count2_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
+                               C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
+        else
+            hipLaunchKernelGGL((count_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
+                               C, eps, eps2, lo, hi, ms, full, core, mn, cnt, st);
+    } else if (variant & 8)   // cheap rows
+        hipLaunchKernelGGL((count4_kernel<T, D, M, ST, false>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                           Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st,
+                           BorderLists{nullptr, nullptr, nullptr, 0u});
     else if (variant & 1)
         hipLaunchKernelGGL((count2_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
                            C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
@@ -3333,7 +3448,10 @@ void launch_border(int variant, hipStream_t s, const T* Xs, uint32_t NL, const u
                    const Cells& C, double eps, double eps2, float lo, float hi,
                    const uint32_t* vals, const uint32_t* par, const uint32_t* gmin,
                    const uint32_t* wroot, uint32_t* key_out, uint32_t* rec_out = nullptr) {
-    if ((variant & 16) && !wroot)   // cheap rows
+    if ((variant & 144) == 144 && !wroot)   // cheap rows, registers for 8 waves per SIMD
+        hipLaunchKernelGGL((border4_kernel<T, D, M, 8>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs,
+                           NL, list, C, eps, eps2, lo, hi, vals, par, gmin, key_out, rec_out);
+    else if ((variant & 16) && !wroot)   // cheap rows
         hipLaunchKernelGGL((border4_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
                            list, C, eps, eps2, lo, hi, vals, par, gmin, key_out, rec_out);
     else if (variant & 4)
@@ -3350,17 +3468,8 @@ template <typename Pred>
 uint32_t select_records(Ctx& ctx, const char* name, uint32_t R, Pred pred, uint32_t** out,
                         hipStream_t s) {
     uint32_t* list = ctx.arena.get<uint32_t>(name, R);
-    uint32_t* dcount = ctx.arena.get<uint32_t>("sel_count", 4);
-    rocprim::counting_iterator<uint32_t> it(0u);
-    size_t tb = 0;
-    PD_HIP(rocprim::select(nullptr, tb, it, list, dcount, (size_t)R, pred, s));
-    void* tmp = ctx.arena.get<char>("sel_tmp", tb);
-    PD_HIP(rocprim::select(tmp, tb, it, list, dcount, (size_t)R, pred, s));
-    uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t));
-    PD_HIP(hipMemcpyAsync(h, dcount, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    sync(s);
     *out = list;
-    return *h;
+    return (uint32_t)compact_ordered(ctx, "sel_cmp", (uint64_t)R, pred, list, nullptr, s);
 }
 
 // Phase A: halo records, sort, cell directory, core counts, union-find,
@@ -3573,17 +3682,30 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         PD_HIP(hipMemsetAsync(sst, 0, sizeof(unsigned long long) * 10, s));
     }
     const int mode = ctx.link_mode;
+    // border lists: entries <= min_samples per listed record; the cap bounds
+    // the buffer (records beyond it are swept in phase B as before)
+    BorderLists bl{nullptr, nullptr, nullptr, 0u};
+    const bool lists = R && border_lists_on(ctx, (uint32_t)a.min_samples);
+    if (lists) {
+        const uint64_t want = (uint64_t)R * (uint64_t)std::max(a.min_samples, 2) / 2 + 64;
+        const uint64_t tot = std::min<uint64_t>(want, 1ull << 29);
+        bl.cap = (uint32_t)(tot / kListStripes + 64);
+        bl.list = ctx.arena.get<uint32_t>("blist", (size_t)bl.cap * kListStripes);
+        bl.off = ctx.arena.get<uint32_t>("blist_off", R);
+        bl.count = ctx.arena.get<uint32_t>("blist_count", kListStripes);
+        PD_HIP(hipMemsetAsync(bl.count, 0, sizeof(uint32_t) * kListStripes, s));
+    }
     if (R) {
         if (sst)
             launch_count<T, D, M, true>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
                                         (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
                                         ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu,
-                                        core, mn, cnt_rec, sst);
+                                        core, mn, cnt_rec, sst, lists ? &bl : nullptr);
         else
             launch_count<T, D, M, false>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
                                          (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
                                          ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu,
-                                         core, mn, cnt_rec, sst);
+                                         core, mn, cnt_rec, sst, lists ? &bl : nullptr);
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 5
@@ -3796,6 +3918,8 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     st.cnt_rec = cnt_rec;
     st.mn = mn;
     st.wroot = wroot_final;
+    st.blist = lists ? bl.list : nullptr;
+    st.blist_off = lists ? bl.off : nullptr;
     st.n_exports = 0;
     if (a.phase == 1 && R && a.xr) {
         uint32_t* elist = nullptr;
@@ -3866,13 +3990,14 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         // the rest
         const bool single = (ctx.variant & 8) && st.mn;
         hipLaunchKernelGGL(owner_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core, par, gmin,
-                           st.cnt_rec, single ? (const uint2*)st.mn : nullptr, core_mask,
+                           st.cnt_rec, single ? (const uint2*)st.mn : nullptr, st.blist,
+                           st.blist_off, core_mask,
                            bucketed ? nullptr : key_out, a.core, a.counts,
                            tcnt, recs);
         const uint32_t NB = (uint32_t)tile_offsets(ctx, tcnt, tiles, toff, s, true);
         if (NB)
             hipLaunchKernelGGL(border_list_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core,
-                               single ? 1 : 0, toff, blist);
+                               single ? 1 : 0, st.blist ? st.blist_off : nullptr, toff, blist);
         if (NB)
             launch_border<T, D, M>(ctx.variant, s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par,
                                    gmin, st.wroot, key_out, recs ? (uint32_t*)recs + 1 : nullptr);

@@ -82,6 +82,8 @@ struct PhaseState {
     uint32_t* cnt_rec = nullptr;
     uint32_t* mn = nullptr;      // per record: the two smallest neighbours the count sweep saw
     uint32_t* wroot = nullptr;   // directory-word roots of the final forest (border fast path)
+    uint32_t* blist = nullptr;   // border lists of the count sweep (null: none this train)
+    uint32_t* blist_off = nullptr;
     uint32_t* exp_gid = nullptr;
     uint32_t* exp_key = nullptr;
 };
@@ -167,6 +169,7 @@ struct Ctx {
                                  // more directory words than points
     int dense_prune = 1;         // dense count pass: projection-window tiles only (2: per-band runs)
     bool shard_core_bit = false; // PD_OPT_SHARD_CORE_BIT: sharded phase B keys carry the core flag
+    bool border_lists = false;   // PD_OPT_BORDER_LISTS: count sweep lists border neighbours
     int dense_screen = 1;        // dense count pass screen: 1 e4m3 (32x32x64), 0 bf16 hi.hi
     bool sort_payload = false;   // fp32 3-D: coordinates ride the sort (PD_OPT_SORT_PAYLOAD)
     int label_buckets = -1;      // labels to input order by bucketed pair passes (PD_OPT_LABEL_BUCKETS;

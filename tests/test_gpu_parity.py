@@ -231,7 +231,7 @@ def test_train_matches_oracle(native, case):
 @pytest.mark.parametrize("variant,link_mode,border_roots",
                          [(0, 5, 0), (7, 3, 1), (5, 0, 0), (7, 2, 0), (5, 4, 0), (5, 3, 0),
                           (5, 6, 0), (0, 6, 0), (13, 6, 0), (15, 3, 1), (8, 0, 0), (29, 6, 0),
-                          (24, 3, 0), (61, 6, 0), (40, 0, 0), (45, 3, 1)])
+                          (24, 3, 0), (61, 6, 0), (40, 0, 0), (45, 3, 1), (221, 6, 0)])
 def test_sweep_variants_exact(native, variant, link_mode, border_roots):
     """PD_OPT_SWEEP_VARIANT x PD_OPT_LINK_MODE: the row-by-row and the
     batched sweep kernels, and the sampled-union + cell-verify link (3) or the
@@ -273,6 +273,48 @@ def test_sweep_variants_exact(native, variant, link_mode, border_roots):
         ctx.set_option(native.PD_OPT_SWEEP_VARIANT, native.SWEEP_VARIANT_DEFAULT)
         ctx.set_option(native.PD_OPT_LINK_MODE, native.LINK_MODE_DEFAULT)
         ctx.set_option(native.PD_OPT_BORDER_ROOTS, 0)
+
+
+@pytest.mark.parametrize("lists", [1, 0])
+def test_border_lists_exact(native, lists):
+    """PD_OPT_BORDER_LISTS: border points attached from the count sweep's
+    neighbour lists (on) or by the second sweep (off) give the oracle's
+    labels: every CASES set, min_samples 2 / 20 / 33 (the largest listed) /
+    34 (beyond: swept), full counts, the sharded phases (1-rank RCCL) and the
+    goldens."""
+    from pypardis_amd import DBSCAN, distributed, synth
+    ctx = native.context()
+    ctx.set_option(native.PD_OPT_BORDER_LISTS, lists)
+    try:
+        for _, kw, eps, ms, metric, P in CASES:
+            X = synth.blobs_noise(**kw)
+            lab_o, core_o, cnt_o, _ = oracle.dbscan(X, eps, ms, metric)
+            m = DBSCAN(eps=eps, min_samples=ms, metric=metric, max_partitions=P).train(_dev(X))
+            assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o), kw
+            assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_o), kw
+            lab, core, ncl, cnt = _cluster(native, X, eps, ms, metric, full=True)
+            assert np.array_equal(cnt, cnt_o) and np.array_equal(lab, lab_o), kw
+        X = synth.blobs_noise(40_000, 3, side=5.0, n_centers=4, sigma=0.3, noise_frac=0.3,
+                              seed=71)
+        for ms in (2, 20, 33, 34):
+            lab_o, core_o, _, _ = oracle.dbscan(X, 0.06, ms)
+            m = DBSCAN(eps=0.06, min_samples=ms, max_partitions=6).train(_dev(X))
+            assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o), ms
+            assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_o), ms
+        comm = distributed.device_comms([0])[0]
+        res = distributed.train_threads([_dev(X)], 0.06, 10, [comm],
+                                        [distributed.NativeOps(torch.device("cuda", 0))],
+                                        max_partitions=8)
+        lab_o, core_o, _, _ = oracle.dbscan(X, 0.06, 10)
+        np.testing.assert_array_equal(res[0].local_labels.cpu().numpy().astype(np.int64), lab_o)
+        np.testing.assert_array_equal(res[0].local_core.cpu().numpy(), core_o)
+        for name in ("b3d_20k", "b2d_20k", "c0_p5_cityblock", "dup_1d"):
+            gd = load_golden(name)
+            lab, core, _ = _cluster(native, gd["X"], float(gd["eps"]), int(gd["min_samples"]),
+                                    _metric(gd))
+            assert np.array_equal(lab, gd["sk_labels"]) and np.array_equal(core, gd["sk_core"])
+    finally:
+        ctx.set_option(native.PD_OPT_BORDER_LISTS, 0)
 
 
 def test_fp64_input_exact(native):

@@ -24,6 +24,22 @@ print('v$v rep$rep', round(b['ms_per_step'],2), 'count', s['count'], 'border', s
       'staged', w.get('s_count_staged'), '/', w.get('s_count_batches'), 'cand', w.get('s_count_cand'))"
   done
 done
+# ABX: '|'-separated bench argument sets, alternated twice (e.g. "--border-lists 0|--border-lists 1")
+if [ -n "${ABX:-}" ]; then
+  IFS='|' read -ra SETS <<< "$ABX"
+  for rep in 1 2; do
+    i=0
+    for a in "${SETS[@]}"; do
+      i=$((i+1))
+      timeout -k 10 300 python -u bench.py --config ${CFG:-C2} --steps 10 --warmup 2 --no-cpu --no-host \
+          $a --json-out gpurun_out/r4_abx_${i}_$rep.json > gpurun_out/r4_abx_${i}_$rep.log 2>&1 \
+          || { tail -5 gpurun_out/r4_abx_${i}_$rep.log; exit 1; }
+      python -c "
+import json; b=json.load(open('gpurun_out/r4_abx_${i}_$rep.json')); s=b['stages_ms']
+print('[$a] rep$rep', round(b['ms_per_step'],2), {k: s[k] for k in ('count','link','border','roots','label') if k in s})"
+    done
+  done
+fi
 if [ -n "${PMCV:-}" ]; then
   export PROF_VARIANT=$PMCV PROF_REPS=1
   T=_v$PMCV

@@ -91,7 +91,7 @@ enum pd_option {
                                candidate windows from LDS (fp32, 2-4 D); bit 6 with bit 3
                                / bit 7 with bit 4: the count / border kernel compiled for
                                8 waves per SIMD (at most 64 VGPRs).
-                               Default 29 (the measured best on MI355X). */
+                               Default 221 = 29 | 64 | 128 (the measured best on MI355X). */
     PD_OPT_BORDER_ROOTS = 10, /* batched border sweep: skip or stop early where the stencil's
                                 directory words hold at most one cluster root (tuning; same
                                 labels; default 0 — slower on C2) */

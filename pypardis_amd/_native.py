@@ -34,7 +34,7 @@ PD_OPT_DIR_PAGED = 17
 PD_OPT_DENSE_SCREEN = 18
 PD_OPT_SHARD_CORE_BIT = 19
 PD_OPT_BORDER_LISTS = 20
-SWEEP_VARIANT_DEFAULT = 29
+SWEEP_VARIANT_DEFAULT = 221
 LINK_MODE_DEFAULT = 6
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",

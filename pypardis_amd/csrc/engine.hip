@@ -704,7 +704,7 @@ __device__ __forceinline__ K key_of(const T (&tv)[D], const KeyGrid<D>& g) {
 // computed for all lanes at once and stored after the loop, so one step's
 // stores are contiguous; the extra records of the few halo duplicates follow.
 template <typename T, int D, typename K, bool MASK>
-__global__ __launch_bounds__(kBlock) void halo_write_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void halo_write_kernel(
     const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
     const int32_t* __restrict__ owner, KdTree tree, const uint64_t* __restrict__ tile_off,
     K* __restrict__ keys, uint32_t* __restrict__ vals, float4* __restrict__ pay) {
@@ -1258,28 +1258,70 @@ __global__ __launch_bounds__(kBlock) void roots_kernel(uint32_t R, const uint32_
                                                        uint32_t* __restrict__ gmin,
                                                        uint32_t* __restrict__ root_list,
                                                        uint32_t* __restrict__ counts, int stats) {
+    // kSubTiles record tiles of kBlock per block; a lane's kSubTiles records
+    // are read together (parents, first parent step, point ids) and their
+    // minima folded per root in the lane before the wave-aggregated atomics:
+    // one aggregation per distinct root of the lane (usually one), not one
+    // per record
     uint32_t ncore = 0;
-    for (int q = 0; q < kSubTiles; ++q) {   // kSubTiles record tiles of kBlock per block
-        const uint32_t r = (blockIdx.x * kSubTiles + q) * kBlock + threadIdx.x;
-        const uint32_t x0 = r < R ? par[r] : kNone;
-        const bool core = x0 != kNone;
-        uint32_t root = 0;
-        if (core) {
-            uint32_t x = x0;
+    uint32_t rr[kSubTiles], x0[kSubTiles], root[kSubTiles], pt[kSubTiles];
+    bool core[kSubTiles];
+#pragma unroll
+    for (int q = 0; q < kSubTiles; ++q) {
+        rr[q] = (blockIdx.x * kSubTiles + q) * kBlock + threadIdx.x;
+        x0[q] = rr[q] < R ? par[rr[q]] : kNone;
+        core[q] = x0[q] != kNone;
+    }
+#pragma unroll
+    for (int q = 0; q < kSubTiles; ++q) {
+        root[q] = core[q] ? par[x0[q]] : 0u;   // the first step, all four in flight
+        pt[q] = core[q] ? (vals[rr[q]] & kIdMask) : kNone;
+    }
+#pragma unroll
+    for (int q = 0; q < kSubTiles; ++q) {
+        if (!core[q]) continue;
+        uint32_t x = root[q] == x0[q] ? x0[q] : root[q];
+        if (x != x0[q]) {   // longer chain (rare after the link's flattening)
             while (true) {
                 const uint32_t p = par[x];
                 if (p == x) break;
                 x = p;
             }
-            if (x != x0) par[r] = x;
-            root = x;
+            par[rr[q]] = x;
         }
-        uint32_t pt = core ? (vals[r] & kIdMask) : kNone;
-        if (core && gid) pt = gid[pt];
-        wave_atomic_min(gmin, core, root, pt);
-        // roots are rare (one per component): a wave-aggregated append is cheap
-        if (root_list) wave_append(root_list, counts, core && root == r, r);
-        ncore += core ? 1u : 0u;
+        root[q] = x;
+        if (gid) pt[q] = gid[pt[q]];
+        ncore += 1u;
+    }
+    bool left[kSubTiles];
+#pragma unroll
+    for (int q = 0; q < kSubTiles; ++q) left[q] = core[q];
+    while (true) {
+        // the lane's first remaining root and the smallest point id under it
+        bool have = false;
+        uint32_t key = 0, m = kNone;
+#pragma unroll
+        for (int q = 0; q < kSubTiles; ++q) {
+            if (left[q] && !have) {
+                have = true;
+                key = root[q];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kSubTiles; ++q) {
+            if (left[q] && root[q] == key) {
+                m = pt[q] < m ? pt[q] : m;
+                left[q] = false;
+            }
+        }
+        if (!__any(have)) break;
+        wave_atomic_min(gmin, have, key, m);
+    }
+    // roots are rare (one per component): a wave-aggregated append is cheap
+    if (root_list) {
+#pragma unroll
+        for (int q = 0; q < kSubTiles; ++q)
+            wave_append(root_list, counts, core[q] && root[q] == rr[q], rr[q]);
     }
     if (stats) {   // core records (sweep statistics): one atomic per block
         const uint32_t c = block_sum_u32(ncore);
@@ -2866,7 +2908,7 @@ __global__ __launch_bounds__(kBlock) void flag_list_kernel(const uint8_t* __rest
 // whose words hold another root, the neighbouring cells whose root differs
 // are deferred as cell pairs.
 template <typename T, int D, int M, typename K>
-__global__ __launch_bounds__(kBlock) void cell_verify_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void cell_verify_kernel(
     const T* __restrict__ Xs, const K* __restrict__ keys, const uint32_t* __restrict__ clist,
     uint32_t nlist, const uint32_t* __restrict__ croot, const uint32_t* __restrict__ wroot,
     Cells C, int xsub, double eps, double eps2, float lo, float hi, uint32_t* __restrict__ par,

@@ -174,7 +174,7 @@ struct Ctx {
     bool sort_payload = false;   // fp32 3-D: coordinates ride the sort (PD_OPT_SORT_PAYLOAD)
     int label_buckets = -1;      // labels to input order by bucketed pair passes (PD_OPT_LABEL_BUCKETS;
                                  // -1: from 2^28 points on, where they beat the direct scatter)
-    int variant = 29;            // PD_OPT_SWEEP_VARIANT: cheap-row count (bit 3; bit 0 the batched
+    int variant = 221;           // PD_OPT_SWEEP_VARIANT: cheap-row count (bit 3; bit 0 the batched
                                  // count2), cheap-row border (bit 4; bit 2 the batched border2),
                                  // row-wise link
     Timings t;

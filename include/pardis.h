@@ -142,7 +142,10 @@ enum pd_option {
                                 min_samples - 1) and the owner pass attaches a border point
                                 from that list instead of a second sweep over its candidates
                                 (default 0, measured: C2 count +0.8 ms for border -0.9 ms,
-                                C4 count +6.7 ms for no border gain; same labels either way) */
+                                C4 count +6.7 ms for no border gain; same labels either way) */,
+    PD_OPT_LINK_JUMPS = 21    /* link modes 3-6: pointer-jumping rounds over the count pass's
+                                smallest-neighbour forest before the window union (default 0;
+                                same labels) */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -34,6 +34,7 @@ PD_OPT_DIR_PAGED = 17
 PD_OPT_DENSE_SCREEN = 18
 PD_OPT_SHARD_CORE_BIT = 19
 PD_OPT_BORDER_LISTS = 20
+PD_OPT_LINK_JUMPS = 21
 SWEEP_VARIANT_DEFAULT = 221
 LINK_MODE_DEFAULT = 6
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",

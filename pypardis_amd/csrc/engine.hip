@@ -704,7 +704,7 @@ __device__ __forceinline__ K key_of(const T (&tv)[D], const KeyGrid<D>& g) {
 // computed for all lanes at once and stored after the loop, so one step's
 // stores are contiguous; the extra records of the few halo duplicates follow.
 template <typename T, int D, typename K, bool MASK>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void halo_write_kernel(
+__global__ __launch_bounds__(kBlock) void halo_write_kernel(
     const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
     const int32_t* __restrict__ owner, KdTree tree, const uint64_t* __restrict__ tile_off,
     K* __restrict__ keys, uint32_t* __restrict__ vals, float4* __restrict__ pay) {
@@ -2908,7 +2908,7 @@ __global__ __launch_bounds__(kBlock) void flag_list_kernel(const uint8_t* __rest
 // whose words hold another root, the neighbouring cells whose root differs
 // are deferred as cell pairs.
 template <typename T, int D, int M, typename K>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void cell_verify_kernel(
+__global__ __launch_bounds__(kBlock) void cell_verify_kernel(
     const T* __restrict__ Xs, const K* __restrict__ keys, const uint32_t* __restrict__ clist,
     uint32_t nlist, const uint32_t* __restrict__ croot, const uint32_t* __restrict__ wroot,
     Cells C, int xsub, double eps, double eps2, float lo, float hi, uint32_t* __restrict__ par,
@@ -3756,6 +3756,10 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     if (R && (mode == 3 || mode == 4 || mode == 5 || mode == 6)) {
         // forest from the count pass's smallest neighbour (links across rows)
         hipLaunchKernelGGL(init_kernel, dim3(sub_blocks(R)), dim3(kBlock), 0, s, R, core, mn, 1, par);
+        // PD_OPT_LINK_JUMPS: pointer jumping over the smallest-neighbour
+        // forest (its chains run across a row's cells) before the window union
+        for (int it = 0; it < ctx.link_jumps; ++it)
+            hipLaunchKernelGGL(jump_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
         if (mode != 6)
             hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
         if (mode == 6) {

@@ -156,6 +156,7 @@ struct Ctx {
                                  // 3 centre-row union + cell verify;
                                  // 4 cell verify alone; 0 init forest + jumps + union sweep; 2 union sweep only
     int jump_rounds = 4;
+    int link_jumps = 0;          // PD_OPT_LINK_JUMPS
     int xsub = 2;                // axis-0 sub-cells per eps
     int centre_window = -1;      // link modes 5/6: records after each record tested (2..64);
                                  // mode 3: forward candidates per centre-row union (0: all);

@@ -112,3 +112,45 @@ def test_bench_gpus2_rehearse_line():
     assert rec["value"] > 0 and rec["ms_per_step"] > 0
     st = rec["shard_stats"]
     assert st["rank"] in (0, 1) and len(st["rank_seconds"]) == 2
+
+
+def test_train_roofline_sums_kernels_times_launches():
+    """bench.train_roofline: every kernel's per-launch PMC bytes x its
+    launches per train, over the step time (the whole train's HBM fraction)."""
+    b = _bench()
+    pmc = {"_meta": {"trains": 2},
+           "count4_kernel": {"hbm_bytes_per_launch": 3.0e9, "dispatches_per_train": 1.0},
+           "trampoline_kernel": {"hbm_bytes_per_launch": 2.0e9, "dispatches_per_train": 5.0},
+           "no_bytes_kernel": {"SQ_WAVES": 10.0}}
+    r = b.train_roofline(pmc, "x.json", 10.0)
+    assert r["bytes_per_train"] == 13.0e9
+    assert abs(r["achieved_gbs"] - 1300.0) < 1e-6
+    assert abs(r["frac"] - 1300.0 / 8000.0) < 1e-12
+    assert list(r["top_kernels_bytes"]) == ["trampoline_kernel", "count4_kernel"]
+    assert b.train_roofline({"count4_kernel": {"hbm_bytes_per_launch": 1.0}}, "old", 10.0) is None
+
+
+def test_pmc_summary_counts_launches_per_train(tmp_path, monkeypatch):
+    """tools/pmc_summary.py: mean counter value per dispatch (summed over the
+    counter's instances) and dispatches per profiled train."""
+    import csv
+    d = tmp_path / "pmc_1"
+    d.mkdir()
+    with open(d / "p_counter_collection.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Counter_Name", "Counter_Value",
+                                          "Dispatch_Id"])
+        w.writeheader()
+        for disp in (1, 2, 3, 4):   # two trains x two launches of one kernel
+            for inst in range(2):
+                w.writerow({"Kernel_Name": "void pd::gather_kernel<float, 3>(float const*)",
+                            "Counter_Name": "FETCH_SIZE", "Counter_Value": 5.0,
+                            "Dispatch_Id": disp})
+    monkeypatch.setenv("PROF_REPS", "2")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), str(d)],
+                         capture_output=True, text=True, env=dict(os.environ), check=True)
+    s = json.loads(out.stdout)
+    g = s["gather_kernel"]
+    assert g["FETCH_SIZE"] == 10.0                 # two instances summed per dispatch
+    assert g["dispatches_per_train"] == 2.0
+    assert g["hbm_bytes_per_launch"] == 2 * 10.0 * 1024
+    assert s["_meta"]["trains"] == 2

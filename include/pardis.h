@@ -143,9 +143,12 @@ enum pd_option {
                                 from that list instead of a second sweep over its candidates
                                 (default 0, measured: C2 count +0.8 ms for border -0.9 ms,
                                 C4 count +6.7 ms for no border gain; same labels either way) */,
-    PD_OPT_LINK_JUMPS = 21    /* link modes 3-6: pointer-jumping rounds over the count pass's
+    PD_OPT_LINK_JUMPS = 21,   /* link modes 3-6: pointer-jumping rounds over the count pass's
                                 smallest-neighbour forest before the window union (default 0;
                                 same labels) */
+    PD_OPT_DENSE_PREFETCH = 22 /* d > 4, e4m3 count pass: streamed tiles in flight per block
+                                (2, 4 or 8; a register ring ahead of the LDS stage).  Same
+                                counts either way */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

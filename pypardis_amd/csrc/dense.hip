@@ -329,8 +329,13 @@ struct TileLds8 {
 // KS MFMAs per wave) at one wave per SIMD.
 constexpr int kF8Waves = 3;   // e4m3 count pass: waves per SIMD (no bf16 query fragments held)
 constexpr int kF8QT = 2;      // e4m3 count pass: query tiles (of 32) per wave
-template <typename T, int MODE, int KS, int QT, bool F8>
+// PF: streamed tiles in flight per block (a register ring; the staged tile
+// in LDS aside).  A streamed tile mostly misses L2 (C3: hit 0.24) and comes
+// from the fabric, so the count pass's block of 4 waves needs more than the
+// two tiles of the first form in flight (5 VGPRs per e4m3 stage).
+template <typename T, int MODE, int KS, int QT, bool F8, int PF = 2>
 __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu(F8 ? (KS >= 8 ? 1 : kF8Waves) : ((KS >= 8 || QT > 2) ? 1 : 2)))) void tile_kernel(TileArgs<T> A) {
+    static_assert(PF >= 2 && PF <= 8, "tiles in flight");
     constexpr int TB = tile_threads(KS, MODE);
     constexpr int QW = 32 * QT;                  // query rows per wave
     constexpr int KS8 = (KS + 3) / 4;            // e4m3 k-steps of 64 dims
@@ -528,13 +533,16 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
     };
     // staging: thread k moves 16-byte chunks c = k + q * TB of the tile
     // (hi then lo), plus one norm per thread < 64
-    // Two register stages: the tile two ahead is in flight while the next
-    // one is committed (a streamed tile often misses L2 under pruning)
+    // PF register stages: the tiles up to PF ahead are in flight while the
+    // next one is committed (a streamed tile often misses L2 under pruning)
     struct Stage {
         bf16x8 v[NCH];
         float n;
     };
-    Stage stA, stB;
+    Stage st[PF];
+    uint32_t jq[PF];   // first row of the tile in each stage
+#pragma unroll
+    for (int k = 0; k < PF; ++k) jq[k] = 0u;
     auto fetch = [&](Stage& st, uint32_t j0) {
 #pragma unroll
         for (int q = 0; q < NCH; ++q) {
@@ -571,22 +579,43 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
         if (threadIdx.x < kTile)
             S.nta[buf][threadIdx.x] = -((1.0f + kBandC) * 0.5f) * st.n * (F8 ? kF8Acc : 1.0f);
     };
-    // cursors: current tile (in LDS buf), next (in `ready`), the one after
+    // cursors: current tile (in LDS buf), the frontier (the last tile
+    // fetched) and nq tiles fetched beyond the current one (the stages after
+    // the current tile's, in ring order)
     uint32_t sg = 0, j0 = seg_lo[0];
     bool have = seek(sg, j0);
     if (have) {
-        fetch(stA, j0);
-        commit(stA, 0);
+        fetch(st[0], j0);
+        commit(st[0], 0);
     }
-    uint32_t sn = sg, jn = j0 + kTile;
-    bool more = have && seek(sn, jn);
-    if (more) fetch(stB, jn);
+    uint32_t fs = sg, fj = j0;
+    bool fmore = have;
+    int nq = 0;
+#pragma unroll
+    for (int k = 1; k < PF; ++k) {
+        if (fmore) {
+            fj += kTile;
+            fmore = seek(fs, fj);
+        }
+        if (fmore) {
+            fetch(st[k], fj);
+            jq[k] = fj;
+            ++nq;
+        }
+    }
     __syncthreads();
     int buf = 0;
-    auto step = [&](Stage& ready, Stage& spare) {
-        uint32_t sf = sn, jf = jn + kTile;
-        const bool far = more && seek(sf, jf);
-        if (far) fetch(spare, jf);
+    // ready: the stage of the next tile; spare: the current tile's (committed)
+    auto step = [&](Stage& ready, const uint32_t jready, Stage& spare, uint32_t& jspare) {
+        if (fmore) {
+            fj += kTile;
+            fmore = seek(fs, fj);
+        }
+        if (fmore) {
+            fetch(spare, fj);
+            jspare = fj;
+            ++nq;
+        }
         // link: only j > i; tiles wholly below this wave's diagonal are skipped
         const bool compute = wave_ok && !(MODE == kLink && j0 + kTile <= i0);   // i0: first query
         if (compute) {
@@ -819,20 +848,20 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
                 }
             }
         }
+        const bool more = nq > 0;
         if (more) commit(ready, buf ^ 1);
         __syncthreads();
-        sg = sn;
-        j0 = jn;
+        j0 = jready;
         have = more;
-        sn = sf;
-        jn = jf;
-        more = far;
+        nq -= more ? 1 : 0;
         buf ^= 1;
     };
     while (have) {
-        step(stB, stA);
-        if (!have) break;
-        step(stA, stB);
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            step(st[(u + 1) % PF], jq[(u + 1) % PF], st[u], jq[u]);
+            if (!have) break;
+        }
     }
     if (A.tiles && lane == 0 && ntiles) {
         atomicAdd(A.tiles, (unsigned long long)ntiles);
@@ -1057,6 +1086,7 @@ struct Geometry {
     float elo = 0, ehi = 0;
     bool mfma = false;
     bool f8 = false;       // also build the e4m3 fragments (count pass screen)
+    int pf = 2;            // e4m3 count pass: streamed tiles in flight (PD_OPT_DENSE_PREFETCH)
 };
 
 template <typename T>
@@ -1116,8 +1146,15 @@ void run_tiles(const TileArgs<T>& A, const Geometry& G, int metric, hipStream_t 
                     const unsigned grid8 =
                         A.p3 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (TB / 64 * 32 * QT8))
                              : nblocks((A.I.m + 32 * QT8 - 1) / (32 * QT8), TB / 64);
-                    hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true>), dim3(grid8), dim3(TB),
-                                       0, s, A);
+                    if (G.pf >= 8)
+                        hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true, 8>), dim3(grid8),
+                                           dim3(TB), 0, s, A);
+                    else if (G.pf >= 4)
+                        hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true, 4>), dim3(grid8),
+                                           dim3(TB), 0, s, A);
+                    else
+                        hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true, 2>), dim3(grid8),
+                                           dim3(TB), 0, s, A);
                     return;
                 }
             }
@@ -1225,6 +1262,7 @@ void count_stage(Ctx& ctx, TrainArgs& a, int rank, int world) {
     }
     Geometry G = geometry_of(ds);
     G.f8 = G.mfma && ctx.dense_screen == 1;   // the count pass's e4m3 screen
+    G.pf = ctx.dense_prefetch;
     TileArgs<T> A = base_args<T>(ds);
     A.f8_a = (float)std::ldexp(std::sqrt(64.0 * ((ds.KS + 3) / 4)), -18);
 

@@ -768,6 +768,41 @@ def test_dense_screens_equal(native, case):
         assert 0 < int(core1.sum()) < len(X)
 
 
+@pytest.mark.parametrize("case", ["c3_30k", "d5_blobs", "ties", "c3_1m"])
+def test_dense_prefetch_exact(native, case):
+    """PD_OPT_DENSE_PREFETCH (e4m3 count pass: 2, 4 or 8 streamed tiles in
+    flight per block) changes only the staging ring: identical counts, core
+    flags and labels, and the oracle's where it runs.  Bad depths raise."""
+    from pypardis_amd import synth
+    if case == "ties":
+        g = np.arange(6, dtype=np.float32) * np.float32(0.05)
+        X = np.stack(np.meshgrid(*([g] * 6), indexing="ij"), -1).reshape(-1, 6).astype(np.float32)
+        eps, ms = float(np.float32(0.05)), 7
+    elif case == "c3_1m":
+        X, eps, ms = synth.make_config("C3", n=1_000_000)[0], 0.114028, 10
+    else:
+        c = next(c for c in DENSE if c[0] == case)
+        X, eps, ms = np.ascontiguousarray(c[1]()), c[2], c[3]
+    ctx = native.context()
+    with pytest.raises(native.PardisError):
+        ctx.set_option(native.PD_OPT_DENSE_PREFETCH, 3)
+    outs = []
+    for pf in (2, 4, 8):
+        ctx.set_option(native.PD_OPT_DENSE_PREFETCH, pf)
+        try:
+            outs.append(_cluster(native, X, eps, ms, full=True))
+        finally:
+            ctx.set_option(native.PD_OPT_DENSE_PREFETCH, native.DENSE_PREFETCH_DEFAULT)
+    for lab, core, ncl, cnt in outs[1:]:
+        assert np.array_equal(cnt, outs[0][3])
+        assert np.array_equal(core, outs[0][1])
+        assert np.array_equal(lab, outs[0][0]) and ncl == outs[0][2]
+    if len(X) <= 60_000:
+        lab_o, core_o, cnt_o, nc_o = oracle.dbscan(X, eps, ms)
+        assert np.array_equal(outs[0][3], cnt_o)
+        assert np.array_equal(outs[0][0], lab_o) and outs[0][2] == nc_o
+
+
 def test_dense_edge_cases(native):
     from pypardis_amd import DBSCAN
     X = np.full((300, 16), 0.25, np.float32)   # identical points

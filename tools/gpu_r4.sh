@@ -36,7 +36,8 @@ if [ -n "${ABX:-}" ]; then
           || { tail -5 gpurun_out/r4_abx_${i}_$rep.log; exit 1; }
       python -c "
 import json; b=json.load(open('gpurun_out/r4_abx_${i}_$rep.json')); s=b['stages_ms']
-print('[$a] rep$rep', round(b['ms_per_step'],2), {k: s[k] for k in ('count','link','border','roots','label') if k in s})"
+print('[$a] rep$rep', round(b['ms_per_step'],2), {k: v for k, v in s.items() if k not in ('total', 'grid_grow')},
+      b.get('dense') or '')"
     done
   done
 fi

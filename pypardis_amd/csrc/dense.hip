@@ -99,6 +99,8 @@ struct FragSet {
                            // k8-step s (64 dims) is 64 lanes x 32 bytes, lane 32h + r holding
                            // dims 64s + 32h .. +31 of row 32g + r
     const float* norm;     // [rows_pad]
+    const float* nta8 = nullptr;   // e4m3 count pass: the C operand row term -(1+c)/2 |x|^2 x
+                                   // 2^16 (the LDS-DMA ring's source; tile_kernel PF > 2)
     const float* nmax;     // max norm over the valid rows (device scalar)
     const uint32_t* idx;   // row -> point id (null: identity)
     uint32_t m;            // valid rows
@@ -183,6 +185,14 @@ __global__ __launch_bounds__(kBlock) void prep8_kernel(const T* __restrict__ X, 
 }
 
 // |v|^2 of the scaled fp32 coordinates (the values the fragments split).
+// The e4m3 count pass's row term, as the register-staged tiles compute it
+// when they commit a tile to LDS (bit-identical).
+__global__ __launch_bounds__(kBlock) void nta8_kernel(const float* __restrict__ norm, uint32_t rp,
+                                                      float* __restrict__ nta8) {
+    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
+    if (r < rp) nta8[r] = -((1.0f + kBandC) * 0.5f) * norm[r] * kF8Acc;
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void norm_kernel(const T* __restrict__ X, int d,
                                                       const uint32_t* __restrict__ idx, uint32_t m,
@@ -318,10 +328,21 @@ struct TileLds {
 };
 // e4m3 screen: the staged tile is the e4m3 fragments only (4 KiB per 64 rows
 // of up to 64 dims)
-template <int KS8>
+template <int KS8, int NB = 2>
 struct TileLds8 {
-    i32x8 f8[2][2][KS8][64];   // [buffer][row group][k8-step][lane]
-    float nta[2][kTile];
+    i32x8 f8[NB][2][KS8][64];   // [buffer][row group][k8-step][lane]
+    float nta[NB][kTile];
+};
+// All of a tile block's LDS in one object: with LDS-DMA writes in flight the
+// compiler cannot tell a second __shared__ object from the staging buffers
+// and waits for the DMA before reading it (cdna_hip_programming.md,
+// "Projection GEMM at M = 256" item 4(a)).
+template <typename TL>
+struct TileShared {
+    TL t;
+    uint32_t seg_lo[kMaxSeg], seg_hi[kMaxSeg];
+    uint32_t bk_lo[kMaxBand], bk_off[kMaxBand + 1];
+    uint32_t nseg, fallback;
 };
 
 // QT: 32-query groups per wave (B operand tiles held in registers).  QT = 4
@@ -329,13 +350,44 @@ struct TileLds8 {
 // KS MFMAs per wave) at one wave per SIMD.
 constexpr int kF8Waves = 3;   // e4m3 count pass: waves per SIMD (no bf16 query fragments held)
 constexpr int kF8QT = 2;      // e4m3 count pass: query tiles (of 32) per wave
-// PF: streamed tiles in flight per block (a register ring; the staged tile
-// in LDS aside).  A streamed tile mostly misses L2 (C3: hit 0.24) and comes
-// from the fabric, so the count pass's block of 4 waves needs more than the
-// two tiles of the first form in flight (5 VGPRs per e4m3 stage).
+// LDS reads beside an LDS-DMA ring.  The compiler cannot tell which LDS a
+// global_load_lds in flight writes, so it waits for every one of them
+// (vmcnt(0)) before any LDS read it emits; these reads are its own, inline,
+// so the ring stays in flight (the reader orders them after the counted
+// wait and barrier that retire the buffer it reads).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ uint32_t lds_ld_u32(const uint32_t* p) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+    return v;
+}
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 lds_ld_b128_nowait(uint32_t a) {
+    i32x4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+__device__ __forceinline__ void lds_wait(i32x4& v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v) : : "memory");
+}
+
+// PF (e4m3 count pass): 2 = two register stages ahead of a double-buffered
+// LDS tile (the first form); PF > 2 = a ring of PF LDS buffers filled by
+// LDS-DMA (global_load_lds), PF - 1 tiles in flight per block.  The C3 count
+// pass fetches its streamed tiles from the Infinity Cache at ~3.3 TB/s with
+// ~24 KiB in flight per CU (3 blocks x 2 tiles x 4 KiB); the guide's
+// gather-into-LDS rate is 8.6 TB/s at 72 KiB in flight per CU
+// (MI355X_MICROARCH.md, "Indexed rows: gather into LDS").  No VGPRs: the
+// 2-stage kernel already spills at its 168-VGPR budget.
 template <typename T, int MODE, int KS, int QT, bool F8, int PF = 2>
-__global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu(F8 ? (KS >= 8 ? 1 : kF8Waves) : ((KS >= 8 || QT > 2) ? 1 : 2)))) void tile_kernel(TileArgs<T> A) {
-    static_assert(PF >= 2 && PF <= 8, "tiles in flight");
+__global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu(F8 ? (KS >= 8 ? 1 : (PF > 2 ? 2 : kF8Waves)) : ((KS >= 8 || QT > 2) ? 1 : 2)))) void tile_kernel(TileArgs<T> A) {
+    // (the ring runs 2 waves per SIMD: a spill reload is a VMEM load whose
+    // wait would drain the ring)
+    constexpr bool RING = F8 && PF > 2;
+    constexpr int NB = RING ? PF : 2;   // LDS tile buffers
+    static_assert(!RING || PF <= 8, "ring depth");
     constexpr int TB = tile_threads(KS, MODE);
     constexpr int QW = 32 * QT;                  // query rows per wave
     constexpr int KS8 = (KS + 3) / 4;            // e4m3 k-steps of 64 dims
@@ -347,7 +399,8 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
     // 16-byte chunks per staged tile (e4m3: two per lane fragment)
     constexpr int NC = F8 ? 2 * KS8 * 64 * 2 : (LO ? 2 : 1) * 2 * KS * 64;
     constexpr int NCH = (NC + TB - 1) / TB;      // per thread
-    __shared__ std::conditional_t<F8, TileLds8<KS8>, TileLds<KS, LO>> S;
+    __shared__ TileShared<std::conditional_t<F8, TileLds8<KS8, NB>, TileLds<KS, LO>>> SH;
+    auto& S = SH.t;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // block -> query rows.  Pruned count: bands are dealt round-robin to the
     // 8 XCDs (dispatch puts block id b on XCD b % 8), a band's blocks kept
@@ -418,10 +471,12 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
 
     // streamed segments [seg_lo, seg_hi) of J rows (tile-aligned starts):
     // all of J, from the diagonal (link), or one per band in the window
-    __shared__ uint32_t seg_lo[kMaxSeg], seg_hi[kMaxSeg];
-    __shared__ uint32_t nseg_s;
-    __shared__ uint32_t bk_lo[kMaxBand], bk_off[kMaxBand + 1];
-    __shared__ uint32_t fallback_s;
+    uint32_t(&seg_lo)[kMaxSeg] = SH.seg_lo;
+    uint32_t(&seg_hi)[kMaxSeg] = SH.seg_hi;
+    uint32_t& nseg_s = SH.nseg;
+    uint32_t(&bk_lo)[kMaxBand] = SH.bk_lo;
+    uint32_t(&bk_off)[kMaxBand + 1] = SH.bk_off;
+    uint32_t& fallback_s = SH.fallback;
     if (A.p3 && blk_i0 < A.I.m) {
         const uint32_t b = blk_i0 / A.band;                 // a block lies in one band
         const uint32_t k = (blk_i0 - b * A.band) / A.sub;   // ... and one sub-band
@@ -524,25 +579,26 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
     const uint32_t nseg = nseg_s;
     uint32_t ntiles = 0, nrefined = 0;
     // cursor over the tiles of the segments; false at the end
+    auto seg_at = [&](const uint32_t* p) -> uint32_t {
+        if constexpr (RING) return lds_ld_u32(p);
+        else return *p;
+    };
     auto seek = [&](uint32_t& sg, uint32_t& j) -> bool {
         while (sg < nseg) {
-            if (j < seg_hi[sg]) return true;
-            if (++sg < nseg) j = seg_lo[sg];
+            if (j < seg_at(&seg_hi[sg])) return true;
+            if (++sg < nseg) j = seg_at(&seg_lo[sg]);
         }
         return false;
     };
     // staging: thread k moves 16-byte chunks c = k + q * TB of the tile
     // (hi then lo), plus one norm per thread < 64
-    // PF register stages: the tiles up to PF ahead are in flight while the
-    // next one is committed (a streamed tile often misses L2 under pruning)
+    // Two register stages: the tile two ahead is in flight while the next
+    // one is committed (a streamed tile often misses L2 under pruning)
     struct Stage {
         bf16x8 v[NCH];
         float n;
     };
-    Stage st[PF];
-    uint32_t jq[PF];   // first row of the tile in each stage
-#pragma unroll
-    for (int k = 0; k < PF; ++k) jq[k] = 0u;
+    Stage stA, stB;
     auto fetch = [&](Stage& st, uint32_t j0) {
 #pragma unroll
         for (int q = 0; q < NCH; ++q) {
@@ -579,43 +635,11 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
         if (threadIdx.x < kTile)
             S.nta[buf][threadIdx.x] = -((1.0f + kBandC) * 0.5f) * st.n * (F8 ? kF8Acc : 1.0f);
     };
-    // cursors: current tile (in LDS buf), the frontier (the last tile
-    // fetched) and nq tiles fetched beyond the current one (the stages after
-    // the current tile's, in ring order)
-    uint32_t sg = 0, j0 = seg_lo[0];
-    bool have = seek(sg, j0);
-    if (have) {
-        fetch(st[0], j0);
-        commit(st[0], 0);
-    }
-    uint32_t fs = sg, fj = j0;
-    bool fmore = have;
-    int nq = 0;
-#pragma unroll
-    for (int k = 1; k < PF; ++k) {
-        if (fmore) {
-            fj += kTile;
-            fmore = seek(fs, fj);
-        }
-        if (fmore) {
-            fetch(st[k], fj);
-            jq[k] = fj;
-            ++nq;
-        }
-    }
-    __syncthreads();
+    uint32_t j0 = 0;
     int buf = 0;
-    // ready: the stage of the next tile; spare: the current tile's (committed)
-    auto step = [&](Stage& ready, const uint32_t jready, Stage& spare, uint32_t& jspare) {
-        if (fmore) {
-            fj += kTile;
-            fmore = seek(fs, fj);
-        }
-        if (fmore) {
-            fetch(spare, fj);
-            jspare = fj;
-            ++nq;
-        }
+    // one streamed tile (rows j0.., staged in LDS buffer buf) against the
+    // wave's queries
+    auto work = [&]() {
         // link: only j > i; tiles wholly below this wave's diagonal are skipped
         const bool compute = wave_ok && !(MODE == kLink && j0 + kTile <= i0);   // i0: first query
         if (compute) {
@@ -668,15 +692,51 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
                 // count pass, e4m3 screen (kScreen8C, in the x 2^16 units of
                 // the e4m3 products); a kept tile recomputes the split-bf16
                 // product from scratch, hi and lo from global memory
+                // ring: the wave's operands of the tile by inline LDS reads
+                i32x8 a8r[RING ? 2 : 1][RING ? KS8 : 1];
+                f32x16 ntr[RING ? 2 : 1];
+                if constexpr (RING) {
+                    i32x4 pf[2][KS8][2], pn[2][4];
+                    const uint32_t fa = lds_addr(&S.f8[buf][0][0][lane]);
+                    const uint32_t na = lds_addr(&S.nta[buf][4 * h]);
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                        for (int s = 0; s < KS8; ++s)
+#pragma unroll
+                            for (int k = 0; k < 2; ++k)
+                                pf[u][s][k] = lds_ld_b128_nowait(fa + (uint32_t)((u * KS8 + s) * 64 * 32 + 16 * k));
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            pn[u][q] = lds_ld_b128_nowait(na + (uint32_t)((32 * u + 8 * q) * 4));
+                    }
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                        for (int s = 0; s < KS8; ++s) {
+                            lds_wait(pf[u][s][0]);
+                            lds_wait(pf[u][s][1]);
+                            a8r[u][s] = __builtin_shufflevector(pf[u][s][0], pf[u][s][1], 0, 1, 2, 3, 4, 5, 6, 7);
+                        }
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            lds_wait(pn[u][q]);
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) ntr[u][4 * q + e] = __int_as_float(pn[u][q][e]);
+                        }
+                    }
+                }
 #pragma unroll
                 for (int s = 0; s < KS8; ++s) {
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
-                        const i32x8 a8 = S.f8[buf][u][s][lane];
+                        const i32x8 a8 = RING ? a8r[RING ? u : 0][RING ? s : 0] : S.f8[buf][u][s][lane];
 #pragma unroll
                         for (int t = 0; t < QT; ++t)
                             acc[u][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
-                                a8, bq8[t][s], s == 0 ? nt_of(u) : acc[u][t], 0, 0, 0, 0, 0, 0);
+                                a8, bq8[t][s],
+                                s == 0 ? (RING ? ntr[RING ? u : 0] : nt_of(u)) : acc[u][t], 0, 0,
+                                0, 0, 0, 0);
                     }
                 }
                 bool mb = false;
@@ -692,7 +752,8 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
                 if (refine) {
                     const uint32_t iw = (wave_ok ? i0 : 0) / 32;
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) nt[u] = nt_of(u) * (1.0f / kF8Acc);   // exact
+                    for (int u = 0; u < 2; ++u)   // exact
+                        nt[u] = (RING ? ntr[RING ? u : 0] : nt_of(u)) * (1.0f / kF8Acc);
 #pragma unroll
                     for (int s = 0; s < KS; ++s) {
                         bf16x8 ah[2], al[2], qh[QT], ql[QT];
@@ -848,20 +909,113 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
                 }
             }
         }
-        const bool more = nq > 0;
+    };
+    if constexpr (!RING) {
+    // cursors: current tile (in LDS buf), next (in `ready`), the one after
+    uint32_t sg = 0;
+    j0 = seg_lo[0];
+    bool have = seek(sg, j0);
+    if (have) {
+        fetch(stA, j0);
+        commit(stA, 0);
+    }
+    uint32_t sn = sg, jn = j0 + kTile;
+    bool more = have && seek(sn, jn);
+    if (more) fetch(stB, jn);
+    __syncthreads();
+    auto step = [&](Stage& ready, Stage& spare) {
+        uint32_t sf = sn, jf = jn + kTile;
+        const bool far = more && seek(sf, jf);
+        if (far) fetch(spare, jf);
+        work();
         if (more) commit(ready, buf ^ 1);
         __syncthreads();
-        j0 = jready;
+        sg = sn;
+        j0 = jn;
         have = more;
-        nq -= more ? 1 : 0;
+        sn = sf;
+        jn = jf;
+        more = far;
         buf ^= 1;
     };
     while (have) {
+        step(stB, stA);
+        if (!have) break;
+        step(stA, stB);
+    }
+    } else {
+        // LDS-DMA ring: tile t in buffer t % NB.  Each wave issues G
+        // global_load_lds per tile (its 1 KiB pieces of the e4m3 fragments,
+        // and 16 of the 64 row terms); before tile t: wait until only the
+        // tiles issued after it are outstanding (counted vmcnt), one raw
+        // barrier (tile t landed for every wave, buffer (t - 1) % NB read by
+        // every wave), then refill that buffer with tile t + NB - 1.
+        constexpr int G = NCH + 1;
+        static_assert(NC % TB == 0, "whole pieces per wave");
+        auto issue = [&](int b, uint32_t jt) {
+            const char* src = reinterpret_cast<const char*>(A.J.f8) + (uint64_t)(jt / 32) * KS8 * 64 * 32;
 #pragma unroll
-        for (int u = 0; u < PF; ++u) {
-            step(st[(u + 1) % PF], jq[(u + 1) % PF], st[u], jq[u]);
-            if (!have) break;
+            for (int q = 0; q < NCH; ++q) {
+                const int c0 = wave * 64 + q * TB;   // this wave instruction's first 16-B piece
+                __builtin_amdgcn_global_load_lds(
+                    (const void*)(src + (uint64_t)(c0 + lane) * 16),
+                    (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(&S.f8[b][0][0][0]) + c0 * 16),
+                    16, 0, 0);
+            }
+            if (lane < 16)
+                __builtin_amdgcn_global_load_lds(
+                    (const void*)(A.J.nta8 + jt + wave * 16 + lane),
+                    (__attribute__((address_space(3))) void*)&S.nta[b][wave * 16], 4, 0, 0);
+        };
+        uint32_t fs = 0, fj = seg_lo[0];   // the next tile to issue
+        bool fmore = seek(fs, fj);
+        uint32_t cs = fs, cj = fj;         // the current tile (NB - 1 behind)
+        int issued = 0, t = 0;
+#pragma unroll
+        for (int k = 0; k < NB - 1; ++k) {
+            if (fmore) {
+                issue(k, fj);
+                ++issued;
+                fj += kTile;
+                fmore = seek(fs, fj);
+            }
         }
+        bool have = issued > 0;
+        int b = 0;                         // t % NB
+#pragma unroll 1
+        while (have) {
+            if (issued - t - 1 >= NB - 2) {
+                if constexpr (G * (NB - 2) == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else if constexpr (G * (NB - 2) == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else if constexpr (G * (NB - 2) == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                else if constexpr (G * (NB - 2) == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else if constexpr (G * (NB - 2) == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+                else if constexpr (G * (NB - 2) == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+                else if constexpr (G * (NB - 2) == 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (fmore) {   // into buffer (t - 1) % NB, read by every wave before the barrier
+                issue(b == 0 ? NB - 1 : b - 1, fj);
+                ++issued;
+                fj += kTile;
+                fmore = seek(fs, fj);
+            }
+            j0 = cj;
+            buf = b;
+            work();
+            ++t;
+            b = b == NB - 1 ? 0 : b + 1;
+            have = t < issued;
+            if (have) {
+                cj += kTile;
+                (void)seek(cs, cj);
+            }
+        }
+        // no DMA outstanding at exit (the last tile was waited for)
     }
     if (A.tiles && lane == 0 && ntiles) {
         atomicAdd(A.tiles, (unsigned long long)ntiles);
@@ -1086,7 +1240,7 @@ struct Geometry {
     float elo = 0, ehi = 0;
     bool mfma = false;
     bool f8 = false;       // also build the e4m3 fragments (count pass screen)
-    int pf = 2;            // e4m3 count pass: streamed tiles in flight (PD_OPT_DENSE_PREFETCH)
+    int pf = 2;            // e4m3 count pass: LDS tile buffers (PD_OPT_DENSE_PREFETCH)
 };
 
 template <typename T>
@@ -1119,6 +1273,11 @@ FragSet make_frags(Ctx& ctx, const std::string& tag, const T* X, int d, const ui
                        X, d, idx, m, rp, G.KS, G.center, G.scale, hi, lo);
     hipLaunchKernelGGL(norm_kernel<T>, dim3(nblocks(rp)), dim3(kBlock), 0, s, X, d, idx, m, rp,
                        G.center, G.scale, nrm, nmax);
+    if (G.f8 && G.pf > 2) {
+        float* nt8 = ctx.arena.get<float>(tag + "_nta8", rp);
+        hipLaunchKernelGGL(nta8_kernel, dim3(nblocks(rp)), dim3(kBlock), 0, s, nrm, rp, nt8);
+        F.nta8 = nt8;
+    }
     PD_HIP(hipGetLastError());
     F.hi = hi;
     F.lo = lo;

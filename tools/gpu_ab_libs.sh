@@ -11,7 +11,7 @@ for i in $(seq 1 ${REPS:-2}); do
         || { tail -5 gpurun_out/abl_${tag}_$i.log; exit 1; }
     python -c "
 import json; b=json.load(open('gpurun_out/abl_${tag}_$i.json')); s=b['stages_ms']
-print('$tag', $i, round(b['ms_per_step'],2), {k: s[k] for k in ('halo','cells','count','link','roots','border') if k in s})"
+print('$tag', $i, round(b['ms_per_step'],2), {k: v for k, v in s.items() if v and k not in ('total', 'grid_grow')})"
   done
 done
 echo "ab ok"

@@ -146,9 +146,10 @@ enum pd_option {
     PD_OPT_LINK_JUMPS = 21,   /* link modes 3-6: pointer-jumping rounds over the count pass's
                                 smallest-neighbour forest before the window union (default 0;
                                 same labels) */
-    PD_OPT_DENSE_PREFETCH = 22 /* d > 4, e4m3 count pass: streamed tiles in flight per block
-                                (2, 4 or 8; a register ring ahead of the LDS stage).  Same
-                                counts either way */
+    PD_OPT_DENSE_PREFETCH = 22 /* d > 4, e4m3 count pass: 2 (default) = two register stages
+                                ahead of a double-buffered LDS tile; 4 or 8 = a ring of that many
+                                LDS buffers filled by global_load_lds (measured slower on C3: 29.9
+                                vs 21.3 ms).  Same counts either way */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -350,6 +350,7 @@ struct TileShared {
 // KS MFMAs per wave) at one wave per SIMD.
 constexpr int kF8Waves = 3;   // e4m3 count pass: waves per SIMD (no bf16 query fragments held)
 constexpr int kF8QT = 2;      // e4m3 count pass: query tiles (of 32) per wave
+constexpr int kF8RingWaves = 3;   // ... with the LDS-DMA ring (PF > 2)
 // LDS reads beside an LDS-DMA ring.  The compiler cannot tell which LDS a
 // global_load_lds in flight writes, so it waits for every one of them
 // (vmcnt(0)) before any LDS read it emits; these reads are its own, inline,
@@ -382,7 +383,7 @@ __device__ __forceinline__ void lds_wait(i32x4& v) {
 // (MI355X_MICROARCH.md, "Indexed rows: gather into LDS").  No VGPRs: the
 // 2-stage kernel already spills at its 168-VGPR budget.
 template <typename T, int MODE, int KS, int QT, bool F8, int PF = 2>
-__global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu(F8 ? (KS >= 8 ? 1 : (PF > 2 ? 2 : kF8Waves)) : ((KS >= 8 || QT > 2) ? 1 : 2)))) void tile_kernel(TileArgs<T> A) {
+__global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu(F8 ? (KS >= 8 ? 1 : (PF > 2 ? kF8RingWaves : kF8Waves)) : ((KS >= 8 || QT > 2) ? 1 : 2)))) void tile_kernel(TileArgs<T> A) {
     // (the ring runs 2 waves per SIMD: a spill reload is a VMEM load whose
     // wait would drain the ring)
     constexpr bool RING = F8 && PF > 2;
@@ -580,7 +581,7 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
     uint32_t ntiles = 0, nrefined = 0;
     // cursor over the tiles of the segments; false at the end
     auto seg_at = [&](const uint32_t* p) -> uint32_t {
-        if constexpr (RING) return lds_ld_u32(p);
+        if constexpr (RING) return __builtin_amdgcn_readfirstlane(lds_ld_u32(p));   // uniform
         else return *p;
     };
     auto seek = [&](uint32_t& sg, uint32_t& j) -> bool {
@@ -952,20 +953,27 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
         // every wave), then refill that buffer with tile t + NB - 1.
         constexpr int G = NCH + 1;
         static_assert(NC % TB == 0, "whole pieces per wave");
+        // (addresses from wave-uniform scalars plus the lane: nothing held
+        // across the loop, so no spill reload — a VMEM load whose wait would
+        // drain the ring — lands between the pieces)
+        const int wu = __builtin_amdgcn_readfirstlane(wave);
         auto issue = [&](int b, uint32_t jt) {
+            jt = __builtin_amdgcn_readfirstlane(jt);
+            uint32_t ln;   // the lane, recomputed here (a hoisted copy got spilled)
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
             const char* src = reinterpret_cast<const char*>(A.J.f8) + (uint64_t)(jt / 32) * KS8 * 64 * 32;
 #pragma unroll
             for (int q = 0; q < NCH; ++q) {
-                const int c0 = wave * 64 + q * TB;   // this wave instruction's first 16-B piece
+                const int c0 = wu * 64 + q * TB;   // this wave instruction's first 16-B piece
                 __builtin_amdgcn_global_load_lds(
-                    (const void*)(src + (uint64_t)(c0 + lane) * 16),
+                    (const void*)(src + (uint64_t)c0 * 16 + ln * 16u),
                     (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(&S.f8[b][0][0][0]) + c0 * 16),
                     16, 0, 0);
             }
-            if (lane < 16)
+            if (ln < 16)
                 __builtin_amdgcn_global_load_lds(
-                    (const void*)(A.J.nta8 + jt + wave * 16 + lane),
-                    (__attribute__((address_space(3))) void*)&S.nta[b][wave * 16], 4, 0, 0);
+                    (const void*)(A.J.nta8 + (jt + wu * 16) + ln),
+                    (__attribute__((address_space(3))) void*)&S.nta[b][wu * 16], 4, 0, 0);
         };
         uint32_t fs = 0, fj = seg_lo[0];   // the next tile to issue
         bool fmore = seek(fs, fj);

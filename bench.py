@@ -105,6 +105,8 @@ def parse():
                     help="PD_OPT_LINK_JUMPS override (pointer jumps before the window union)")
     ap.add_argument("--dense-prefetch", type=int, default=None,
                     help="PD_OPT_DENSE_PREFETCH override (e4m3 count pass tiles in flight: 2/4/8)")
+    ap.add_argument("--dense-waves", type=int, default=None,
+                    help="PD_OPT_DENSE_WAVES override (e4m3 count pass waves per block: 1/2/4)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
@@ -478,7 +480,8 @@ def main():
                      (_native.PD_OPT_DENSE_SCREEN, args.dense_screen),
                      (_native.PD_OPT_BORDER_LISTS, args.border_lists),
                      (_native.PD_OPT_LINK_JUMPS, args.link_jumps),
-                     (_native.PD_OPT_DENSE_PREFETCH, args.dense_prefetch)):
+                     (_native.PD_OPT_DENSE_PREFETCH, args.dense_prefetch),
+                     (_native.PD_OPT_DENSE_WAVES, args.dense_waves)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None

@@ -149,7 +149,10 @@ enum pd_option {
     PD_OPT_DENSE_PREFETCH = 22 /* d > 4, e4m3 count pass: 2 (default) = two register stages
                                 ahead of a double-buffered LDS tile; 4 or 8 = a ring of that many
                                 LDS buffers filled by global_load_lds (measured slower on C3: 29.9
-                                vs 21.3 ms).  Same counts either way */
+                                vs 21.3 ms).  Same counts either way */,
+    PD_OPT_DENSE_WAVES = 23   /* d > 4, e4m3 count pass with 2 register stages: waves per tile
+                                block (1, 2 or 4 = default; 64 query rows per wave).  Same
+                                counts either way */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

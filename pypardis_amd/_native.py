@@ -36,8 +36,10 @@ PD_OPT_SHARD_CORE_BIT = 19
 PD_OPT_BORDER_LISTS = 20
 PD_OPT_LINK_JUMPS = 21
 PD_OPT_DENSE_PREFETCH = 22
+PD_OPT_DENSE_WAVES = 23
 SWEEP_VARIANT_DEFAULT = 221
 DENSE_PREFETCH_DEFAULT = 2   # ctx.dense_prefetch (internal.hpp)
+DENSE_WAVES_DEFAULT = 4      # ctx.dense_waves
 LINK_MODE_DEFAULT = 6
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",

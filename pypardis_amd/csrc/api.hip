@@ -181,6 +181,10 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             if (value != 2 && value != 4 && value != 8)
                 throw Error(PD_EINVAL, "dense prefetch is 2, 4 or 8 tiles");
             ctx->c.dense_prefetch = (int)value;
+        } else if (option == PD_OPT_DENSE_WAVES) {
+            if (value != 1 && value != 2 && value != 4)
+                throw Error(PD_EINVAL, "dense waves is 1, 2 or 4");
+            ctx->c.dense_waves = (int)value;
         } else if (option == PD_OPT_LINK_JUMPS) {
             if (value < 0 || value > 16) throw Error(PD_EINVAL, "link jumps must be in [0, 16]");
             ctx->c.link_jumps = (int)value;

@@ -313,7 +313,7 @@ __device__ __forceinline__ void tile_hit(const TileArgs<T>& A, uint32_t i, uint3
 // 110 ms — an 8-wave barrier per tile, one block per CU.)
 constexpr int kCountWaves = 4;   // waves per count-pass block (each staged tile feeds them all; 8:
                                  // 41.4 vs 36.1 ms on C3 — wider windows per block, more tiles)
-constexpr int tile_threads(int, int mode) { return mode == kCount ? 64 * kCountWaves : 256; }
+constexpr int tile_threads(int, int mode, int cw = kCountWaves) { return mode == kCount ? 64 * cw : 256; }
 constexpr int kCountQT = 2;   // query tiles (of 32) per wave in the count pass (4: one
                               // wave per SIMD, measured 125 vs 74 ms on C3)
 
@@ -382,14 +382,18 @@ __device__ __forceinline__ void lds_wait(i32x4& v) {
 // gather-into-LDS rate is 8.6 TB/s at 72 KiB in flight per CU
 // (MI355X_MICROARCH.md, "Indexed rows: gather into LDS").  No VGPRs: the
 // 2-stage kernel already spills at its 168-VGPR budget.
-template <typename T, int MODE, int KS, int QT, bool F8, int PF = 2>
-__global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu(F8 ? (KS >= 8 ? 1 : (PF > 2 ? kF8RingWaves : kF8Waves)) : ((KS >= 8 || QT > 2) ? 1 : 2)))) void tile_kernel(TileArgs<T> A) {
+// CW: waves per count-pass block (PD_OPT_DENSE_WAVES; the e4m3 pass): a
+// block's window is the union of its rows' p3 windows, so smaller blocks
+// stream fewer tiles per query and wait at a narrower barrier, larger ones
+// share each staged tile across more queries.
+template <typename T, int MODE, int KS, int QT, bool F8, int PF = 2, int CW = kCountWaves>
+__global__ __launch_bounds__(tile_threads(KS, MODE, CW)) __attribute__((amdgpu_waves_per_eu(F8 ? (KS >= 8 ? 1 : (PF > 2 ? kF8RingWaves : kF8Waves)) : ((KS >= 8 || QT > 2) ? 1 : 2)))) void tile_kernel(TileArgs<T> A) {
     // (the ring runs 2 waves per SIMD: a spill reload is a VMEM load whose
     // wait would drain the ring)
     constexpr bool RING = F8 && PF > 2;
     constexpr int NB = RING ? PF : 2;   // LDS tile buffers
     static_assert(!RING || PF <= 8, "ring depth");
-    constexpr int TB = tile_threads(KS, MODE);
+    constexpr int TB = tile_threads(KS, MODE, CW);
     constexpr int QW = 32 * QT;                  // query rows per wave
     constexpr int KS8 = (KS + 3) / 4;            // e4m3 k-steps of 64 dims
     static_assert(!F8 || MODE == kCount, "the e4m3 screen is the count pass's");
@@ -1249,6 +1253,7 @@ struct Geometry {
     bool mfma = false;
     bool f8 = false;       // also build the e4m3 fragments (count pass screen)
     int pf = 2;            // e4m3 count pass: LDS tile buffers (PD_OPT_DENSE_PREFETCH)
+    int cw = kCountWaves;  // e4m3 count pass: waves per block (PD_OPT_DENSE_WAVES)
 };
 
 template <typename T>
@@ -1310,9 +1315,20 @@ void run_tiles(const TileArgs<T>& A, const Geometry& G, int metric, hipStream_t 
             if constexpr (MODE == kCount) {
                 if (A.I.f8 && A.J.f8) {
                     constexpr int QT8 = KS <= 4 ? kF8QT : 2;
+                    const int cw = G.pf == 2 ? G.cw : kCountWaves;
                     const unsigned grid8 =
-                        A.p3 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (TB / 64 * 32 * QT8))
-                             : nblocks((A.I.m + 32 * QT8 - 1) / (32 * QT8), TB / 64);
+                        A.p3 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (cw * 32 * QT8))
+                             : nblocks((A.I.m + 32 * QT8 - 1) / (32 * QT8), cw);
+                    if (cw == 1) {
+                        hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true, 2, 1>), dim3(grid8),
+                                           dim3(64), 0, s, A);
+                        return;
+                    }
+                    if (cw == 2) {
+                        hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true, 2, 2>), dim3(grid8),
+                                           dim3(128), 0, s, A);
+                        return;
+                    }
                     if (G.pf >= 8)
                         hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true, 8>), dim3(grid8),
                                            dim3(TB), 0, s, A);
@@ -1430,6 +1446,7 @@ void count_stage(Ctx& ctx, TrainArgs& a, int rank, int world) {
     Geometry G = geometry_of(ds);
     G.f8 = G.mfma && ctx.dense_screen == 1;   // the count pass's e4m3 screen
     G.pf = ctx.dense_prefetch;
+    G.cw = ctx.dense_waves;
     TileArgs<T> A = base_args<T>(ds);
     A.f8_a = (float)std::ldexp(std::sqrt(64.0 * ((ds.KS + 3) / 4)), -18);
 

@@ -173,6 +173,7 @@ struct Ctx {
     bool border_lists = false;   // PD_OPT_BORDER_LISTS: count sweep lists border neighbours
     int dense_screen = 1;        // dense count pass screen: 1 e4m3 (32x32x64), 0 bf16 hi.hi
     int dense_prefetch = 2;      // e4m3 count pass: streamed tiles in flight (2, 4 or 8)
+    int dense_waves = 4;         // e4m3 count pass: waves per tile block (1, 2 or 4)
     bool sort_payload = false;   // fp32 3-D: coordinates ride the sort (PD_OPT_SORT_PAYLOAD)
     int label_buckets = -1;      // labels to input order by bucketed pair passes (PD_OPT_LABEL_BUCKETS;
                                  // -1: from 2^28 points on, where they beat the direct scatter)

@@ -771,8 +771,9 @@ def test_dense_screens_equal(native, case):
 @pytest.mark.parametrize("case", ["c3_30k", "d5_blobs", "ties", "c3_1m"])
 def test_dense_prefetch_exact(native, case):
     """PD_OPT_DENSE_PREFETCH (e4m3 count pass: 2, 4 or 8 streamed tiles in
-    flight per block) changes only the staging ring: identical counts, core
-    flags and labels, and the oracle's where it runs.  Bad depths raise."""
+    flight per block) and PD_OPT_DENSE_WAVES (1, 2 or 4 waves per block)
+    change only the staging and the block shape: identical counts, core flags
+    and labels, and the oracle's where it runs.  Bad values raise."""
     from pypardis_amd import synth
     if case == "ties":
         g = np.arange(6, dtype=np.float32) * np.float32(0.05)
@@ -786,13 +787,19 @@ def test_dense_prefetch_exact(native, case):
     ctx = native.context()
     with pytest.raises(native.PardisError):
         ctx.set_option(native.PD_OPT_DENSE_PREFETCH, 3)
+    with pytest.raises(native.PardisError):
+        ctx.set_option(native.PD_OPT_DENSE_WAVES, 3)
     outs = []
-    for pf in (2, 4, 8):
+    # (tiles in flight, waves per block): the LDS-DMA ring, and the
+    # register-staged blocks of 1 / 2 / 4 waves
+    for pf, cw in ((2, 4), (4, 4), (8, 4), (2, 2), (2, 1)):
         ctx.set_option(native.PD_OPT_DENSE_PREFETCH, pf)
+        ctx.set_option(native.PD_OPT_DENSE_WAVES, cw)
         try:
             outs.append(_cluster(native, X, eps, ms, full=True))
         finally:
             ctx.set_option(native.PD_OPT_DENSE_PREFETCH, native.DENSE_PREFETCH_DEFAULT)
+            ctx.set_option(native.PD_OPT_DENSE_WAVES, native.DENSE_WAVES_DEFAULT)
     for lab, core, ncl, cnt in outs[1:]:
         assert np.array_equal(cnt, outs[0][3])
         assert np.array_equal(core, outs[0][1])

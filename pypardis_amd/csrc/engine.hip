@@ -1239,12 +1239,36 @@ __global__ __launch_bounds__(kBlock) void merge_kernel(const uint32_t* __restric
                                                        const uint32_t* __restrict__ vals,
                                                        const uint32_t* __restrict__ rep,
                                                        uint32_t* __restrict__ par) {
+    // The copies of a cluster's boundary points all join the same two trees:
+    // thousands of lanes racing one CAS on the same root (C2: 0.56 ms for
+    // 2.2M listed records).  Each lane finds its pair of roots first and
+    // skips the union when the lane before holds the same pair (the list is
+    // in record order, so a wave's neighbours mostly do).
     const uint32_t nl = *count;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nl; i += gridDim.x * kBlock) {
-        const uint32_t r = list[i];
-        if (ld_rlx(par + r) == kNone) continue;   // not core (par is the core flag)
-        const uint32_t q = rep[vals[r] & kIdMask];
-        if (q != r) uf_unite(par, r, q);
+    const int lane = threadIdx.x & 63;
+    for (uint32_t b0 = blockIdx.x * kBlock; b0 < nl; b0 += gridDim.x * kBlock) {   // uniform
+        const uint32_t i = b0 + threadIdx.x;
+        uint32_t ra = kNone, rb = kNone;
+        if (i < nl) {
+            const uint32_t r = list[i];
+            if (ld_rlx(par + r) != kNone) {   // core (par is the core flag)
+                const uint32_t q = rep[vals[r] & kIdMask];
+                if (q != r) {
+                    ra = uf_find(par, r);
+                    rb = uf_find(par, q);
+                    if (ra > rb) {
+                        const uint32_t t = ra;
+                        ra = rb;
+                        rb = t;
+                    }
+                    if (ra == rb) ra = rb = kNone;
+                }
+            }
+        }
+        const uint32_t pa = (uint32_t)__shfl_up((int)ra, 1, 64);
+        const uint32_t pb = (uint32_t)__shfl_up((int)rb, 1, 64);
+        const bool same = lane > 0 && pa == ra && pb == rb;
+        if (ra != kNone && !same) uf_unite(par, ra, rb);
     }
 }
 

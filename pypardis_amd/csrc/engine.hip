@@ -974,18 +974,26 @@ __global__ __launch_bounds__(kBlock) void word_write_kernel(const K* __restrict_
     }
     const uint64_t wp = (uint64_t)__shfl_up((long long)word, 1, 64);
     const uint64_t w63 = (uint64_t)__shfl((long long)word, 63, 64);
+    // Only the wave's last word can continue into the next wave (a word has
+    // <= 64 cells, so it ends there): the whole wave reads the next 64 cells
+    // and ORs their bits (a serial walk of up to 63 cells by the word's first
+    // lane held its wave on C4's dense rows: word_write 6.8 ms).
+    const uint32_t cb = c - (uint32_t)lane;   // the wave's first cell (uniform)
+    unsigned long long vx = 0;
+    if (cb + 64 < nc && ((uint64_t)ckeys[cb + 64] >> 6) == w63) {   // uniform
+        const uint32_t c2 = cb + 64 + (uint32_t)lane;
+        const uint64_t k2 = c2 < nc ? (uint64_t)ckeys[c2] : ~0ull;
+        vx = c2 < nc && (k2 >> 6) == w63 ? 1ull << (k2 & 63) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) vx |= (unsigned long long)__shfl_xor((long long)vx, o, 64);
+    }
     if (!in) return;
     bool first = c == 0;
     if (!first) first = lane ? wp != word : ((uint64_t)ckeys[c - 1] >> 6) != word;
     bool occ;
     const uint64_t slot = page_slot(pages[word >> 6], word, occ);
     if (first) {
-        if (w63 == word)   // the word continues past this wave
-            for (uint32_t c2 = c - (uint32_t)lane + 64; c2 < nc; ++c2) {
-                const uint64_t k2 = (uint64_t)ckeys[c2];
-                if ((k2 >> 6) != word) break;
-                v |= 1ull << (k2 & 63);
-            }
+        if (w63 == word) v |= vx;   // the word continues past this wave
         words[slot] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), c, 0u);
     }
     if (c == nc - 1) words[slot + 1] = make_uint4(0u, 0u, nc, 0u);

@@ -932,7 +932,11 @@ __global__ __launch_bounds__(kBlock) void dir_bits_kernel(const K* __restrict__ 
                                                           const uint32_t* __restrict__ ncells,
                                                           uint4* __restrict__ dir) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    const bool in = c < *ncells;
+    const uint32_t nc = *ncells;
+    // the grid covers the records (the cell count stays on the device): the
+    // waves past the last cell (C4: 2/3 of them) leave before the scan
+    if (c - (uint32_t)(threadIdx.x & 63) >= nc) return;
+    const bool in = c < nc;
     const uint64_t k = in ? ((uint64_t)ckeys[c] >> SH) : ~0ull;
     const uint64_t word = k >> 6;
     unsigned long long v = in ? (1ull << (k & 63)) : 0ull;
@@ -961,6 +965,7 @@ __global__ __launch_bounds__(kBlock) void word_write_kernel(const K* __restrict_
                                                             uint4* __restrict__ words) {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t nc = *ncells;
+    if (c - (uint32_t)(threadIdx.x & 63) >= nc) return;   // a wave past the last cell
     const bool in = c < nc;
     const uint64_t k = in ? (uint64_t)ckeys[c] : ~0ull;
     const uint64_t word = k >> 6;
@@ -2686,6 +2691,7 @@ __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const uint32_t nc = *ncells;
+    if (c - (uint32_t)lane >= nc) return;   // a wave past the last cell (grid over records)
     uint32_t v = kNone;
     uint64_t word = ~0ull;
     uint32_t sz = 0, s = 0;
@@ -2903,6 +2909,10 @@ __global__ __launch_bounds__(kBlock) void verify_screen_kernel(
     constexpr int NF = ForwardRows<D, K>::NF;
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t nc = *ncells;
+    if (blockIdx.x * kBlock >= nc) {   // a tile past the last cell (grid over records)
+        if (threadIdx.x == 0) tile_cnt[blockIdx.x] = 0;
+        return;
+    }
     const uint32_t rc = c < nc ? croot[c] : kNone;
     bool work = rc == kMixed;
     if (rc != kNone && rc != kMixed) {
@@ -2930,7 +2940,9 @@ __global__ __launch_bounds__(kBlock) void flag_list_kernel(const uint8_t* __rest
                                                            const uint64_t* __restrict__ tile_off,
                                                            uint32_t* __restrict__ list) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const bool f = i < *n_dev && flags[i];
+    const uint32_t nd = *n_dev;
+    if (blockIdx.x * kBlock >= nd) return;   // a tile past the last cell: no entries
+    const bool f = i < nd && flags[i];
     uint32_t btot;
     const uint32_t off = block_excl_scan(f ? 1u : 0u, btot);
     if (f) list[tile_off[blockIdx.x] + off] = i;

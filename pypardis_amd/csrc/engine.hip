@@ -920,6 +920,25 @@ __global__ __launch_bounds__(kBlock) void cell_write_kernel(const K* __restrict_
     }
 }
 
+// Wave shuffles of a directory word / page id: 32-bit when the ids fit (one
+// ds_bpermute per step instead of two; W32 below — C2's 32-bit keys always,
+// C4's 37-bit ones too), else 64-bit.
+template <typename WT>
+__device__ __forceinline__ WT shfl_up_w(WT x, int o) {
+    if constexpr (sizeof(WT) == 4) return (WT)__shfl_up((int)x, o, 64);
+    else return (WT)__shfl_up((long long)x, o, 64);
+}
+template <typename WT>
+__device__ __forceinline__ WT shfl_down_w(WT x, int o) {
+    if constexpr (sizeof(WT) == 4) return (WT)__shfl_down((int)x, o, 64);
+    else return (WT)__shfl_down((long long)x, o, 64);
+}
+template <typename WT>
+__device__ __forceinline__ WT shfl_w(WT x, int l) {
+    if constexpr (sizeof(WT) == 4) return (WT)__shfl((int)x, l, 64);
+    else return (WT)__shfl((long long)x, l, 64);
+}
+
 // Directory occupancy bits, one lane per cell: the cells are sorted, so the
 // lanes of one directory word are contiguous and a segmented OR-scan across
 // the wave (Hillis-Steele; equal words at distance o imply equal words in
@@ -927,7 +946,7 @@ __global__ __launch_bounds__(kBlock) void cell_write_kernel(const K* __restrict_
 // one atomicOr (a word can continue into the neighbouring waves).
 // SH = 6: the paged directory's page masks (one bit per occupied word of
 // the page; the units are then words, k >> 6).
-template <typename K, int SH>
+template <typename K, int SH, bool W32>
 __global__ __launch_bounds__(kBlock) void dir_bits_kernel(const K* __restrict__ ckeys,
                                                           const uint32_t* __restrict__ ncells,
                                                           uint4* __restrict__ dir) {
@@ -937,19 +956,20 @@ __global__ __launch_bounds__(kBlock) void dir_bits_kernel(const K* __restrict__ 
     // waves past the last cell (C4: 2/3 of them) leave before the scan
     if (c - (uint32_t)(threadIdx.x & 63) >= nc) return;
     const bool in = c < nc;
+    using WT = std::conditional_t<W32, uint32_t, uint64_t>;
     const uint64_t k = in ? ((uint64_t)ckeys[c] >> SH) : ~0ull;
-    const uint64_t word = k >> 6;
+    const WT word = (WT)(k >> 6);   // W32: ids < 2^31, the sentinel 0xFFFFFFFF
     unsigned long long v = in ? (1ull << (k & 63)) : 0ull;
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t wo = (uint64_t)__shfl_up((long long)word, o, 64);
+        const WT wo = shfl_up_w(word, o);
         const unsigned long long vo = (unsigned long long)__shfl_up((long long)v, o, 64);
         if (lane >= o && wo == word) v |= vo;
     }
-    const uint64_t wn = (uint64_t)__shfl_down((long long)word, 1, 64);
+    const WT wn = shfl_down_w(word, 1);
     const bool last = lane == 63 || wn != word;
-    if (in && last) atomicOr(reinterpret_cast<unsigned long long*>(dir + word), v);
+    if (in && last) atomicOr(reinterpret_cast<unsigned long long*>(dir + (uint64_t)word), v);
 }
 
 // Paged directory, the occupied words (pages already hold their masks and
@@ -958,7 +978,7 @@ __global__ __launch_bounds__(kBlock) void dir_bits_kernel(const K* __restrict__ 
 // whose cells run past the wave's last lane continues with a serial walk of
 // at most 63 cells), z = that cell's index (the occupied cells before the
 // word).  The last cell also writes the terminal word {0, 0, ncells}.
-template <typename K>
+template <typename K, bool W32>
 __global__ __launch_bounds__(kBlock) void word_write_kernel(const K* __restrict__ ckeys,
                                                             const uint32_t* __restrict__ ncells,
                                                             const uint4* __restrict__ pages,
@@ -967,36 +987,37 @@ __global__ __launch_bounds__(kBlock) void word_write_kernel(const K* __restrict_
     const uint32_t nc = *ncells;
     if (c - (uint32_t)(threadIdx.x & 63) >= nc) return;   // a wave past the last cell
     const bool in = c < nc;
+    using WT = std::conditional_t<W32, uint32_t, uint64_t>;
     const uint64_t k = in ? (uint64_t)ckeys[c] : ~0ull;
-    const uint64_t word = k >> 6;
+    const WT word = (WT)(k >> 6);   // W32: ids < 2^31, the sentinel 0xFFFFFFFF
     unsigned long long v = in ? (1ull << (k & 63)) : 0ull;
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t wo = (uint64_t)__shfl_down((long long)word, o, 64);
+        const WT wo = shfl_down_w(word, o);
         const unsigned long long vo = (unsigned long long)__shfl_down((long long)v, o, 64);
         if (lane + o < 64 && wo == word) v |= vo;
     }
-    const uint64_t wp = (uint64_t)__shfl_up((long long)word, 1, 64);
-    const uint64_t w63 = (uint64_t)__shfl((long long)word, 63, 64);
+    const WT wp = shfl_up_w(word, 1);
+    const WT w63 = shfl_w(word, 63);
     // Only the wave's last word can continue into the next wave (a word has
     // <= 64 cells, so it ends there): the whole wave reads the next 64 cells
     // and ORs their bits (a serial walk of up to 63 cells by the word's first
     // lane held its wave on C4's dense rows: word_write 6.8 ms).
     const uint32_t cb = c - (uint32_t)lane;   // the wave's first cell (uniform)
     unsigned long long vx = 0;
-    if (cb + 64 < nc && ((uint64_t)ckeys[cb + 64] >> 6) == w63) {   // uniform
+    if (cb + 64 < nc && (WT)((uint64_t)ckeys[cb + 64] >> 6) == w63) {   // uniform
         const uint32_t c2 = cb + 64 + (uint32_t)lane;
         const uint64_t k2 = c2 < nc ? (uint64_t)ckeys[c2] : ~0ull;
-        vx = c2 < nc && (k2 >> 6) == w63 ? 1ull << (k2 & 63) : 0ull;
+        vx = c2 < nc && (WT)(k2 >> 6) == w63 ? 1ull << (k2 & 63) : 0ull;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) vx |= (unsigned long long)__shfl_xor((long long)vx, o, 64);
     }
     if (!in) return;
     bool first = c == 0;
-    if (!first) first = lane ? wp != word : ((uint64_t)ckeys[c - 1] >> 6) != word;
+    if (!first) first = lane ? wp != word : (WT)((uint64_t)ckeys[c - 1] >> 6) != word;
     bool occ;
-    const uint64_t slot = page_slot(pages[word >> 6], word, occ);
+    const uint64_t slot = page_slot(pages[(uint64_t)word >> 6], (uint64_t)word, occ);
     if (first) {
         if (w63 == word) v |= vx;   // the word continues past this wave
         words[slot] = make_uint4((uint32_t)v, (uint32_t)(v >> 32), c, 0u);
@@ -2682,7 +2703,7 @@ __device__ __forceinline__ void word_merge(uint32_t* wroot, uint64_t w, uint32_t
 // whole wave on C4's dense cells: 55 ms of the 1B-point link.
 constexpr uint32_t kMidCell = 16, kWordBig = 1024;
 
-template <typename K>
+template <typename K, bool W32>
 __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
     const uint32_t* __restrict__ cstart, const uint32_t* __restrict__ ncells,
     const K* __restrict__ ckeys, uint32_t* __restrict__ par, uint32_t* __restrict__ croot,
@@ -2692,13 +2713,14 @@ __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
     const int lane = threadIdx.x & 63;
     const uint32_t nc = *ncells;
     if (c - (uint32_t)lane >= nc) return;   // a wave past the last cell (grid over records)
+    using WT = std::conditional_t<W32, uint32_t, uint64_t>;   // W32: slots < 2^32 - 1
     uint32_t v = kNone;
-    uint64_t word = ~0ull;
+    WT word = (WT)~0ull;
     uint32_t sz = 0, s = 0;
     if (c < nc) {
         s = cstart[c];
         sz = cstart[c + 1] - s;
-        word = word_slot(pages, (uint64_t)ckeys[c]);
+        word = (WT)word_slot(pages, (uint64_t)ckeys[c]);
     }
     // the larger cells' roots join their words in the mid / big kernels
     wave_append(mid, nmid, sz > kMidCell && sz <= kWordBig, c);
@@ -2710,11 +2732,11 @@ __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t nv = (uint32_t)__shfl_up((int)v, o, 64);
-        const uint64_t nw = (uint64_t)__shfl_up((long long)word, o, 64);
+        const WT nw = shfl_up_w(word, o);
         if (lane >= o && nw == word) v = root_merge(v, nv);
     }
-    const uint64_t next = (uint64_t)__shfl_down((long long)word, 1, 64);
-    if (c < nc && (lane == 63 || next != word)) word_merge(wroot, word, v);
+    const WT next = shfl_down_w(word, 1);
+    if (c < nc && (lane == 63 || next != word)) word_merge(wroot, (uint64_t)word, v);
 }
 
 template <typename K>
@@ -3722,9 +3744,14 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         W = (Gtot >> 6) + 2;
         dir = ctx.arena.get<uint4>("dir", W);
         PD_HIP(hipMemsetAsync(dir, 0, sizeof(uint4) * W, s));
-        if (R)
-            hipLaunchKernelGGL((dir_bits_kernel<K, 0>), dim3(blocks(R)), dim3(kBlock), 0, s, ckeys,
-                               dncells, dir);
+        if (R) {
+            if (sizeof(K) == 4 || key_bits <= 37)   // word ids < 2^31
+                hipLaunchKernelGGL((dir_bits_kernel<K, 0, true>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                                   ckeys, dncells, dir);
+            else
+                hipLaunchKernelGGL((dir_bits_kernel<K, 0, false>), dim3(blocks(R)), dim3(kBlock), 0,
+                                   s, ckeys, dncells, dir);
+        }
         prefix_words(dir, W, false);
     } else {
         // pages: word masks, then the occupied words before each page (the
@@ -3732,15 +3759,26 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         const uint64_t NP = (Gtot >> 12) + 2;
         pages = ctx.arena.get<uint4>("dir_pages", NP);
         PD_HIP(hipMemsetAsync(pages, 0, sizeof(uint4) * NP, s));
-        if (R)
-            hipLaunchKernelGGL((dir_bits_kernel<K, 6>), dim3(blocks(R)), dim3(kBlock), 0, s, ckeys,
-                               dncells, pages);
+        if (R) {
+            if (sizeof(K) == 4 || key_bits <= 43)   // page ids < 2^31
+                hipLaunchKernelGGL((dir_bits_kernel<K, 6, true>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                                   ckeys, dncells, pages);
+            else
+                hipLaunchKernelGGL((dir_bits_kernel<K, 6, false>), dim3(blocks(R)), dim3(kBlock), 0,
+                                   s, ckeys, dncells, pages);
+        }
         const uint64_t nw = prefix_words(pages, NP, true);
         W = nw + 1;
         dir = ctx.arena.get<uint4>("dir", W);
         if (R)
-            hipLaunchKernelGGL((word_write_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s, ckeys,
-                               dncells, pages, dir);
+        {
+            if (sizeof(K) == 4 || key_bits <= 37)   // word ids < 2^31
+                hipLaunchKernelGGL((word_write_kernel<K, true>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                                   ckeys, dncells, pages, dir);
+            else
+                hipLaunchKernelGGL((word_write_kernel<K, false>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                                   ckeys, dncells, pages, dir);
+        }
         else
             PD_HIP(hipMemsetAsync(dir, 0, sizeof(uint4), s));
     }
@@ -3872,9 +3910,14 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
             uint32_t* nbig = ctx.arena.get<uint32_t>("big_count", 4);   // [0] big, [1] mid
             PD_HIP(hipMemsetAsync(nbig, 0, 2 * sizeof(uint32_t), s));
             PD_HIP(hipMemsetAsync(wroot, 0xFF, sizeof(uint32_t) * W, s));
-            hipLaunchKernelGGL((cell_word_root_kernel<K>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                               cstart, dncells, ckeys, par, croot, wroot, mid, nbig + 1, big, nbig,
-                               pages);
+            if ((uint64_t)W < 0xFFFFFFFFull)   // directory slots < 2^32 - 1
+                hipLaunchKernelGGL((cell_word_root_kernel<K, true>), dim3(blocks(R)), dim3(kBlock), 0,
+                                   s, cstart, dncells, ckeys, par, croot, wroot, mid, nbig + 1, big,
+                                   nbig, pages);
+            else
+                hipLaunchKernelGGL((cell_word_root_kernel<K, false>), dim3(blocks(R)), dim3(kBlock),
+                                   0, s, cstart, dncells, ckeys, par, croot, wroot, mid, nbig + 1,
+                                   big, nbig, pages);
             hipLaunchKernelGGL((mid_cell_word_root_kernel<K>), dim3(2048), dim3(kBlock), 0, s,
                                cstart, ckeys, mid, nbig + 1, par, croot, wroot, pages);
             hipLaunchKernelGGL((big_cell_word_root_kernel<K>), dim3(1024), dim3(kBlock), 0, s,

@@ -2726,7 +2726,31 @@ __global__ __launch_bounds__(kBlock) void cell_word_root_kernel(
     wave_append(mid, nmid, sz > kMidCell && sz <= kWordBig, c);
     wave_append(big, nbig, sz > kWordBig, c);
     if (c < nc && sz <= kMidCell) {
-        for (uint32_t r = s; r < s + sz; ++r) v = root_merge(v, core_root(par, r));
+        // four records at a time: their parents, then the parents' parents,
+        // all in flight together (core_root walked one record's chain after
+        // another: C4's 3.4e8 cells took 8.4 ms)
+        for (uint32_t b = s; b < s + sz; b += 4) {
+            uint32_t p0[4], p1[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) p0[q] = b + q < s + sz ? par[b + q] : kNone;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) p1[q] = p0[q] != kNone ? par[p0[q]] : kNone;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (p0[q] == kNone) continue;   // not core
+                uint32_t x = p0[q];
+                if (p1[q] != x) {               // p0 is not a root: walk on
+                    x = p1[q];
+                    while (true) {
+                        const uint32_t y = par[x];
+                        if (y == x) break;
+                        x = y;
+                    }
+                    par[b + q] = x;             // the flatten (core_root's write)
+                }
+                v = root_merge(v, x);
+            }
+        }
         croot[c] = v;
     }
 #pragma unroll

@@ -81,16 +81,10 @@ def parse():
     ap.add_argument("--cpu-n", type=int, default=None,
                     help="CPU baseline sample size (default 1M; 10M for C4; 20k for d > 15)")
     ap.add_argument("--json-out", default=None)
-    ap.add_argument("--link-mode", type=int, default=None, help="PD_OPT_LINK_MODE override")
     ap.add_argument("--dir-budget", type=int, default=None,
                     help="PD_OPT_DIR_BUDGET override (bytes of the eps-grid directory)")
-    ap.add_argument("--sweep-variant", type=int, default=None,
-                    help="PD_OPT_SWEEP_VARIANT override (bit 0 count, 1 link, 2 border)")
     ap.add_argument("--count-rotate", type=int, default=None,
                     help="PD_OPT_COUNT_ROTATE override (0 = count sweeps always start at the row)")
-    ap.add_argument("--jump-rounds", type=int, default=None, help="PD_OPT_JUMP_ROUNDS override")
-    ap.add_argument("--sort-payload", type=int, default=None,
-                    help="PD_OPT_SORT_PAYLOAD override (1: coordinates ride the sort)")
     ap.add_argument("--dense-screen", type=int, default=None,
                     help="PD_OPT_DENSE_SCREEN override (1 e4m3, 0 bf16 hi.hi)")
     ap.add_argument("--dir-paged", type=int, default=None,
@@ -99,14 +93,6 @@ def parse():
                     help="PD_OPT_LABEL_BUCKETS override (0: one scattered label write per record)")
     ap.add_argument("--centre-window", type=int, default=None,
                     help="PD_OPT_CENTRE_WINDOW override (link window length)")
-    ap.add_argument("--border-lists", type=int, default=None,
-                    help="PD_OPT_BORDER_LISTS override (0: border points by a second sweep)")
-    ap.add_argument("--link-jumps", type=int, default=None,
-                    help="PD_OPT_LINK_JUMPS override (pointer jumps before the window union)")
-    ap.add_argument("--dense-prefetch", type=int, default=None,
-                    help="PD_OPT_DENSE_PREFETCH override (e4m3 count pass tiles in flight: 2/4/8)")
-    ap.add_argument("--dense-waves", type=int, default=None,
-                    help="PD_OPT_DENSE_WAVES override (e4m3 count pass waves per block: 1/2/4)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
@@ -468,20 +454,12 @@ def main():
     n, d = X.shape
     eps, ms, P = cfg["eps"], cfg["min_samples"], cfg.get("max_partitions") or 1
     ctx = _native.context(local_rank)
-    for opt, val in ((_native.PD_OPT_SWEEP_VARIANT, args.sweep_variant),
-                     (_native.PD_OPT_CENTRE_WINDOW, args.centre_window),
+    for opt, val in ((_native.PD_OPT_CENTRE_WINDOW, args.centre_window),
                      (_native.PD_OPT_COUNT_ROTATE, args.count_rotate),
-                     (_native.PD_OPT_LINK_MODE, args.link_mode),
-                     (_native.PD_OPT_JUMP_ROUNDS, args.jump_rounds),
                      (_native.PD_OPT_DIR_BUDGET, args.dir_budget),
                      (_native.PD_OPT_LABEL_BUCKETS, args.label_buckets),
-                     (_native.PD_OPT_SORT_PAYLOAD, args.sort_payload),
                      (_native.PD_OPT_DIR_PAGED, args.dir_paged),
-                     (_native.PD_OPT_DENSE_SCREEN, args.dense_screen),
-                     (_native.PD_OPT_BORDER_LISTS, args.border_lists),
-                     (_native.PD_OPT_LINK_JUMPS, args.link_jumps),
-                     (_native.PD_OPT_DENSE_PREFETCH, args.dense_prefetch),
-                     (_native.PD_OPT_DENSE_WAVES, args.dense_waves)):
+                     (_native.PD_OPT_DENSE_SCREEN, args.dense_screen)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None

@@ -58,20 +58,6 @@ enum pd_option {
                                       the reference's single-slice aggregate (slow; for
                                       bit-identical split boundaries).  Default: correctly
                                       rounded, order-independent double-double sums. */
-    PD_OPT_LINK_MODE = 4,  /* union strategy (tuning; labels identical).  6 (default): forest
-                              from the count pass's two smallest neighbours; a union over the
-                              PD_OPT_CENTRE_WINDOW records after each record, staged per wave
-                              in LDS with each record's root (the flatten), its edges reduced
-                              in an LDS forest so that one global union runs per pair of trees
-                              the window joins; then one pass over neighbouring cells that
-                              tests record pairs only where the cells' roots differ (cells
-                              whose rows hold one root are screened out first); 5: the same
-                              with a separate flatten and a global find per window edge; 3:
-                              a union over each core record's own row instead of the window;
-                              4: no window union; 0: initial forest + pointer jumping, then a
-                              lock-free union sweep over all core-core edges; 2 that sweep
-                              alone */
-    PD_OPT_JUMP_ROUNDS = 5, /* pointer-jumping rounds for link mode 0 (default 4) */
     PD_OPT_XSUB = 6,        /* sub-cells per eps along axis 0 (default 2): finer rows follow
                                the eps-ball's chord more tightly, at 1/xsub the directory
                                density */
@@ -80,21 +66,6 @@ enum pd_option {
                                (default 1; results are identical with 0) */
     PD_OPT_SWEEP_STATS = 8, /* tally the neighbour sweeps' candidates and union-find outcomes
                                into the PD_T_S_* slots (instrumented kernels; default 0) */
-    PD_OPT_SWEEP_VARIANT = 9, /* kernel variant per neighbour sweep (tuning; results are
-                               identical): bit 0 count, bit 1 link, bit 2 border; a set bit
-                               selects the batched lane kernel (wave-uniform grid in scalar
-                               registers, three rows swept as one list), a clear bit the
-                               row-by-row kernel; bit 3 (count) and bit 4 (border) the
-                               batched kernels with fp32-chord rows keyed off the query cell
-                               (override bits 0 / 2; bit 4 not with PD_OPT_BORDER_ROOTS);
-                               bit 5 with bit 3: the count sweep reads each batch's
-                               candidate windows from LDS (fp32, 2-4 D); bit 6 with bit 3
-                               / bit 7 with bit 4: the count / border kernel compiled for
-                               8 waves per SIMD (at most 64 VGPRs).
-                               Default 221 = 29 | 64 | 128 (the measured best on MI355X). */
-    PD_OPT_BORDER_ROOTS = 10, /* batched border sweep: skip or stop early where the stencil's
-                                directory words hold at most one cluster root (tuning; same
-                                labels; default 0 — slower on C2) */
     PD_OPT_DENSE_PRUNE = 11   /* d > 4 count pass: stream only the tiles inside the three-axis
                                 projection window (exact; default 1; 0 = all n^2 pairs;
                                 2 = per-band runs, the path a block takes when its segment
@@ -103,12 +74,11 @@ enum pd_option {
                                 record (r & ~255) when that lies in the query's own row, and
                                 wraps (dense cells: spreads the row-start hot spot; same
                                 counts, same labels); default 1024, 0 = never */,
-    PD_OPT_CENTRE_WINDOW = 13 /* link modes 5/6: records after each record tested by the window
-                                union (2, 4, 8, 16, 32 or 64); mode 3: forward candidates each
-                                core record tests in the centre-row union (0 = all).  Default -1:
-                                mode 6 takes 4 when cells hold <= 4 records on average, else 16
-                                (modes 3/5: 16).  A heuristic either way: the cell verify proves
-                                or tests every edge, so labels are the same */,
+    PD_OPT_CENTRE_WINDOW = 13 /* link stage: records after each record tested by the window union
+                                (2, 4, 8, 16, 32 or 64).  Default -1: 4 when cells hold <= 4
+                                records on average, else 16.  A heuristic either way: the cell
+                                verify proves or tests every core-core edge, so labels are the
+                                same */,
     PD_OPT_DIR_BUDGET = 14    /* bytes the eps-grid directory may take (flat: 20 B per 64 cells;
                                 paged: 16 B per 4096 cells + 40 B per point); beyond it every cell
                                 grows by a common factor until it fits (exact at any width >= eps;
@@ -120,9 +90,6 @@ enum pd_option {
                                 record: 1 on, 0 off, -1 (default) from 2^28 points on, where
                                 it is faster (C4 1e9: border 42 -> 38 ms; C2 1e8: slower).
                                 Same labels either way */,
-    PD_OPT_SORT_PAYLOAD = 16  /* fp32 3-D: the halo records carry their coordinates through the
-                                radix sort (16-B values) instead of a gather after it
-                                (default 0 — see DESIGN.md §6 for the measured A/B) */,
     PD_OPT_DIR_PAGED = 17     /* eps-grid directory layout: 1 paged (pages of 4096 cells hold a
                                 mask of their occupied 64-cell words; only occupied words are
                                 stored: memory and build time follow the occupied cells, not the
@@ -136,23 +103,14 @@ enum pd_option {
     PD_OPT_SHARD_CORE_BIT = 19 /* pd_train_end: 1 = the caller guarantees every global id is
                                 < 2^31, so the core flags ride bit 31 of the keys and reach
                                 core_out by one coalesced pass instead of a byte scattered per
-                                owner record (default 0; same outputs) */,
-    PD_OPT_BORDER_LISTS = 20  /* grid path, min_samples <= 33: the count sweep keeps the
-                                neighbours of every record that ends non-core (at most
-                                min_samples - 1) and the owner pass attaches a border point
-                                from that list instead of a second sweep over its candidates
-                                (default 0, measured: C2 count +0.8 ms for border -0.9 ms,
-                                C4 count +6.7 ms for no border gain; same labels either way) */,
-    PD_OPT_LINK_JUMPS = 21,   /* link modes 3-6: pointer-jumping rounds over the count pass's
-                                smallest-neighbour forest before the window union (default 0;
-                                same labels) */
-    PD_OPT_DENSE_PREFETCH = 22 /* d > 4, e4m3 count pass: 2 (default) = two register stages
-                                ahead of a double-buffered LDS tile; 4 or 8 = a ring of that many
-                                LDS buffers filled by global_load_lds (measured slower on C3: 29.9
-                                vs 21.3 ms).  Same counts either way */,
-    PD_OPT_DENSE_WAVES = 23   /* d > 4, e4m3 count pass with 2 register stages: waves per tile
-                                block (1, 2 or 4 = default; 64 query rows per wave).  Same
-                                counts either way */
+                                owner record (default 0; same outputs).  pd_train_end checks
+                                the guarantee on the device (every component key < 2^31) and
+                                returns PD_EINVAL when a key breaks it */
+    /* Retired in round 5 (measured A/Bs whose losing kernels were removed;
+       pd_ctx_set_option returns PD_EINVAL for them, and the numbers are not
+       reused): 4 LINK_MODE, 5 JUMP_ROUNDS, 9 SWEEP_VARIANT, 10 BORDER_ROOTS,
+       16 SORT_PAYLOAD, 20 BORDER_LISTS, 21 LINK_JUMPS, 22 DENSE_PREFETCH,
+       23 DENSE_WAVES.  DESIGN.md §6 keeps their measurements. */
 };
 
 /* pd_ctx_timings() slots (ms from HIP events on the call's stream; counters) */

@@ -20,27 +20,18 @@ LIB_PATH = os.environ.get("PYPARDIS_LIB") or os.path.join(HERE, "libpardis.so") 
 PD_F32, PD_F64 = 0, 1
 PD_EUCLIDEAN, PD_CITYBLOCK = 0, 1
 PD_OPT_TIMING, PD_OPT_FULL_COUNTS, PD_OPT_SEQUENTIAL_MOMENTS = 1, 2, 3
-PD_OPT_LINK_MODE, PD_OPT_JUMP_ROUNDS, PD_OPT_XSUB, PD_OPT_FP32_SCREEN = 4, 5, 6, 7
+PD_OPT_XSUB, PD_OPT_FP32_SCREEN = 6, 7
 PD_OPT_SWEEP_STATS = 8
-PD_OPT_SWEEP_VARIANT = 9
-PD_OPT_BORDER_ROOTS = 10
 PD_OPT_DENSE_PRUNE = 11
 PD_OPT_COUNT_ROTATE = 12
 PD_OPT_CENTRE_WINDOW = 13
 PD_OPT_DIR_BUDGET = 14
 PD_OPT_LABEL_BUCKETS = 15
-PD_OPT_SORT_PAYLOAD = 16
 PD_OPT_DIR_PAGED = 17
 PD_OPT_DENSE_SCREEN = 18
 PD_OPT_SHARD_CORE_BIT = 19
-PD_OPT_BORDER_LISTS = 20
-PD_OPT_LINK_JUMPS = 21
-PD_OPT_DENSE_PREFETCH = 22
-PD_OPT_DENSE_WAVES = 23
-SWEEP_VARIANT_DEFAULT = 221
-DENSE_PREFETCH_DEFAULT = 2   # ctx.dense_prefetch (internal.hpp)
-DENSE_WAVES_DEFAULT = 4      # ctx.dense_waves
-LINK_MODE_DEFAULT = 6
+# retired in round 5 (pardis.h): set_option raises for them
+PD_OPT_RETIRED = (4, 5, 9, 10, 16, 20, 21, 22, 23)
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
                 "s_count_cand", "s_link_cand", "s_link_hit", "s_link_core", "s_link_same",

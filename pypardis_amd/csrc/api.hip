@@ -136,10 +136,6 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.full_counts = value != 0;
         else if (option == PD_OPT_SEQUENTIAL_MOMENTS)
             ctx->c.seq_moments = value != 0;
-        else if (option == PD_OPT_LINK_MODE)
-            ctx->c.link_mode = (int)value;
-        else if (option == PD_OPT_JUMP_ROUNDS)
-            ctx->c.jump_rounds = (int)value;
         else if (option == PD_OPT_FP32_SCREEN)
             ctx->c.screen = value != 0;
         else if (option == PD_OPT_SWEEP_STATS)
@@ -147,11 +143,6 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         else if (option == PD_OPT_DENSE_PRUNE) {
             if (value < 0 || value > 2) throw Error(PD_EINVAL, "dense prune is 0, 1 or 2");
             ctx->c.dense_prune = (int)value;
-        } else if (option == PD_OPT_BORDER_ROOTS)
-            ctx->c.border_roots = value != 0;
-        else if (option == PD_OPT_SWEEP_VARIANT) {
-            if (value < 0 || value > 255) throw Error(PD_EINVAL, "sweep variant is an 8-bit mask");
-            ctx->c.variant = (int)value;
         } else if (option == PD_OPT_COUNT_ROTATE) {
             if (value < 0 || value > 0x7FFFFFFF) throw Error(PD_EINVAL, "count rotate must be >= 0");
             ctx->c.count_rotate = (int)value;
@@ -164,8 +155,6 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         } else if (option == PD_OPT_XSUB) {
             if (value < 1 || value > 16) throw Error(PD_EINVAL, "xsub must be in [1, 16]");
             ctx->c.xsub = (int)value;
-        } else if (option == PD_OPT_SORT_PAYLOAD) {
-            ctx->c.sort_payload = value != 0;
         } else if (option == PD_OPT_LABEL_BUCKETS) {
             ctx->c.label_buckets = value < 0 ? -1 : (value ? 1 : 0);
         } else if (option == PD_OPT_DIR_PAGED) {
@@ -175,21 +164,13 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.dense_screen = (int)value;
         } else if (option == PD_OPT_SHARD_CORE_BIT) {
             ctx->c.shard_core_bit = value != 0;
-        } else if (option == PD_OPT_BORDER_LISTS) {
-            ctx->c.border_lists = value != 0;
-        } else if (option == PD_OPT_DENSE_PREFETCH) {
-            if (value != 2 && value != 4 && value != 8)
-                throw Error(PD_EINVAL, "dense prefetch is 2, 4 or 8 tiles");
-            ctx->c.dense_prefetch = (int)value;
-        } else if (option == PD_OPT_DENSE_WAVES) {
-            if (value != 1 && value != 2 && value != 4)
-                throw Error(PD_EINVAL, "dense waves is 1, 2 or 4");
-            ctx->c.dense_waves = (int)value;
-        } else if (option == PD_OPT_LINK_JUMPS) {
-            if (value < 0 || value > 16) throw Error(PD_EINVAL, "link jumps must be in [0, 16]");
-            ctx->c.link_jumps = (int)value;
-        }
-        else
+        } else if (option == 4 || option == 5 || option == 9 || option == 10 || option == 16 ||
+                   (option >= 20 && option <= 23)) {
+            // retired tuning knobs (round 5): measured A/Bs whose losing
+            // kernels were removed; pardis.h lists them
+            throw Error(PD_EINVAL, "option " + std::to_string(option) +
+                                       " was retired (see pardis.h, pd_option)");
+        } else
             throw Error(PD_EINVAL, "unknown option");
     });
 }

@@ -99,8 +99,6 @@ struct FragSet {
                            // k8-step s (64 dims) is 64 lanes x 32 bytes, lane 32h + r holding
                            // dims 64s + 32h .. +31 of row 32g + r
     const float* norm;     // [rows_pad]
-    const float* nta8 = nullptr;   // e4m3 count pass: the C operand row term -(1+c)/2 |x|^2 x
-                                   // 2^16 (the LDS-DMA ring's source; tile_kernel PF > 2)
     const float* nmax;     // max norm over the valid rows (device scalar)
     const uint32_t* idx;   // row -> point id (null: identity)
     uint32_t m;            // valid rows
@@ -182,15 +180,6 @@ __global__ __launch_bounds__(kBlock) void prep8_kernel(const T* __restrict__ X, 
         v[w] = x;
     }
     F8[((uint64_t)(r >> 5) * KS8 + s) * 64 + 32 * h + (r & 31)] = v;
-}
-
-// |v|^2 of the scaled fp32 coordinates (the values the fragments split).
-// The e4m3 count pass's row term, as the register-staged tiles compute it
-// when they commit a tile to LDS (bit-identical).
-__global__ __launch_bounds__(kBlock) void nta8_kernel(const float* __restrict__ norm, uint32_t rp,
-                                                      float* __restrict__ nta8) {
-    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r < rp) nta8[r] = -((1.0f + kBandC) * 0.5f) * norm[r] * kF8Acc;
 }
 
 template <typename T>
@@ -313,7 +302,7 @@ __device__ __forceinline__ void tile_hit(const TileArgs<T>& A, uint32_t i, uint3
 // 110 ms — an 8-wave barrier per tile, one block per CU.)
 constexpr int kCountWaves = 4;   // waves per count-pass block (each staged tile feeds them all; 8:
                                  // 41.4 vs 36.1 ms on C3 — wider windows per block, more tiles)
-constexpr int tile_threads(int, int mode, int cw = kCountWaves) { return mode == kCount ? 64 * cw : 256; }
+constexpr int tile_threads(int, int mode) { return mode == kCount ? 64 * kCountWaves : 256; }
 constexpr int kCountQT = 2;   // query tiles (of 32) per wave in the count pass (4: one
                               // wave per SIMD, measured 125 vs 74 ms on C3)
 
@@ -333,10 +322,8 @@ struct TileLds8 {
     i32x8 f8[NB][2][KS8][64];   // [buffer][row group][k8-step][lane]
     float nta[NB][kTile];
 };
-// All of a tile block's LDS in one object: with LDS-DMA writes in flight the
-// compiler cannot tell a second __shared__ object from the staging buffers
-// and waits for the DMA before reading it (cdna_hip_programming.md,
-// "Projection GEMM at M = 256" item 4(a)).
+// All of a tile block's LDS in one object (staging buffers and the segment
+// list of its projection window).
 template <typename TL>
 struct TileShared {
     TL t;
@@ -350,50 +337,15 @@ struct TileShared {
 // KS MFMAs per wave) at one wave per SIMD.
 constexpr int kF8Waves = 3;   // e4m3 count pass: waves per SIMD (no bf16 query fragments held)
 constexpr int kF8QT = 2;      // e4m3 count pass: query tiles (of 32) per wave
-constexpr int kF8RingWaves = 3;   // ... with the LDS-DMA ring (PF > 2)
-// LDS reads beside an LDS-DMA ring.  The compiler cannot tell which LDS a
-// global_load_lds in flight writes, so it waits for every one of them
-// (vmcnt(0)) before any LDS read it emits; these reads are its own, inline,
-// so the ring stays in flight (the reader orders them after the counted
-// wait and barrier that retire the buffer it reads).
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ uint32_t lds_ld_u32(const uint32_t* p) {
-    uint32_t v;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
-    return v;
-}
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ i32x4 lds_ld_b128_nowait(uint32_t a) {
-    i32x4 v;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
-    return v;
-}
-__device__ __forceinline__ void lds_wait(i32x4& v) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v) : : "memory");
-}
 
-// PF (e4m3 count pass): 2 = two register stages ahead of a double-buffered
-// LDS tile (the first form); PF > 2 = a ring of PF LDS buffers filled by
-// LDS-DMA (global_load_lds), PF - 1 tiles in flight per block.  The C3 count
-// pass fetches its streamed tiles from the Infinity Cache at ~3.3 TB/s with
-// ~24 KiB in flight per CU (3 blocks x 2 tiles x 4 KiB); the guide's
-// gather-into-LDS rate is 8.6 TB/s at 72 KiB in flight per CU
-// (MI355X_MICROARCH.md, "Indexed rows: gather into LDS").  No VGPRs: the
-// 2-stage kernel already spills at its 168-VGPR budget.
-// CW: waves per count-pass block (PD_OPT_DENSE_WAVES; the e4m3 pass): a
-// block's window is the union of its rows' p3 windows, so smaller blocks
-// stream fewer tiles per query and wait at a narrower barrier, larger ones
-// share each staged tile across more queries.
-template <typename T, int MODE, int KS, int QT, bool F8, int PF = 2, int CW = kCountWaves>
-__global__ __launch_bounds__(tile_threads(KS, MODE, CW)) __attribute__((amdgpu_waves_per_eu(F8 ? (KS >= 8 ? 1 : (PF > 2 ? kF8RingWaves : kF8Waves)) : ((KS >= 8 || QT > 2) ? 1 : 2)))) void tile_kernel(TileArgs<T> A) {
-    // (the ring runs 2 waves per SIMD: a spill reload is a VMEM load whose
-    // wait would drain the ring)
-    constexpr bool RING = F8 && PF > 2;
-    constexpr int NB = RING ? PF : 2;   // LDS tile buffers
-    static_assert(!RING || PF <= 8, "ring depth");
-    constexpr int TB = tile_threads(KS, MODE, CW);
+// The e4m3 count pass streams each tile through two register stages ahead of
+// a double-buffered LDS tile.  (Measured and retired in round 4: an LDS-DMA
+// ring of 4 or 8 buffers — 29.9 ms vs 21.3 at 2 waves/SIMD, depth never
+// mattered — and blocks of 1 or 2 waves — 38.2 / 24.7 ms)
+template <typename T, int MODE, int KS, int QT, bool F8>
+__global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu(F8 ? (KS >= 8 ? 1 : kF8Waves) : ((KS >= 8 || QT > 2) ? 1 : 2)))) void tile_kernel(TileArgs<T> A) {
+    constexpr int NB = 2;                        // LDS tile buffers
+    constexpr int TB = tile_threads(KS, MODE);
     constexpr int QW = 32 * QT;                  // query rows per wave
     constexpr int KS8 = (KS + 3) / 4;            // e4m3 k-steps of 64 dims
     static_assert(!F8 || MODE == kCount, "the e4m3 screen is the count pass's");
@@ -584,10 +536,7 @@ __global__ __launch_bounds__(tile_threads(KS, MODE, CW)) __attribute__((amdgpu_w
     const uint32_t nseg = nseg_s;
     uint32_t ntiles = 0, nrefined = 0;
     // cursor over the tiles of the segments; false at the end
-    auto seg_at = [&](const uint32_t* p) -> uint32_t {
-        if constexpr (RING) return __builtin_amdgcn_readfirstlane(lds_ld_u32(p));   // uniform
-        else return *p;
-    };
+    auto seg_at = [&](const uint32_t* p) -> uint32_t { return *p; };
     auto seek = [&](uint32_t& sg, uint32_t& j) -> bool {
         while (sg < nseg) {
             if (j < seg_at(&seg_hi[sg])) return true;
@@ -697,50 +646,16 @@ __global__ __launch_bounds__(tile_threads(KS, MODE, CW)) __attribute__((amdgpu_w
                 // count pass, e4m3 screen (kScreen8C, in the x 2^16 units of
                 // the e4m3 products); a kept tile recomputes the split-bf16
                 // product from scratch, hi and lo from global memory
-                // ring: the wave's operands of the tile by inline LDS reads
-                i32x8 a8r[RING ? 2 : 1][RING ? KS8 : 1];
-                f32x16 ntr[RING ? 2 : 1];
-                if constexpr (RING) {
-                    i32x4 pf[2][KS8][2], pn[2][4];
-                    const uint32_t fa = lds_addr(&S.f8[buf][0][0][lane]);
-                    const uint32_t na = lds_addr(&S.nta[buf][4 * h]);
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-                        for (int s = 0; s < KS8; ++s)
-#pragma unroll
-                            for (int k = 0; k < 2; ++k)
-                                pf[u][s][k] = lds_ld_b128_nowait(fa + (uint32_t)((u * KS8 + s) * 64 * 32 + 16 * k));
-#pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            pn[u][q] = lds_ld_b128_nowait(na + (uint32_t)((32 * u + 8 * q) * 4));
-                    }
-#pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-#pragma unroll
-                        for (int s = 0; s < KS8; ++s) {
-                            lds_wait(pf[u][s][0]);
-                            lds_wait(pf[u][s][1]);
-                            a8r[u][s] = __builtin_shufflevector(pf[u][s][0], pf[u][s][1], 0, 1, 2, 3, 4, 5, 6, 7);
-                        }
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            lds_wait(pn[u][q]);
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) ntr[u][4 * q + e] = __int_as_float(pn[u][q][e]);
-                        }
-                    }
-                }
 #pragma unroll
                 for (int s = 0; s < KS8; ++s) {
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
-                        const i32x8 a8 = RING ? a8r[RING ? u : 0][RING ? s : 0] : S.f8[buf][u][s][lane];
+                        const i32x8 a8 = S.f8[buf][u][s][lane];
 #pragma unroll
                         for (int t = 0; t < QT; ++t)
                             acc[u][t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
                                 a8, bq8[t][s],
-                                s == 0 ? (RING ? ntr[RING ? u : 0] : nt_of(u)) : acc[u][t], 0, 0,
+                                s == 0 ? nt_of(u) : acc[u][t], 0, 0,
                                 0, 0, 0, 0);
                     }
                 }
@@ -758,7 +673,7 @@ __global__ __launch_bounds__(tile_threads(KS, MODE, CW)) __attribute__((amdgpu_w
                     const uint32_t iw = (wave_ok ? i0 : 0) / 32;
 #pragma unroll
                     for (int u = 0; u < 2; ++u)   // exact
-                        nt[u] = (RING ? ntr[RING ? u : 0] : nt_of(u)) * (1.0f / kF8Acc);
+                        nt[u] = nt_of(u) * (1.0f / kF8Acc);
 #pragma unroll
                     for (int s = 0; s < KS; ++s) {
                         bf16x8 ah[2], al[2], qh[QT], ql[QT];
@@ -915,7 +830,6 @@ __global__ __launch_bounds__(tile_threads(KS, MODE, CW)) __attribute__((amdgpu_w
             }
         }
     };
-    if constexpr (!RING) {
     // cursors: current tile (in LDS buf), next (in `ready`), the one after
     uint32_t sg = 0;
     j0 = seg_lo[0];
@@ -947,87 +861,6 @@ __global__ __launch_bounds__(tile_threads(KS, MODE, CW)) __attribute__((amdgpu_w
         step(stB, stA);
         if (!have) break;
         step(stA, stB);
-    }
-    } else {
-        // LDS-DMA ring: tile t in buffer t % NB.  Each wave issues G
-        // global_load_lds per tile (its 1 KiB pieces of the e4m3 fragments,
-        // and 16 of the 64 row terms); before tile t: wait until only the
-        // tiles issued after it are outstanding (counted vmcnt), one raw
-        // barrier (tile t landed for every wave, buffer (t - 1) % NB read by
-        // every wave), then refill that buffer with tile t + NB - 1.
-        constexpr int G = NCH + 1;
-        static_assert(NC % TB == 0, "whole pieces per wave");
-        // (addresses from wave-uniform scalars plus the lane: nothing held
-        // across the loop, so no spill reload — a VMEM load whose wait would
-        // drain the ring — lands between the pieces)
-        const int wu = __builtin_amdgcn_readfirstlane(wave);
-        auto issue = [&](int b, uint32_t jt) {
-            jt = __builtin_amdgcn_readfirstlane(jt);
-            uint32_t ln;   // the lane, recomputed here (a hoisted copy got spilled)
-            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-            const char* src = reinterpret_cast<const char*>(A.J.f8) + (uint64_t)(jt / 32) * KS8 * 64 * 32;
-#pragma unroll
-            for (int q = 0; q < NCH; ++q) {
-                const int c0 = wu * 64 + q * TB;   // this wave instruction's first 16-B piece
-                __builtin_amdgcn_global_load_lds(
-                    (const void*)(src + (uint64_t)c0 * 16 + ln * 16u),
-                    (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(&S.f8[b][0][0][0]) + c0 * 16),
-                    16, 0, 0);
-            }
-            if (ln < 16)
-                __builtin_amdgcn_global_load_lds(
-                    (const void*)(A.J.nta8 + (jt + wu * 16) + ln),
-                    (__attribute__((address_space(3))) void*)&S.nta[b][wu * 16], 4, 0, 0);
-        };
-        uint32_t fs = 0, fj = seg_lo[0];   // the next tile to issue
-        bool fmore = seek(fs, fj);
-        uint32_t cs = fs, cj = fj;         // the current tile (NB - 1 behind)
-        int issued = 0, t = 0;
-#pragma unroll
-        for (int k = 0; k < NB - 1; ++k) {
-            if (fmore) {
-                issue(k, fj);
-                ++issued;
-                fj += kTile;
-                fmore = seek(fs, fj);
-            }
-        }
-        bool have = issued > 0;
-        int b = 0;                         // t % NB
-#pragma unroll 1
-        while (have) {
-            if (issued - t - 1 >= NB - 2) {
-                if constexpr (G * (NB - 2) == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                else if constexpr (G * (NB - 2) == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-                else if constexpr (G * (NB - 2) == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-                else if constexpr (G * (NB - 2) == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                else if constexpr (G * (NB - 2) == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-                else if constexpr (G * (NB - 2) == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-                else if constexpr (G * (NB - 2) == 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            if (fmore) {   // into buffer (t - 1) % NB, read by every wave before the barrier
-                issue(b == 0 ? NB - 1 : b - 1, fj);
-                ++issued;
-                fj += kTile;
-                fmore = seek(fs, fj);
-            }
-            j0 = cj;
-            buf = b;
-            work();
-            ++t;
-            b = b == NB - 1 ? 0 : b + 1;
-            have = t < issued;
-            if (have) {
-                cj += kTile;
-                (void)seek(cs, cj);
-            }
-        }
-        // no DMA outstanding at exit (the last tile was waited for)
     }
     if (A.tiles && lane == 0 && ntiles) {
         atomicAdd(A.tiles, (unsigned long long)ntiles);
@@ -1252,8 +1085,6 @@ struct Geometry {
     float elo = 0, ehi = 0;
     bool mfma = false;
     bool f8 = false;       // also build the e4m3 fragments (count pass screen)
-    int pf = 2;            // e4m3 count pass: LDS tile buffers (PD_OPT_DENSE_PREFETCH)
-    int cw = kCountWaves;  // e4m3 count pass: waves per block (PD_OPT_DENSE_WAVES)
 };
 
 template <typename T>
@@ -1286,11 +1117,6 @@ FragSet make_frags(Ctx& ctx, const std::string& tag, const T* X, int d, const ui
                        X, d, idx, m, rp, G.KS, G.center, G.scale, hi, lo);
     hipLaunchKernelGGL(norm_kernel<T>, dim3(nblocks(rp)), dim3(kBlock), 0, s, X, d, idx, m, rp,
                        G.center, G.scale, nrm, nmax);
-    if (G.f8 && G.pf > 2) {
-        float* nt8 = ctx.arena.get<float>(tag + "_nta8", rp);
-        hipLaunchKernelGGL(nta8_kernel, dim3(nblocks(rp)), dim3(kBlock), 0, s, nrm, rp, nt8);
-        F.nta8 = nt8;
-    }
     PD_HIP(hipGetLastError());
     F.hi = hi;
     F.lo = lo;
@@ -1315,29 +1141,11 @@ void run_tiles(const TileArgs<T>& A, const Geometry& G, int metric, hipStream_t 
             if constexpr (MODE == kCount) {
                 if (A.I.f8 && A.J.f8) {
                     constexpr int QT8 = KS <= 4 ? kF8QT : 2;
-                    const int cw = G.pf == 2 ? G.cw : kCountWaves;
                     const unsigned grid8 =
-                        A.p3 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (cw * 32 * QT8))
-                             : nblocks((A.I.m + 32 * QT8 - 1) / (32 * QT8), cw);
-                    if (cw == 1) {
-                        hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true, 2, 1>), dim3(grid8),
-                                           dim3(64), 0, s, A);
-                        return;
-                    }
-                    if (cw == 2) {
-                        hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true, 2, 2>), dim3(grid8),
-                                           dim3(128), 0, s, A);
-                        return;
-                    }
-                    if (G.pf >= 8)
-                        hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true, 8>), dim3(grid8),
-                                           dim3(TB), 0, s, A);
-                    else if (G.pf >= 4)
-                        hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true, 4>), dim3(grid8),
-                                           dim3(TB), 0, s, A);
-                    else
-                        hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true, 2>), dim3(grid8),
-                                           dim3(TB), 0, s, A);
+                        A.p3 ? 8u * ((A.nband + 7u) / 8u) * (A.band / (TB / 64 * 32 * QT8))
+                             : nblocks((A.I.m + 32 * QT8 - 1) / (32 * QT8), TB / 64);
+                    hipLaunchKernelGGL((tile_kernel<T, MODE, KS, QT8, true>), dim3(grid8),
+                                       dim3(TB), 0, s, A);
                     return;
                 }
             }
@@ -1445,8 +1253,6 @@ void count_stage(Ctx& ctx, TrainArgs& a, int rank, int world) {
     }
     Geometry G = geometry_of(ds);
     G.f8 = G.mfma && ctx.dense_screen == 1;   // the count pass's e4m3 screen
-    G.pf = ctx.dense_prefetch;
-    G.cw = ctx.dense_waves;
     TileArgs<T> A = base_args<T>(ds);
     A.f8_a = (float)std::ldexp(std::sqrt(64.0 * ((ds.KS + 3) / 4)), -18);
 

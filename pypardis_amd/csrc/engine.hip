@@ -334,16 +334,6 @@ __device__ __forceinline__ bool in_box_t(const T (&v)[D], const PartGrid& g) {
 }
 
 
-// Directory word (16 B, one load): occupancy bits of 64 consecutive cell
-// keys + the number of occupied cells before them.
-__device__ __forceinline__ uint32_t rank_lt(const uint4* __restrict__ dir, uint64_t k) {
-    const uint4 w = dir[k >> 6];
-    const uint64_t bits = ((uint64_t)w.y << 32) | (uint64_t)w.x;
-    const uint32_t b = (uint32_t)(k & 63);
-    const uint64_t m = b ? (bits & ((~0ull) >> (64 - b))) : 0ull;
-    return w.z + (uint32_t)__popcll(m);
-}
-
 // Partition of a record: part_start is sorted.
 __device__ __forceinline__ int part_of(const uint32_t* __restrict__ ps, int P, uint32_t r) {
     int lo = 0, hi = P - 1;
@@ -375,98 +365,6 @@ template <int D>
 struct NRows {
     static constexpr int v = (D == 1) ? 1 : (D == 2 ? 3 : (D == 3 ? 9 : 27));
 };
-
-// The 3^(D-1) candidate rows around a record's cell.  For each row the
-// candidate x-range is the chord of the eps-ball at the query point: the
-// distance from the point to the row's slab in the other axes leaves a
-// half-width w = sqrt(eps^2 - d^2) (cityblock: eps - d) along axis 0, and
-// rows the ball cannot reach are skipped.  d is shrunk and w grown by a
-// 2^-20 relative slack, far above any rounding, so no pair the exact
-// predicate accepts is ever cut.  Each range is one contiguous record range.
-// Row q enumerates offsets in ascending key order.
-//
-// Latency: the grid fields are copied to registers once, keys for a batch
-// of rows are computed first, then the batch's directory words are loaded
-// together, then its cstart words — two round trips per batch instead of
-// two per row (the compiler otherwise serialises them behind the per-row
-// branches: ~36 dependent loads per record).
-// The query point's cell and in-cell fractions in its neighbourhood's grid
-// (grid fields copied to registers once).
-template <int D>
-struct QueryCell {
-    double lo[D], inv[D], cs[D], f[D];
-    int64_t nc[D], c[D];
-    uint64_t base;
-};
-
-template <int D>
-__device__ __forceinline__ QueryCell<D> query_cell(const PartGrid* gp, const double (&a)[D]) {
-    QueryCell<D> Q;
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        Q.lo[j] = gp->lo[j];
-        Q.inv[j] = gp->inv[j];
-        Q.cs[j] = gp->cs[j];
-        Q.nc[j] = gp->nc[j];
-    }
-    Q.base = gp->base;
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        const double u = (a[j] - Q.lo[j]) * Q.inv[j];
-        int64_t q = (int64_t)floor(u);
-        q = q < 0 ? 0 : q;
-        q = q >= Q.nc[j] ? Q.nc[j] - 1 : q;
-        Q.c[j] = q;
-        const double fr = u - (double)q;
-        Q.f[j] = fr < 0.0 ? 0.0 : (fr > 1.0 ? 1.0 : fr);
-    }
-    return Q;
-}
-
-// Key range [k0, k1) of candidate row q (offsets of axes 1.. in base 3, axis
-// 1 fastest), clipped to the eps-ball's chord; false if the ball misses it.
-template <int D, int M>
-__device__ __forceinline__ bool row_keys(const QueryCell<D>& Q, const double (&a)[D], double eps,
-                                         int q, uint64_t& k0, uint64_t& k1) {
-    const double slack = eps * (1.0 / 1048576.0);
-    int t = q;
-    bool okq = true;
-    double d2 = 0.0, d1 = 0.0;
-    int64_t cc[D];
-#pragma unroll
-    for (int j = 1; j < D; ++j) {
-        const int o = (t % 3) - 1;
-        t /= 3;
-        const int64_t v = Q.c[j] + o;
-        okq &= (v >= 0) & (v < Q.nc[j]);
-        cc[j] = v;
-        double dist = o == 0 ? 0.0 : (o < 0 ? Q.f[j] : 1.0 - Q.f[j]) * Q.cs[j] - slack;
-        dist = dist > 0.0 ? dist : 0.0;
-        d2 += dist * dist;
-        d1 += dist;
-    }
-    double w;
-    if constexpr (M == 0) {
-        okq &= d2 <= eps * eps;
-        w = sqrt(fmax(eps * eps - d2, 0.0));
-    } else {
-        okq &= d1 <= eps;
-        w = eps - d1;
-    }
-    w = w * (1.0 + 1.0 / 1048576.0) + slack;
-    int64_t x0 = (int64_t)floor((a[0] - w - Q.lo[0]) * Q.inv[0]);
-    int64_t x1 = (int64_t)floor((a[0] + w - Q.lo[0]) * Q.inv[0]);
-    x0 = x0 < 0 ? 0 : x0;
-    x1 = x1 >= Q.nc[0] ? Q.nc[0] - 1 : x1;
-    cc[0] = x0;
-    uint64_t lin = 0;
-#pragma unroll
-    for (int j = D - 1; j >= 0; --j) lin = lin * (uint64_t)Q.nc[j] + (uint64_t)cc[j];
-    const uint64_t kk0 = Q.base + lin;
-    k0 = okq ? kk0 : 0;
-    k1 = okq ? kk0 + (uint64_t)(x1 - x0) + 1 : 0;
-    return okq;
-}
 
 // Occupied cells with key < k, from the key's directory word.
 __device__ __forceinline__ uint32_t dir_rank(const uint4& w, uint64_t k) {
@@ -521,40 +419,6 @@ __device__ __forceinline__ uint32_t word_root_at(const Cells& C, const uint32_t*
     bool occ;
     const uint64_t s = page_slot(C.pages[k >> 12], k >> 6, occ);
     return occ ? wroot[s] : kNone;
-}
-
-template <int D, int M>
-__device__ __forceinline__ void row_ranges(const Cells& C, const double (&a)[D], int L, double eps,
-                                           uint32_t (&s)[NRows<D>::v],
-                                           uint32_t (&e)[NRows<D>::v]) {
-    constexpr int NR = NRows<D>::v;
-    constexpr int B = NR < 3 ? NR : 3;   // rows per batch
-    const QueryCell<D> Q = query_cell<D>(C.parts + L, a);
-#pragma unroll
-    for (int q0 = 0; q0 < NR; q0 += B) {
-        uint64_t k0[B], k1[B];
-        bool ok[B];
-#pragma unroll
-        for (int b = 0; b < B; ++b) ok[b] = row_keys<D, M>(Q, a, eps, q0 + b, k0[b], k1[b]);
-        uint4 w0[B], w1[B];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            w0[b] = dir_word(C, k0[b]);
-            w1[b] = dir_word(C, k1[b]);
-        }
-        uint32_t i0[B], i1[B];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            i0[b] = dir_rank(w0[b], k0[b]);
-            i1[b] = dir_rank(w1[b], k1[b]);
-        }
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-            const uint32_t sv = C.cstart[i0[b]], ev = C.cstart[i1[b]];
-            s[q0 + b] = ok[b] ? sv : 0u;
-            e[q0 + b] = ok[b] ? ev : 0u;
-        }
-    }
 }
 
 // Partition of a record.  Waves almost always sit inside one partition: try
@@ -707,7 +571,7 @@ template <typename T, int D, typename K, bool MASK>
 __global__ __launch_bounds__(kBlock) void halo_write_kernel(
     const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
     const int32_t* __restrict__ owner, KdTree tree, const uint64_t* __restrict__ tile_off,
-    K* __restrict__ keys, uint32_t* __restrict__ vals, float4* __restrict__ pay) {
+    K* __restrict__ keys, uint32_t* __restrict__ vals) {
     uint64_t idx[4];
     T v[4][D];
     unsigned long long m[4];
@@ -769,15 +633,7 @@ __global__ __launch_bounds__(kBlock) void halo_write_kernel(
                 mm &= mm - 1;
                 const K key = key_of<T, D, K>(v[q], kg[L]);
                 keys[o] = key;
-                const uint32_t vb = tag | (own == L ? kOwnerBit : 0u);
-                if constexpr (std::is_same<T, float>::value && D == 3) {
-                    if (pay) {   // the sort carries the coordinates (PD_OPT_SORT_PAYLOAD)
-                        pay[o] = make_float4(v[q][0], v[q][1], v[q][2], __uint_as_float(vb));
-                        ++o;
-                        continue;
-                    }
-                }
-                vals[o] = vb;
+                vals[o] = tag | (own == L ? kOwnerBit : 0u);
                 ++o;
             } while (mm);
         } else {
@@ -787,15 +643,7 @@ __global__ __launch_bounds__(kBlock) void halo_write_kernel(
                 K key;
                 halo_record<T, D, K>(v[q], g, key);
                 keys[o] = key;
-                const uint32_t vb = tag | (own == L ? kOwnerBit : 0u);
-                if constexpr (std::is_same<T, float>::value && D == 3) {
-                    if (pay) {
-                        pay[o] = make_float4(v[q][0], v[q][1], v[q][2], __uint_as_float(vb));
-                        ++o;
-                        continue;
-                    }
-                }
-                vals[o] = vb;
+                vals[o] = tag | (own == L ? kOwnerBit : 0u);
                 ++o;
             }
         }
@@ -818,20 +666,6 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const T* __restrict__ X,
 #pragma unroll
         for (int j = 0; j < S; ++j) Xs[r * S + j] = j < D ? X[i * D + j] : T(0);
     }
-    wave_append(dup_list, dup_count, r < R && (v & kDupBit), (uint32_t)r);
-}
-
-// PD_OPT_SORT_PAYLOAD: the sorted (x, y, z, vals) payload is Xs as it is
-// (3-D records padded to 4, the 4th word unread as a coordinate); vals and
-// the duplicate list come out of its 4th word.
-__global__ __launch_bounds__(kBlock) void payload_vals_kernel(const float4* __restrict__ pay,
-                                                              uint64_t R,
-                                                              uint32_t* __restrict__ vals,
-                                                              uint32_t* __restrict__ dup_list,
-                                                              uint32_t* __restrict__ dup_count) {
-    const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t v = r < R ? __float_as_uint(pay[r].w) : 0u;
-    if (r < R) vals[r] = v;
     wave_append(dup_list, dup_count, r < R && (v & kDupBit), (uint32_t)r);
 }
 
@@ -1063,71 +897,6 @@ __global__ __launch_bounds__(kBlock) void dir_write_kernel(uint4* __restrict__ d
     }
 }
 
-// Neighbour count + core flag: the roofline kernel (SURVEY.md §8(d) B_nc).
-// Centre row first (the early exit usually fires inside it), candidates four
-// at a time so each lane keeps four 16-byte gathers in flight.  It also keeps
-// the smallest neighbour index it saw: for a core record whose smallest seen
-// neighbour is core and below it, that is a free initial parent for the
-// union-find (ECL-CC's init step without a sweep of its own).
-template <typename T, int D, int M, bool ST>
-__global__ __launch_bounds__(kBlock) void count_kernel(const T* __restrict__ Xs, uint32_t R,
-                                                       Cells C, double eps, double eps2,
-                                                       float lo, float hi, uint32_t ms, int full,
-                                                       uint8_t* __restrict__ core,
-                                                       uint32_t* __restrict__ mn_out,
-                                                       uint32_t* __restrict__ cnt_out,
-                                                       unsigned long long* __restrict__ stats) {
-    constexpr int NR = NRows<D>::v;
-    const uint32_t r = rec_index();
-    if (r >= R) return;
-    double a[D];
-    load_rec<T, D>(Xs, r, a);
-    const int L = part_of_wave(C.part_start, C.P, r);
-    uint32_t s[NR], e[NR];
-    row_ranges<D, M>(C, a, L, eps, s, e);
-    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
-    uint32_t cnt = 0, mn = r;
-    uint32_t n_cand = 0;
-    const uint32_t stop = full ? 0xFFFFFFFFu : ms;
-#pragma unroll
-    for (int qq = 0; qq < NR; ++qq) {
-        const int q = (qq + NR / 2) % NR;
-        uint32_t j = s[q];
-        const uint32_t end = e[q];
-        for (; j + 4 <= end; j += 4) {
-            T b0[D], b1[D], b2[D], b3[D];
-            load_raw<T, D>(Xs, j, b0);
-            load_raw<T, D>(Xs, j + 1, b1);
-            load_raw<T, D>(Xs, j + 2, b2);
-            load_raw<T, D>(Xs, j + 3, b3);
-            const bool w0 = pr(b0), w1 = pr(b1),
-                       w2 = pr(b2), w3 = pr(b3);
-            if constexpr (ST) n_cand += 4;
-            cnt += (uint32_t)w0 + (uint32_t)w1 + (uint32_t)w2 + (uint32_t)w3;
-            const uint32_t h = w0 ? j : (w1 ? j + 1 : (w2 ? j + 2 : (w3 ? j + 3 : mn)));
-            mn = h < mn ? h : mn;
-            if (cnt >= stop) goto done;
-        }
-        for (; j < end; ++j) {
-            T b0[D];
-            load_raw<T, D>(Xs, j, b0);
-            if constexpr (ST) ++n_cand;
-            if (pr(b0)) {
-                ++cnt;
-                mn = j < mn ? j : mn;
-            }
-            if (cnt >= stop) goto done;
-        }
-    }
-done:
-    // bit0: core; bit1: has a neighbour besides itself (else it is noise and
-    // the border pass skips it)
-    core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
-    reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, kNone);
-    if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
-    if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
-}
-
 // Initial forest.  parent doubles as the core flag: kNone marks a non-core
 // record, so an edge test costs one load.
 // The count pass keeps the two smallest neighbours it saw (mn2[r]): the
@@ -1158,100 +927,9 @@ __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t R, const uint8_t*
     }
 }
 
-// Core-core edges (j > r only; the predicate is symmetric) → union-find.
-// The caller's root is cached: an edge to a record already under it costs
-// one L1 load, no find and no CAS.  The distance test comes first (its
-// operands are already loaded); the core flag is read only for neighbours.
-// Sweep statistics (PD_OPT_SWEEP_STATS): per-lane tallies, one atomic each
-// at the end.  ST = false compiles them away.
 struct LinkStats {
     uint32_t cand = 0, hit = 0, core = 0, same = 0, find_same = 0, unions = 0;
 };
-
-template <bool ST>
-struct Linker {
-    uint32_t* par;
-    uint32_t rr;
-    LinkStats st;
-    __device__ __forceinline__ void edge(uint32_t j) { edge(j, ld_l1(par + j)); }
-    // pj: parent[j] read ahead of the distance test (stale is fine: an older
-    // ancestor still proves membership, and a mismatch falls through to find)
-    __device__ __forceinline__ void edge(uint32_t j, uint32_t pj) {
-        if constexpr (ST) {
-            ++st.hit;
-            st.core += pj != kNone;
-            st.same += pj == rr;
-        }
-        if (pj == kNone || pj == rr) return;   // non-core, or already under our root
-        const uint32_t rj = uf_find_l1(par, pj);
-        if constexpr (ST) st.find_same += rj == rr;
-        if (rj == rr) return;
-        if constexpr (ST) ++st.unions;
-        rr = uf_link_roots(par, rr, rj);
-    }
-};
-
-template <typename T, int D, int M, bool ST>
-__global__ __launch_bounds__(kBlock) void link_kernel(const T* __restrict__ Xs, uint32_t NL,
-                                                      const uint32_t* __restrict__ list, Cells C,
-                                                      double eps, double eps2, float lo, float hi,
-                                                      uint32_t* __restrict__ par,
-                                                      unsigned long long* __restrict__ stats) {
-    constexpr int NR = NRows<D>::v;
-    const uint32_t i = rec_index();
-    if (i >= NL) return;
-    const uint32_t r = list[i];   // core records, ascending
-    double a[D];
-    load_rec<T, D>(Xs, r, a);
-    const int L = part_of_wave(C.part_start, C.P, r);
-    uint32_t s[NR], e[NR];
-    row_ranges<D, M>(C, a, L, eps, s, e);
-    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
-    Linker<ST> lk{par, uf_find_l1(par, r), {}};
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-        uint32_t j = s[q] > r + 1 ? s[q] : r + 1;
-        const uint32_t end = e[q];
-        for (; j + 4 <= end; j += 4) {
-            // coordinates and parents of four candidates in flight together
-            T b0[D], b1[D], b2[D], b3[D];
-            load_raw<T, D>(Xs, j, b0);
-            load_raw<T, D>(Xs, j + 1, b1);
-            load_raw<T, D>(Xs, j + 2, b2);
-            load_raw<T, D>(Xs, j + 3, b3);
-            const uint32_t p0 = ld_l1(par + j), p1 = ld_l1(par + j + 1), p2 = ld_l1(par + j + 2),
-                           p3 = ld_l1(par + j + 3);
-            if constexpr (ST) lk.st.cand += 4;
-            if (pr(b0)) lk.edge(j, p0);
-            if (pr(b1)) lk.edge(j + 1, p1);
-            if (pr(b2)) lk.edge(j + 2, p2);
-            if (pr(b3)) lk.edge(j + 3, p3);
-        }
-        for (; j < end; ++j) {
-            T b0[D];
-            load_raw<T, D>(Xs, j, b0);
-            const uint32_t p0 = ld_l1(par + j);
-            if constexpr (ST) ++lk.st.cand;
-            if (pr(b0)) lk.edge(j, p0);
-        }
-    }
-    if constexpr (ST) {
-        atomicAdd(stats + 1, (unsigned long long)lk.st.cand);
-        atomicAdd(stats + 2, (unsigned long long)lk.st.hit);
-        atomicAdd(stats + 3, (unsigned long long)lk.st.core);
-        atomicAdd(stats + 4, (unsigned long long)lk.st.same);
-        atomicAdd(stats + 5, (unsigned long long)lk.st.find_same);
-        atomicAdd(stats + 6, (unsigned long long)lk.st.unions);
-    }
-}
-
-// One pointer-jumping round over the core records: par[r] = par[par[r]].
-__global__ __launch_bounds__(kBlock) void jump_kernel(uint32_t R, const uint8_t* __restrict__ core,
-                                                      uint32_t* __restrict__ par) {
-    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R || !(core[r] & 1)) return;
-    par[r] = par[par[r]];   // chains hold core records only
-}
 
 // A point's copies in several neighbourhoods (the dup list): link every core
 // copy to one representative (the smallest record), gluing the
@@ -1404,26 +1082,6 @@ __global__ __launch_bounds__(kBlock) void root_rank_kernel(const uint32_t* __res
     if (i < C) gmin[roots_sorted[i]] = i;
 }
 
-__global__ __launch_bounds__(kBlock) void flatten_kernel(uint32_t R,
-                                                         const uint8_t* __restrict__ core,
-                                                         uint32_t* __restrict__ par) {
-    // par doubles as the core flag (kNone: not core, init_kernel), so the
-    // core array is not read; records already under their root are not
-    // written (most of them, after the first flatten)
-    (void)core;
-    const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
-    if (r >= R) return;
-    const uint32_t x0 = par[r];
-    if (x0 == kNone) return;
-    uint32_t x = x0;
-    while (true) {
-        const uint32_t p = par[x];
-        if (p == x) break;
-        x = p;
-    }
-    if (x != x0) par[r] = x;
-}
-
 // Sharded train, phase A exports: (global id, local component key) of every
 // core record whose point was also routed to another device.
 struct IsExport {
@@ -1452,15 +1110,20 @@ __global__ __launch_bounds__(kBlock) void export_kernel(uint32_t NL,
 }
 
 // Phase B: replace each local component's key by its global key (ids in no
-// export keep their own: the component never left this device).
+// export keep their own: the component never left this device).  Every key
+// a record of this device can take is such a root's; with the core flag in
+// the keys (core_mask, PD_OPT_SHARD_CORE_BIT) a key with that bit already set
+// would be read back as a core flag, so it raises *err instead.
 __global__ __launch_bounds__(kBlock) void remap_kernel(uint32_t R, const uint8_t* __restrict__ core,
                                                        const uint32_t* __restrict__ par,
                                                        const uint32_t* __restrict__ map_ids,
                                                        const uint32_t* __restrict__ map_keys,
-                                                       uint32_t n_map, uint32_t* __restrict__ gmin) {
+                                                       uint32_t n_map, uint32_t core_mask,
+                                                       uint32_t* __restrict__ gmin,
+                                                       uint32_t* __restrict__ err) {
     const uint32_t r = blockIdx.x * kBlock + threadIdx.x;
     if (r >= R || !(core[r] & 1) || par[r] != r) return;
-    const uint32_t k = gmin[r];
+    uint32_t k = gmin[r];
     uint32_t lo = 0, hi = n_map;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -1469,7 +1132,11 @@ __global__ __launch_bounds__(kBlock) void remap_kernel(uint32_t R, const uint8_t
         else
             hi = mid;
     }
-    if (lo < n_map && map_ids[lo] == k) gmin[r] = map_keys[lo];
+    if (lo < n_map && map_ids[lo] == k) {
+        k = map_keys[lo];
+        gmin[r] = k;
+    }
+    if (k & core_mask) atomicOr(err, 1u);
 }
 
 // Owner records: publish core flag / count, and the cluster key of core
@@ -1487,8 +1154,6 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
                                                        const uint32_t* __restrict__ gmin,
                                                        const uint32_t* __restrict__ cnt_rec,
                                                        const uint2* __restrict__ mn,
-                                                       const uint32_t* __restrict__ blist,
-                                                       const uint32_t* __restrict__ boff,
                                                        uint32_t core_mask,
                                                        uint32_t* __restrict__ key_out,
                                                        uint8_t* __restrict__ core_out,
@@ -1506,23 +1171,11 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
         const bool own = r < R && (v & kOwnerBit);
         const uint8_t fl = own ? core[r] : 0;
         // the record's key: core -> its component's; a border record with a
-        // list of its neighbours (count sweep) -> the smallest key among the
-        // core ones, a border record with a single neighbour (bit 2) -> that
-        // neighbour's if it is core (the border sweep's smallest core key,
-        // over one candidate); else none
+        // single neighbour (bit 2) -> that neighbour's if it is core (the
+        // border sweep's smallest core key, over one candidate); else none
         uint32_t key = kNone;
-        bool listed = false;
         if (fl & 1) {
             key = gmin[par[r]] | core_mask;
-        } else if ((fl & 3) == 2 && blist && boff[r] != kNone) {
-            listed = true;
-            const uint32_t o = boff[r], len = blist[o];
-            for (uint32_t k = 0; k < len; ++k) {
-                const uint32_t j = blist[o + 1 + k];
-                const uint32_t pj = j < R ? par[j] : kNone;
-                const uint32_t kk = pj != kNone ? gmin[pj] : kNone;
-                key = kk < key ? kk : key;
-            }
         } else if ((fl & 7) == 6 && mn) {
             const uint2 m = mn[r];
             const uint32_t j = m.x == r ? m.y : m.x;
@@ -1538,7 +1191,7 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
             if (key != kNone && key_out) key_out[pt] = key;
         }
         // the rest of the border candidates go to the sweep
-        nb += own && (fl & 3) == 2 && !listed && !((fl & 4) && mn) ? 1u : 0u;
+        nb += own && (fl & 3) == 2 && !((fl & 4) && mn) ? 1u : 0u;
     }
     // border candidates (owner record, not core, has a neighbour) per tile;
     // border_list_kernel lists them in order after a scan of the counts
@@ -1549,8 +1202,6 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
 __global__ __launch_bounds__(kBlock) void border_list_kernel(uint32_t R,
                                                              const uint32_t* __restrict__ vals,
                                                              const uint8_t* __restrict__ core,
-                                                             int single_done,
-                                                             const uint32_t* __restrict__ boff,
                                                              const uint64_t* __restrict__ tile_off,
                                                              uint32_t* __restrict__ blist) {
     // the owner_kernel tiling: kOwnPer consecutive records per thread, so the
@@ -1562,11 +1213,8 @@ __global__ __launch_bounds__(kBlock) void border_list_kernel(uint32_t R,
     for (int q = 0; q < kOwnPer; ++q) {
         const uint32_t r = r0 + q;
         const uint8_t fl = r < R ? core[r] : 0;
-        // (owner_kernel's rule: listed records and, without a list, single-
-        // neighbour records are attached there)
-        const bool listed = boff && r < R && (fl & 3) == 2 && boff[r] != kNone;
-        cand[q] = r < R && (vals[r] & kOwnerBit) && (fl & 3) == 2 && !listed &&
-                  !(single_done && (fl & 4));
+        // (owner_kernel's rule: single-neighbour records are attached there)
+        cand[q] = r < R && (vals[r] & kOwnerBit) && (fl & 3) == 2 && !(fl & 4);
         nc += cand[q] ? 1u : 0u;
     }
     uint32_t btot;
@@ -1578,69 +1226,12 @@ __global__ __launch_bounds__(kBlock) void border_list_kernel(uint32_t R,
         if (cand[q]) blist[base + off++] = r0 + q;
 }
 
-struct IsCore {
-    const uint8_t* core;
-    __device__ bool operator()(uint32_t r) const { return core[r] & 1; }
-};
-
-// Border records (compacted list): smallest cluster key among the core
-// neighbours — sklearn's first-discovered-cluster rule.
-template <typename T, int D, int M>
-__global__ __launch_bounds__(kBlock) void border_kernel(
-    const T* __restrict__ Xs, uint32_t NL, const uint32_t* __restrict__ list, Cells C, double eps,
-    double eps2, float lo, float hi, const uint32_t* __restrict__ vals,
-    const uint32_t* __restrict__ par,
-    const uint32_t* __restrict__ gmin, uint32_t* __restrict__ key_out) {
-    const uint32_t i = rec_index();
-    if (i >= NL) return;
-    const uint32_t r = list[i];   // owner, non-core records with a neighbour, ascending
-    const uint32_t pt = vals[r] & kIdMask;
-    constexpr int NR = NRows<D>::v;
-    double a[D];
-    load_rec<T, D>(Xs, r, a);
-    const int L = part_of_wave(C.part_start, C.P, r);
-    uint32_t s[NR], e[NR];
-    row_ranges<D, M>(C, a, L, eps, s, e);
-    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
-    uint32_t best = kNone;
-    auto take = [&](uint32_t pj) {
-        if (pj == kNone) return;   // not core
-        const uint32_t k = gmin[pj];
-        best = k < best ? k : best;
-    };
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-        uint32_t j = s[q];
-        const uint32_t end = e[q];
-        for (; j + 4 <= end; j += 4) {
-            T b0[D], b1[D], b2[D], b3[D];
-            load_raw<T, D>(Xs, j, b0);
-            load_raw<T, D>(Xs, j + 1, b1);
-            load_raw<T, D>(Xs, j + 2, b2);
-            load_raw<T, D>(Xs, j + 3, b3);
-            const uint32_t p0 = par[j], p1 = par[j + 1], p2 = par[j + 2], p3 = par[j + 3];
-            if (pr(b0)) take(p0);
-            if (pr(b1)) take(p1);
-            if (pr(b2)) take(p2);
-            if (pr(b3)) take(p3);
-        }
-        for (; j < end; ++j) {
-            T b0[D];
-            load_raw<T, D>(Xs, j, b0);
-            const uint32_t p0 = par[j];
-            if (pr(b0)) take(p0);
-        }
-    }
-    key_out[pt] = best;
-}
-
-// ------------------------------------------------------------------ batched lane sweeps
-// One lane per record (as above), restructured for latency (PD_OPT_SWEEP_VARIANT
-// bits): the neighbourhood index is made wave-uniform (a waterfall over the
-// wave's distinct neighbourhoods — almost always one), so the grid parameters
-// sit in scalar registers; rows are taken three at a time and the three
-// ranges are swept as ONE virtual list, four candidates per round trip with
-// no per-row remainder loops.  Fewer live registers, more waves in flight.
+// ------------------------------------------------------------------ lane sweeps
+// One lane per record, restructured for latency: the neighbourhood index is
+// made wave-uniform (almost always one per wave), so the grid parameters sit
+// in scalar registers; rows are taken three at a time and the three ranges
+// are swept as ONE virtual list, four candidates per round trip with no
+// per-row remainder loops.  Fewer live registers, more waves in flight.
 __device__ __forceinline__ double uniform_f64(double v) {
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xFFFFFFFFll));
@@ -1651,31 +1242,6 @@ __device__ __forceinline__ int64_t uniform_i64(int64_t v) {
     const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xFFFFFFFFll));
     const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
     return ((int64_t)hi << 32) | (unsigned int)lo;
-}
-
-// Grid of neighbourhood L (wave-uniform L) in scalar registers + the query's cell.
-template <int D>
-__device__ __forceinline__ QueryCell<D> query_cell_u(const PartGrid* gp, const double (&a)[D]) {
-    QueryCell<D> Q;
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        Q.lo[j] = uniform_f64(gp->lo[j]);
-        Q.inv[j] = uniform_f64(gp->inv[j]);
-        Q.cs[j] = uniform_f64(gp->cs[j]);
-        Q.nc[j] = uniform_i64(gp->nc[j]);
-    }
-    Q.base = (uint64_t)uniform_i64((int64_t)gp->base);
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        const double u = (a[j] - Q.lo[j]) * Q.inv[j];
-        int64_t q = (int64_t)floor(u);
-        q = q < 0 ? 0 : q;
-        q = q >= Q.nc[j] ? Q.nc[j] - 1 : q;
-        Q.c[j] = q;
-        const double fr = u - (double)q;
-        Q.f[j] = fr < 0.0 ? 0.0 : (fr > 1.0 ? 1.0 : fr);
-    }
-    return Q;
 }
 
 // Runs body(L, uniform): when the whole wave lies in one neighbourhood (all
@@ -1693,158 +1259,27 @@ __device__ __forceinline__ void with_part(const uint32_t* __restrict__ ps, int P
         body(part_of(ps, P, r), std::false_type{});
 }
 
-template <int D>
-struct RowBatch {
-    static constexpr int NR = NRows<D>::v;
-    static constexpr int B = NR < 3 ? NR : 3;   // rows per batch
-    static constexpr int NB = NR / B;           // batches
-};
-
-// Ranges of the rows of batch `bt` (row order within the batch: centre row
-// first when centre_first), clipped below at clip, as one virtual list:
-// position v < tot maps to record v + off[k] for v in [pre[k], pre[k+1]).
-template <int D, int M>
-__device__ __forceinline__ uint32_t batch_list(const Cells& C, const QueryCell<D>& Q,
-                                               const double (&a)[D], double eps, int bt,
-                                               bool centre_first, uint32_t clip,
-                                               uint32_t (&pre)[RowBatch<D>::B],
-                                               uint32_t (&off)[RowBatch<D>::B]) {
-    constexpr int B = RowBatch<D>::B;
-    uint64_t k0[B], k1[B];
-    bool ok[B];
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-        const int bb = (centre_first && B == 3) ? (b == 0 ? 1 : (b == 1 ? 0 : 2)) : b;
-        ok[b] = row_keys<D, M>(Q, a, eps, bt * B + bb, k0[b], k1[b]);
-    }
-    uint4 w0[B], w1[B];
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-        w0[b] = dir_word(C, k0[b]);
-        w1[b] = dir_word(C, k1[b]);
-    }
-    uint32_t i0[B], i1[B];
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-        i0[b] = dir_rank(w0[b], k0[b]);
-        i1[b] = dir_rank(w1[b], k1[b]);
-    }
-    uint32_t tot = 0;
-#pragma unroll
-    for (int b = 0; b < B; ++b) {
-        const uint32_t sv = C.cstart[i0[b]], ev = C.cstart[i1[b]];
-        uint32_t st = ok[b] ? sv : 0u;
-        const uint32_t en = ok[b] ? ev : 0u;
-        st = st > clip ? st : clip;
-        const uint32_t len = en > st ? en - st : 0u;
-        pre[b] = tot;
-        off[b] = st - tot;
-        tot += len;
-    }
-    return tot;
-}
-
-template <int B>
-__device__ __forceinline__ uint32_t bpos(uint32_t v, const uint32_t (&pre)[B],
-                                         const uint32_t (&off)[B]) {
-    uint32_t o = off[0];
-#pragma unroll
-    for (int b = 1; b < B; ++b) o = v >= pre[b] ? off[b] : o;
-    return v + o;
-}
-
+// A long centre list (dense cells, PD_OPT_COUNT_ROTATE): the sweep starts at
+// record r & ~(kRotAlign - 1) when that lies in the query's centre row, and
+// wraps.  The records of a dense row then do not all stream the same first
+// lines (one hot L2 channel per row start), the early exit comes sooner (the
+// block's records are in the query's own cell), and the smallest neighbour
+// found is still near a shared record, so the initial forest stays shallow.
 constexpr uint32_t kRotAlign = 256;
 
-template <typename T, int D, int M, bool ST>
-__global__ __launch_bounds__(kBlock) void count2_kernel(const T* __restrict__ Xs, uint32_t R,
-                                                        Cells C, double eps, double eps2,
-                                                        float lo, float hi, uint32_t ms, int full,
-                                                        uint32_t rot_min,
-                                                        uint8_t* __restrict__ core,
-                                                        uint32_t* __restrict__ mn_out,
-                                                        uint32_t* __restrict__ cnt_out,
-                                                        unsigned long long* __restrict__ stats) {
-    constexpr int B = RowBatch<D>::B, NB = RowBatch<D>::NB;
-    const uint32_t r = rec_index();
-    if (r >= R) return;
-    double a[D];
-    load_rec<T, D>(Xs, r, a);
-    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
-    const uint32_t stop = full ? 0xFFFFFFFFu : ms;
-    uint32_t cnt = 0, mn = kNone, mn2 = kNone, n_cand = 0;
-    with_part(C.part_start, C.P, r, [&](int L, auto U) {
-        const QueryCell<D> Q = decltype(U)::value ? query_cell_u<D>(C.parts + L, a)
-                                                  : query_cell<D>(C.parts + L, a);
-        for (int bq = 0; bq < NB; ++bq) {
-            const int bt = (bq + NB / 2) % NB;   // centre batch first
-            uint32_t pre[B], off[B];
-            const uint32_t tot = batch_list<D, M>(C, Q, a, eps, bt, true, 0u, pre, off);
-            // a long list (dense cells): start at record r & ~(kRotAlign-1)
-            // when it lies in the query's centre row (the first row of the
-            // centre batch), and wrap.  The records of a dense row then do
-            // not all stream the same first lines (one hot L2 channel per
-            // row start), the early exit comes sooner (the block's records
-            // are in the query's own cell), and the smallest neighbour
-            // found is still near a shared record, so the initial forest
-            // stays shallow (one tree per aligned block, joined by the
-            // centre-row union)
-            uint32_t v0 = 0;
-            if (bq == 0 && tot > rot_min) {
-                const uint32_t vr = (r & ~(kRotAlign - 1u)) - off[0];
-                const uint32_t clen = B > 1 ? pre[B > 1 ? 1 : 0] : tot;   // centre row
-                v0 = vr < clen ? vr : 0u;
-            }
-            // the wrap costs two ops per candidate: only waves with a
-            // rotated lane pay it
-            auto sweep = [&](auto ROT) -> bool {
-                for (uint32_t v = 0; v < tot; v += 4) {
-                    uint32_t j[4];
-                    T b[4][D];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        uint32_t w = v + u;
-                        if constexpr (decltype(ROT)::value) {
-                            w += v0;
-                            w = w >= tot ? w - tot : w;
-                        }
-                        j[u] = v + u < tot ? bpos<B>(w, pre, off) : r;
-                        load_raw<T, D>(Xs, j[u], b[u]);
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const bool h = (v + u < tot) && pr(b[u]);
-                        cnt += h ? 1u : 0u;
-                        const uint32_t jj = h ? j[u] : kNone;
-                        mn2 = min(mn2, max(mn, jj));   // the two smallest hits
-                        mn = min(mn, jj);
-                    }
-                    if constexpr (ST) n_cand += (tot - v < 4u ? tot - v : 4u);
-                    if (cnt >= stop) return true;
-                }
-                return false;
-            };
-            const bool stopped = __any(v0 != 0) ? sweep(std::true_type{}) : sweep(std::false_type{});
-            if (stopped) return;
-        }
-    });
-    core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0);
-    reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, mn2);
-    if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
-    if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
-}
-
 // ------------------------------------------------------------------ cheap-row count
-// count4_kernel (PD_OPT_SWEEP_VARIANT bit 3, the default): count2_kernel's
-// lockstep sweep — three rows as one virtual list, centre batch first, the
-// rotated start in long centre rows, four candidates per round trip — with a
-// row's candidate range at about a third of the instructions.  count2 spent
-// 3.29e9 VALU instructions per C2 launch (PMC), and the fp64 chord of every
-// row (sqrt, two floors, 64-bit key arithmetic from the cell coordinates:
-// ~130 instructions a row, nine rows) was most of them.  (At the guide's
-// issue rate — a wave64 VALU instruction takes 2 cycles on a SIMD-32, so 2
-// wave-instructions per CU per cycle — count4's 2.66e9 are 0.44 of the issue
-// budget of its 4.87 ms: the sweep is bound by the vector-memory path, see
-// count5_kernel.)  Here, per record once: the fp64 cell index exactly as the
+// count4_kernel: the neighbour count sweep.  Rows are taken three at a time
+// (centre batch first, centre row first) and the three record ranges swept
+// as ONE virtual list, four candidates per round trip, with a rotated start
+// in long centre rows.  A row's candidate range costs about a third of the
+// instructions of the fp64 chord (sqrt, two floors, 64-bit key arithmetic
+// from the cell coordinates: ~130 instructions a row, nine rows, which was
+// most of the earlier sweep's 3.29e9 VALU instructions per C2 launch).  (At
+// the guide's issue rate — a wave64 VALU instruction takes 2 cycles on a
+// SIMD-32, so 2 wave-instructions per CU per cycle — count4's 2.66e9 are
+// 0.44 of the issue budget: the sweep is bound by the latency of its
+// dependent record -> directory word -> cell start -> candidate chain;
+// DESIGN.md §4.)  Here, per record once: the fp64 cell index exactly as the
 // record keys were built, the in-cell fractions, the squared distances to the
 // neighbour rows; per row: the chord in fp32 from those (distances shrunk by
 // 2^-16 relative + 2^-20 of a cell, the chord grown by 2^-16 relative + 2^-16
@@ -1977,56 +1412,19 @@ __device__ __forceinline__ void row_range3(const Cells& C, const Count3Grid<T, D
     e = e > s ? e : s;
 }
 
-// Border lists (PD_OPT_BORDER_LISTS, min_samples <= kListMax + 1 = 33): a record
-// that ends the sweep non-core has met every neighbour it has (no early exit
-// below min_samples), at most min_samples - 1 of them.  The sweep keeps its
-// hits in LDS as it goes (slot = hits so far, lane fastest: conflict-free)
-// and, at the end, a non-core record with a neighbour besides itself writes
-// them to a compact list — [len, hits...] at BorderLists::off[r], one
-// wave-aggregated reservation per wave.  The owner pass then attaches such a
-// border record from its list (the smallest key among its core neighbours:
-// one gather per hit) instead of a second sweep over every candidate; a
-// record whose list did not fit (cap) gets kNone and is swept as before.
-constexpr int kListMax = 32;
-
-// The list buffer is cut into kListStripes stripes, each with its own
-// reservation counter (stripe = block id mod kListStripes): one counter for
-// every wave of the grid serialised ~1.6e6 same-address atomics on C2.
-constexpr uint32_t kListStripes = 256;
-
-struct BorderLists {
-    uint32_t* list;    // [kListStripes * cap]: per listed record len, then len hit records
-    uint32_t* off;     // [R]: list offset of a non-core record with a neighbour, or kNone
-    uint32_t* count;   // [kListStripes]: entries reserved so far in each stripe
-    uint32_t cap;      // entries per stripe
-};
-
 // WPE: the minimum waves per SIMD the register allocation must allow (1: no
-// constraint; 8: at most 64 VGPRs — PD_OPT_SWEEP_VARIANT bit 6)
-template <typename T, int D, int M, bool ST, bool LST, int WPE = 1>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void count4_kernel(const T* __restrict__ Xs, uint32_t R,
-                                                        Cells C, double eps, double eps2,
-                                                        float lo, float hi, uint32_t ms, int full,
-                                                        uint32_t rot_min,
-                                                        uint8_t* __restrict__ core,
-                                                        uint32_t* __restrict__ mn_out,
-                                                        uint32_t* __restrict__ cnt_out,
-                                                        unsigned long long* __restrict__ stats,
-                                                        BorderLists BL) {
+// constraint, the instrumented sweep; 8: at most 64 VGPRs, the default — the
+// candidate gathers want the occupancy: C2 count 4.87 -> 4.58 ms)
+template <typename T, int D, int M, bool ST, int WPE = 1>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void count4_kernel(
+    const T* __restrict__ Xs, uint32_t R, Cells C, double eps, double eps2, float lo, float hi,
+    uint32_t ms, int full, uint32_t rot_min, uint8_t* __restrict__ core,
+    uint32_t* __restrict__ mn_out, uint32_t* __restrict__ cnt_out,
+    unsigned long long* __restrict__ stats) {
     constexpr int NR = NRows<D>::v;
     constexpr int B = NR < 3 ? NR : 3, NB = NR / B;
-    // LST: min_samples - 1 hit slots per lane (dynamic LDS, lane fastest)
-    // (not named L: the neighbourhood index of with_part's body is)
-    extern __shared__ uint32_t s_list_dyn[];
-    const uint32_t n_slots = ms > 1 ? ms - 1 : 1;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t* s_hit = s_list_dyn + (size_t)wv * n_slots * 64 + lane;
-    (void)s_hit;
-    const uint32_t r0 = rec_index();
-    // with lists the whole wave stays to the end (the reservation scans it)
-    if (!LST && r0 >= R) return;
-    const bool live = r0 < R;
-    const uint32_t r = live ? r0 : R - 1;
+    const uint32_t r = rec_index();
+    if (r >= R) return;
     double a[D];
     load_rec<T, D>(Xs, r, a);
     const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
@@ -2052,7 +1450,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
                 return j;
             };
             // a long centre batch: start at record r & ~(kRotAlign - 1) when it
-            // lies in the centre row (count2_kernel's rotation) and wrap
+            // lies in the centre row, and wrap
             uint32_t v0 = 0;
             if (bt == 0 && tot > rot_min) {
                 const uint32_t vr = (r & ~(kRotAlign - 1u)) - s0;
@@ -2075,9 +1473,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const bool h = (v + u < tot) && pr(b[u]);
-                        if constexpr (LST) {
-                            if (h && cnt < n_slots) s_hit[cnt * 64] = j[u];
-                        }
                         cnt += h ? 1u : 0u;
                         const uint32_t x = h ? j[u] : kNone;
                         mn2 = min(mn2, max(mn, x));   // the two smallest hits
@@ -2092,33 +1487,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
             if (stopped) return;
         }
     });
-    if constexpr (LST) {
-        // non-core with a neighbour besides itself: its hits (self included)
-        // go to the compact list; the whole wave is active here
-        const bool want = live && cnt >= 2 && cnt < ms;
-        const uint32_t need = want ? cnt + 1u : 0u;
-        uint32_t incl = need;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
-            if (lane >= o) incl += y;
-        }
-        const uint32_t wtot = (uint32_t)__shfl((int)incl, 63, 64);
-        const uint32_t stripe = blockIdx.x % kListStripes;
-        uint32_t base = 0;
-        if (lane == 0 && wtot) base = atomicAdd(BL.count + stripe, wtot);
-        base = (uint32_t)__shfl((int)base, 0, 64) + (incl - need);
-        if (want) {
-            const bool fits = (uint64_t)base + need <= (uint64_t)BL.cap;
-            const uint32_t o = stripe * BL.cap + base;
-            BL.off[r] = fits ? o : kNone;
-            if (fits) {
-                BL.list[o] = cnt;
-                for (uint32_t k = 0; k < cnt; ++k) BL.list[o + 1 + k] = s_hit[k * 64];
-            }
-        }
-        if (!live) return;
-    }
     // bit 2: exactly one neighbour besides the record itself (no early exit
     // below min_samples, so the sweep saw it, and it is the other of the two
     // smallest hits): owner_kernel attaches such a border record directly
@@ -2128,356 +1496,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) v
     if constexpr (ST) atomicAdd(stats + 0, (unsigned long long)n_cand);
 }
 
-// ------------------------------------------------------------------ staged count
-// count5_kernel (PD_OPT_SWEEP_VARIANT bit 5, the default for fp32 2-D / 3-D /
-// 4-D): count4_kernel with each batch's candidates read from LDS.  PMC of
-// count4 (C2): 89 vector-memory instructions per 64-record wave, ~65 of them
-// candidate gathers, the texture addresser busy ~0.73 of the kernel and the
-// VALU ~0.44 of its issue rate: the sweep is bound by the vector-memory path
-// (addresses and round-trip latency), not by DRAM.  A wave's 64 records are
-// cell-sorted (~28 cells of one grid row for C2), so each row slot of a
-// batch covers one short, contiguous record window for the whole wave — the
-// union of the lanes' chord ranges, ~75 records per row.  When the three
-// windows of a batch fit the wave's LDS slice (kStageRecs records), the wave
-// copies them with coalesced 16-B loads (a few instructions for ~220
-// records) and every lane sweeps its own ranges out of LDS; otherwise (a wave
-// spanning grid rows, dense cells, a wave spanning neighbourhoods) it sweeps
-// from global memory exactly as count4.  Candidate order, early exit and
-// outputs are count4's (a batch staged or not visits the same positions in
-// the same order), so counts, core flags and the two smallest hits are
-// identical (`test_sweep_variants_exact`).
-extern "C" __device__ uint32_t __ockl_wfred_min_u32(uint32_t);
-extern "C" __device__ uint32_t __ockl_wfred_max_u32(uint32_t);
-
-// Order this wave's LDS writes before its lanes' reads of other lanes' data
-// (one wave: no workgroup barrier; waves of a block run different batch counts).
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-constexpr int kStageBytes = 5120;   // per wave: 320 3-D records (20 KiB per block)
-
-template <int S>
-struct StageVec {
-    using type = typename std::conditional<S == 4, float4, float2>::type;
-};
-
-template <typename T, int D, int M, bool ST>
-__global__ __launch_bounds__(kBlock) void count5_kernel(const T* __restrict__ Xs, uint32_t R,
-                                                        Cells C, double eps, double eps2,
-                                                        float lo, float hi, uint32_t ms, int full,
-                                                        uint32_t rot_min,
-                                                        uint8_t* __restrict__ core,
-                                                        uint32_t* __restrict__ mn_out,
-                                                        uint32_t* __restrict__ cnt_out,
-                                                        unsigned long long* __restrict__ stats) {
-    static_assert(std::is_same<T, float>::value, "fp32 records only");
-    constexpr int NR = NRows<D>::v;
-    constexpr int B = NR < 3 ? NR : 3, NB = NR / B;
-    constexpr int S = Stride<D>::v;
-    static_assert(S == 2 || S == 4, "2-D, 3-D or 4-D records");
-    using V = typename StageVec<S>::type;
-    constexpr uint32_t CAP = kStageBytes / sizeof(V);
-    __shared__ V stage[kBlock / 64][CAP];
-    if (R == 0) return;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t r0 = rec_index();
-    const bool live = r0 < R;
-    // no lane leaves early: the window reductions below need the whole wave
-    // (a tail lane mirrors the last record and is done from the start)
-    const uint32_t r = live ? r0 : R - 1;
-    double a[D];
-    load_rec<T, D>(Xs, r, a);
-    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
-    const uint32_t stop = full ? 0xFFFFFFFFu : ms;
-    float e2 = M == 0 ? (float)eps2 : (float)eps;
-    e2 = e2 * (1.0f + 1.0f / 65536.0f);
-    uint32_t cnt = 0, mn = kNone, mn2 = kNone, n_cand = 0, n_staged = 0, n_batches = 0;
-    bool done = !live;
-    const V* __restrict__ Xv = reinterpret_cast<const V*>(Xs);
-    with_part(C.part_start, C.P, r, [&](int L, auto U) {
-        Count3Grid<T, D, M, decltype(U)::value> g;
-        g.load(C.parts + L);
-        const RowGeo<D> geo = row_geo<T, D, M, decltype(U)::value>(g, a);
-        for (int bt = 0; bt < NB; ++bt) {   // batch 0: the centre batch, centre row first
-            uint32_t s0 = 0, e0 = 0, s1 = 0, e1 = 0, s2 = 0, e2r = 0;
-            if (!done) {
-                row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B, s0, e0);
-                if constexpr (B > 1) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 1, s1, e1);
-                if constexpr (B > 2) row_range3<T, D, M, decltype(U)::value>(C, g, geo, e2, bt * B + 2, s2, e2r);
-            }
-            const uint32_t l0 = e0 - s0, l01 = l0 + (e1 - s1), tot = l01 + (e2r - s2);
-            // the wave's window per row slot: [min s, max e) over the lanes
-            // with a non-empty range (uniform; the whole wave is active here)
-            bool staged = false;
-            uint32_t io0 = 0, io1 = 0, io2 = 0;   // per-slot position -> LDS slot offsets
-            if constexpr (decltype(U)::value) {
-                const uint32_t lo0 = __ockl_wfred_min_u32(e0 > s0 ? s0 : kNone);
-                const uint32_t hi0 = __ockl_wfred_max_u32(e0 > s0 ? e0 : 0u);
-                uint32_t lo1 = 0, hi1 = 0, lo2 = 0, hi2 = 0;
-                if constexpr (B > 1) {
-                    lo1 = __ockl_wfred_min_u32(e1 > s1 ? s1 : kNone);
-                    hi1 = __ockl_wfred_max_u32(e1 > s1 ? e1 : 0u);
-                }
-                if constexpr (B > 2) {
-                    lo2 = __ockl_wfred_min_u32(e2r > s2 ? s2 : kNone);
-                    hi2 = __ockl_wfred_max_u32(e2r > s2 ? e2r : 0u);
-                }
-                const uint32_t q1 = hi0 > lo0 ? hi0 - lo0 : 0u;
-                const uint32_t q2 = q1 + (hi1 > lo1 ? hi1 - lo1 : 0u);
-                const uint32_t total = q2 + (hi2 > lo2 ? hi2 - lo2 : 0u);
-                staged = total <= CAP;
-                if (staged && total) {
-                    for (uint32_t i = (uint32_t)lane; i < total; i += 64) {
-                        const uint32_t rec = i < q1 ? lo0 + i : (i < q2 ? lo1 + (i - q1) : lo2 + (i - q2));
-                        stage[wv][i] = Xv[rec];
-                    }
-                    wave_lds_sync();
-                }
-                io0 = s0 - lo0;
-                io1 = q1 + (s1 - lo1) - l0;
-                io2 = q2 + (s2 - lo2) - l01;
-                if constexpr (ST) {
-                    n_batches += 1;
-                    n_staged += staged ? 1 : 0;
-                }
-            }
-            if (staged) {
-                for (uint32_t v = 0; v < tot && !done; v += 4) {
-                    uint32_t j[4];
-                    T b[4][D];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint32_t w = v + u;
-                        uint32_t jj = s0 + w, ii = io0 + w;
-                        if constexpr (B > 1) {
-                            jj = w >= l0 ? s1 + (w - l0) : jj;
-                            ii = w >= l0 ? io1 + w : ii;
-                        }
-                        if constexpr (B > 2) {
-                            jj = w >= l01 ? s2 + (w - l01) : jj;
-                            ii = w >= l01 ? io2 + w : ii;
-                        }
-                        j[u] = jj;
-                        const V x = stage[wv][w < tot ? ii : 0u];
-                        b[u][0] = x.x;
-                        b[u][1] = x.y;
-                        if constexpr (D >= 3) b[u][2] = x.z;
-                        if constexpr (D == 4) b[u][3] = x.w;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const bool h = (v + u < tot) && pr(b[u]);
-                        cnt += h ? 1u : 0u;
-                        const uint32_t x = h ? j[u] : kNone;
-                        mn2 = min(mn2, max(mn, x));   // the two smallest hits
-                        mn = min(mn, x);
-                    }
-                    if constexpr (ST) n_cand += (tot - v < 4u ? tot - v : 4u);
-                    if (cnt >= stop) done = true;
-                }
-            } else {
-                auto jpos = [&](uint32_t w) -> uint32_t {
-                    uint32_t j = s0 + w;
-                    if constexpr (B > 1) j = w >= l0 ? s1 + (w - l0) : j;
-                    if constexpr (B > 2) j = w >= l01 ? s2 + (w - l01) : j;
-                    return j;
-                };
-                uint32_t v0 = 0;
-                if (bt == 0 && tot > rot_min) {
-                    const uint32_t vr = (r & ~(kRotAlign - 1u)) - s0;
-                    v0 = vr < l0 ? vr : 0u;
-                }
-                auto sweep = [&](auto ROT) {
-                    for (uint32_t v = 0; v < tot && !done; v += 4) {
-                        uint32_t j[4];
-                        T b[4][D];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            uint32_t w = v + u;
-                            if constexpr (decltype(ROT)::value) {
-                                w += v0;
-                                w = w >= tot ? w - tot : w;
-                            }
-                            j[u] = jpos(w);
-                            load_raw<T, D>(Xs, v + u < tot ? j[u] : r, b[u]);
-                        }
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const bool h = (v + u < tot) && pr(b[u]);
-                            cnt += h ? 1u : 0u;
-                            const uint32_t x = h ? j[u] : kNone;
-                            mn2 = min(mn2, max(mn, x));
-                            mn = min(mn, x);
-                        }
-                        if constexpr (ST) n_cand += (tot - v < 4u ? tot - v : 4u);
-                        if (cnt >= stop) done = true;
-                    }
-                };
-                if (__any(v0 != 0))
-                    sweep(std::true_type{});
-                else
-                    sweep(std::false_type{});
-            }
-            if (__all(done)) break;
-            if constexpr (decltype(U)::value) {
-                // every lane's reads of this batch's window are issued before
-                // the next batch's copy overwrites it
-                if (staged) wave_lds_sync();
-            }
-        }
-    });
-    if constexpr (ST) {
-        if (live) atomicAdd(stats + 0, (unsigned long long)n_cand);
-        if (lane == 0) {
-            atomicAdd(stats + 8, (unsigned long long)n_batches);
-            atomicAdd(stats + 9, (unsigned long long)n_staged);
-        }
-    }
-    if (!live) return;
-    core[r] = (cnt >= ms ? 1 : 0) | (cnt >= 2 ? 2 : 0) | (cnt == 2 ? 4 : 0);
-    reinterpret_cast<uint2*>(mn_out)[r] = make_uint2(mn, mn2);
-    if (cnt_out) cnt_out[r] = full ? cnt : (cnt < ms ? cnt : ms);
-}
-
-// ------------------------------------------------------------------ link mode 3
-// (1) on the forest of the count pass's smallest neighbours (init_kernel),
-// union over the centre row only (each core record with the core records of
-// its own row within eps, j > r): the densest part of every neighbourhood,
-// and nearly every cluster is one tree after it (tools/forest_sim.py: 99.9 %
-// of the core-core edges of a C2 slice already join one root); (2) flatten;
-// (3) per cell, the common root of its core records (kNone: no core record,
-// kMixed: several roots); (4) per cell, its forward neighbour cells (higher
-// index, within the eps stencil): a pair of cells whose roots agree — in the
-// snapshot or, re-read live, after earlier unions — is already connected and
-// skipped (a directory-word summary lets whole neighbour rows go unread);
-// only the rest test their core records against each other.  Every
-// core-core edge lies in one cell or two neighbouring cells, so every edge is
-// either proven connected or tested: the same guarantee as link_kernel.
+// ------------------------------------------------------------------ link
+// The union-find over core-core edges (sklearn's dbscan_inner components,
+// SK:cluster/_dbscan_inner.pyx:19-41): (1) an initial forest from the count
+// sweep's two smallest neighbours (init_kernel); (2) a union over record
+// windows (window_uf_kernel: each core record against the W records after it
+// in key order, its own cell and row first); (3) per cell the common root of
+// its core records (kMixed: several roots) and per directory word the common
+// root of its cells; (4) per cell its forward neighbour cells (higher key,
+// within the eps stencil): a pair of cells whose roots agree is already
+// connected and skipped (a directory-word summary lets whole neighbour rows
+// go unread), only the rest test their core records against each other.
+// Every core-core edge lies in one cell or two neighbouring cells, so every
+// edge is either proven connected or tested; (1) and (2) are heuristics that
+// make (4) cheap, never a source of labels.
 constexpr uint32_t kMixed = 0xFFFFFFFEu;
-constexpr uint32_t kCentreSettle = 16;   // centre-row hits already under our root before stopping
-
-template <typename T, int D, int M>
-__global__ __launch_bounds__(kBlock) void centre_link_kernel(const T* __restrict__ Xs, uint32_t R,
-                                                             Cells C, double eps, double eps2,
-                                                             float lo, float hi, uint32_t window,
-                                                             uint32_t* __restrict__ par) {
-    const uint32_t r = rec_index();
-    if (r >= R || par[r] == kNone) return;   // not core
-    double a[D];
-    load_rec<T, D>(Xs, r, a);
-    const int L = part_of_wave(C.part_start, C.P, r);
-    const QueryCell<D> Q = query_cell<D>(C.parts + L, a);
-    uint64_t k0, k1;
-    const bool ok = row_keys<D, M>(Q, a, eps, NRows<D>::v / 2, k0, k1);
-    const uint32_t s0 = C.cstart[dir_rank(dir_word(C, k0), k0)];
-    const uint32_t e0 = C.cstart[dir_rank(dir_word(C, k1), k1)];
-    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
-    Linker<false> lk{par, uf_find_l1(par, r), {}};
-    uint32_t j = s0 > r + 1 ? s0 : r + 1;
-    // at most `window` forward candidates: the union is only a
-    // heuristic (cell_verify proves or tests every core-core edge), and in a
-    // dense cell overlapping windows already join the whole row — an
-    // uncapped sweep is quadratic in the occupancy (C4 city centres)
-    const uint32_t cap = window > 0xFFFFFFFFu - j ? 0xFFFFFFFFu : j + window;
-    const uint32_t end = ok ? (e0 < cap ? e0 : cap) : 0u;
-    uint32_t settled = 0;
-    for (; j + 4 <= end; j += 4) {
-        T b0[D], b1[D], b2[D], b3[D];
-        load_raw<T, D>(Xs, j, b0);
-        load_raw<T, D>(Xs, j + 1, b1);
-        load_raw<T, D>(Xs, j + 2, b2);
-        load_raw<T, D>(Xs, j + 3, b3);
-        const uint32_t p0 = ld_l1(par + j), p1 = ld_l1(par + j + 1), p2 = ld_l1(par + j + 2),
-                       p3 = ld_l1(par + j + 3);
-        const bool h0 = pr(b0), h1 = pr(b1), h2 = pr(b2), h3 = pr(b3);
-        // neighbours already under our root: a dense row is joined; stop
-        settled += (h0 && p0 == lk.rr) + (h1 && p1 == lk.rr) + (h2 && p2 == lk.rr) +
-                   (h3 && p3 == lk.rr);
-        if (h0) lk.edge(j, p0);
-        if (h1) lk.edge(j + 1, p1);
-        if (h2) lk.edge(j + 2, p2);
-        if (h3) lk.edge(j + 3, p3);
-        if (settled >= kCentreSettle) return;
-    }
-    for (; j < end; ++j) {
-        T b0[D];
-        load_raw<T, D>(Xs, j, b0);
-        const uint32_t p0 = ld_l1(par + j);
-        if (pr(b0)) lk.edge(j, p0);
-    }
-}
-
-// Link mode 5: the union over record windows.  A wave stages its 64
-// records plus the W after them (coordinates and parents of the smallest-
-// neighbour forest, flattened) in LDS once; each core lane then tests the W
-// records that follow it in key order — its own cell and row first, the
-// next rows after — and unions the core ones within eps whose root differs.
-// No per-record row lookup, no global candidate loads: the same role as the
-// centre-row union of mode 3 (a heuristic; the cell verify proves or tests
-// every core-core edge, so the labels are the same) at a fraction of the
-// fixed cost per record.
-template <typename T, int D, int M, int W, bool ST>
-__global__ __launch_bounds__(kBlock) void window_link_kernel(const T* __restrict__ Xs, uint32_t R,
-                                                             double eps, double eps2, float lo,
-                                                             float hi, uint32_t* __restrict__ par,
-                                                             unsigned long long* __restrict__ stats) {
-    constexpr int E = 64 + W;
-    __shared__ T sx[kBlock / 64][E][D];
-    __shared__ uint32_t sp[kBlock / 64][E];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t b = xcd_block(blockIdx.x, gridDim.x) * kBlock + w * 64;
-    for (int e = lane; e < E; e += 64) {
-        const uint32_t j = b + e;
-        T v[D];
-        uint32_t p = kNone;
-        if (j < R) {
-            load_raw<T, D>(Xs, j, v);
-            p = ld_l1(par + j);
-        } else {
-#pragma unroll
-            for (int k = 0; k < D; ++k) v[k] = T(0);
-        }
-#pragma unroll
-        for (int k = 0; k < D; ++k) sx[w][e][k] = v[k];
-        sp[w][e] = p;
-    }
-    __syncthreads();
-    const uint32_t r = b + lane;
-    const uint32_t p0 = r < R ? sp[w][lane] : kNone;
-    if (p0 == kNone) return;   // not core
-    Pred<T, D, M> pr;
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-        pr.ar[k] = sx[w][lane][k];
-        pr.a[k] = (double)pr.ar[k];
-    }
-    pr.eps = eps;
-    pr.eps2 = eps2;
-    pr.lo = lo;
-    pr.hi = hi;
-    Linker<ST> lk{par, p0, {}};
-#pragma unroll 4
-    for (int k = 1; k <= W; ++k) {
-        const uint32_t pj = sp[w][lane + k];
-        if (pj == kNone || pj == lk.rr || r + k >= R) continue;   // non-core / same tree
-        T bj[D];
-#pragma unroll
-        for (int q = 0; q < D; ++q) bj[q] = sx[w][lane + k][q];
-        if constexpr (ST) ++lk.st.cand;
-        if (pr(bj)) lk.edge(r + k, pj);
-    }
-    if constexpr (ST) {
-        atomicAdd(stats + 1, (unsigned long long)lk.st.cand);
-        atomicAdd(stats + 2, (unsigned long long)lk.st.hit);
-        atomicAdd(stats + 3, (unsigned long long)lk.st.core);
-        atomicAdd(stats + 4, (unsigned long long)lk.st.same);
-        atomicAdd(stats + 5, (unsigned long long)lk.st.find_same);
-        atomicAdd(stats + 6, (unsigned long long)lk.st.unions);
-    }
-}
 
 // Root of x without path writes (L1 reads: a stale parent is still an
 // ancestor, so the walk ends at a root of some moment).
@@ -2514,8 +1547,8 @@ __device__ __forceinline__ void lds_union(uint32_t* lp, uint32_t a, uint32_t b) 
     }
 }
 
-// Link mode 6: the window union of mode 5 with the flatten fused into the
-// staging and the edges reduced in LDS first.  A wave stages its 64 records
+// The window union (link step 2), with the flatten fused into the staging
+// and the edges reduced in LDS first.  A wave stages its 64 records
 // and the W after them with each one's current root (own records get it
 // written back: the flatten), each core lane tests the W records after it
 // and unions the core ones within eps of another tree in an LDS forest over
@@ -2611,12 +1644,7 @@ __global__ __launch_bounds__(kBlock) void window_uf_kernel(const T* __restrict__
 // Per cell, the common root of its core records (kNone: no core record,
 // kMixed: several roots); also flattens: each core record gets its root
 // written back, so no separate flatten pass runs before (no unions run
-// concurrently, so a chain read by another cell stays valid).  One thread
-// per cell walks its records; a cell of more than kBigCell records goes to a
-// list handled by big_cell_root_kernel, one block per cell (a serial walk of
-// a ~1e4-record C4 city-centre cell took 44 ms).
-constexpr uint32_t kBigCell = 256;
-
+// concurrently, so a chain read by another cell stays valid).
 __device__ __forceinline__ uint32_t root_merge(uint32_t a, uint32_t b) {
     return a == kNone ? b : (b == kNone ? a : (a == b ? a : kMixed));
 }
@@ -2634,50 +1662,6 @@ __device__ __forceinline__ uint32_t core_root(uint32_t* __restrict__ par, uint32
     return p;
 }
 
-__global__ __launch_bounds__(kBlock) void cell_root_kernel(const uint32_t* __restrict__ cstart,
-                                                           const uint32_t* __restrict__ ncells,
-                                                           uint32_t* __restrict__ par,
-                                                           uint32_t* __restrict__ croot,
-                                                           uint32_t* __restrict__ big,
-                                                           uint32_t* __restrict__ nbig) {
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    if (c >= *ncells) return;
-    const uint32_t s = cstart[c], e = cstart[c + 1];
-    if (e - s > kBigCell) {
-        big[atomicAdd(nbig, 1u)] = c;
-        return;
-    }
-    uint32_t v = kNone;
-    for (uint32_t r = s; r < e; ++r) v = root_merge(v, core_root(par, r));
-    croot[c] = v;
-}
-
-__global__ __launch_bounds__(kBlock) void big_cell_root_kernel(const uint32_t* __restrict__ cstart,
-                                                               const uint32_t* __restrict__ big,
-                                                               const uint32_t* __restrict__ nbig,
-                                                               uint32_t* __restrict__ par,
-                                                               uint32_t* __restrict__ croot) {
-    __shared__ uint32_t part[kBlock / 64];
-    const uint32_t nb = *nbig;
-    for (uint32_t i = blockIdx.x; i < nb; i += gridDim.x) {
-        const uint32_t c = big[i];
-        const uint32_t e = cstart[c + 1];
-        uint32_t v = kNone;
-        for (uint32_t r = cstart[c] + threadIdx.x; r < e; r += kBlock) v = root_merge(v, core_root(par, r));
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v = root_merge(v, (uint32_t)__shfl_xor((int)v, o, 64));
-        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t w = kNone;
-#pragma unroll
-            for (int k = 0; k < kBlock / 64; ++k) w = root_merge(w, part[k]);
-            croot[c] = w;
-        }
-        __syncthreads();
-    }
-}
-
 // wroot[w] = root_merge(wroot[w], v) atomically (monotone: kNone -> a root
 // -> kMixed).
 __device__ __forceinline__ void word_merge(uint32_t* wroot, uint64_t w, uint32_t v) {
@@ -2692,12 +1676,12 @@ __device__ __forceinline__ void word_merge(uint32_t* wroot, uint64_t w, uint32_t
     }
 }
 
-// cell_root_kernel with the word roots fused in: the cells of a wave are
+// Cell roots with the word roots fused in: the cells of a wave are
 // consecutive in key order, so lanes of one directory word (key >> 6) merge
 // their cell roots by a segmented shuffle scan and the segment's last lane
 // merges the result into the word atomically (a word can span two waves).
 // wroot must start at kNone.
-// Mode 6 tiers: a thread walks a cell of <= kMidCell records, a wave one of
+// Tiers: a thread walks a cell of <= kMidCell records, a wave one of
 // <= kWordBig (mid_cell_word_root_kernel), a block a larger one
 // (big_cell_word_root_kernel).  A thread walking up to 256 records held its
 // whole wave on C4's dense cells: 55 ms of the 1B-point link.
@@ -2812,31 +1796,6 @@ __global__ __launch_bounds__(kBlock) void big_cell_word_root_kernel(
         }
         __syncthreads();
     }
-}
-
-// Per directory word (64 consecutive cell keys of a row): the common root of
-// its cells' core records (kNone: none, kMixed: several) — lets a cell skip a
-// whole neighbour row whose words hold no other root.
-__global__ __launch_bounds__(kBlock) void word_root_kernel(const uint4* __restrict__ dir,
-                                                           uint64_t W,
-                                                           const uint32_t* __restrict__ croot,
-                                                           uint32_t* __restrict__ wroot) {
-    const uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (w >= W) return;
-    const uint4 d = dir[w];
-    const int nc = __popc(d.x) + __popc(d.y);
-    uint32_t v = kNone;
-    for (int i = 0; i < nc; ++i) {
-        const uint32_t cr = croot[d.z + i];
-        if (cr == kNone) continue;
-        if (v == kNone) {
-            v = cr;
-        } else if (cr != v) {
-            v = kMixed;
-            break;
-        }
-    }
-    wroot[w] = v;
 }
 
 // Test the core records of [s0, e0) against those of [s1, e1) (b > a when the
@@ -3100,143 +2059,8 @@ __global__ __launch_bounds__(kBlock) void pair_kernel(const T* __restrict__ Xs,
     }
 }
 
-template <typename T, int D, int M, bool ST>
-__global__ __launch_bounds__(kBlock) void link2_kernel(const T* __restrict__ Xs, uint32_t NL,
-                                                       const uint32_t* __restrict__ list, Cells C,
-                                                       double eps, double eps2, float lo, float hi,
-                                                       uint32_t* __restrict__ par,
-                                                       unsigned long long* __restrict__ stats) {
-    constexpr int B = RowBatch<D>::B, NB = RowBatch<D>::NB;
-    const uint32_t i = rec_index();
-    if (i >= NL) return;
-    const uint32_t r = list[i];   // core records, ascending
-    double a[D];
-    load_rec<T, D>(Xs, r, a);
-    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
-    Linker<ST> lk{par, uf_find_l1(par, r), {}};
-    with_part(C.part_start, C.P, r, [&](int L, auto U) {
-        const QueryCell<D> Q = decltype(U)::value ? query_cell_u<D>(C.parts + L, a)
-                                                  : query_cell<D>(C.parts + L, a);
-        for (int bt = 0; bt < NB; ++bt) {
-            uint32_t pre[B], off[B];
-            // edges j > r only (the predicate is symmetric)
-            const uint32_t tot = batch_list<D, M>(C, Q, a, eps, bt, false, r + 1, pre, off);
-            for (uint32_t v = 0; v < tot; v += 4) {
-                uint32_t j[4], pj[4];
-                T b[4][D];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    j[u] = v + u < tot ? bpos<B>(v + u, pre, off) : r;
-                    load_raw<T, D>(Xs, j[u], b[u]);
-                    pj[u] = ld_l1(par + j[u]);
-                }
-                if constexpr (ST) lk.st.cand += (tot - v < 4u ? tot - v : 4u);
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (v + u < tot && pr(b[u])) lk.edge(j[u], pj[u]);
-            }
-        }
-    });
-    if constexpr (ST) {
-        atomicAdd(stats + 1, (unsigned long long)lk.st.cand);
-        atomicAdd(stats + 2, (unsigned long long)lk.st.hit);
-        atomicAdd(stats + 3, (unsigned long long)lk.st.core);
-        atomicAdd(stats + 4, (unsigned long long)lk.st.same);
-        atomicAdd(stats + 5, (unsigned long long)lk.st.find_same);
-        atomicAdd(stats + 6, (unsigned long long)lk.st.unions);
-    }
-}
-
-// wroot (nullable; directory-word roots of the final forest): when every word
-// of the stencil holds no root but one, R, the smallest adjacent key can only
-// be R's — one core neighbour within eps proves it, so the sweep stops at the
-// first (centre row first); no root at all means noise, without a sweep.
-template <typename T, int D, int M>
-__global__ __launch_bounds__(kBlock) void border2_kernel(
-    const T* __restrict__ Xs, uint32_t NL, const uint32_t* __restrict__ list, Cells C, double eps,
-    double eps2, float lo, float hi, const uint32_t* __restrict__ vals,
-    const uint32_t* __restrict__ par, const uint32_t* __restrict__ gmin,
-    const uint32_t* __restrict__ wroot, uint32_t* __restrict__ key_out) {
-    constexpr int B = RowBatch<D>::B, NB = RowBatch<D>::NB;
-    constexpr int NR = NRows<D>::v;
-    const uint32_t i = rec_index();
-    if (i >= NL) return;
-    const uint32_t r = list[i];   // owner, non-core records with a neighbour, ascending
-    double a[D];
-    load_rec<T, D>(Xs, r, a);
-    const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
-    uint32_t best = kNone;
-    with_part(C.part_start, C.P, r, [&](int L, auto U) {
-        const QueryCell<D> Q = decltype(U)::value ? query_cell_u<D>(C.parts + L, a)
-                                                  : query_cell<D>(C.parts + L, a);
-        if (wroot) {
-            uint32_t R = kNone;
-            bool mixed = false;
-            for (int q = 0; q < NR; ++q) {
-                uint64_t k0, k1;
-                if (!row_keys<D, M>(Q, a, eps, q, k0, k1)) continue;
-                const uint32_t w2[2] = {word_root_at(C, wroot, k0), word_root_at(C, wroot, k1 - 1)};
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t w = w2[h];
-                    if (w == kMixed || (w != kNone && R != kNone && w != R)) mixed = true;
-                    if (w != kNone && w != kMixed) R = w;
-                }
-            }
-            if (!mixed) {
-                if (R == kNone) return;   // no core record anywhere near: noise
-                for (int bq = 0; bq < NB; ++bq) {
-                    const int bt = (bq + NB / 2) % NB;
-                    uint32_t pre[B], off[B];
-                    const uint32_t tot = batch_list<D, M>(C, Q, a, eps, bt, true, 0u, pre, off);
-                    for (uint32_t v = 0; v < tot; v += 4) {
-                        uint32_t j[4], pj[4];
-                        T b[4][D];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            j[u] = v + u < tot ? bpos<B>(v + u, pre, off) : r;
-                            load_raw<T, D>(Xs, j[u], b[u]);
-                            pj[u] = par[j[u]];
-                        }
-                        bool hit = false;
-#pragma unroll
-                        for (int u = 0; u < 4; ++u)
-                            hit |= v + u < tot && pj[u] != kNone && pr(b[u]);
-                        if (hit) {
-                            best = gmin[R];
-                            return;
-                        }
-                    }
-                }
-                return;
-            }
-        }
-        for (int bt = 0; bt < NB; ++bt) {
-            uint32_t pre[B], off[B];
-            const uint32_t tot = batch_list<D, M>(C, Q, a, eps, bt, false, 0u, pre, off);
-            for (uint32_t v = 0; v < tot; v += 4) {
-                uint32_t j[4], pj[4];
-                T b[4][D];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    j[u] = v + u < tot ? bpos<B>(v + u, pre, off) : r;
-                    load_raw<T, D>(Xs, j[u], b[u]);
-                    pj[u] = par[j[u]];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (v + u < tot && pj[u] != kNone && pr(b[u])) {
-                        const uint32_t k = gmin[pj[u]];
-                        best = k < best ? k : best;
-                    }
-            }
-        }
-    });
-    key_out[vals[r] & kIdMask] = best;
-}
-
-// border4_kernel (PD_OPT_SWEEP_VARIANT bit 4, the default): border2's plain
-// sweep (the smallest cluster key among the core neighbours, every row) with
+// border4_kernel: the smallest cluster key among the core neighbours of a
+// border candidate (sklearn's first-discovered-cluster rule, every row), with
 // count4's cheap rows.
 template <typename T, int D, int M, int WPE = 1>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void border4_kernel(
@@ -3497,101 +2321,28 @@ uint64_t tile_offsets(Ctx& ctx, uint32_t* cnt, unsigned tiles, uint64_t* off, hi
 }
 inline int xsub_of(const Ctx& ctx) { return ctx.xsub < 1 ? 1 : ctx.xsub; }
 
-// Cell roots (link mode 3, border fast path); also flattens the core records.
-void cell_roots(Ctx& ctx, hipStream_t s, uint32_t R, const uint32_t* cstart, const uint32_t* dncells,
-                uint32_t* par, uint32_t* croot) {
-    uint32_t* big = ctx.arena.get<uint32_t>("big_cells", R / (kBigCell + 1) + 1);
-    uint32_t* nbig = ctx.arena.get<uint32_t>("big_count", 4);
-    PD_HIP(hipMemsetAsync(nbig, 0, sizeof(uint32_t), s));
-    hipLaunchKernelGGL(cell_root_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, cstart, dncells, par,
-                       croot, big, nbig);
-    hipLaunchKernelGGL(big_cell_root_kernel, dim3(1024), dim3(kBlock), 0, s, cstart, big, nbig, par,
-                       croot);
-}
-
-// Launch helpers for the three neighbour sweeps: bit k of `variant`
-// (PD_OPT_SWEEP_VARIANT) selects the batched lane kernel for sweep k (0
-// count, 1 link, 2 border) instead of the row-by-row one.
-// Whether the count sweep records border lists (count4 only, min_samples <=
-// kListMax + 1, PD_OPT_BORDER_LISTS).
-inline bool border_lists_on(const Ctx& ctx, uint32_t ms) {
-    return ctx.border_lists && (ctx.variant & 8) && (ctx.variant & 40) != 40 &&
-           ms <= (uint32_t)kListMax + 1u;
-}
-
+// Launch helpers for the two neighbour sweeps.  The count sweep runs at 8
+// waves per SIMD (64 VGPRs); its instrumented form (PD_OPT_SWEEP_STATS)
+// without the register cap.
 template <typename T, int D, int M, bool ST>
-void launch_count(int variant, hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double eps,
-                  double eps2, float lo, float hi, uint32_t ms, int full, uint32_t rot_min,
-                  uint8_t* core, uint32_t* mn, uint32_t* cnt, unsigned long long* st,
-                  const BorderLists* bl = nullptr) {
-    constexpr bool kStageable = std::is_same<T, float>::value && (D >= 2 && D <= 4);
-    if constexpr (kStageable) {
-        if ((variant & 40) == 40) {   // cheap rows + LDS-staged windows
-            hipLaunchKernelGGL((count5_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                               Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
-            return;
-        }
-    }
-    if ((variant & 8) && bl)   // cheap rows, border lists (min_samples - 1 LDS slots per lane)
-        hipLaunchKernelGGL((count4_kernel<T, D, M, ST, true>), dim3(blocks(R)), dim3(kBlock),
-                           (size_t)kBlock * (ms > 1 ? ms - 1 : 1) * sizeof(uint32_t), s,
-                           Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st, *bl);
-    else if constexpr (!ST) {
-        if ((variant & 72) == 72)   // cheap rows, registers for 8 waves per SIMD
-            hipLaunchKernelGGL((count4_kernel<T, D, M, false, false, 8>), dim3(blocks(R)),
-                               dim3(kBlock), 0, s, Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min,
-                               core, mn, cnt, st, BorderLists{nullptr, nullptr, nullptr, 0u});
-        else if (variant & 8)
-            hipLaunchKernelGGL((count4_kernel<T, D, M, false, false>), dim3(blocks(R)),
-                               dim3(kBlock), 0, s, Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min,
-                               core, mn, cnt, st, BorderLists{nullptr, nullptr, nullptr, 0u});
-        else if (variant & 1)
-            hipLaunchKernelGGL((count2_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
-                               C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
-        else
-            hipLaunchKernelGGL((count_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
-                               C, eps, eps2, lo, hi, ms, full, core, mn, cnt, st);
-    } else if (variant & 8)   // cheap rows
-        hipLaunchKernelGGL((count4_kernel<T, D, M, ST, false>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                           Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st,
-                           BorderLists{nullptr, nullptr, nullptr, 0u});
-    else if (variant & 1)
-        hipLaunchKernelGGL((count2_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
-                           C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
+void launch_count(hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double eps, double eps2,
+                  float lo, float hi, uint32_t ms, int full, uint32_t rot_min, uint8_t* core,
+                  uint32_t* mn, uint32_t* cnt, unsigned long long* st) {
+    if constexpr (ST)
+        hipLaunchKernelGGL((count4_kernel<T, D, M, true, 1>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                           Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
     else
-        hipLaunchKernelGGL((count_kernel<T, D, M, ST>), dim3(blocks(R)), dim3(kBlock), 0, s, Xs, R,
-                           C, eps, eps2, lo, hi, ms, full, core, mn, cnt, st);
-}
-
-template <typename T, int D, int M, bool ST>
-void launch_link(int variant, hipStream_t s, const T* Xs, uint32_t NL, const uint32_t* list,
-                 const Cells& C, double eps, double eps2, float lo, float hi, uint32_t* par,
-                 unsigned long long* st) {
-    if (variant & 2)
-        hipLaunchKernelGGL((link2_kernel<T, D, M, ST>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs,
-                           NL, list, C, eps, eps2, lo, hi, par, st);
-    else
-        hipLaunchKernelGGL((link_kernel<T, D, M, ST>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs,
-                           NL, list, C, eps, eps2, lo, hi, par, st);
+        hipLaunchKernelGGL((count4_kernel<T, D, M, false, 8>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                           Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
 }
 
 template <typename T, int D, int M>
-void launch_border(int variant, hipStream_t s, const T* Xs, uint32_t NL, const uint32_t* list,
-                   const Cells& C, double eps, double eps2, float lo, float hi,
-                   const uint32_t* vals, const uint32_t* par, const uint32_t* gmin,
-                   const uint32_t* wroot, uint32_t* key_out, uint32_t* rec_out = nullptr) {
-    if ((variant & 144) == 144 && !wroot)   // cheap rows, registers for 8 waves per SIMD
-        hipLaunchKernelGGL((border4_kernel<T, D, M, 8>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs,
-                           NL, list, C, eps, eps2, lo, hi, vals, par, gmin, key_out, rec_out);
-    else if ((variant & 16) && !wroot)   // cheap rows
-        hipLaunchKernelGGL((border4_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
-                           list, C, eps, eps2, lo, hi, vals, par, gmin, key_out, rec_out);
-    else if (variant & 4)
-        hipLaunchKernelGGL((border2_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
-                           list, C, eps, eps2, lo, hi, vals, par, gmin, wroot, key_out);
-    else
-        hipLaunchKernelGGL((border_kernel<T, D, M>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
-                           list, C, eps, eps2, lo, hi, vals, par, gmin, key_out);
+void launch_border(hipStream_t s, const T* Xs, uint32_t NL, const uint32_t* list, const Cells& C,
+                   double eps, double eps2, float lo, float hi, const uint32_t* vals,
+                   const uint32_t* par, const uint32_t* gmin, uint32_t* key_out,
+                   uint32_t* rec_out = nullptr) {
+    hipLaunchKernelGGL((border4_kernel<T, D, M, 8>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
+                       list, C, eps, eps2, lo, hi, vals, par, gmin, key_out, rec_out);
 }
 
 // Ordered compaction of record ids satisfying `pred` (keeps the spatial
@@ -3684,31 +2435,17 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         tree.ax_new = (const int32_t*)dt + nslot;
         tree.bound = (const double*)(dt + db);
     }
-    // PD_OPT_SORT_PAYLOAD (fp32, 3-D): the records carry their coordinates
-    // through the sort (16-B values) instead of a gather after it
-    const bool payload = ctx.sort_payload && std::is_same<T, float>::value && D == 3;
-    float4* pay = payload ? ctx.arena.get<float4>("pay", R) : nullptr;
     if (P <= 64)
         hipLaunchKernelGGL((halo_write_kernel<T, D, K, true>), dim3(htiles), dim3(kBlock), 0, s, X,
-                           n, parts, P, a.owner, tree, toff, keys, vals, pay);
+                           n, parts, P, a.owner, tree, toff, keys, vals);
     else
         hipLaunchKernelGGL((halo_write_kernel<T, D, K, false>), dim3(htiles), dim3(kBlock), 0, s,
-                           X, n, parts, P, a.owner, tree, toff, keys, vals, pay);
+                           X, n, parts, P, a.owner, tree, toff, keys, vals);
     PD_HIP(hipGetLastError());
     tm.mark();   // 1
 
     // ---- shuffle by neighbourhood == sort by (neighbourhood, cell) key
-    if (payload) {
-        float4* pay2 = ctx.arena.get<float4>("pay2", R);
-        rocprim::double_buffer<K> kb(keys, keys2);
-        rocprim::double_buffer<float4> vb(pay, pay2);
-        size_t tb = 0;
-        PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
-        void* tmp = ctx.arena.get<char>("sort_tmp", tb);
-        PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
-        keys = kb.current();
-        pay = vb.current();
-    } else {
+    {
         rocprim::double_buffer<K> kb(keys, keys2);
         rocprim::double_buffer<uint32_t> vb(vals, vals2);
         size_t tb = 0;
@@ -3719,16 +2456,12 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         vals = vb.current();
     }
     tm.mark();   // 2
-    T* Xs = payload ? reinterpret_cast<T*>(pay) : ctx.arena.get<T>("Xs", (size_t)R * Stride<D>::v);
+    T* Xs = ctx.arena.get<T>("Xs", (size_t)R * Stride<D>::v);
     uint32_t* dup_list = ctx.arena.get<uint32_t>("dup_list", R);
     uint32_t* lcount = ctx.arena.get<uint32_t>("list_counts", 8);   // dup, roots, core, border
     PD_HIP(hipMemsetAsync(lcount, 0, sizeof(uint32_t) * 8, s));
-    if (payload)
-        hipLaunchKernelGGL(payload_vals_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, pay, (uint64_t)R,
-                           vals, dup_list, lcount);
-    else
-        hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X,
-                           (uint64_t)R, vals, Xs, dup_list, lcount);
+    hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X,
+                       (uint64_t)R, vals, Xs, dup_list, lcount);
     tm.mark();   // 3
 
     // ---- cell directory
@@ -3829,106 +2562,59 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         sst = ctx.arena.get<unsigned long long>("sweep_stats", 10);
         PD_HIP(hipMemsetAsync(sst, 0, sizeof(unsigned long long) * 10, s));
     }
-    const int mode = ctx.link_mode;
-    // border lists: entries <= min_samples per listed record; the cap bounds
-    // the buffer (records beyond it are swept in phase B as before)
-    BorderLists bl{nullptr, nullptr, nullptr, 0u};
-    const bool lists = R && border_lists_on(ctx, (uint32_t)a.min_samples);
-    if (lists) {
-        const uint64_t want = (uint64_t)R * (uint64_t)std::max(a.min_samples, 2) / 2 + 64;
-        const uint64_t tot = std::min<uint64_t>(want, 1ull << 29);
-        bl.cap = (uint32_t)(tot / kListStripes + 64);
-        bl.list = ctx.arena.get<uint32_t>("blist", (size_t)bl.cap * kListStripes);
-        bl.off = ctx.arena.get<uint32_t>("blist_off", R);
-        bl.count = ctx.arena.get<uint32_t>("blist_count", kListStripes);
-        PD_HIP(hipMemsetAsync(bl.count, 0, sizeof(uint32_t) * kListStripes, s));
-    }
     if (R) {
+        const uint32_t rot = ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu;
         if (sst)
-            launch_count<T, D, M, true>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
-                                        (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
-                                        ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu,
-                                        core, mn, cnt_rec, sst, lists ? &bl : nullptr);
+            launch_count<T, D, M, true>(s, Xs, R, C, eps, eps2, slo, shi, (uint32_t)a.min_samples,
+                                        ctx.full_counts ? 1 : 0, rot, core, mn, cnt_rec, sst);
         else
-            launch_count<T, D, M, false>(ctx.variant, s, Xs, R, C, eps, eps2, slo, shi,
-                                         (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0,
-                                         ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu,
-                                         core, mn, cnt_rec, sst, lists ? &bl : nullptr);
+            launch_count<T, D, M, false>(s, Xs, R, C, eps, eps2, slo, shi, (uint32_t)a.min_samples,
+                                         ctx.full_counts ? 1 : 0, rot, core, mn, cnt_rec, sst);
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 5
 
     uint32_t* par = ctx.arena.get<uint32_t>("parent", R);
-    if (R && (mode == 3 || mode == 4 || mode == 5 || mode == 6)) {
-        // forest from the count pass's smallest neighbour (links across rows)
+    if (R) {
+        // (1) forest from the count pass's two smallest neighbours
         hipLaunchKernelGGL(init_kernel, dim3(sub_blocks(R)), dim3(kBlock), 0, s, R, core, mn, 1, par);
-        // PD_OPT_LINK_JUMPS: pointer jumping over the smallest-neighbour
-        // forest (its chains run across a row's cells) before the window union
-        for (int it = 0; it < ctx.link_jumps; ++it)
-            hipLaunchKernelGGL(jump_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
-        if (mode != 6)
-            hipLaunchKernelGGL(flatten_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par);
-        if (mode == 6) {
-            // auto window (PD_OPT_CENTRE_WINDOW < 0): sparse cells (a few
-            // records each, C2: 2.3) gain little from the window beyond the
-            // fused flatten, so a short one is cheapest (C2 link 6.59 -> 5.96
-            // ms at 16 -> 4); dense cells (C4 city centres) want the long one
-            // (C4 link 71.5 -> 60.6 ms at 4 -> 16)
-            int cw = ctx.centre_window;
-            if (cw < 0) {
-                uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t));
-                PD_HIP(hipMemcpyAsync(h, dncells, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-                sync(s);
-                const uint32_t nc = *h ? *h : 1u;
-                cw = (uint64_t)R <= 4ull * nc ? 4 : 16;
-            }
-            auto go = [&](auto Wc) {
-                constexpr int Wv = decltype(Wc)::value;
-                if (sst)
-                    hipLaunchKernelGGL((window_uf_kernel<T, D, M, Wv, true>), dim3(blocks(R)),
-                                       dim3(kBlock), 0, s, Xs, R, eps, eps2, slo, shi, par, sst);
-                else
-                    hipLaunchKernelGGL((window_uf_kernel<T, D, M, Wv, false>), dim3(blocks(R)),
-                                       dim3(kBlock), 0, s, Xs, R, eps, eps2, slo, shi, par, sst);
-            };
-            if (cw <= 2)
-                go(std::integral_constant<int, 2>{});
-            else if (cw <= 4)
-                go(std::integral_constant<int, 4>{});
-            else if (cw <= 8)
-                go(std::integral_constant<int, 8>{});
-            else if (cw <= 16)
-                go(std::integral_constant<int, 16>{});
-            else if (cw <= 32)
-                go(std::integral_constant<int, 32>{});
-            else
-                go(std::integral_constant<int, 64>{});
-        } else if (mode == 3) {
-            hipLaunchKernelGGL((centre_link_kernel<T, D, M>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                               Xs, R, C, eps, eps2, slo, shi,
-                               ctx.centre_window < 0 ? 16u
-                               : ctx.centre_window ? (uint32_t)ctx.centre_window : 0xFFFFFFFFu, par);
-        } else if (mode == 5) {
-            const int cw = ctx.centre_window < 0 ? 16 : ctx.centre_window;
-            auto go = [&](auto Wc) {
-                constexpr int Wv = decltype(Wc)::value;
-                if (sst)
-                    hipLaunchKernelGGL((window_link_kernel<T, D, M, Wv, true>), dim3(blocks(R)),
-                                       dim3(kBlock), 0, s, Xs, R, eps, eps2, slo, shi, par, sst);
-                else
-                    hipLaunchKernelGGL((window_link_kernel<T, D, M, Wv, false>), dim3(blocks(R)),
-                                       dim3(kBlock), 0, s, Xs, R, eps, eps2, slo, shi, par, sst);
-            };
-            if (cw <= 16)
-                go(std::integral_constant<int, 16>{});
-            else if (cw <= 32)
-                go(std::integral_constant<int, 32>{});
-            else
-                go(std::integral_constant<int, 64>{});
+        // (2) window union.  Auto window (PD_OPT_CENTRE_WINDOW < 0): sparse
+        // cells (a few records each, C2: 2.3) gain little from the window
+        // beyond the fused flatten, so a short one is cheapest (C2 link 6.59
+        // -> 5.96 ms at 16 -> 4); dense cells (C4 city centres) want the long
+        // one (C4 link 71.5 -> 60.6 ms at 4 -> 16)
+        int cw = ctx.centre_window;
+        if (cw < 0) {
+            uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+            PD_HIP(hipMemcpyAsync(h, dncells, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            sync(s);
+            const uint32_t nc = *h ? *h : 1u;
+            cw = (uint64_t)R <= 4ull * nc ? 4 : 16;
         }
+        auto go = [&](auto Wc) {
+            constexpr int Wv = decltype(Wc)::value;
+            if (sst)
+                hipLaunchKernelGGL((window_uf_kernel<T, D, M, Wv, true>), dim3(blocks(R)),
+                                   dim3(kBlock), 0, s, Xs, R, eps, eps2, slo, shi, par, sst);
+            else
+                hipLaunchKernelGGL((window_uf_kernel<T, D, M, Wv, false>), dim3(blocks(R)),
+                                   dim3(kBlock), 0, s, Xs, R, eps, eps2, slo, shi, par, sst);
+        };
+        if (cw <= 2)
+            go(std::integral_constant<int, 2>{});
+        else if (cw <= 4)
+            go(std::integral_constant<int, 4>{});
+        else if (cw <= 8)
+            go(std::integral_constant<int, 8>{});
+        else if (cw <= 16)
+            go(std::integral_constant<int, 16>{});
+        else if (cw <= 32)
+            go(std::integral_constant<int, 32>{});
+        else
+            go(std::integral_constant<int, 64>{});
         uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
         uint32_t* wroot = ctx.arena.get<uint32_t>("word_root", W);
-        if (mode == 6) {   // cell and word roots in one pass
+        {   // (3) cell and word roots in one pass
             uint32_t* big = ctx.arena.get<uint32_t>("big_cells", R / (kWordBig + 1) + 1);
             uint32_t* mid = ctx.arena.get<uint32_t>("mid_cells", R / (kMidCell + 1) + 1);
             uint32_t* nbig = ctx.arena.get<uint32_t>("big_count", 4);   // [0] big, [1] mid
@@ -3946,16 +2632,12 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
                                cstart, ckeys, mid, nbig + 1, par, croot, wroot, pages);
             hipLaunchKernelGGL((big_cell_word_root_kernel<K>), dim3(1024), dim3(kBlock), 0, s,
                                cstart, ckeys, big, nbig, par, croot, wroot, pages);
-        } else {
-            cell_roots(ctx, s, R, cstart, dncells, par, croot);
-            hipLaunchKernelGGL(word_root_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, W, croot,
-                               wroot);
         }
         const uint32_t pcap = (uint32_t)std::min<uint64_t>(R, 64ull << 20);
         uint2* plist = ctx.arena.get<uint2>("pair_list", pcap);
         uint32_t* pcount = ctx.arena.get<uint32_t>("pair_count", 4);
         PD_HIP(hipMemsetAsync(pcount, 0, sizeof(uint32_t), s));
-        // verify: screen every cell, then work on the flagged ones only
+        // (4) verify: screen every cell, then work on the flagged ones only
         const unsigned vtiles = blocks(R);
         uint8_t* vflag = ctx.arena.get<uint8_t>("verify_flags", R);
         uint32_t* vlist = ctx.arena.get<uint32_t>("verify_list", R);
@@ -3973,24 +2655,6 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         }
         hipLaunchKernelGGL((pair_kernel<T, D, M>), dim3(std::min(blocks(pcap), 4096u)), dim3(kBlock), 0, s, Xs, plist,
                            pcount, pcap, cstart, croot, eps, eps2, slo, shi, par);
-    } else if (R) {
-        hipLaunchKernelGGL(init_kernel, dim3(sub_blocks(R)), dim3(kBlock), 0, s, R, core, mn,
-                           mode == 0 ? 1 : 0, par);
-        {
-            if (mode == 0)
-                for (int it = 0; it < ctx.jump_rounds; ++it)
-                    hipLaunchKernelGGL(jump_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core,
-                                       par);
-            uint32_t* clist = nullptr;
-            const uint32_t NC = select_records(ctx, "core_list", R, IsCore{core}, &clist, s);
-            ctx.t.core_records = NC;
-            if (NC && sst)
-                launch_link<T, D, M, true>(ctx.variant, s, Xs, NC, clist, C, eps, eps2, slo, shi,
-                                           par, sst);
-            else if (NC)
-                launch_link<T, D, M, false>(ctx.variant, s, Xs, NC, clist, C, eps, eps2, slo, shi,
-                                            par, sst);
-        }
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 6
@@ -4035,17 +2699,6 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         }
     }
     ctx.st.n_roots = n_roots;
-    // final cell / word roots for the border sweep's single-root fast path
-    // (PD_OPT_BORDER_ROOTS; off by default: on C2 the extra root passes and
-    // the 9-row word checks cost more than the sweep they save)
-    uint32_t* wroot_final = nullptr;
-    if (R && (ctx.variant & 4) && ctx.border_roots) {
-        uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
-        cell_roots(ctx, s, R, cstart, dncells, par, croot);
-        wroot_final = ctx.arena.get<uint32_t>("word_root", W);
-        hipLaunchKernelGGL(word_root_kernel, dim3(blocks(W)), dim3(kBlock), 0, s, dir, W, croot,
-                           wroot_final);
-    }
     PD_HIP(hipGetLastError());
     tm.mark();   // 8
 
@@ -4074,9 +2727,6 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     st.gmin = gmin;
     st.cnt_rec = cnt_rec;
     st.mn = mn;
-    st.wroot = wroot_final;
-    st.blist = lists ? bl.list : nullptr;
-    st.blist_off = lists ? bl.off : nullptr;
     st.n_exports = 0;
     if (a.phase == 1 && R && a.xr) {
         uint32_t* elist = nullptr;
@@ -4112,11 +2762,17 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
                   (const uint4*)st.pages};
     const double eps = st.eps, eps2 = st.eps * st.eps;
     const float slo = st.slo, shi = st.shi;
+    uint32_t* shard_err = nullptr;
     if (a.phase == 2) {
         tm.mark();   // 0
-        if (a.n_map > 0 && R)
+        const uint32_t cm = ctx.shard_core_bit ? 0x80000000u : 0u;
+        if (cm) {
+            shard_err = ctx.arena.get<uint32_t>("shard_err", 1);
+            PD_HIP(hipMemsetAsync(shard_err, 0, sizeof(uint32_t), s));
+        }
+        if ((a.n_map > 0 || cm) && R)
             hipLaunchKernelGGL(remap_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par,
-                               a.map_ids, a.map_keys, (uint32_t)a.n_map, gmin);
+                               a.map_ids, a.map_keys, (uint32_t)a.n_map, cm, gmin, shard_err);
     }
     uint32_t* key_out = a.phase == 2 ? a.keys_out : ctx.arena.get<uint32_t>("key_out", n);
     // core flags travel in the keys: single device bit 30 (ids < 2^30);
@@ -4127,12 +2783,11 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     const int core_bit = a.phase == 2 ? 0 : 1;
     PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
     if (a.core && !core_mask) PD_HIP(hipMemsetAsync(a.core, 0, n, s));
-    // single device, no counts wanted, the cheap-row border: labels reach
-    // input order through the bucketed pair passes instead of owner_kernel's
-    // scatter (ctx.label_buckets, PD_OPT_LABEL_BUCKETS)
+    // single device, no counts wanted: labels reach input order through the
+    // bucketed pair passes instead of owner_kernel's scatter
+    // (ctx.label_buckets, PD_OPT_LABEL_BUCKETS)
     const bool want_buckets = ctx.label_buckets > 0 || (ctx.label_buckets < 0 && n >= (1ull << 28));
-    const bool bucketed = a.phase != 2 && core_bit && !a.counts && want_buckets &&
-                          (ctx.variant & 16) && !st.wroot && n > 0;
+    const bool bucketed = a.phase != 2 && core_bit && !a.counts && want_buckets && n > 0;
     if (R) {
         uint32_t* blist = ctx.arena.get<uint32_t>("border_list", R);
         const unsigned tiles = (unsigned)(((uint64_t)R + kOwnTile - 1) / kOwnTile);
@@ -4141,23 +2796,19 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         // bucketed: owner_kernel writes the (point, key) pairs in record order
         // instead of scattering key_out; the border sweep fills in its keys
         uint2* recs = bucketed ? ctx.arena.get<uint2>("lab_recs", R) : nullptr;
-        // count4 (variant bit 3) flags records with exactly one neighbour
-        // besides themselves (core bit 2): owner_kernel attaches those border
-        // records from the count pass's two smallest hits, the sweep takes
-        // the rest
-        const bool single = (ctx.variant & 8) && st.mn;
+        // count4 flags records with exactly one neighbour besides themselves
+        // (core bit 2): owner_kernel attaches those border records from the
+        // count pass's two smallest hits, the sweep takes the rest
         hipLaunchKernelGGL(owner_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core, par, gmin,
-                           st.cnt_rec, single ? (const uint2*)st.mn : nullptr, st.blist,
-                           st.blist_off, core_mask,
-                           bucketed ? nullptr : key_out, a.core, a.counts,
-                           tcnt, recs);
+                           st.cnt_rec, (const uint2*)st.mn, core_mask,
+                           bucketed ? nullptr : key_out, a.core, a.counts, tcnt, recs);
         const uint32_t NB = (uint32_t)tile_offsets(ctx, tcnt, tiles, toff, s, true);
         if (NB)
             hipLaunchKernelGGL(border_list_kernel, dim3(tiles), dim3(kBlock), 0, s, R, vals, core,
-                               single ? 1 : 0, st.blist ? st.blist_off : nullptr, toff, blist);
+                               toff, blist);
         if (NB)
-            launch_border<T, D, M>(ctx.variant, s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par,
-                                   gmin, st.wroot, key_out, recs ? (uint32_t*)recs + 1 : nullptr);
+            launch_border<T, D, M>(s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par, gmin,
+                                   key_out, recs ? (uint32_t*)recs + 1 : nullptr);
         if (bucketed) {
             // buckets of 2^19 points: a bucket's 2 MB of key_out stays in one
             // XCD's 4 MB L2 (C4 border: 2^20 29.2, 2^19 27.9, 2^18 29.5 ms)
@@ -4184,6 +2835,14 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
                                core_mask, a.core);
         PD_HIP(hipGetLastError());
         tm.mark();
+        if (shard_err) {   // PD_OPT_SHARD_CORE_BIT's guarantee, checked
+            uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+            PD_HIP(hipMemcpyAsync(h, shard_err, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            sync(s);
+            if (*h)
+                throw Error(-1, "PD_OPT_SHARD_CORE_BIT: a cluster key (global id) is >= 2^31; "
+                                "the keys cannot carry the core flag — unset the option");
+        }
         return;
     }
     // single device: key_out already holds ranks (root_rank_kernel)

@@ -81,9 +81,6 @@ struct PhaseState {
     uint32_t* gmin = nullptr;
     uint32_t* cnt_rec = nullptr;
     uint32_t* mn = nullptr;      // per record: the two smallest neighbours the count sweep saw
-    uint32_t* wroot = nullptr;   // directory-word roots of the final forest (border fast path)
-    uint32_t* blist = nullptr;   // border lists of the count sweep (null: none this train)
-    uint32_t* blist_off = nullptr;
     uint32_t* exp_gid = nullptr;
     uint32_t* exp_key = nullptr;
 };
@@ -152,34 +149,20 @@ struct Ctx {
     bool timing = false;
     bool full_counts = false;    // debug: count every neighbour (no early exit)
     bool seq_moments = false;    // reference-order (sequential) KD moment sums
-    int link_mode = 6;           // 6 LDS-reduced window union + cell verify; 5 window union + cell verify;
-                                 // 3 centre-row union + cell verify;
-                                 // 4 cell verify alone; 0 init forest + jumps + union sweep; 2 union sweep only
-    int jump_rounds = 4;
-    int link_jumps = 0;          // PD_OPT_LINK_JUMPS
     int xsub = 2;                // axis-0 sub-cells per eps
-    int centre_window = -1;      // link modes 5/6: records after each record tested (2..64);
-                                 // mode 3: forward candidates per centre-row union (0: all);
-                                 // < 0 (default): mode 6 picks 4 or 16 by cell occupancy, else 16
+    int centre_window = -1;      // window union: records after each record tested (2..64);
+                                 // < 0 (default): 4 or 16 by cell occupancy
     int count_rotate = 1024;     // count sweep: lists longer than this start near the query (0: off)
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
-    bool border_roots = false;   // border sweep's single-root fast path (tuning)
     int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow
     int dir_paged = -1;          // PD_OPT_DIR_PAGED: 1 paged, 0 flat, -1 paged when the grid has
                                  // more directory words than points
     int dense_prune = 1;         // dense count pass: projection-window tiles only (2: per-band runs)
     bool shard_core_bit = false; // PD_OPT_SHARD_CORE_BIT: sharded phase B keys carry the core flag
-    bool border_lists = false;   // PD_OPT_BORDER_LISTS: count sweep lists border neighbours
     int dense_screen = 1;        // dense count pass screen: 1 e4m3 (32x32x64), 0 bf16 hi.hi
-    int dense_prefetch = 2;      // e4m3 count pass: streamed tiles in flight (2, 4 or 8)
-    int dense_waves = 4;         // e4m3 count pass: waves per tile block (1, 2 or 4)
-    bool sort_payload = false;   // fp32 3-D: coordinates ride the sort (PD_OPT_SORT_PAYLOAD)
     int label_buckets = -1;      // labels to input order by bucketed pair passes (PD_OPT_LABEL_BUCKETS;
                                  // -1: from 2^28 points on, where they beat the direct scatter)
-    int variant = 221;           // PD_OPT_SWEEP_VARIANT: cheap-row count (bit 3; bit 0 the batched
-                                 // count2), cheap-row border (bit 4; bit 2 the batched border2),
-                                 // row-wise link
     Timings t;
     PhaseState st;
     DenseState dn;

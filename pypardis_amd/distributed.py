@@ -540,9 +540,19 @@ def _kd_device(X, kdlab, levels, ops, comm, dev):
             ops.kdx_axes(comm.all_gather_t(part).to(dev), W, lv)
         cnt = ops.kdx_counts(X, kdlab, lv, S)
         ops.kdx_boundary(comm.all_reduce_t(cnt, "sum").to(dev), lv)
-    trace, lo, hi, bad = ops.kdx_end(X, kdlab, sum(len(lv) for lv in levels), True)
+    try:
+        trace, lo, hi, bad = ops.kdx_end(X, kdlab, sum(len(lv) for lv in levels), True)
+    except Exception:
+        # every slice empty: the level decisions ran over zero moments; name
+        # that (all ranks hold the same sizes, so all raise the same) rather
+        # than whatever the empty KD failed on
+        if int(sizes_dev.sum().item()) == 0:
+            raise ValueError("no points on any rank") from None
+        raise
     # the KD trace read above synchronised the stream: this copy waits on nothing
     sizes = sizes_dev.cpu().numpy().astype(np.int64)
+    if int(sizes.sum()) == 0:
+        raise ValueError("no points on any rank")
     if bad:
         raise ValueError("Input contains NaN or infinity.")
     data_box = np.concatenate([lo, hi])

@@ -148,6 +148,20 @@ def test_train_threads_local_comm():
     assert {r.n_clusters for r in res} == {int(g["sk_labels"].max()) + 1}
 
 
+def test_all_slices_empty_raises_clearly():
+    """Every rank's slice empty: the sharded train names that ("no points on
+    any rank") on every rank, not an error of the empty KD."""
+    from local_comm import local_comms
+    from pypardis_amd.distributed import train_threads
+    from sharded_ops import OracleOps
+    import torch
+    W = 2
+    slices = [torch.zeros((0, 3), dtype=torch.float32) for _ in range(W)]
+    with pytest.raises(ValueError, match="no points on any rank"):
+        train_threads(slices, 0.1, 5, local_comms(W), [OracleOps() for _ in range(W)],
+                      max_partitions=4, abort_timeout=30.0)
+
+
 def test_train_threads_rank_failure_aborts():
     """A rank that fails alone (here: its ops raise in phase A) must not leave
     the other ranks waiting for it for ever: train_threads aborts the

@@ -228,21 +228,17 @@ def test_train_matches_oracle(native, case):
     assert m.n_clusters_ == ncl
 
 
-@pytest.mark.parametrize("variant,link_mode,border_roots",
-                         [(0, 5, 0), (7, 3, 1), (5, 0, 0), (7, 2, 0), (5, 4, 0), (5, 3, 0),
-                          (5, 6, 0), (0, 6, 0), (13, 6, 0), (15, 3, 1), (8, 0, 0), (29, 6, 0),
-                          (24, 3, 0), (61, 6, 0), (40, 0, 0), (45, 3, 1), (221, 6, 0)])
-def test_sweep_variants_exact(native, variant, link_mode, border_roots):
-    """PD_OPT_SWEEP_VARIANT x PD_OPT_LINK_MODE: the row-by-row and the
-    batched sweep kernels, and the sampled-union + cell-verify link (3) or the
-    full union sweeps (0, 2), give identical counts, core flags and labels
-    (= oracle) on every case: 1-D..4-D, cityblock, fp64, exact ties,
-    min_samples 1, several neighbourhoods (waves straddling two)."""
-    from pypardis_amd import DBSCAN, synth
+@pytest.mark.parametrize("stats", [0, 1])
+def test_sweeps_exact(native, stats):
+    """The shipped sweeps — the count sweep at 8 waves per SIMD, its
+    instrumented form (PD_OPT_SWEEP_STATS), the window union + cell verify
+    link and the border sweep — give the oracle's counts, core flags and
+    labels on every case: 1-D..4-D, cityblock, fp64, exact ties,
+    min_samples 1..34, several neighbourhoods (waves straddling two), the
+    sharded phases (1-rank RCCL) and the goldens."""
+    from pypardis_amd import DBSCAN, distributed, synth
     ctx = native.context()
-    ctx.set_option(native.PD_OPT_SWEEP_VARIANT, variant)
-    ctx.set_option(native.PD_OPT_LINK_MODE, link_mode)
-    ctx.set_option(native.PD_OPT_BORDER_ROOTS, border_roots)
+    ctx.set_option(native.PD_OPT_SWEEP_STATS, stats)
     try:
         for _, kw, eps, ms, metric, P in CASES:
             X = synth.blobs_noise(**kw)
@@ -264,36 +260,6 @@ def test_sweep_variants_exact(native, variant, link_mode, border_roots):
             lab_o, core_o, _, _ = oracle.dbscan(Y, 0.06, ms)
             m = DBSCAN(eps=0.06, min_samples=ms, max_partitions=6).train(_dev(Y))
             assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o), ms
-        for name in ("b3d_20k", "c0_p5_cityblock", "dup_1d"):
-            gd = load_golden(name)
-            lab, core, _ = _cluster(native, gd["X"], float(gd["eps"]), int(gd["min_samples"]),
-                                    _metric(gd))
-            assert np.array_equal(lab, gd["sk_labels"]) and np.array_equal(core, gd["sk_core"])
-    finally:
-        ctx.set_option(native.PD_OPT_SWEEP_VARIANT, native.SWEEP_VARIANT_DEFAULT)
-        ctx.set_option(native.PD_OPT_LINK_MODE, native.LINK_MODE_DEFAULT)
-        ctx.set_option(native.PD_OPT_BORDER_ROOTS, 0)
-
-
-@pytest.mark.parametrize("lists", [1, 0])
-def test_border_lists_exact(native, lists):
-    """PD_OPT_BORDER_LISTS: border points attached from the count sweep's
-    neighbour lists (on) or by the second sweep (off) give the oracle's
-    labels: every CASES set, min_samples 2 / 20 / 33 (the largest listed) /
-    34 (beyond: swept), full counts, the sharded phases (1-rank RCCL) and the
-    goldens."""
-    from pypardis_amd import DBSCAN, distributed, synth
-    ctx = native.context()
-    ctx.set_option(native.PD_OPT_BORDER_LISTS, lists)
-    try:
-        for _, kw, eps, ms, metric, P in CASES:
-            X = synth.blobs_noise(**kw)
-            lab_o, core_o, cnt_o, _ = oracle.dbscan(X, eps, ms, metric)
-            m = DBSCAN(eps=eps, min_samples=ms, metric=metric, max_partitions=P).train(_dev(X))
-            assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o), kw
-            assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_o), kw
-            lab, core, ncl, cnt = _cluster(native, X, eps, ms, metric, full=True)
-            assert np.array_equal(cnt, cnt_o) and np.array_equal(lab, lab_o), kw
         X = synth.blobs_noise(40_000, 3, side=5.0, n_centers=4, sigma=0.3, noise_frac=0.3,
                               seed=71)
         for ms in (2, 20, 33, 34):
@@ -301,20 +267,31 @@ def test_border_lists_exact(native, lists):
             m = DBSCAN(eps=0.06, min_samples=ms, max_partitions=6).train(_dev(X))
             assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o), ms
             assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_o), ms
-        comm = distributed.device_comms([0])[0]
-        res = distributed.train_threads([_dev(X)], 0.06, 10, [comm],
-                                        [distributed.NativeOps(torch.device("cuda", 0))],
-                                        max_partitions=8)
-        lab_o, core_o, _, _ = oracle.dbscan(X, 0.06, 10)
-        np.testing.assert_array_equal(res[0].local_labels.cpu().numpy().astype(np.int64), lab_o)
-        np.testing.assert_array_equal(res[0].local_core.cpu().numpy(), core_o)
+        if stats:
+            comm = distributed.device_comms([0])[0]
+            res = distributed.train_threads([_dev(X)], 0.06, 10, [comm],
+                                            [distributed.NativeOps(torch.device("cuda", 0))],
+                                            max_partitions=8)
+            lab_o, core_o, _, _ = oracle.dbscan(X, 0.06, 10)
+            np.testing.assert_array_equal(res[0].local_labels.cpu().numpy().astype(np.int64),
+                                          lab_o)
+            np.testing.assert_array_equal(res[0].local_core.cpu().numpy(), core_o)
         for name in ("b3d_20k", "b2d_20k", "c0_p5_cityblock", "dup_1d"):
             gd = load_golden(name)
             lab, core, _ = _cluster(native, gd["X"], float(gd["eps"]), int(gd["min_samples"]),
                                     _metric(gd))
             assert np.array_equal(lab, gd["sk_labels"]) and np.array_equal(core, gd["sk_core"])
     finally:
-        ctx.set_option(native.PD_OPT_BORDER_LISTS, 0)
+        ctx.set_option(native.PD_OPT_SWEEP_STATS, 0)
+
+
+def test_retired_options_raise(native):
+    """The tuning knobs retired in round 5 (their losing kernels are gone)
+    are refused, not silently ignored."""
+    ctx = native.context()
+    for opt in native.PD_OPT_RETIRED:
+        with pytest.raises(native.PardisError):
+            ctx.set_option(opt, 1)
 
 
 def test_fp64_input_exact(native):
@@ -768,48 +745,6 @@ def test_dense_screens_equal(native, case):
         assert 0 < int(core1.sum()) < len(X)
 
 
-@pytest.mark.parametrize("case", ["c3_30k", "d5_blobs", "ties", "c3_1m"])
-def test_dense_prefetch_exact(native, case):
-    """PD_OPT_DENSE_PREFETCH (e4m3 count pass: 2, 4 or 8 streamed tiles in
-    flight per block) and PD_OPT_DENSE_WAVES (1, 2 or 4 waves per block)
-    change only the staging and the block shape: identical counts, core flags
-    and labels, and the oracle's where it runs.  Bad values raise."""
-    from pypardis_amd import synth
-    if case == "ties":
-        g = np.arange(6, dtype=np.float32) * np.float32(0.05)
-        X = np.stack(np.meshgrid(*([g] * 6), indexing="ij"), -1).reshape(-1, 6).astype(np.float32)
-        eps, ms = float(np.float32(0.05)), 7
-    elif case == "c3_1m":
-        X, eps, ms = synth.make_config("C3", n=1_000_000)[0], 0.114028, 10
-    else:
-        c = next(c for c in DENSE if c[0] == case)
-        X, eps, ms = np.ascontiguousarray(c[1]()), c[2], c[3]
-    ctx = native.context()
-    with pytest.raises(native.PardisError):
-        ctx.set_option(native.PD_OPT_DENSE_PREFETCH, 3)
-    with pytest.raises(native.PardisError):
-        ctx.set_option(native.PD_OPT_DENSE_WAVES, 3)
-    outs = []
-    # (tiles in flight, waves per block): the LDS-DMA ring, and the
-    # register-staged blocks of 1 / 2 / 4 waves
-    for pf, cw in ((2, 4), (4, 4), (8, 4), (2, 2), (2, 1)):
-        ctx.set_option(native.PD_OPT_DENSE_PREFETCH, pf)
-        ctx.set_option(native.PD_OPT_DENSE_WAVES, cw)
-        try:
-            outs.append(_cluster(native, X, eps, ms, full=True))
-        finally:
-            ctx.set_option(native.PD_OPT_DENSE_PREFETCH, native.DENSE_PREFETCH_DEFAULT)
-            ctx.set_option(native.PD_OPT_DENSE_WAVES, native.DENSE_WAVES_DEFAULT)
-    for lab, core, ncl, cnt in outs[1:]:
-        assert np.array_equal(cnt, outs[0][3])
-        assert np.array_equal(core, outs[0][1])
-        assert np.array_equal(lab, outs[0][0]) and ncl == outs[0][2]
-    if len(X) <= 60_000:
-        lab_o, core_o, cnt_o, nc_o = oracle.dbscan(X, eps, ms)
-        assert np.array_equal(outs[0][3], cnt_o)
-        assert np.array_equal(outs[0][0], lab_o) and outs[0][2] == nc_o
-
-
 def test_dense_edge_cases(native):
     from pypardis_amd import DBSCAN
     X = np.full((300, 16), 0.25, np.float32)   # identical points
@@ -851,19 +786,16 @@ def test_c4_skew_vs_oracle(native, case):
         assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), want), P
         assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_w), P
     # dense-cell tuning knobs change the work order, never the answer:
-    # rotated count starts on every long list / never; centre-row union
-    # window of 1 candidate / unbounded
+    # rotated count starts on every long list / never; window union of 2 /
+    # 4 / 16 / 64 records
     ctx = native.context()
-    LM, CW = native.LINK_MODE_DEFAULT, -1
+    CW = -1
     for opts in (((native.PD_OPT_COUNT_ROTATE, 16, 1024),),
                  ((native.PD_OPT_COUNT_ROTATE, 0, 1024),),
                  ((native.PD_OPT_CENTRE_WINDOW, 64, CW),),
+                 ((native.PD_OPT_CENTRE_WINDOW, 16, CW),),
                  ((native.PD_OPT_CENTRE_WINDOW, 2, CW),),
-                 ((native.PD_OPT_CENTRE_WINDOW, 4, CW),),
-                 ((native.PD_OPT_LINK_MODE, 3, LM), (native.PD_OPT_CENTRE_WINDOW, 1, CW)),
-                 ((native.PD_OPT_LINK_MODE, 3, LM), (native.PD_OPT_CENTRE_WINDOW, 0, CW)),
-                 ((native.PD_OPT_LINK_MODE, 5, LM),),
-                 ((native.PD_OPT_LINK_MODE, 5, LM), (native.PD_OPT_CENTRE_WINDOW, 64, CW))):
+                 ((native.PD_OPT_CENTRE_WINDOW, 4, CW),)):
         for opt, val, _ in opts:
             ctx.set_option(opt, val)
         try:
@@ -1182,31 +1114,3 @@ def test_label_buckets_equal_direct_scatter(native, cfg, n):
     assert outs[0][2] == outs[1][2]
     lab = outs[0][0]
     assert bool((lab == -1).any()) and bool((lab >= 0).any())
-
-
-def test_sort_payload_equals_gather(native):
-    """PD_OPT_SORT_PAYLOAD (fp32 3-D): coordinates carried through the radix
-    sort instead of gathered after it — identical labels and core flags,
-    several neighbourhoods (duplicate halo records), and the exact labels of
-    the oracle on a golden."""
-    from pypardis_amd import DBSCAN, synth
-    ctx = native.context()
-    X, c = synth.make_config("C2", n=1_500_000)
-    outs = []
-    for on in (1, 0):
-        ctx.set_option(native.PD_OPT_SORT_PAYLOAD, on)
-        try:
-            m = DBSCAN(eps=c["eps"], min_samples=c["min_samples"], max_partitions=8).train(_dev(X))
-        finally:
-            ctx.set_option(native.PD_OPT_SORT_PAYLOAD, 0)
-        outs.append((m.labels_.clone(), m.core_sample_mask_.clone(), m.n_clusters_))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    g = load_golden("b3d_20k")
-    ctx.set_option(native.PD_OPT_SORT_PAYLOAD, 1)
-    try:
-        m = DBSCAN(eps=float(g["eps"]), min_samples=int(g["min_samples"]),
-                   max_partitions=4).train(_dev(g["X"].astype(np.float32)))
-    finally:
-        ctx.set_option(native.PD_OPT_SORT_PAYLOAD, 0)
-    lab_o = oracle.dbscan(g["X"].astype(np.float32), float(g["eps"]), int(g["min_samples"]))[0]
-    assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)

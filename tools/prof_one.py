@@ -7,13 +7,6 @@ import torch
 
 from pypardis_amd import DBSCAN, _native, synth
 
-if "PROF_SORT_PAYLOAD" in os.environ:   # A/B: coordinates ride the radix sort
-    _native.context(0).set_option(_native.PD_OPT_SORT_PAYLOAD,
-                                  int(os.environ["PROF_SORT_PAYLOAD"]))
-for env, opt in (("PROF_VARIANT", _native.PD_OPT_SWEEP_VARIANT),
-                 ("PROF_LINK_MODE", _native.PD_OPT_LINK_MODE)):
-    if env in os.environ:   # A/B of a sweep kernel variant / link mode
-        _native.context(0).set_option(opt, int(os.environ[env]))
 n = int(os.environ.get("PROF_N", "100000000"))
 name = os.environ.get("PROF_CFG", "C2")
 X, cfg = synth.make_config(name, n=n, device="cuda" if name == "C4" else "cpu")

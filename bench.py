@@ -62,11 +62,10 @@ HBM_PEAK_GBS = 8000.0
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # dense bf16 (MI355X_MICROARCH.md; no sparsity)
 MFMA_FP8_PEAK_TFLOPS = 5000.0    # dense e4m3 (32x32x64 f8f6f4: 2x bf16 per clock)
 BASELINE_METRIC = "points clustered/sec (whole node), 100M 3-D pts, 1/2/4/8 GPUs; % HBM roofline"
-LINK_KERNELS = ("init_kernel", "flatten_kernel", "window_link_kernel", "window_uf_kernel",
-                "centre_link_kernel", "link_kernel", "link2_kernel", "cell_root_kernel",
-                "big_cell_root_kernel", "cell_word_root_kernel", "mid_cell_word_root_kernel",
-                "big_cell_word_root_kernel", "word_root_kernel", "verify_screen_kernel",
+LINK_KERNELS = ("init_kernel", "window_uf_kernel", "cell_word_root_kernel",
+                "mid_cell_word_root_kernel", "big_cell_word_root_kernel", "verify_screen_kernel",
                 "flag_list_kernel", "cell_verify_kernel", "pair_kernel")
+L2_PEAK_GBS = 34500.0            # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate
 
 
 def parse():
@@ -93,6 +92,8 @@ def parse():
                     help="PD_OPT_LABEL_BUCKETS override (0: one scattered label write per record)")
     ap.add_argument("--centre-window", type=int, default=None,
                     help="PD_OPT_CENTRE_WINDOW override (link window length)")
+    ap.add_argument("--legacy-sort", type=int, default=None,
+                    help="PD_OPT_LEGACY_SORT override (1: onesweep pairs + gather)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
@@ -126,6 +127,18 @@ def load_pmc(config="C2"):
                     reverse=True):
         if tag(f) != config:
             continue
+        try:
+            return json.load(open(f)), os.path.basename(f)
+        except Exception:
+            continue
+    return None, None
+
+
+def load_ceiling():
+    """Newest count-sweep latency ceiling (profiles/rNN_vMM_count_ceiling.json,
+    tools/count_ceiling.py): the shipped count kernel on L2-resident C2 slices."""
+    fs = sorted(glob.glob(os.path.join(HERE, "profiles", "*count_ceiling*.json")), key=_order)
+    for f in reversed(fs):
         try:
             return json.load(open(f)), os.path.basename(f)
         except Exception:
@@ -241,6 +254,15 @@ def grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages):
             roof["hbm_frac"] = f["hbm_bytes"] / (t_cnt * 1e-3) / (HBM_PEAK_GBS * 1e9)
         if "l2_hit" in f:
             roof["l2_hit"] = f["l2_hit"]
+        req = k.get("TCP_TCC_READ_REQ_sum")
+        if req:
+            # L1 -> L2 read requests of 64-128 B (request size uncalibrated):
+            # the L2 fraction at 128 B is an upper bound
+            roof["l2_read_requests"] = req
+            roof["l2_frac"] = req * 128 / (t_cnt * 1e-3) / (L2_PEAK_GBS * 1e9)
+            roof["l2_frac_at_64B"] = req * 64 / (t_cnt * 1e-3) / (L2_PEAK_GBS * 1e9)
+            roof["l2_note"] = ("TCP_TCC_READ_REQ_sum x 128 B (x 64 B) per launch / kernel time "
+                               "/ the guide's 34.5 TB/s aggregate L2 rate")
     if sweep and sweep.get("s_count_cand") and rec:
         cand = sweep["s_count_cand"]
         roof["limiter"] = {
@@ -249,6 +271,15 @@ def grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages):
             "candidate_tests": cand, "candidate_tests_per_record": cand / rec,
             "candidate_tests_per_s": cand / (t_cnt * 1e-3),
             "records_per_s": rec / (t_cnt * 1e-3)}
+        ceil, ceil_src = load_ceiling()
+        if ceil and ceil.get("ceiling_candidate_tests_per_s"):
+            # the same kernel with every load of its chain an L2 hit
+            roof["latency_frac"] = (cand / (t_cnt * 1e-3)) / ceil["ceiling_candidate_tests_per_s"]
+            roof["latency_ceiling"] = {
+                "candidate_tests_per_s": ceil["ceiling_candidate_tests_per_s"],
+                "points": ceil.get("ceiling_points"), "source": ceil_src,
+                "note": "count4_kernel on a density-preserving C2 slice whose records, "
+                        "directory and cell starts fit each XCD's L2 (tools/count_ceiling.py)"}
     stage = None
     if pmc and stages.get("link"):
         kb = {}
@@ -459,7 +490,8 @@ def main():
                      (_native.PD_OPT_DIR_BUDGET, args.dir_budget),
                      (_native.PD_OPT_LABEL_BUCKETS, args.label_buckets),
                      (_native.PD_OPT_DIR_PAGED, args.dir_paged),
-                     (_native.PD_OPT_DENSE_SCREEN, args.dense_screen)):
+                     (_native.PD_OPT_DENSE_SCREEN, args.dense_screen),
+                     (_native.PD_OPT_LEGACY_SORT, args.legacy_sort)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None
@@ -517,12 +549,11 @@ def main():
         ctx.set_option(_native.PD_OPT_SWEEP_STATS, 0)
         sweep = {k: int(v) for k, v in ctx.timings().items()
                  if k.startswith("s_") or k in ("records", "core_records")}
-        # the default link (mode 6) tallies candidates, hits and unions only;
-        # the other s_link_* slots belong to modes 0-3
-        if args.link_mode in (None, 5, 6):
-            for k in ("s_link_core", "s_link_same", "s_link_find_same"):
-                if not sweep.get(k):
-                    sweep.pop(k, None)
+        # the window union tallies candidates, hits and unions only (the
+        # other s_link_* slots belonged to the retired link modes)
+        for k in ("s_link_core", "s_link_same", "s_link_find_same", "s_count_staged"):
+            if not sweep.get(k):
+                sweep.pop(k, None)
     ms_step = 1e3 * el / args.steps
     value = n * args.steps / el
     ncl = m.n_clusters_

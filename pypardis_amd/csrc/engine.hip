@@ -517,17 +517,31 @@ __device__ __forceinline__ uint32_t block_sum_u32(uint32_t v) {
     return t;
 }
 
+// A tile kernel's count (tile_offsets scans tiles + 1 entries): block 0 also
+// zeroes the trailing entry, so no fill runs before the scan.
+__device__ __forceinline__ void tile_count_out(uint32_t* tile_cnt, uint32_t c) {
+    tile_cnt[blockIdx.x] = c;
+    if (blockIdx.x == 0) tile_cnt[gridDim.x] = 0;
+}
+
+constexpr int kCtrs = 16;   // train counters: [0..7] lists, [8..9] big / mid cells, [10] pairs
+
 template <typename T, int D>
 __global__ __launch_bounds__(kBlock) void halo_tile_kernel(const T* __restrict__ X, uint64_t n,
                                                            const PartGrid* __restrict__ parts,
-                                                           int P, uint32_t* __restrict__ tile_cnt) {
+                                                           int P, uint32_t* __restrict__ tile_cnt,
+                                                           uint32_t* __restrict__ ctrs) {
+    // the train's small counters (dup / root / core / border lists, big and
+    // mid cells, cell pairs): zeroed here, the first kernel of the train,
+    // instead of by fills
+    if (blockIdx.x == 0 && threadIdx.x < kCtrs) ctrs[threadIdx.x] = 0;
     uint64_t idx[4];
     T v[4][D];
     unsigned long long m[4];
     uint32_t cnt[4];
     halo_points<T, D, false>(X, n, parts, P, idx, v, m, cnt);
     const uint32_t t = block_sum_u32(cnt[0] + cnt[1] + cnt[2] + cnt[3]);
-    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = t;
+    if (threadIdx.x == 0) tile_count_out(tile_cnt, t);
 }
 
 template <typename T, int D, typename K>
@@ -651,13 +665,15 @@ __global__ __launch_bounds__(kBlock) void halo_write_kernel(
 }
 
 // Coordinates into key order (padded rows); also lists the records of halo
-// points that live in several neighbourhoods (the merge only touches those).
+// points that live in several neighbourhoods (the merge only touches those)
+// and starts those points' merge representative (rep) at kNone.
 template <typename T, int D>
 __global__ __launch_bounds__(kBlock) void gather_kernel(const T* __restrict__ X, uint64_t R,
                                                         const uint32_t* __restrict__ vals,
                                                         T* __restrict__ Xs,
                                                         uint32_t* __restrict__ dup_list,
-                                                        uint32_t* __restrict__ dup_count) {
+                                                        uint32_t* __restrict__ dup_count,
+                                                        uint32_t* __restrict__ rep) {
     const uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     const uint32_t v = r < R ? vals[r] : 0u;
     if (r < R) {
@@ -665,9 +681,12 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const T* __restrict__ X,
         constexpr int S = Stride<D>::v;
 #pragma unroll
         for (int j = 0; j < S; ++j) Xs[r * S + j] = j < D ? X[i * D + j] : T(0);
+        if (rep && (v & kDupBit)) rep[i] = kNone;
     }
     wave_append(dup_list, dup_count, r < R && (v & kDupBit), (uint32_t)r);
 }
+
+#include "bsort.hpp"
 
 template <typename K>
 __global__ void part_start_kernel(const K* __restrict__ keys, uint64_t R,
@@ -725,7 +744,7 @@ __global__ __launch_bounds__(kBlock) void cell_tile_kernel(const K* __restrict__
     uint64_t kv[4];
     const uint64_t r0 = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
     const uint32_t t = block_sum_u32(cell_starts4<K>(keys, R, r0, st, kv));
-    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = t;
+    if (threadIdx.x == 0) tile_count_out(tile_cnt, t);
 }
 
 template <typename K>
@@ -882,7 +901,7 @@ __global__ __launch_bounds__(kBlock) void dir_tile_kernel(const uint4* __restric
     uint32_t pc[4];
     const uint32_t t =
         block_sum_u32(dir_popc4(dir, W, ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4, pc));
-    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = t;
+    if (threadIdx.x == 0) tile_count_out(tile_cnt, t);
 }
 
 __global__ __launch_bounds__(kBlock) void dir_write_kernel(uint4* __restrict__ dir, uint64_t W,
@@ -903,15 +922,22 @@ __global__ __launch_bounds__(kBlock) void dir_write_kernel(uint4* __restrict__ d
 // parent is the smaller of them that is core and below r — two candidates
 // leave about half the trees of one (tools/init_forest_study.py).
 constexpr int kSubTiles = 4;   // init_kernel / roots_kernel: record tiles per block
+// Also starts the per-record component keys (gmin) and the directory-word
+// roots (wroot, W words) at kNone — the fills they needed before.
 __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t R, const uint8_t* __restrict__ core,
                                                       const uint32_t* __restrict__ mn,
-                                                      int use_mn, uint32_t* __restrict__ par) {
+                                                      int use_mn, uint32_t* __restrict__ par,
+                                                      uint32_t* __restrict__ gmin,
+                                                      uint32_t* __restrict__ wroot, uint64_t W) {
     // kSubTiles record tiles of kBlock per block (fewer workgroups for the
     // light per-record passes over 1e9 records)
 #pragma unroll
     for (int q = 0; q < kSubTiles; ++q) {
-        const uint32_t r = (blockIdx.x * kSubTiles + q) * kBlock + threadIdx.x;
-        if (r >= R) return;
+        const uint64_t r64 = ((uint64_t)blockIdx.x * kSubTiles + q) * kBlock + threadIdx.x;
+        if (r64 < W) wroot[r64] = kNone;
+        if (r64 >= R) continue;
+        const uint32_t r = (uint32_t)r64;
+        gmin[r] = kNone;
         uint32_t p = kNone;
         if (core[r] & 1) {
             p = r;
@@ -1196,7 +1222,7 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
     // border candidates (owner record, not core, has a neighbour) per tile;
     // border_list_kernel lists them in order after a scan of the counts
     const uint32_t c = block_sum_u32(nb);
-    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = c;
+    if (threadIdx.x == 0) tile_count_out(tile_cnt, c);
 }
 
 __global__ __launch_bounds__(kBlock) void border_list_kernel(uint32_t R,
@@ -1915,7 +1941,7 @@ __global__ __launch_bounds__(kBlock) void verify_screen_kernel(
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t nc = *ncells;
     if (blockIdx.x * kBlock >= nc) {   // a tile past the last cell (grid over records)
-        if (threadIdx.x == 0) tile_cnt[blockIdx.x] = 0;
+        if (threadIdx.x == 0) tile_count_out(tile_cnt, 0);
         return;
     }
     const uint32_t rc = c < nc ? croot[c] : kNone;
@@ -1935,7 +1961,7 @@ __global__ __launch_bounds__(kBlock) void verify_screen_kernel(
     }
     if (c < nc) flags[c] = work ? 1 : 0;
     const uint32_t t = block_sum_u32(work ? 1u : 0u);
-    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = t;
+    if (threadIdx.x == 0) tile_count_out(tile_cnt, t);
 }
 
 // Ordered list of the indices i < n with flags[i] set (tile offsets from a
@@ -2306,7 +2332,7 @@ inline unsigned sub_blocks(uint64_t n) {
 // total); with `read_total` the total is copied back (syncs) and returned.
 uint64_t tile_offsets(Ctx& ctx, uint32_t* cnt, unsigned tiles, uint64_t* off, hipStream_t s,
                       bool read_total) {
-    PD_HIP(hipMemsetAsync(cnt + tiles, 0, sizeof(uint32_t), s));
+    // (cnt[tiles] = 0: written by the tile kernel's block 0, tile_count_out)
     size_t tb = 0;
     PD_HIP(rocprim::exclusive_scan(nullptr, tb, cnt, off, (uint64_t)0, (size_t)tiles + 1,
                                    rocprim::plus<uint64_t>(), s));
@@ -2377,8 +2403,9 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     const unsigned htiles = (unsigned)std::max<uint64_t>(1, (n + 4 * kBlock - 1) / (4 * kBlock));
     uint32_t* tcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)htiles + 1);
     uint64_t* toff = ctx.arena.get<uint64_t>("tile_off", (size_t)htiles + 1);
+    uint32_t* ctrs = ctx.arena.get<uint32_t>("train_ctrs", kCtrs);
     hipLaunchKernelGGL((halo_tile_kernel<T, D>), dim3(htiles), dim3(kBlock), 0, s, X, n, parts, P,
-                       tcnt);
+                       tcnt, ctrs);
     const uint64_t R64 = tile_offsets(ctx, tcnt, htiles, toff, s, true);
     if (R64 >= 0xFFFFFFFEull) throw Error(-5, "more than 2^32-2 halo records on one device");
     const uint32_t R = (uint32_t)R64;
@@ -2435,17 +2462,33 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         tree.ax_new = (const int32_t*)dt + nslot;
         tree.bound = (const double*)(dt + db);
     }
+    // the records in input order (the bucketed sort's level-1 input)
+    K* rkeys = ctx.legacy_sort ? keys : keys2;
+    uint32_t* rvals = ctx.legacy_sort ? vals : vals2;
     if (P <= 64)
         hipLaunchKernelGGL((halo_write_kernel<T, D, K, true>), dim3(htiles), dim3(kBlock), 0, s, X,
-                           n, parts, P, a.owner, tree, toff, keys, vals);
+                           n, parts, P, a.owner, tree, toff, rkeys, rvals);
     else
         hipLaunchKernelGGL((halo_write_kernel<T, D, K, false>), dim3(htiles), dim3(kBlock), 0, s,
-                           X, n, parts, P, a.owner, tree, toff, keys, vals);
+                           X, n, parts, P, a.owner, tree, toff, rkeys, rvals);
     PD_HIP(hipGetLastError());
     tm.mark();   // 1
 
-    // ---- shuffle by neighbourhood == sort by (neighbourhood, cell) key
-    {
+    // ---- shuffle by neighbourhood == sort by (neighbourhood, cell) key, the
+    // coordinates carried along (bsort.hpp); PD_OPT_LEGACY_SORT: rocPRIM's
+    // onesweep over (key, id) pairs, then a gather of the coordinates
+    T* Xs = ctx.arena.get<T>("Xs", (size_t)R * Stride<D>::v);
+    uint32_t* dup_list = ctx.arena.get<uint32_t>("dup_list", R);
+    uint32_t* lcount = ctrs;   // dup, roots, core, border (zeroed by halo_tile_kernel)
+    // the merge's representative per point, initialised for the points of the
+    // duplicated records only (by the pass that lists them), not a fill over n
+    uint32_t* rep = P > 1 ? ctx.arena.get<uint32_t>("rep", n) : nullptr;
+    if (!ctx.legacy_sort) {
+        ctx.t.sort_levels = bucket_sort<T, D, K>(ctx, s, R, key_bits, X, rkeys, rvals, keys, vals,
+                                                 Xs, dup_list, lcount, rep);
+        tm.mark();   // 2
+        tm.mark();   // 3 (no gather)
+    } else {
         rocprim::double_buffer<K> kb(keys, keys2);
         rocprim::double_buffer<uint32_t> vb(vals, vals2);
         size_t tb = 0;
@@ -2454,15 +2497,11 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
         keys = kb.current();
         vals = vb.current();
+        tm.mark();   // 2
+        hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X,
+                           (uint64_t)R, vals, Xs, dup_list, lcount, rep);
+        tm.mark();   // 3
     }
-    tm.mark();   // 2
-    T* Xs = ctx.arena.get<T>("Xs", (size_t)R * Stride<D>::v);
-    uint32_t* dup_list = ctx.arena.get<uint32_t>("dup_list", R);
-    uint32_t* lcount = ctx.arena.get<uint32_t>("list_counts", 8);   // dup, roots, core, border
-    PD_HIP(hipMemsetAsync(lcount, 0, sizeof(uint32_t) * 8, s));
-    hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X,
-                       (uint64_t)R, vals, Xs, dup_list, lcount);
-    tm.mark();   // 3
 
     // ---- cell directory
     uint32_t* part_start = ctx.arena.get<uint32_t>("part_start", P + 1);
@@ -2575,9 +2614,12 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     tm.mark();   // 5
 
     uint32_t* par = ctx.arena.get<uint32_t>("parent", R);
+    uint32_t* gmin = ctx.arena.get<uint32_t>("gmin", R);
     if (R) {
         // (1) forest from the count pass's two smallest neighbours
-        hipLaunchKernelGGL(init_kernel, dim3(sub_blocks(R)), dim3(kBlock), 0, s, R, core, mn, 1, par);
+        uint32_t* wroot = ctx.arena.get<uint32_t>("word_root", W);
+        hipLaunchKernelGGL(init_kernel, dim3(sub_blocks(std::max<uint64_t>(R, W))), dim3(kBlock), 0,
+                           s, R, core, mn, 1, par, gmin, wroot, (uint64_t)W);
         // (2) window union.  Auto window (PD_OPT_CENTRE_WINDOW < 0): sparse
         // cells (a few records each, C2: 2.3) gain little from the window
         // beyond the fused flatten, so a short one is cheapest (C2 link 6.59
@@ -2613,13 +2655,11 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         else
             go(std::integral_constant<int, 64>{});
         uint32_t* croot = ctx.arena.get<uint32_t>("cell_root", R);
-        uint32_t* wroot = ctx.arena.get<uint32_t>("word_root", W);
         {   // (3) cell and word roots in one pass
             uint32_t* big = ctx.arena.get<uint32_t>("big_cells", R / (kWordBig + 1) + 1);
             uint32_t* mid = ctx.arena.get<uint32_t>("mid_cells", R / (kMidCell + 1) + 1);
-            uint32_t* nbig = ctx.arena.get<uint32_t>("big_count", 4);   // [0] big, [1] mid
-            PD_HIP(hipMemsetAsync(nbig, 0, 2 * sizeof(uint32_t), s));
-            PD_HIP(hipMemsetAsync(wroot, 0xFF, sizeof(uint32_t) * W, s));
+            uint32_t* nbig = ctrs + 8;   // [0] big, [1] mid (zeroed by halo_tile_kernel)
+            // (wroot starts at kNone: init_kernel)
             if ((uint64_t)W < 0xFFFFFFFFull)   // directory slots < 2^32 - 1
                 hipLaunchKernelGGL((cell_word_root_kernel<K, true>), dim3(blocks(R)), dim3(kBlock), 0,
                                    s, cstart, dncells, ckeys, par, croot, wroot, mid, nbig + 1, big,
@@ -2635,8 +2675,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         }
         const uint32_t pcap = (uint32_t)std::min<uint64_t>(R, 64ull << 20);
         uint2* plist = ctx.arena.get<uint2>("pair_list", pcap);
-        uint32_t* pcount = ctx.arena.get<uint32_t>("pair_count", 4);
-        PD_HIP(hipMemsetAsync(pcount, 0, sizeof(uint32_t), s));
+        uint32_t* pcount = ctrs + 10;   // (zeroed by halo_tile_kernel)
         // (4) verify: screen every cell, then work on the flagged ones only
         const unsigned vtiles = blocks(R);
         uint8_t* vflag = ctx.arena.get<uint8_t>("verify_flags", R);
@@ -2660,8 +2699,6 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     tm.mark();   // 6
     if (P > 1 && R) {
         // the merge touches only the records of points in several neighbourhoods
-        uint32_t* rep = ctx.arena.get<uint32_t>("rep", n);
-        PD_HIP(hipMemsetAsync(rep, 0xFF, sizeof(uint32_t) * n, s));
         const unsigned gb = std::min(blocks(R), 2048u);
         hipLaunchKernelGGL(rep_kernel, dim3(gb), dim3(kBlock), 0, s, dup_list, lcount, vals, par,
                            rep);
@@ -2669,13 +2706,12 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
                            par);
     }
     tm.mark();   // 7
-    uint32_t* gmin = ctx.arena.get<uint32_t>("gmin", R);
     uint32_t n_roots = 0;
     if (R) {
         // single device: the components are listed so that their keys can be
         // ranked here (labels); sharded: keys stay global ids (merge first)
         uint32_t* root_list = a.phase == 0 ? ctx.arena.get<uint32_t>("root_list", R) : nullptr;
-        PD_HIP(hipMemsetAsync(gmin, 0xFF, sizeof(uint32_t) * R, s));
+        // (gmin starts at kNone: init_kernel)
         hipLaunchKernelGGL(roots_kernel, dim3(sub_blocks(R)), dim3(kBlock), 0, s, R, vals, a.gid, par,
                            gmin, root_list, lcount + 1, ctx.sweep_stats ? 1 : 0);
         uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t) * 4);

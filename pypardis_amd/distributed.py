@@ -218,15 +218,47 @@ def dd_combine(parts):
     return mom
 
 
-def partition_ranks(P, world):
-    """Neighbourhood -> rank (contiguous blocks of KD labels) and each
-    neighbourhood's index among its rank's neighbourhoods."""
-    part_rank = np.array([L * world // P for L in range(P)], np.int32)
+def partition_ranks(P, world, weights=None):
+    """Neighbourhood -> rank, and each neighbourhood's index among its rank's
+    neighbourhoods (ascending label, so a rank's records keep the KD order).
+
+    Without weights, or with P <= world: contiguous blocks of KD labels.  With
+    weights (points per KD leaf) and P > world: longest-processing-time-first
+    placement — leaves by decreasing weight (ties: smaller label), each to the
+    least-loaded rank (ties: smaller rank).  The static analogue of Spark
+    scheduling the reference's P partition tasks over its executors as they
+    free up (R:dbscan/dbscan.py:116-124); labels do not depend on the
+    placement (any assignment of neighbourhoods to ranks is exact)."""
+    if weights is None or P <= world:
+        part_rank = np.array([L * world // P for L in range(P)], np.int32)
+    else:
+        w = np.asarray(weights, np.float64)
+        if w.shape != (P,):
+            raise ValueError("one weight per partition expected")
+        part_rank = np.zeros(P, np.int32)
+        load = np.zeros(world, np.float64)
+        for L in sorted(range(P), key=lambda L: (-w[L], L)):
+            r = int(np.argmin(load))   # first minimum: the smallest rank on ties
+            part_rank[L] = r
+            load[r] += w[L]
     local_index = np.zeros(P, np.int32)
     for r in range(world):
         idx = np.nonzero(part_rank == r)[0]
         local_index[idx] = np.arange(len(idx), dtype=np.int32)
     return part_rank, local_index
+
+
+def leaf_sizes(splits, n_total, P):
+    """Points per KD leaf from the split trace (R:dbscan/partition.py:151-152:
+    each split leaves n_left points with the label and moves n_right to the
+    new one) — equal on every rank (the trace's counts are global)."""
+    size = np.zeros(P, np.int64)
+    size[0] = n_total
+    for sp in splits:
+        cur, nl, n_left, n_right = sp[0], sp[1], sp[4], sp[5]
+        size[cur] = n_left
+        size[nl] = n_right
+    return size
 
 
 _TORCH_OPS = {"sum": dist.ReduceOp.SUM, "min": dist.ReduceOp.MIN, "max": dist.ReduceOp.MAX}
@@ -627,7 +659,7 @@ def _exclusive(c):
 
 def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitions=None,
                   group=None, ops=None, split_method='min_var', comm=None, return_local=True,
-                  keep_owned=False):
+                  keep_owned=False, placement=None):
     """Sharded DBSCAN train over the ranks of ``group`` (default: world).
 
     X: this rank's (n_i, d) slice (float32/float64, on this rank's GPU for
@@ -641,7 +673,13 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     the owned records instead.  ``keep_owned``: keep the records this rank
     owns (``gid`` / ``labels`` / ``core`` of the result, ~13 B of HBM per
     received record while the result lives); off by default.
+    ``placement``: KD leaves -> ranks.  None (default): LPT on the leaves'
+    point counts when max_partitions > world size, else contiguous label
+    blocks; 'lpt' / 'blocks' force one (partition_ranks).  Labels do not
+    depend on it.
     """
+    if placement not in (None, "lpt", "blocks"):
+        raise ValueError("placement must be None, 'lpt' or 'blocks'")
     if split_method not in ('min_var', 'rotation'):
         split_method = 'min_var'   # the reference's fallback (R:dbscan/partition.py:129-130)
     if X.dim() != 2:
@@ -691,7 +729,13 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     # ---- route + exchange (R:dbscan/dbscan.py:114-118,136-151): one ordered
     # pass packs every destination (the self block straight into the receive
     # buffers), one grouped exchange moves all fields
-    part_rank, local_index = partition_ranks(P, W)
+    # KD leaves -> ranks: LPT on the leaves' point counts when there are more
+    # leaves than ranks (placement=None), else contiguous label blocks
+    weights = None
+    if placement == "lpt" or (placement is None and P > W):
+        weights = leaf_sizes(splits, n_total, P)
+    part_rank, local_index = partition_ranks(P, W, weights)
+    stats["placement"] = "lpt" if weights is not None and P > W else "blocks"
     if W == 1:
         # every neighbourhood is here: the slice is the record set as it is
         Xr, gid, owner, xr = X, None, kdlab, None
@@ -836,7 +880,7 @@ def _train_dense(X, eps, min_samples, metric, comm, ops, gid_off, data_box, kd, 
 
 def train_threads(slices, eps, min_samples, comms, ops, metric=_native.PD_EUCLIDEAN,
                   max_partitions=None, split_method='min_var', abort_timeout=60.0,
-                  keep_owned=False):
+                  keep_owned=False, placement=None):
     """One process driving several devices: rank r = thread r runs
     ``train_sharded`` on slices[r] with comms[r] (e.g. RcclComm over
     pd_comm_init_all) and ops[r].  Returns the per-rank results in rank order;
@@ -856,7 +900,8 @@ def train_threads(slices, eps, min_samples, comms, ops, metric=_native.PD_EUCLID
                 torch.cuda.set_device(torch.device(dev))
             out[r] = train_sharded(slices[r], eps, min_samples, metric=metric,
                                    max_partitions=max_partitions, ops=ops[r], comm=comms[r],
-                                   split_method=split_method, keep_owned=keep_owned)
+                                   split_method=split_method, keep_owned=keep_owned,
+                                   placement=placement)
         except BaseException as e:   # noqa: B902 - re-raised below
             errs[r] = e
             order.append(r)

@@ -20,7 +20,7 @@ def cut_points(n, world):
 
 
 def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native,
-             split_method='min_var', api=False, keyed=False):
+             split_method='min_var', api=False, keyed=False, placement=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -67,20 +67,20 @@ def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native,
             loc = model.labels_.cpu().numpy(), model.core_sample_mask_.cpu().numpy()
         else:
             res = train_sharded(Xi, eps, min_samples, metric=metric, max_partitions=P, ops=ops,
-                                split_method=split_method, keep_owned=True)
+                                split_method=split_method, keep_owned=True, placement=placement)
             loc = res.local_labels.cpu().numpy(), res.local_core.cpu().numpy()
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), gid=res.gid.cpu().numpy(),
                  labels=res.labels.cpu().numpy(), core=res.core.cpu().numpy(),
                  ncl=np.int64(res.n_clusters), splits=np.array(res.splits, np.float64),
                  ebox=res.boxes, exports=np.int64(res.stats["exports"]),
                  received=np.int64(res.stats["received"]), loc_labels=loc[0], loc_core=loc[1],
-                 lo=np.int64(cuts[rank]), **extra)
+                 lo=np.int64(cuts[rank]), placement=str(res.stats.get("placement")), **extra)
     finally:
         dist.destroy_process_group()
 
 
 def run_world(world, X, eps, min_samples, metric, P, out_dir, native=False, timeout=600,
-              split_method='min_var', api=False, keyed=False):
+              split_method='min_var', api=False, keyed=False, placement=None):
     """Spawn `world` ranks; return the assembled (labels, core, n_clusters,
     splits) over all points."""
     import socket
@@ -93,7 +93,7 @@ def run_world(world, X, eps, min_samples, metric, P, out_dir, native=False, time
     ctx = mp.get_context("spawn")
     procs = [ctx.Process(target=run_rank,
                          args=(r, world, port, X, eps, min_samples, metric, P, out_dir, native,
-                               split_method, api, keyed))
+                               split_method, api, keyed, placement))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -41,6 +41,52 @@ def test_sharded_labels_equal_sklearn(tmp_path, name, world, P):
         np.testing.assert_array_equal(sp, np.array(kd["splits"], np.float64))
 
 
+def test_partition_ranks_lpt():
+    """LPT placement of KD leaves: heaviest leaf first onto the
+    least-loaded rank — non-contiguous label sets, loads within one leaf of
+    each other; contiguous blocks without weights or when P <= world."""
+    from pypardis_amd.distributed import partition_ranks, leaf_sizes
+    pr, li = partition_ranks(6, 2, [10, 1, 1, 10, 5, 5])
+    assert pr.tolist() == [0, 0, 1, 1, 0, 1]
+    assert li.tolist() == [0, 1, 0, 1, 2, 2]
+    pr, _ = partition_ranks(6, 2)
+    assert pr.tolist() == [0, 0, 0, 1, 1, 1]
+    pr, _ = partition_ranks(2, 4, [5, 7])
+    assert pr.tolist() == [0, 2]
+    rng = np.random.default_rng(0)
+    w = rng.zipf(1.5, 64).astype(np.float64)
+    pr, _ = partition_ranks(64, 8, w)
+    load = np.bincount(pr, weights=w, minlength=8)
+    assert load.max() - load.min() <= w.max() + 1e-9
+    # leaf sizes from a split trace (cur, new, axis, cand, n_left, n_right, ...)
+    sp = [(0, 1, 0, 3, 60, 40, 0., 0., 0.), (0, 2, 1, 3, 25, 35, 0., 0., 0.),
+          (1, 3, 1, 3, 30, 10, 0., 0., 0.)]
+    assert leaf_sizes(sp, 100, 4).tolist() == [25, 30, 35, 10]
+
+
+@pytest.mark.parametrize("name,world,P", [("b3d_20k", 3, 8), ("lattice_900", 2, 8)])
+def test_sharded_lpt_equals_blocks(tmp_path, name, world, P):
+    """The sharded train with LPT leaf placement (non-contiguous label sets
+    per rank; the default when max_partitions > world) and with contiguous
+    blocks: both give sklearn's labels and core flags on every point."""
+    from pypardis_amd.distributed import partition_ranks, leaf_sizes
+    g = load_golden(name)
+    X = g["X"]
+    kd = oracle.kd_partition(X, P, sums="exact")
+    pr, _ = partition_ranks(P, world, leaf_sizes(kd["splits"], len(X), P))
+    for placement in ("lpt", "blocks"):
+        (tmp_path / placement).mkdir()
+        out = run_world(world, X, float(g["eps"]), int(g["min_samples"]), 0, P,
+                        str(tmp_path / placement), placement=placement)
+        assert (out["seen"] == 1).all()
+        np.testing.assert_array_equal(out["labels"], g["sk_labels"])
+        np.testing.assert_array_equal(out["core"], g["sk_core"].astype(np.uint8))
+        np.testing.assert_array_equal(out["loc_labels"], g["sk_labels"])
+        assert {str(r["placement"]) for r in out["ranks"]} == {placement}
+    if name == "b3d_20k":   # the case really is non-contiguous
+        assert any(pr[i] > pr[i + 1] for i in range(P - 1)), pr
+
+
 @pytest.mark.parametrize("name,world,P", [("b3d_20k", 2, 8), ("c0", 3, 5)])
 def test_sharded_rotation_split(tmp_path, name, world, P):
     """split_method='rotation' over ranks: the all-reduced digit histograms

@@ -4,8 +4,10 @@ C4 = 1B 2-D GPS-like points, eps 0.001, min_samples 20.  The
 reference's rule splits each KD box at the first of seven candidate bounds
 (mean + (i-3)*0.3*std) that best balances the two halves
 (R:dbscan/partition.py:58-65), which cannot follow Zipf-distributed cities.
-For max_partitions P in {8, 16, 32, 64} with neighbourhood L on GPU
-L * 8 // P (distributed.partition_ranks), per GPU: the points it owns, the
+For max_partitions P in {8, 16, 32, 64} and each placement of the KD leaves
+on the GPUs (distributed.partition_ranks: 'blocks' = neighbourhood L on GPU
+L * 8 // P; 'lpt' = longest-processing-time-first on the leaves' point
+counts, the sharded train's default when P > 8), per GPU: the points it owns, the
 halo records it clusters (its neighbourhoods' 2*eps boxes), and the time of
 one device train over exactly those records (pd_train, the phase-A + B work
 of that rank, timed with HIP events on this one MI355X).  Prints one JSON line
@@ -25,12 +27,13 @@ import numpy as np
 import torch
 
 from pypardis_amd import KDPartitioner, _native, synth
-from pypardis_amd.distributed import partition_ranks
+from pypardis_amd.distributed import leaf_sizes, partition_ranks
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=1_000_000_000)
 ap.add_argument("--gpus", type=int, default=8)
 ap.add_argument("--parts", default="8,16,32,64")
+ap.add_argument("--placements", default="blocks,lpt")
 ap.add_argument("--out", default=None)
 args = ap.parse_args()
 W = args.gpus
@@ -40,14 +43,20 @@ eps, ms = cfg["eps"], cfg["min_samples"]
 ctx = _native.context(0)
 report = {"config": f"C4 gps_skew n={args.n} eps={eps} min_samples={ms}", "gpus": W,
           "rule": "R:dbscan/partition.py:58-65 (7 candidate bounds, best balance)", "by_P": {}}
-for P in [int(p) for p in args.parts.split(",")]:
+for P, placement in [(int(p), pl) for p in args.parts.split(",")
+                     for pl in args.placements.split(",")]:
+    if placement == "lpt" and P <= W:
+        continue   # one leaf per GPU: the blocks placement
     t0 = time.perf_counter()
     kd = KDPartitioner(X, P)
     lab = kd.labels
     ebox = np.stack([kd.bounding_boxes[L].expand(2 * eps).as_array()
                      for L in sorted(kd.bounding_boxes)])
     owned = torch.bincount(lab.long(), minlength=P).cpu().numpy()
-    part_rank, local_index = partition_ranks(P, W)
+    weights = leaf_sizes(kd.splits, int(X.shape[0]), P) if placement == "lpt" else None
+    if weights is not None:
+        assert np.array_equal(weights, owned), "leaf sizes from the trace = label counts"
+    part_rank, local_index = partition_ranks(P, W, weights)
     halo, _ = _native.halo_members(X, ebox)     # records per neighbourhood
     del _
     torch.cuda.empty_cache()
@@ -89,7 +98,8 @@ for P in [int(p) for p in args.parts.split(",")]:
     pts = np.array([x["owned_points"] for x in ranks], np.float64)
     rec = np.array([x["halo_records"] for x in ranks], np.float64)
     ms_ = np.array([x["train_ms"] for x in ranks], np.float64)
-    report["by_P"][str(P)] = {
+    report["by_P"][f"{P}_{placement}"] = {
+        "placement": placement,
         "per_gpu": ranks,
         "owned_max_over_mean": float(pts.max() / pts.mean()),
         "records_max_over_mean": float(rec.max() / rec.mean()),
@@ -99,7 +109,7 @@ for P in [int(p) for p in args.parts.split(",")]:
         "implied_speedup_8gpu_vs_sum": float(ms_.sum() / ms_.max()),
         "kd_and_probe_s": round(time.perf_counter() - t0, 1),
         "neighbourhood_records": [int(h) for h in halo]}
-    print(json.dumps({"P": P, **{k: v for k, v in report["by_P"][str(P)].items()
+    print(json.dumps({"P": P, **{k: v for k, v in report["by_P"][f"{P}_{placement}"].items()
                                   if k not in ("per_gpu", "neighbourhood_records")}}), flush=True)
 line = json.dumps(report)
 print(line, flush=True)

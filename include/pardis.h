@@ -105,11 +105,7 @@ enum pd_option {
                                 core_out by one coalesced pass instead of a byte scattered per
                                 owner record (default 0; same outputs).  pd_train_end checks
                                 the guarantee on the device (every component key < 2^31) and
-                                returns PD_EINVAL when a key breaks it */,
-    PD_OPT_LEGACY_SORT = 24   /* grid path: 1 = sort the halo records with rocPRIM's onesweep
-                                radix sort of (key, id) pairs and gather the coordinates after
-                                it (the round-4 path, kept for A/B); 0 (default) = the bucketed
-                                sort that carries the coordinates (bsort.hpp).  Same results */
+                                returns PD_EINVAL when a key breaks it */
     /* Retired in round 5 (measured A/Bs whose losing kernels were removed;
        pd_ctx_set_option returns PD_EINVAL for them, and the numbers are not
        reused): 4 LINK_MODE, 5 JUMP_ROUNDS, 9 SWEEP_VARIANT, 10 BORDER_ROOTS,
@@ -133,8 +129,6 @@ enum pd_timing_slot {
     PD_T_DIR_WORDS,            /* directory words it allocated (paged: occupied + 1) */
     PD_T_S_COUNT_BATCHES,      /* count sweep (PD_OPT_SWEEP_STATS): wave batches swept */
     PD_T_S_COUNT_STAGED,       /*   (retired LDS-staged count sweep: always 0) */
-    PD_T_SORT_LEVELS,          /* scatter levels of the last train's bucketed record sort
-                                  (0: PD_OPT_LEGACY_SORT) */
     PD_T_NSLOTS
 };
 

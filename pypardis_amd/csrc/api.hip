@@ -120,8 +120,6 @@ int32_t pd_ctx_destroy(pd_ctx* ctx) {
     int32_t rc = guard(ctx, [&] {
         ctx->c.arena.release();
         if (ctx->c.pinned) (void)hipHostFree(ctx->c.pinned);
-        if (ctx->c.bs_pinned) (void)hipHostFree(ctx->c.bs_pinned);
-        if (ctx->c.bs_ev) (void)hipEventDestroy(ctx->c.bs_ev);
         for (auto& e : ctx->c.ev)
             if (e) (void)hipEventDestroy(e);
     });
@@ -166,8 +164,6 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.dense_screen = (int)value;
         } else if (option == PD_OPT_SHARD_CORE_BIT) {
             ctx->c.shard_core_bit = value != 0;
-        } else if (option == PD_OPT_LEGACY_SORT) {
-            ctx->c.legacy_sort = value != 0;
         } else if (option == 4 || option == 5 || option == 9 || option == 10 || option == 16 ||
                    (option >= 20 && option <= 23)) {
             // retired tuning knobs (round 5): measured A/Bs whose losing
@@ -194,7 +190,7 @@ int32_t pd_ctx_timings(pd_ctx* ctx, double* out, int32_t n) {
                                        (double)t.sweep[6], (double)t.sweep[7], t.grid_grow,
                                        (double)t.count_kernel, (double)t.dir_paged,
                                        (double)t.dir_words, (double)t.sweep[8],
-                                       (double)t.sweep[9], (double)t.sort_levels};
+                                       (double)t.sweep[9]};
         for (int i = 0; i < n && i < PD_T_NSLOTS; ++i) out[i] = v[i];
     });
 }

@@ -686,8 +686,6 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const T* __restrict__ X,
     wave_append(dup_list, dup_count, r < R && (v & kDupBit), (uint32_t)r);
 }
 
-#include "bsort.hpp"
-
 template <typename K>
 __global__ void part_start_kernel(const K* __restrict__ keys, uint64_t R,
                                   const PartGrid* __restrict__ parts, int P,
@@ -2462,33 +2460,27 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         tree.ax_new = (const int32_t*)dt + nslot;
         tree.bound = (const double*)(dt + db);
     }
-    // the records in input order (the bucketed sort's level-1 input)
-    K* rkeys = ctx.legacy_sort ? keys : keys2;
-    uint32_t* rvals = ctx.legacy_sort ? vals : vals2;
     if (P <= 64)
         hipLaunchKernelGGL((halo_write_kernel<T, D, K, true>), dim3(htiles), dim3(kBlock), 0, s, X,
-                           n, parts, P, a.owner, tree, toff, rkeys, rvals);
+                           n, parts, P, a.owner, tree, toff, keys, vals);
     else
         hipLaunchKernelGGL((halo_write_kernel<T, D, K, false>), dim3(htiles), dim3(kBlock), 0, s,
-                           X, n, parts, P, a.owner, tree, toff, rkeys, rvals);
+                           X, n, parts, P, a.owner, tree, toff, keys, vals);
     PD_HIP(hipGetLastError());
     tm.mark();   // 1
 
-    // ---- shuffle by neighbourhood == sort by (neighbourhood, cell) key, the
-    // coordinates carried along (bsort.hpp); PD_OPT_LEGACY_SORT: rocPRIM's
-    // onesweep over (key, id) pairs, then a gather of the coordinates
+    // ---- shuffle by neighbourhood == sort by (neighbourhood, cell) key:
+    // rocPRIM's onesweep over (key, id) pairs, then a gather of the
+    // coordinates into key order.  (Round 5 measured an MSD bucket sort that
+    // carries the coordinate rows instead — slower: C2 8.76 vs 5.91 ms, C4
+    // 84 vs 64 ms; DESIGN.md §6, tools/msd_probe.hip.)
     T* Xs = ctx.arena.get<T>("Xs", (size_t)R * Stride<D>::v);
     uint32_t* dup_list = ctx.arena.get<uint32_t>("dup_list", R);
     uint32_t* lcount = ctrs;   // dup, roots, core, border (zeroed by halo_tile_kernel)
     // the merge's representative per point, initialised for the points of the
-    // duplicated records only (by the pass that lists them), not a fill over n
+    // duplicated records only (by the gather, which lists them), not a fill over n
     uint32_t* rep = P > 1 ? ctx.arena.get<uint32_t>("rep", n) : nullptr;
-    if (!ctx.legacy_sort) {
-        ctx.t.sort_levels = bucket_sort<T, D, K>(ctx, s, R, key_bits, X, rkeys, rvals, keys, vals,
-                                                 Xs, dup_list, lcount, rep);
-        tm.mark();   // 2
-        tm.mark();   // 3 (no gather)
-    } else {
+    {
         rocprim::double_buffer<K> kb(keys, keys2);
         rocprim::double_buffer<uint32_t> vb(vals, vals2);
         size_t tb = 0;
@@ -2497,11 +2489,11 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
         keys = kb.current();
         vals = vb.current();
-        tm.mark();   // 2
-        hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X,
-                           (uint64_t)R, vals, Xs, dup_list, lcount, rep);
-        tm.mark();   // 3
     }
+    tm.mark();   // 2
+    hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X, (uint64_t)R,
+                       vals, Xs, dup_list, lcount, rep);
+    tm.mark();   // 3
 
     // ---- cell directory
     uint32_t* part_start = ctx.arena.get<uint32_t>("part_start", P + 1);

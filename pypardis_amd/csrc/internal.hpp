@@ -54,7 +54,6 @@ struct Timings {
     int64_t dir_words = 0;       // directory words allocated (paged: occupied + 1)
     int dir_paged = 0;           // the last train's directory layout
     float count_kernel = 0;      // dense path: the count pass's tile kernel alone (ms)
-    int sort_levels = 0;         // bucketed sort: scatter levels of the last train
 };
 
 // Device state carried from phase A (local clustering) to phase B (border
@@ -170,11 +169,6 @@ struct Ctx {
     KdxState kdx;
     RouteState rt;
     hipEvent_t ev[16] = {};
-    // bucket sort (bsort.hpp): grow-only pinned staging of its level lists
-    void* bs_pinned = nullptr;
-    size_t bs_pinned_bytes = 0;
-    hipEvent_t bs_ev = nullptr;
-    int legacy_sort = 0;         // PD_OPT_LEGACY_SORT: rocPRIM onesweep + gather (A/B)
 };
 
 struct TrainArgs {

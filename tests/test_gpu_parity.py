@@ -1114,64 +1114,3 @@ def test_label_buckets_equal_direct_scatter(native, cfg, n):
     assert outs[0][2] == outs[1][2]
     lab = outs[0][0]
     assert bool((lab == -1).any()) and bool((lab >= 0).any())
-
-
-@pytest.mark.parametrize("case", ["c2_1500k", "c4_3m", "c1_500k", "f64_3d", "d1_dups", "d4_blobs",
-                                  "tiny"])
-def test_bucket_sort_equals_legacy(native, case):
-    """The bucketed record sort that carries the coordinates (bsort.hpp, the
-    default) and the rocPRIM onesweep pair sort + gather (PD_OPT_LEGACY_SORT)
-    give identical labels, core flags and counts — one to four scatter levels
-    (C4's 37-bit keys and dense cells), u32 and u64 keys, fp32 / fp64, 1-D to
-    4-D, duplicate halo records (P = 8) — and the oracle's where it runs."""
-    from pypardis_amd import DBSCAN, synth
-    ctx = native.context()
-    P = 8
-    if case == "c2_1500k":
-        X, c = synth.make_config("C2", n=1_500_000)
-        eps, ms = c["eps"], c["min_samples"]
-    elif case == "c4_3m":
-        X, c = synth.make_config("C4", n=3_000_000)
-        eps, ms = c["eps"], c["min_samples"]
-    elif case == "c1_500k":
-        X, c = synth.make_config("C1", n=500_000)
-        eps, ms, P = c["eps"], c["min_samples"], 1
-    elif case == "f64_3d":
-        X = synth.blobs_noise(60_000, 3, side=5.0, n_centers=5, sigma=0.3, seed=81).astype(np.float64)
-        X += np.random.default_rng(3).uniform(-1e-9, 1e-9, X.shape)
-        eps, ms = 0.07, 6
-    elif case == "d1_dups":
-        X = np.repeat(np.random.default_rng(4).uniform(0, 50, 20_000).astype(np.float32), 3)[:, None]
-        eps, ms = 0.01, 4
-    elif case == "d4_blobs":
-        X = synth.blobs_noise(50_000, 4, side=3.0, n_centers=6, sigma=0.25, seed=83)
-        eps, ms = 0.12, 7
-    else:
-        X = synth.blobs_noise(700, 2, side=2.0, n_centers=3, sigma=0.2, seed=85)
-        eps, ms = 0.1, 5
-    Xd = _dev(X)
-    outs = []
-    for legacy in (0, 1):
-        ctx.set_option(native.PD_OPT_LEGACY_SORT, legacy)
-        try:
-            m = DBSCAN(eps=eps, min_samples=ms, max_partitions=P).train(Xd)
-            lv = ctx.timings()["sort_levels"]
-        finally:
-            ctx.set_option(native.PD_OPT_LEGACY_SORT, 0)
-        outs.append((m.labels_.clone(), m.core_sample_mask_.clone(), m.n_clusters_, lv))
-    assert outs[0][3] >= 1 and outs[1][3] == 0
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    assert outs[0][2] == outs[1][2]
-    if len(X) <= 200_000:
-        lab_o, core_o, _, _ = oracle.dbscan(np.asarray(X), eps, ms)
-        assert np.array_equal(outs[0][0].cpu().numpy().astype(np.int64), lab_o)
-        assert np.array_equal(outs[0][1].cpu().numpy(), core_o)
-    # counts through pd_cluster (one neighbourhood): the sorted records' counts
-    if len(X) <= 200_000:
-        lab, core, ncl, cnt = _cluster(native, np.asarray(X), eps, ms, full=True)
-        ctx.set_option(native.PD_OPT_LEGACY_SORT, 1)
-        try:
-            lab1, core1, ncl1, cnt1 = _cluster(native, np.asarray(X), eps, ms, full=True)
-        finally:
-            ctx.set_option(native.PD_OPT_LEGACY_SORT, 0)
-        assert np.array_equal(cnt, cnt1) and np.array_equal(lab, lab1) and ncl == ncl1

@@ -4,6 +4,12 @@
 // or scattered directly; and how fast does a one-workgroup LDS radix sort of
 // <= 16k-record segments (rocprim block_radix_sort) write them out in order?
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/msd_probe.hip -o tools/msd_probe
+// Result on one MI355X (profiles/r05_v1_msd_probe.txt, 1e8 records): one
+// staged scatter pass 2.0-2.8 ms (1.7-2.4 TB/s of 48 B per record) for 256 to
+// 4096 buckets, 1.0-1.2 TB/s scattered directly; the final LDS sort 2.4-4.1
+// ms.  The full bucketed sort built from them (round 5, later removed) took
+// C2 8.76 ms against the onesweep + gather's 5.91 ms
+// (profiles/r05_v1_ab_bucket_sort.txt).
 #include <hip/hip_runtime.h>
 #include <cstring>
 #include <rocprim/rocprim.hpp>

@@ -105,7 +105,13 @@ enum pd_option {
                                 core_out by one coalesced pass instead of a byte scattered per
                                 owner record (default 0; same outputs).  pd_train_end checks
                                 the guarantee on the device (every component key < 2^31) and
-                                returns PD_EINVAL when a key breaks it */
+                                returns PD_EINVAL when a key breaks it */,
+    PD_OPT_COUNT_REPLAY = 24  /* measurement only (tools/count_ceiling.py): after the grid train's
+                                count sweep, run the same sweep again over this many replicas of
+                                the records (lane i sweeps record i mod R; replicas write the
+                                same values) and put its time in PD_T_COUNT_KERNEL — on a record
+                                set small enough to stay in L2, the sweep's latency ceiling.
+                                Default 0 (off) */
     /* Retired in round 5 (measured A/Bs whose losing kernels were removed;
        pd_ctx_set_option returns PD_EINVAL for them, and the numbers are not
        reused): 4 LINK_MODE, 5 JUMP_ROUNDS, 9 SWEEP_VARIANT, 10 BORDER_ROOTS,

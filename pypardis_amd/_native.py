@@ -30,6 +30,7 @@ PD_OPT_LABEL_BUCKETS = 15
 PD_OPT_DIR_PAGED = 17
 PD_OPT_DENSE_SCREEN = 18
 PD_OPT_SHARD_CORE_BIT = 19
+PD_OPT_COUNT_REPLAY = 24
 # retired in round 5 (pardis.h): set_option raises for them
 PD_OPT_RETIRED = (4, 5, 9, 10, 16, 20, 21, 22, 23)
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",

@@ -164,6 +164,9 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.dense_screen = (int)value;
         } else if (option == PD_OPT_SHARD_CORE_BIT) {
             ctx->c.shard_core_bit = value != 0;
+        } else if (option == PD_OPT_COUNT_REPLAY) {
+            if (value < 0 || value > 65536) throw Error(PD_EINVAL, "count replay must be in [0, 65536]");
+            ctx->c.count_replay = (int)value;
         } else if (option == 4 || option == 5 || option == 9 || option == 10 || option == 16 ||
                    (option >= 20 && option <= 23)) {
             // retired tuning knobs (round 5): measured A/Bs whose losing

@@ -1438,17 +1438,24 @@ __device__ __forceinline__ void row_range3(const Cells& C, const Count3Grid<T, D
 
 // WPE: the minimum waves per SIMD the register allocation must allow (1: no
 // constraint, the instrumented sweep; 8: at most 64 VGPRs, the default — the
-// candidate gathers want the occupancy: C2 count 4.87 -> 4.58 ms)
-template <typename T, int D, int M, bool ST, int WPE = 1>
+// candidate gathers want the occupancy: C2 count 4.87 -> 4.58 ms).
+// REPLAY (measurement only, PD_OPT_COUNT_REPLAY): R launched lanes sweep
+// record r % rmod — replicas of a small record set whose chain of loads
+// (record, directory words, cell starts, candidates) stays in L2, at full
+// occupancy and steady state: the sweep's latency ceiling
+// (tools/count_ceiling.py).  Replicas write the same values.
+template <typename T, int D, int M, bool ST, int WPE = 1, bool REPLAY = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void count4_kernel(
     const T* __restrict__ Xs, uint32_t R, Cells C, double eps, double eps2, float lo, float hi,
     uint32_t ms, int full, uint32_t rot_min, uint8_t* __restrict__ core,
     uint32_t* __restrict__ mn_out, uint32_t* __restrict__ cnt_out,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, uint32_t rmod) {
     constexpr int NR = NRows<D>::v;
     constexpr int B = NR < 3 ? NR : 3, NB = NR / B;
-    const uint32_t r = rec_index();
+    uint32_t r = rec_index();
     if (r >= R) return;
+    if constexpr (REPLAY) r = r % rmod;
+    (void)rmod;
     double a[D];
     load_rec<T, D>(Xs, r, a);
     const Pred<T, D, M> pr = make_pred<T, D, M>(Xs, r, a, eps, eps2, lo, hi);
@@ -2354,10 +2361,35 @@ void launch_count(hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double
                   uint32_t* mn, uint32_t* cnt, unsigned long long* st) {
     if constexpr (ST)
         hipLaunchKernelGGL((count4_kernel<T, D, M, true, 1>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                           Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
+                           Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st, 0u);
     else
         hipLaunchKernelGGL((count4_kernel<T, D, M, false, 8>), dim3(blocks(R)), dim3(kBlock), 0, s,
-                           Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st);
+                           Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st, 0u);
+}
+
+// PD_OPT_COUNT_REPLAY (measurement): the shipped count sweep over `reps`
+// replicas of the R records (lane i sweeps record i % R), timed with its own
+// events into PD_T_COUNT_KERNEL.
+template <typename T, int D, int M>
+float replay_count(hipStream_t s, const T* Xs, uint32_t R, uint32_t reps, const Cells& C,
+                   double eps, double eps2, float lo, float hi, uint32_t ms, int full,
+                   uint32_t rot_min, uint8_t* core, uint32_t* mn, uint32_t* cnt) {
+    const uint64_t RL = (uint64_t)R * reps;
+    if (RL >= 0xFFFFFFFFull) throw Error(-1, "count replay: more than 2^32 - 1 lanes");
+    hipEvent_t e0, e1;
+    PD_HIP(hipEventCreate(&e0));
+    PD_HIP(hipEventCreate(&e1));
+    PD_HIP(hipEventRecord(e0, s));
+    hipLaunchKernelGGL((count4_kernel<T, D, M, false, 8, true>), dim3(blocks(RL)), dim3(kBlock), 0,
+                       s, Xs, (uint32_t)RL, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt,
+                       (unsigned long long*)nullptr, R);
+    PD_HIP(hipEventRecord(e1, s));
+    PD_HIP(hipEventSynchronize(e1));
+    float msec = 0;
+    PD_HIP(hipEventElapsedTime(&msec, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return msec;
 }
 
 template <typename T, int D, int M>
@@ -2601,6 +2633,10 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         else
             launch_count<T, D, M, false>(s, Xs, R, C, eps, eps2, slo, shi, (uint32_t)a.min_samples,
                                          ctx.full_counts ? 1 : 0, rot, core, mn, cnt_rec, sst);
+        if (ctx.count_replay > 0 && !sst)
+            ctx.t.count_kernel = replay_count<T, D, M>(
+                s, Xs, R, (uint32_t)ctx.count_replay, C, eps, eps2, slo, shi,
+                (uint32_t)a.min_samples, ctx.full_counts ? 1 : 0, rot, core, mn, cnt_rec);
     }
     PD_HIP(hipGetLastError());
     tm.mark();   // 5

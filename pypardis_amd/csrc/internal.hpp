@@ -153,6 +153,7 @@ struct Ctx {
     int centre_window = -1;      // window union: records after each record tested (2..64);
                                  // < 0 (default): 4 or 16 by cell occupancy
     int count_rotate = 1024;     // count sweep: lists longer than this start near the query (0: off)
+    int count_replay = 0;        // PD_OPT_COUNT_REPLAY: replicas of the count sweep to time (0: off)
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
     int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow

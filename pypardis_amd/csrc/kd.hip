@@ -1377,7 +1377,12 @@ constexpr int kTrace = 13;
 
 __global__ void kdb_axes_kernel(const double* __restrict__ mom, int S, int D, int G,
                                 int32_t* __restrict__ axis, double* __restrict__ bounds,
-                                double* __restrict__ trace) {
+                                double* __restrict__ trace,
+                                unsigned long long* __restrict__ zero_cnt) {
+    // zero_cnt (nullable): the level's count slots (S x 8), zeroed here for
+    // the counts pass that follows (one launch, one block: no fill)
+    if (zero_cnt)
+        for (int i = threadIdx.x; i < S * 8; i += blockDim.x) zero_cnt[i] = 0ull;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= S) return;
     const double* p = mom + (size_t)k * G;
@@ -1553,8 +1558,7 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                 }
                 double* tr = trace + (size_t)first[l] * kTrace;
                 hipLaunchKernelGGL(kdb_axes_kernel, dim3(1), dim3(kTabLds), 0, s, m, S, D, G,
-                                   lv[l].axis, lv[l].bounds, tr);
-                PD_HIP(hipMemsetAsync(dcnt, 0, sizeof(unsigned long long) * S * 8, s));
+                                   lv[l].axis, lv[l].bounds, tr, dcnt);
                 const unsigned nb4 = grid_for((n + 3) / 4, 2048);
                 if (S <= 4) {
                     auto go = [&](auto NSc) {
@@ -1783,7 +1787,8 @@ void kdx_axes(Ctx& ctx, const double* gathered, int n_ranks, int level, hipStrea
                        n_ranks, len, S * G, G, d, k.mom, k.bbox);
     const KdxLv v = kdx_level(k, level);
     hipLaunchKernelGGL(kdb_axes_kernel, dim3(1), dim3(kTabLds), 0, s, k.mom, S, d, G, v.axis,
-                       v.bounds, k.trace + (size_t)k.first[level] * kTrace);
+                       v.bounds, k.trace + (size_t)k.first[level] * kTrace,
+                       (unsigned long long*)nullptr);
     PD_HIP(hipGetLastError());
 }
 

@@ -218,34 +218,91 @@ def dd_combine(parts):
     return mom
 
 
-def partition_ranks(P, world, weights=None):
+def partition_ranks(P, world, weights=None, order=None, method=None):
     """Neighbourhood -> rank, and each neighbourhood's index among its rank's
     neighbourhoods (ascending label, so a rank's records keep the KD order).
 
     Without weights, or with P <= world: contiguous blocks of KD labels.  With
-    weights (points per KD leaf) and P > world: longest-processing-time-first
-    placement — leaves by decreasing weight (ties: smaller label), each to the
-    least-loaded rank (ties: smaller rank).  The static analogue of Spark
+    weights (points per KD leaf) and P > world — the static analogue of Spark
     scheduling the reference's P partition tasks over its executors as they
-    free up (R:dbscan/dbscan.py:116-124); labels do not depend on the
-    placement (any assignment of neighbourhoods to ranks is exact)."""
+    free up (R:dbscan/dbscan.py:116-124):
+      'ordered' — the leaves in the KD tree's spatial (depth-first) order
+          (``order``, kd_leaf_order) cut into world contiguous runs with the
+          smallest possible largest load: each rank holds a spatially compact
+          group of leaves, so few points are routed to two ranks;
+      'lpt' — longest-processing-time-first: leaves by decreasing weight
+          (ties: smaller label), each to the least-loaded rank (ties: smaller
+          rank); the better balance on skewed leaves, at no locality;
+      None — 'ordered' unless its largest load exceeds LPT's by more than 5 %.
+    Labels do not depend on the placement (any assignment is exact)."""
     if weights is None or P <= world:
         part_rank = np.array([L * world // P for L in range(P)], np.int32)
     else:
         w = np.asarray(weights, np.float64)
         if w.shape != (P,):
             raise ValueError("one weight per partition expected")
-        part_rank = np.zeros(P, np.int32)
+        lpt = np.zeros(P, np.int32)
         load = np.zeros(world, np.float64)
         for L in sorted(range(P), key=lambda L: (-w[L], L)):
             r = int(np.argmin(load))   # first minimum: the smallest rank on ties
-            part_rank[L] = r
+            lpt[L] = r
             load[r] += w[L]
+        part_rank = lpt
+        if method in (None, "ordered") and order is not None:
+            ordd = _ordered_cut(w, list(order), world)
+            lo = np.bincount(ordd, weights=w, minlength=world).max()
+            ll = np.bincount(lpt, weights=w, minlength=world).max()
+            if method == "ordered" or lo <= 1.05 * ll:
+                part_rank = ordd
     local_index = np.zeros(P, np.int32)
     for r in range(world):
         idx = np.nonzero(part_rank == r)[0]
         local_index[idx] = np.arange(len(idx), dtype=np.int32)
     return part_rank, local_index
+
+
+def _ordered_cut(w, order, world):
+    """Leaves in `order` cut into min(world, P) non-empty contiguous runs with
+    the smallest possible largest run weight (dynamic programme over the
+    prefix sums, O(world P^2)); run k -> rank k."""
+    ws = np.array([float(w[L]) for L in order], np.float64)
+    P = len(ws)
+    K = min(world, P)
+    S = np.concatenate([[0.0], np.cumsum(ws)])
+    INF = np.inf
+    dp = np.full(P + 1, INF)
+    dp[1:] = S[1:]                       # one run over the first i leaves
+    arg = np.zeros((K + 1, P + 1), np.int64)
+    jj = np.arange(P + 1)[:, None]
+    ii = np.arange(P + 1)[None, :]
+    for k in range(2, K + 1):
+        cost = np.maximum(dp[:, None], S[None, :] - S[:, None])   # [j, i]
+        cost = np.where((jj < ii) & (jj >= k - 1), cost, INF)
+        arg[k] = np.argmin(cost, axis=0)
+        dp = cost[arg[k], np.arange(P + 1)]
+    # walk the cuts back from (K, P)
+    cuts, i = [P], P
+    for k in range(K, 1, -1):
+        i = int(arg[k][i])
+        cuts.append(i)
+    cuts.append(0)
+    cuts = cuts[::-1]                    # run k = leaves [cuts[k], cuts[k + 1])
+    part_rank = np.zeros(len(w), np.int32)
+    for k in range(K):
+        for pos in range(cuts[k], cuts[k + 1]):
+            part_rank[order[pos]] = k
+    return part_rank
+
+
+def kd_leaf_order(splits):
+    """KD leaves in depth-first (spatial) order: a split (cur -> cur, new)
+    replaces cur by [cur (v < boundary), new] (R:dbscan/partition.py:66-68)."""
+    seq = [0]
+    for sp in splits:
+        cur, nl = int(sp[0]), int(sp[1])
+        i = seq.index(cur)
+        seq[i:i + 1] = [cur, nl]
+    return seq
 
 
 def leaf_sizes(splits, n_total, P):
@@ -673,13 +730,13 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     the owned records instead.  ``keep_owned``: keep the records this rank
     owns (``gid`` / ``labels`` / ``core`` of the result, ~13 B of HBM per
     received record while the result lives); off by default.
-    ``placement``: KD leaves -> ranks.  None (default): LPT on the leaves'
-    point counts when max_partitions > world size, else contiguous label
-    blocks; 'lpt' / 'blocks' force one (partition_ranks).  Labels do not
-    depend on it.
+    ``placement``: KD leaves -> ranks when max_partitions > world size.
+    None (default): spatially ordered runs balanced by the leaves' point
+    counts, or LPT when that balances clearly better; 'ordered' / 'lpt' /
+    'blocks' force one (partition_ranks).  Labels do not depend on it.
     """
-    if placement not in (None, "lpt", "blocks"):
-        raise ValueError("placement must be None, 'lpt' or 'blocks'")
+    if placement not in (None, "ordered", "lpt", "blocks"):
+        raise ValueError("placement must be None, 'ordered', 'lpt' or 'blocks'")
     if split_method not in ('min_var', 'rotation'):
         split_method = 'min_var'   # the reference's fallback (R:dbscan/partition.py:129-130)
     if X.dim() != 2:
@@ -729,13 +786,21 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     # ---- route + exchange (R:dbscan/dbscan.py:114-118,136-151): one ordered
     # pass packs every destination (the self block straight into the receive
     # buffers), one grouped exchange moves all fields
-    # KD leaves -> ranks: LPT on the leaves' point counts when there are more
-    # leaves than ranks (placement=None), else contiguous label blocks
-    weights = None
-    if placement == "lpt" or (placement is None and P > W):
+    # KD leaves -> ranks (partition_ranks): with more leaves than ranks,
+    # balanced by the leaves' point counts — spatially ordered runs, or LPT
+    # when that balances clearly better; else contiguous label blocks
+    weights, order = None, None
+    if placement != "blocks" and P > W:
         weights = leaf_sizes(splits, n_total, P)
-    part_rank, local_index = partition_ranks(P, W, weights)
-    stats["placement"] = "lpt" if weights is not None and P > W else "blocks"
+        order = kd_leaf_order(splits)
+    part_rank, local_index = partition_ranks(P, W, weights, order, placement)
+    if weights is None:
+        stats["placement"] = "blocks"
+    elif placement in ("lpt", "ordered"):
+        stats["placement"] = placement
+    else:
+        chk, _ = partition_ranks(P, W, weights, order, "ordered")
+        stats["placement"] = "ordered" if np.array_equal(chk, part_rank) else "lpt"
     if W == 1:
         # every neighbourhood is here: the slice is the record set as it is
         Xr, gid, owner, xr = X, None, kdlab, None

@@ -25,7 +25,11 @@ def test_sharded_labels_equal_sklearn(tmp_path, name, world, P):
     if X.ndim == 1:
         X = X[:, None]
     mcode = 1 if metric in ("cityblock", "manhattan") else 0
-    out = run_world(world, X, float(g["eps"]), int(g["min_samples"]), mcode, P, str(tmp_path))
+    # contiguous label blocks (interleaved halves of the KD tree: many points
+    # on two ranks, the cross-rank merge exercised); the other placements:
+    # test_sharded_lpt_equals_blocks
+    out = run_world(world, X, float(g["eps"]), int(g["min_samples"]), mcode, P, str(tmp_path),
+                    placement="blocks")
     assert (out["seen"] == 1).all(), "every point owned by exactly one rank"
     np.testing.assert_array_equal(out["labels"], g["sk_labels"])
     np.testing.assert_array_equal(out["core"], g["sk_core"].astype(np.uint8))
@@ -64,17 +68,48 @@ def test_partition_ranks_lpt():
     assert leaf_sizes(sp, 100, 4).tolist() == [25, 30, 35, 10]
 
 
+def test_partition_ranks_ordered():
+    """Spatially ordered placement: the KD leaves' depth-first order (a BFS
+    schedule of 8 leaves: 0 4 2 6 1 5 3 7) cut into balanced contiguous runs
+    — for equal leaves exactly the subtrees (2 ranks: the two halves of the
+    first split; 4 ranks: the four quarters); the default picks LPT only when
+    it balances more than 5 % better."""
+    from pypardis_amd.distributed import kd_leaf_order, partition_ranks
+    order = kd_leaf_order([(a, b, 0, 0, 0, 0) for a, b in
+                           [(0, 1), (0, 2), (1, 3), (0, 4), (1, 5), (2, 6), (3, 7)]])
+    assert order == [0, 4, 2, 6, 1, 5, 3, 7]
+    pr, _ = partition_ranks(8, 2, np.ones(8), order)
+    assert pr.tolist() == [0, 1, 0, 1, 0, 1, 0, 1]
+    pr, _ = partition_ranks(8, 4, np.ones(8), order)
+    assert [sorted(np.nonzero(pr == r)[0].tolist()) for r in range(4)] == \
+        [[0, 4], [2, 6], [1, 5], [3, 7]]
+    # skew that contiguous runs cannot balance: LPT is taken
+    w = np.array([1, 1, 1, 1, 1, 1, 9, 9.])   # leaves 6 and 7 in runs 1 and 3
+    pr_o, _ = partition_ranks(8, 2, w, order, "ordered")
+    pr_l, _ = partition_ranks(8, 2, w, order, "lpt")
+    pr_d, _ = partition_ranks(8, 2, w, order)
+    lo = np.bincount(pr_o, weights=w).max()
+    ll = np.bincount(pr_l, weights=w).max()
+    assert ll <= lo
+    assert pr_d.tolist() == (pr_o if lo <= 1.05 * ll else pr_l).tolist()
+    # every rank gets a non-empty run when there are enough leaves
+    rng = np.random.default_rng(3)
+    pr, _ = partition_ranks(64, 8, rng.random(64) + 0.1, list(rng.permutation(64)), "ordered")
+    assert set(pr.tolist()) == set(range(8))
+
+
 @pytest.mark.parametrize("name,world,P", [("b3d_20k", 3, 8), ("lattice_900", 2, 8)])
 def test_sharded_lpt_equals_blocks(tmp_path, name, world, P):
     """The sharded train with LPT leaf placement (non-contiguous label sets
-    per rank; the default when max_partitions > world) and with contiguous
-    blocks: both give sklearn's labels and core flags on every point."""
+    per rank), spatially ordered runs (the default's usual choice) and
+    contiguous label blocks: all give sklearn's labels and core flags on
+    every point."""
     from pypardis_amd.distributed import partition_ranks, leaf_sizes
     g = load_golden(name)
     X = g["X"]
     kd = oracle.kd_partition(X, P, sums="exact")
     pr, _ = partition_ranks(P, world, leaf_sizes(kd["splits"], len(X), P))
-    for placement in ("lpt", "blocks"):
+    for placement in ("lpt", "ordered", "blocks"):
         (tmp_path / placement).mkdir()
         out = run_world(world, X, float(g["eps"]), int(g["min_samples"]), 0, P,
                         str(tmp_path / placement), placement=placement)

@@ -7,7 +7,9 @@ reference's rule splits each KD box at the first of seven candidate bounds
 For max_partitions P in {8, 16, 32, 64} and each placement of the KD leaves
 on the GPUs (distributed.partition_ranks: 'blocks' = neighbourhood L on GPU
 L * 8 // P; 'lpt' = longest-processing-time-first on the leaves' point
-counts, the sharded train's default when P > 8), per GPU: the points it owns, the
+counts; 'ordered' = the leaves in spatial order cut into balanced runs; the
+sharded train's default when P > 8 takes 'ordered' unless LPT balances more
+than 5 % better), per GPU: the points it owns, the
 halo records it clusters (its neighbourhoods' 2*eps boxes), and the time of
 one device train over exactly those records (pd_train, the phase-A + B work
 of that rank, timed with HIP events on this one MI355X).  Prints one JSON line
@@ -27,13 +29,13 @@ import numpy as np
 import torch
 
 from pypardis_amd import KDPartitioner, _native, synth
-from pypardis_amd.distributed import leaf_sizes, partition_ranks
+from pypardis_amd.distributed import kd_leaf_order, leaf_sizes, partition_ranks
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=1_000_000_000)
 ap.add_argument("--gpus", type=int, default=8)
 ap.add_argument("--parts", default="8,16,32,64")
-ap.add_argument("--placements", default="blocks,lpt")
+ap.add_argument("--placements", default="blocks,lpt,ordered")
 ap.add_argument("--out", default=None)
 args = ap.parse_args()
 W = args.gpus
@@ -45,7 +47,7 @@ report = {"config": f"C4 gps_skew n={args.n} eps={eps} min_samples={ms}", "gpus"
           "rule": "R:dbscan/partition.py:58-65 (7 candidate bounds, best balance)", "by_P": {}}
 for P, placement in [(int(p), pl) for p in args.parts.split(",")
                      for pl in args.placements.split(",")]:
-    if placement == "lpt" and P <= W:
+    if placement != "blocks" and P <= W:
         continue   # one leaf per GPU: the blocks placement
     t0 = time.perf_counter()
     kd = KDPartitioner(X, P)
@@ -53,10 +55,11 @@ for P, placement in [(int(p), pl) for p in args.parts.split(",")
     ebox = np.stack([kd.bounding_boxes[L].expand(2 * eps).as_array()
                      for L in sorted(kd.bounding_boxes)])
     owned = torch.bincount(lab.long(), minlength=P).cpu().numpy()
-    weights = leaf_sizes(kd.splits, int(X.shape[0]), P) if placement == "lpt" else None
+    weights = leaf_sizes(kd.splits, int(X.shape[0]), P) if placement != "blocks" else None
     if weights is not None:
         assert np.array_equal(weights, owned), "leaf sizes from the trace = label counts"
-    part_rank, local_index = partition_ranks(P, W, weights)
+    part_rank, local_index = partition_ranks(P, W, weights, kd_leaf_order(kd.splits),
+                                             placement if weights is not None else None)
     halo, _ = _native.halo_members(X, ebox)     # records per neighbourhood
     del _
     torch.cuda.empty_cache()

@@ -3,20 +3,21 @@
 count4_kernel tests ~18 candidates per C2 record through a dependent chain:
 record -> directory word -> cell start -> candidates.  Its PMC shows neither
 DRAM (hbm_frac ~0.09) nor the VALU (0.44 of issue) saturated.  This tool runs
-the SAME kernel (the shipped 8-waves-per-SIMD build, PD_OPT_TIMING events
-around its launch) on density-preserving C2 slices small enough that each
-XCD's share of the sorted records, directory and cell starts stays in its
-4 MiB L2 (0.5M / 1M / 2M points: 1-4 MB of records per XCD), where every
-load of the chain is an L2 hit, at full occupancy (>= 8k waves), and reports
-candidate tests per second.  The best of those rates is the kernel's ceiling
-with L2-resident operands; the full 100M-point rate over it is the fraction of
-that ceiling the headline kernel reaches (bench.py's latency_frac).
+the SAME kernel (the shipped 8-waves-per-SIMD build) in replay mode
+(PD_OPT_COUNT_REPLAY): after a normal train of a small density-preserving C2
+slice (R records), the sweep runs again over m replicas of those records —
+lane i sweeps record i mod R — so the launch has the full run's ~1e8 lanes
+(full occupancy, steady state) while every load of the chain (the record,
+its directory words, cell starts and candidates: R x ~40 B, a few MB) stays
+in L2.  Candidate tests per second of that launch is the sweep's latency
+ceiling; the full 100M-point rate over it is the fraction of that ceiling the
+headline kernel reaches (bench.py's roofline.latency_frac).
 
-Candidates per run come from one extra instrumented step (PD_OPT_SWEEP_STATS,
-same sweep order and early exit), the time from the shipped kernel.
+Candidates per record come from one instrumented step (PD_OPT_SWEEP_STATS;
+same sweep order and early exit), replicas test the same candidates.
 
-  python tools/count_ceiling.py [--sizes 500000,1000000,2000000] [--full 100000000]
-                                [--out gpurun_out/count_ceiling.json]
+  python tools/count_ceiling.py [--sizes 250000,500000,1000000,2000000]
+                                [--full 100000000] [--out gpurun_out/count_ceiling.json]
 """
 import argparse
 import json
@@ -30,7 +31,7 @@ import torch
 from pypardis_amd import _native, synth
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--sizes", default="500000,1000000,2000000")
+ap.add_argument("--sizes", default="250000,500000,1000000,2000000")
 ap.add_argument("--full", type=int, default=100_000_000)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--out", default=None)
@@ -40,7 +41,7 @@ ctx = _native.context(0)
 dev = torch.device("cuda:0")
 
 
-def measure(n):
+def measure(n, replay_lanes=None):
     X, cfg = synth.make_config("C2", n=n)
     Xd = torch.from_numpy(X).to(dev)
     del X
@@ -49,32 +50,42 @@ def measure(n):
     _native.cluster(Xd, eps, ms)
     st = ctx.timings()
     ctx.set_option(_native.PD_OPT_SWEEP_STATS, 0)
-    cand, rec = st["s_count_cand"], st["records"]
+    cand, rec = int(st["s_count_cand"]), int(st["records"])
     _native.cluster(Xd, eps, ms)   # warm
+    m = 0
+    if replay_lanes:
+        m = max(1, replay_lanes // rec)
+        ctx.set_option(_native.PD_OPT_COUNT_REPLAY, m)
     ctx.set_option(_native.PD_OPT_TIMING, 1)
     t = []
     for _ in range(args.reps):
         _native.cluster(Xd, eps, ms)
-        t.append(ctx.timings()["count"])
+        tm = ctx.timings()
+        t.append(tm["count_kernel"] if m else tm["count"])
     ctx.set_option(_native.PD_OPT_TIMING, 0)
+    ctx.set_option(_native.PD_OPT_COUNT_REPLAY, 0)
     del Xd
     torch.cuda.empty_cache()
     tc = float(np.median(t))
-    return {"points": n, "records": int(rec), "candidate_tests": int(cand),
+    lanes = rec * max(m, 1)
+    tests = cand * max(m, 1)
+    return {"points": n, "records": rec, "replicas": m, "lanes": lanes,
+            "candidate_tests": tests, "candidate_tests_per_record": cand / rec,
             "count_ms": tc, "count_ms_all": [round(x, 4) for x in t],
-            "candidate_tests_per_s": cand / (tc * 1e-3), "records_per_s": rec / (tc * 1e-3),
-            "waves": int((rec + 63) // 64)}
+            "candidate_tests_per_s": tests / (tc * 1e-3), "lanes_per_s": lanes / (tc * 1e-3)}
 
 
-small = [measure(int(s)) for s in args.sizes.split(",")]
-for r in small:
-    print(json.dumps(r), flush=True)
 full = measure(args.full)
 print(json.dumps(full), flush=True)
+small = [measure(int(s), replay_lanes=full["records"]) for s in args.sizes.split(",")]
+for r in small:
+    print(json.dumps(r), flush=True)
 best = max(small, key=lambda r: r["candidate_tests_per_s"])
-out = {"tool": "tools/count_ceiling.py", "kernel": "count4_kernel (8 waves/SIMD build)",
-       "config": "C2 density-preserving slices, max_partitions=1 (pd_cluster)",
-       "l2_resident": small, "full": full,
+out = {"tool": "tools/count_ceiling.py",
+       "kernel": "count4_kernel (the shipped 8-waves/SIMD build, replay mode)",
+       "config": "C2 density-preserving slices, max_partitions=1 (pd_cluster), replicated to "
+                 "the full run's lane count",
+       "l2_resident_replay": small, "full": full,
        "ceiling_candidate_tests_per_s": best["candidate_tests_per_s"],
        "ceiling_points": best["points"],
        "latency_frac": full["candidate_tests_per_s"] / best["candidate_tests_per_s"]}

@@ -110,6 +110,52 @@ class _Neighborhoods(dict):
         return iter(self.items())
 
 
+class _PartitionRecords(object):
+    """``DBSCAN.data`` after ``train`` (R:dbscan/dbscan.py:116-125): the
+    records of the per-partition clustering — for each neighbourhood L (the
+    reference's partitionBy order) and each of its points in input order,
+    ``(key, 'L:c')`` or ``(key, 'L:c*')`` with c the neighbourhood's own
+    sklearn label of the point and '*' for a non-core point (dbscan_partition,
+    R:dbscan/dbscan.py:12-34).  Built lazily on first use, one pd_cluster per
+    neighbourhood; the global labels never depend on it."""
+
+    def __init__(self, neighbors, params):
+        self.neighbors = neighbors
+        self.params = params
+        self._recs = None
+
+    def _build(self):
+        if self._recs is None:
+            recs = []
+            pts = self.neighbors.points
+            metric = _native.metric_code(self.params.get('metric', 'euclidean'))
+            for L in sorted(self.neighbors):
+                idx = self.neighbors[L].indices()
+                if not len(idx):
+                    continue
+                X = pts.X[torch.from_numpy(np.asarray(idx, np.int64)).to(pts.X.device)]
+                lab, core, _, _ = _native.cluster(X.contiguous(), self.params['eps'],
+                                                  self.params['min_samples'], metric)
+                lab, core = lab.cpu().numpy(), core.cpu().numpy()
+                keys = self.neighbors[L].keys().tolist()
+                recs.extend((k, '%i:%i%s' % (L, c, '' if f else '*'))
+                            for k, c, f in zip(keys, lab.tolist(), core.tolist()))
+            self._recs = recs
+        return self._recs
+
+    def collect(self):
+        return list(self._build())
+
+    def count(self):
+        return sum(len(nb) for nb in self.neighbors.values())
+
+    def take(self, k):
+        return self._build()[:k]
+
+    def __iter__(self):
+        return iter(self._build())
+
+
 class _Assignments(object):
     """``DBSCAN.result``: (key, cluster id) pairs sorted by key
     (``.sortByKey()``, R:dbscan/dbscan.py:162-164)."""
@@ -269,11 +315,14 @@ class DBSCAN(object):
         points = as_points(data, self.device)
         parts = KDPartitioner(points, self.max_partitions, sums=self.kd_sums)
         self.partitioner = parts
-        self.data = points
         self.bounding_boxes = parts.bounding_boxes
         self.expanded_boxes = {L: box.expand(2 * self.eps)
                                for L, box in sorted(parts.bounding_boxes.items())}
         self.neighbors = _Neighborhoods(points, self.expanded_boxes)
+        # the reference's self.data after train: the per-partition records
+        self.data = _PartitionRecords(self.neighbors, {'eps': self.eps,
+                                                       'min_samples': self.min_samples,
+                                                       'metric': self.metric})
         ebox = np.stack([self.expanded_boxes[L].as_array() for L in sorted(self.expanded_boxes)])
         lo, hi = parts.data_box
         tree = parts.split_tree() if len(ebox) > 1 and points.d <= 4 else None

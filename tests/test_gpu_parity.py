@@ -196,6 +196,26 @@ def test_dbscan_partition_string_records(native):
         assert [(int(k), s) for k, s in out] == want
 
 
+def test_model_data_is_reference_partition_records(native):
+    """DBSCAN.data after train is what the reference leaves there
+    (R:dbscan/dbscan.py:116-125): per KD partition, in partition order, its
+    halo members in input order as (key, 'L:c[*]') with the partition's own
+    sklearn label — equal to the reference's dbscan_partition records
+    (kd_sums='sequential': the reference's boxes)."""
+    from pypardis_amd import DBSCAN
+    g = load_golden("c0_p3")
+    po = g["part_out"]
+    m = DBSCAN(eps=float(g["eps"]), min_samples=int(g["min_samples"]),
+               max_partitions=int(g["P"]), kd_sums="sequential").train(_dev(g["X"]))
+    want = []
+    for L in range(int(g["P"])):
+        for _, k, c, core in po[po[:, 0] == L]:
+            want.append((int(k), "%i:%i%s" % (L, c, "" if core else "*")))
+    got = [(int(k), s) for k, s in m.data.collect()]
+    assert got == want
+    assert m.data.count() == len(want)
+
+
 # ------------------------------------------------------------ larger vs oracle
 CASES = [
     ("2d_c1slice", dict(n=150_000, d=2, side=100 * (0.015 ** 0.5), n_centers=1, sigma=1.0,

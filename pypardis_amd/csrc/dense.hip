@@ -338,27 +338,14 @@ struct TileShared {
 constexpr int kF8Waves = 3;   // e4m3 count pass: waves per SIMD (no bf16 query fragments held)
 constexpr int kF8QT = 2;      // e4m3 count pass: query tiles (of 32) per wave
 
-// Largest of the 32 accumulators of two 32x32 tiles for one query column, as
-// a tree of 3-input maxima (depth 4): the linear fold it replaces was a
-// 16-deep chain of dependent v_max3 per query tile, issued right after the
-// tile's MFMAs and so on the critical path of every streamed tile.  max is
-// exact, so the screen's decision is the same.
-__device__ __forceinline__ float max32(const f32x16& a, const f32x16& b) {
-    float m[11];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) m[k] = fmaxf(fmaxf(a[3 * k], a[3 * k + 1]), a[3 * k + 2]);
-#pragma unroll
-    for (int k = 0; k < 5; ++k) m[5 + k] = fmaxf(fmaxf(b[3 * k], b[3 * k + 1]), b[3 * k + 2]);
-    m[10] = fmaxf(a[15], b[15]);
-    const float n0 = fmaxf(fmaxf(m[0], m[1]), m[2]), n1 = fmaxf(fmaxf(m[3], m[4]), m[5]);
-    const float n2 = fmaxf(fmaxf(m[6], m[7]), m[8]), n3 = fmaxf(m[9], m[10]);
-    return fmaxf(fmaxf(n0, n1), fmaxf(n2, n3));
-}
-
 // The e4m3 count pass streams each tile through two register stages ahead of
 // a double-buffered LDS tile.  (Measured and retired in round 4: an LDS-DMA
 // ring of 4 or 8 buffers — 29.9 ms vs 21.3 at 2 waves/SIMD, depth never
-// mattered — and blocks of 1 or 2 waves — 38.2 / 24.7 ms)
+// mattered — and blocks of 1 or 2 waves — 38.2 / 24.7 ms; DESIGN.md §6.
+// Round 5: a depth-4 tree of maxima for the screen instead of the linear
+// v_max3 fold — C3 count 24.5 vs 24.1 ms, rejected: the screen's hot path is
+// ds_read -> 4 MFMAs -> max fold -> vote with no spills, and the fold is not
+// the limiter; profiles/r05_v3_ab_dense_max_tree.txt.)
 template <typename T, int MODE, int KS, int QT, bool F8>
 __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves_per_eu(F8 ? (KS >= 8 ? 1 : kF8Waves) : ((KS >= 8 || QT > 2) ? 1 : 2)))) void tile_kernel(TileArgs<T> A) {
     constexpr int NB = 2;                        // LDS tile buffers
@@ -678,7 +665,12 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
                 }
                 bool mb = false;
 #pragma unroll
-                for (int t = 0; t < QT; ++t) mb |= max32(acc[0][t], acc[1][t]) >= bc[t];
+                for (int t = 0; t < QT; ++t) {
+                    float m0 = fmaxf(acc[0][t][0], acc[1][t][0]);
+#pragma unroll
+                    for (int r = 1; r < 16; ++r) m0 = fmaxf(fmaxf(m0, acc[0][t][r]), acc[1][t][r]);
+                    mb |= m0 >= bc[t];
+                }
                 refine = __any(mb);
                 nrefined += refine ? 1u : 0u;
                 if (refine) {
@@ -733,7 +725,12 @@ __global__ __launch_bounds__(tile_threads(KS, MODE)) __attribute__((amdgpu_waves
                 // the accumulators are finite), then one compare
                 bool mb = false;
 #pragma unroll
-                for (int t = 0; t < QT; ++t) mb |= max32(acc[0][t], acc[1][t]) >= bc[t];
+                for (int t = 0; t < QT; ++t) {
+                    float m0 = fmaxf(acc[0][t][0], acc[1][t][0]);
+#pragma unroll
+                    for (int r = 1; r < 16; ++r) m0 = fmaxf(fmaxf(m0, acc[0][t][r]), acc[1][t][r]);
+                    mb |= m0 >= bc[t];
+                }
                 refine = __any(mb);
                 nrefined += refine ? 1u : 0u;
                 if (refine) {

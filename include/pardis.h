@@ -369,7 +369,8 @@ int32_t pd_dense_finish(pd_ctx* ctx, const int32_t* best, int32_t* labels, uint8
  * path's fp64 operation order, so the splits equal pd_kd_pass + pd_kd_counts
  * + host decisions bit for bit.  Levels of the BFS schedule: level l splits
  * level_sizes[l] labels, cur[] -> newlab[] (concatenated over levels, the
- * first level's single label 0).  labels (device int32[n], all 0 on entry)
+ * first level's single label 0).  labels (device int32[n]; need not be initialised
+ * when n_levels >= 2 or final_split — every label is then written — else all 0)
  * end as the partition labels.  trace_host: 13 doubles per split — axis,
  * mean, variance, n_less for the 7 bounds, n, candidate index, boundary.
  * lohi_host: bbox (2 d); *bad_host: non-finite coordinates.  d <= 4, labels

@@ -926,13 +926,15 @@ __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t R, const uint8_t*
                                                       const uint32_t* __restrict__ mn,
                                                       int use_mn, uint32_t* __restrict__ par,
                                                       uint32_t* __restrict__ gmin,
-                                                      uint32_t* __restrict__ wroot, uint64_t W) {
+                                                      uint32_t* __restrict__ wroot, uint64_t W,
+                                                      uint32_t* __restrict__ kbits, uint64_t NW) {
     // kSubTiles record tiles of kBlock per block (fewer workgroups for the
     // light per-record passes over 1e9 records)
 #pragma unroll
     for (int q = 0; q < kSubTiles; ++q) {
         const uint64_t r64 = ((uint64_t)blockIdx.x * kSubTiles + q) * kBlock + threadIdx.x;
         if (r64 < W) wroot[r64] = kNone;
+        if (r64 < NW) kbits[r64] = 0u;   // the component-key bitmap (rank_roots)
         if (r64 >= R) continue;
         const uint32_t r = (uint32_t)r64;
         gmin[r] = kNone;
@@ -1090,21 +1092,37 @@ __global__ __launch_bounds__(kBlock) void roots_kernel(uint32_t R, const uint32_
 }
 
 // Single device: each component's key becomes its label — the rank of its
-// smallest core point id among all components (sklearn's numbering), from
-// the sorted (key, root) pairs.
-__global__ __launch_bounds__(kBlock) void root_keys_kernel(const uint32_t* __restrict__ root_list,
-                                                           uint32_t C,
+// smallest core point id among all components (sklearn's numbering).  The
+// keys are distinct point ids < n, so the rank is a bitmap population count:
+// mark each component's key in an n-bit map, scan the words' popcounts, and
+// a root's label is its word's prefix plus the bits below it in the word —
+// no sort, and the component count stays on the device (no host sync).
+__global__ __launch_bounds__(kBlock) void root_mark_kernel(const uint32_t* __restrict__ root_list,
+                                                           const uint32_t* __restrict__ count,
                                                            const uint32_t* __restrict__ gmin,
-                                                           uint32_t* __restrict__ keys) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i < C) keys[i] = gmin[root_list[i]];
+                                                           uint32_t* __restrict__ kbits) {
+    const uint32_t C = *count;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < C; i += gridDim.x * kBlock) {
+        const uint32_t g = gmin[root_list[i]];
+        atomicOr(kbits + (g >> 5), 1u << (g & 31));
+    }
 }
 
-__global__ __launch_bounds__(kBlock) void root_rank_kernel(const uint32_t* __restrict__ roots_sorted,
-                                                           uint32_t C, uint32_t* __restrict__ gmin) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i < C) gmin[roots_sorted[i]] = i;
+__global__ __launch_bounds__(kBlock) void root_rank_kernel(const uint32_t* __restrict__ root_list,
+                                                           const uint32_t* __restrict__ count,
+                                                           const uint32_t* __restrict__ kbits,
+                                                           const uint32_t* __restrict__ kpre,
+                                                           uint32_t* __restrict__ gmin) {
+    const uint32_t C = *count;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < C; i += gridDim.x * kBlock) {
+        const uint32_t r = root_list[i], g = gmin[r];
+        gmin[r] = kpre[g >> 5] + (uint32_t)__popc(kbits[g >> 5] & ((1u << (g & 31)) - 1u));
+    }
 }
+
+struct PopcOp {
+    __device__ uint32_t operator()(uint32_t w) const { return (uint32_t)__popc(w); }
+};
 
 // Sharded train, phase A exports: (global id, local component key) of every
 // core record whose point was also routed to another device.
@@ -1212,6 +1230,9 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
             const uint32_t pt = v & kIdMask;
             if (core_out && !core_mask) core_out[pt] = fl & 1;
             if (cnt_out) cnt_out[pt] = cnt_rec[r];
+            // (noise and unattached border points keep key_out's kNone fill:
+            // writing kNone here instead measured 1.67 -> 2.11 ms on C2, the
+            // extra scattered sectors cost more than the 55 us fill)
             if (key != kNone && key_out) key_out[pt] = key;
         }
         // the rest of the border candidates go to the sweep
@@ -2505,7 +2526,9 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     // rocPRIM's onesweep over (key, id) pairs, then a gather of the
     // coordinates into key order.  (Round 5 measured an MSD bucket sort that
     // carries the coordinate rows instead — slower: C2 8.76 vs 5.91 ms, C4
-    // 84 vs 64 ms; DESIGN.md §6, tools/msd_probe.hip.)
+    // 84 vs 64 ms; DESIGN.md §6, tools/msd_probe.hip.  Also measured: C4's
+    // 37-bit keys in four passes of 10-bit digits, 1024-thread blocks —
+    // sort 46.1 vs 40.6 ms, profiles/r05_v3_ab_sort_10bit.txt.)
     T* Xs = ctx.arena.get<T>("Xs", (size_t)R * Stride<D>::v);
     uint32_t* dup_list = ctx.arena.get<uint32_t>("dup_list", R);
     uint32_t* lcount = ctrs;   // dup, roots, core, border (zeroed by halo_tile_kernel)
@@ -2625,6 +2648,17 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         sst = ctx.arena.get<unsigned long long>("sweep_stats", 10);
         PD_HIP(hipMemsetAsync(sst, 0, sizeof(unsigned long long) * 10, s));
     }
+    // the auto window's cell count (link step 2) is copied back before the
+    // count sweep and waited for after it is queued: the host learns it while
+    // the sweep runs, and the window union launches with no gap
+    uint32_t* h_nc = nullptr;
+    hipEvent_t ev_nc = nullptr;
+    if (R && ctx.centre_window < 0) {
+        h_nc = (uint32_t*)pinned(ctx, sizeof(uint32_t));
+        PD_HIP(hipEventCreateWithFlags(&ev_nc, hipEventDisableTiming));
+        PD_HIP(hipMemcpyAsync(h_nc, dncells, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        PD_HIP(hipEventRecord(ev_nc, s));
+    }
     if (R) {
         const uint32_t rot = ctx.count_rotate ? (uint32_t)ctx.count_rotate : 0xFFFFFFFFu;
         if (sst)
@@ -2646,8 +2680,11 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     if (R) {
         // (1) forest from the count pass's two smallest neighbours
         uint32_t* wroot = ctx.arena.get<uint32_t>("word_root", W);
-        hipLaunchKernelGGL(init_kernel, dim3(sub_blocks(std::max<uint64_t>(R, W))), dim3(kBlock), 0,
-                           s, R, core, mn, 1, par, gmin, wroot, (uint64_t)W);
+        // (single device: the n-bit component-key map of rank_roots, zeroed here)
+        const uint64_t NW = a.phase == 0 ? (n + 31) / 32 : 0;
+        uint32_t* kbits = NW ? ctx.arena.get<uint32_t>("key_bits", NW) : nullptr;
+        hipLaunchKernelGGL(init_kernel, dim3(sub_blocks(std::max<uint64_t>(std::max<uint64_t>(R, W), NW))),
+                           dim3(kBlock), 0, s, R, core, mn, 1, par, gmin, wroot, (uint64_t)W, kbits, NW);
         // (2) window union.  Auto window (PD_OPT_CENTRE_WINDOW < 0): sparse
         // cells (a few records each, C2: 2.3) gain little from the window
         // beyond the fused flatten, so a short one is cheapest (C2 link 6.59
@@ -2655,10 +2692,9 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         // one (C4 link 71.5 -> 60.6 ms at 4 -> 16)
         int cw = ctx.centre_window;
         if (cw < 0) {
-            uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t));
-            PD_HIP(hipMemcpyAsync(h, dncells, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-            sync(s);
-            const uint32_t nc = *h ? *h : 1u;
+            PD_HIP(hipEventSynchronize(ev_nc));
+            (void)hipEventDestroy(ev_nc);
+            const uint32_t nc = *h_nc ? *h_nc : 1u;
             cw = (uint64_t)R <= 4ull * nc ? 4 : 16;
         }
         auto go = [&](auto Wc) {
@@ -2734,7 +2770,6 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
                            par);
     }
     tm.mark();   // 7
-    uint32_t n_roots = 0;
     if (R) {
         // single device: the components are listed so that their keys can be
         // ranked here (labels); sharded: keys stay global ids (merge first)
@@ -2742,27 +2777,32 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         // (gmin starts at kNone: init_kernel)
         hipLaunchKernelGGL(roots_kernel, dim3(sub_blocks(R)), dim3(kBlock), 0, s, R, vals, a.gid, par,
                            gmin, root_list, lcount + 1, ctx.sweep_stats ? 1 : 0);
-        uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t) * 4);
-        PD_HIP(hipMemcpyAsync(h, lcount + 1, sizeof(uint32_t) * 2, hipMemcpyDeviceToHost, s));
-        sync(s);
-        n_roots = a.phase == 0 ? h[0] : 0;
-        if (ctx.sweep_stats) ctx.t.core_records = h[1];
-        if (n_roots) {
-            uint32_t* rk = ctx.arena.get<uint32_t>("root_keys", n_roots);
-            uint32_t* rk2 = ctx.arena.get<uint32_t>("root_keys2", n_roots);
-            uint32_t* rl2 = ctx.arena.get<uint32_t>("root_list2", n_roots);
-            hipLaunchKernelGGL(root_keys_kernel, dim3(blocks(n_roots)), dim3(kBlock), 0, s,
-                               root_list, n_roots, gmin, rk);
-            rocprim::double_buffer<uint32_t> kb(rk, rk2), vb(root_list, rl2);
+        if (a.phase == 0) {
+            // rank the component keys on the device; the component count is
+            // read with the train's last copy back (finish)
+            const uint64_t NW = (n + 31) / 32;
+            uint32_t* kbits = ctx.arena.get<uint32_t>("key_bits", NW);
+            uint32_t* kpre = ctx.arena.get<uint32_t>("key_pre", NW);
+            const unsigned gb = std::min(blocks(R), 1024u);
+            hipLaunchKernelGGL(root_mark_kernel, dim3(gb), dim3(kBlock), 0, s, root_list, lcount + 1,
+                               gmin, kbits);
+            rocprim::transform_iterator<const uint32_t*, PopcOp, uint32_t> pc(kbits, PopcOp{});
             size_t tb = 0;
-            PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)n_roots, 0u, 32u, s));
-            void* tmp = ctx.arena.get<char>("root_sort_tmp", tb);
-            PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)n_roots, 0u, 32u, s));
-            hipLaunchKernelGGL(root_rank_kernel, dim3(blocks(n_roots)), dim3(kBlock), 0, s,
-                               vb.current(), n_roots, gmin);
+            PD_HIP(rocprim::exclusive_scan(nullptr, tb, pc, kpre, 0u, (size_t)NW,
+                                           rocprim::plus<uint32_t>(), s));
+            void* tmp = ctx.arena.get<char>("key_scan_tmp", tb);
+            PD_HIP(rocprim::exclusive_scan(tmp, tb, pc, kpre, 0u, (size_t)NW,
+                                           rocprim::plus<uint32_t>(), s));
+            hipLaunchKernelGGL(root_rank_kernel, dim3(gb), dim3(kBlock), 0, s, root_list, lcount + 1,
+                               kbits, kpre, gmin);
+        } else if (ctx.sweep_stats) {
+            uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t) * 4);
+            PD_HIP(hipMemcpyAsync(h, lcount + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+            sync(s);
+            ctx.t.core_records = h[0];
         }
     }
-    ctx.st.n_roots = n_roots;
+    ctx.st.n_roots = 0;   // single device: set by finish
     PD_HIP(hipGetLastError());
     tm.mark();   // 8
 
@@ -2845,13 +2885,13 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     const uint32_t core_mask =
         a.phase == 2 ? (ctx.shard_core_bit ? 0x80000000u : 0u) : kKeyCoreBit;
     const int core_bit = a.phase == 2 ? 0 : 1;
-    PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
     if (a.core && !core_mask) PD_HIP(hipMemsetAsync(a.core, 0, n, s));
     // single device, no counts wanted: labels reach input order through the
     // bucketed pair passes instead of owner_kernel's scatter
     // (ctx.label_buckets, PD_OPT_LABEL_BUCKETS)
     const bool want_buckets = ctx.label_buckets > 0 || (ctx.label_buckets < 0 && n >= (1ull << 28));
     const bool bucketed = a.phase != 2 && core_bit && !a.counts && want_buckets && n > 0;
+    PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
     if (R) {
         uint32_t* blist = ctx.arena.get<uint32_t>("border_list", R);
         const unsigned tiles = (unsigned)(((uint64_t)R + kOwnTile - 1) / kOwnTile);
@@ -2915,20 +2955,30 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
                            a.labels, a.core);
     PD_HIP(hipGetLastError());
     tm.mark();   // 10
-    a.n_clusters = st.n_roots;
 }
 
 // Host-side bookkeeping after phase A (and B): cell count, stage times.
 void finish(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     hipStream_t s = a.stream;
     if (a.phase != 2) {
-        uint32_t* hnc = (uint32_t*)pinned(ctx, sizeof(uint32_t));
-        *hnc = 0;
-        if (ctx.st.R)
+        // cell count, and (single device) the component count and core
+        // records (roots_kernel's counters): one copy back, one sync
+        uint32_t* hnc = (uint32_t*)pinned(ctx, 4 * sizeof(uint32_t));
+        hnc[0] = hnc[1] = hnc[2] = 0;
+        if (ctx.st.R) {
             PD_HIP(hipMemcpyAsync(hnc, ctx.arena.get<uint32_t>("ncells", 4), sizeof(uint32_t),
                                   hipMemcpyDeviceToHost, s));
+            if (a.phase == 0)
+                PD_HIP(hipMemcpyAsync(hnc + 1, ctx.arena.get<uint32_t>("train_ctrs", kCtrs) + 1,
+                                      2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        }
         sync(s);
-        ctx.t.cells_n = *hnc;
+        ctx.t.cells_n = hnc[0];
+        if (a.phase == 0) {
+            ctx.st.n_roots = hnc[1];
+            a.n_clusters = hnc[1];
+            if (ctx.sweep_stats) ctx.t.core_records = hnc[2];
+        }
         if (ctx.sweep_stats && ctx.st.R) {
             unsigned long long* hs = (unsigned long long*)pinned(ctx, 10 * sizeof(unsigned long long));
             PD_HIP(hipMemcpyAsync(hs, ctx.arena.get<unsigned long long>("sweep_stats", 10),

@@ -367,7 +367,9 @@ __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X
                         changed = true;
                     }
                 }
-                if (changed) store_labels4<true>(labels, ch, m, lab);
+                // (!LAB: every point starts in label 0 and every label is
+                // written — the caller's array need not be initialised)
+                if (changed || !LAB) store_labels4<true>(labels, ch, m, lab);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -805,8 +807,8 @@ __global__ __launch_bounds__(kBlock) void counts_reg_kernel(
          ch += (uint64_t)gridDim.x * kBlock) {
         T v[4][D];
         const int m = load_chunk<T, D, true>(X, n, ch, v);
-        int lab[4];
-        load_labels4<true>(labels, ch, m, lab);
+        int lab[4] = {0, 0, 0, 0};   // labels == nullptr: every point in label 0
+        if (labels) load_labels4<true>(labels, ch, m, lab);
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const int L = lab[p];
@@ -1546,7 +1548,10 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                         for (int g = 0; g < ng; ++g) (&sl.x)[g] = sel[g0 + g];
                         dispatch_ng(ng, [&](auto NGc) {
                             constexpr int NG = decltype(NGc)::value;
-                            if (g0 == 0)
+                            if (g0 == 0 && l == 1)   // labels all 0 so far: not read
+                                run_pass_dev<T, D, false, true, NG, false>(ctx, Xt, n, labels, sp, sl,
+                                                                           mom, s);
+                            else if (g0 == 0)
                                 run_pass_dev<T, D, true, true, NG, false>(ctx, Xt, n, labels, sp, sl,
                                                                           mom, s);
                             else
@@ -1564,7 +1569,7 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                     auto go = [&](auto NSc) {
                         constexpr int NS = decltype(NSc)::value;
                         hipLaunchKernelGGL((counts_reg_kernel<T, D, NS>), dim3(nb4), dim3(kBlock), 0,
-                                           s, Xt, (uint64_t)n, labels, lv[l].slot, ntab[l],
+                                           s, Xt, (uint64_t)n, l == 0 ? nullptr : labels, lv[l].slot, ntab[l],
                                            lv[l].axis, lv[l].bounds, S, dcnt);
                     };
                     if (S == 1)
@@ -1592,8 +1597,12 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                 const Lv& p = lv[n_levels - 1];
                 const SplitTab sp{p.slot, ntab[n_levels - 1], p.axis, p.boundary, p.newlab,
                                   sizes[n_levels - 1]};
-                run_pass_dev<T, D, true, true, 0, false>(ctx, Xt, n, labels, sp,
-                                                         make_int4(-2, -2, -2, -2), nullptr, s);
+                if (n_levels == 1)   // no level pass wrote the labels yet
+                    run_pass_dev<T, D, false, true, 0, false>(ctx, Xt, n, labels, sp,
+                                                              make_int4(-2, -2, -2, -2), nullptr, s);
+                else
+                    run_pass_dev<T, D, true, true, 0, false>(ctx, Xt, n, labels, sp,
+                                                             make_int4(-2, -2, -2, -2), nullptr, s);
             }
             // one copy back: the trace and the bbox
             double* ht = (double*)(h + off[n_levels]);

@@ -90,10 +90,11 @@ class _Neighborhood(object):
 
 
 class _Neighborhoods(dict):
-    def __init__(self, points, expanded):
+    def __init__(self, points, expanded, ebox=None):
         super().__init__()
         self.points = points
-        self._ebox = np.stack([expanded[L].as_array() for L in sorted(expanded)])
+        self._ebox = ebox if ebox is not None else \
+            np.array([expanded[L].as_array() for L in sorted(expanded)], np.float64)
         self._cache = None
         for L in sorted(expanded):
             self[L] = _Neighborhood(self, L)
@@ -318,12 +319,13 @@ class DBSCAN(object):
         self.bounding_boxes = parts.bounding_boxes
         self.expanded_boxes = {L: box.expand(2 * self.eps)
                                for L, box in sorted(parts.bounding_boxes.items())}
-        self.neighbors = _Neighborhoods(points, self.expanded_boxes)
+        ebox = np.array([self.expanded_boxes[L].as_array() for L in sorted(self.expanded_boxes)],
+                        np.float64)
+        self.neighbors = _Neighborhoods(points, self.expanded_boxes, ebox)
         # the reference's self.data after train: the per-partition records
         self.data = _PartitionRecords(self.neighbors, {'eps': self.eps,
                                                        'min_samples': self.min_samples,
                                                        'metric': self.metric})
-        ebox = np.stack([self.expanded_boxes[L].as_array() for L in sorted(self.expanded_boxes)])
         lo, hi = parts.data_box
         tree = parts.split_tree() if len(ebox) > 1 and points.d <= 4 else None
         if tree is not None:

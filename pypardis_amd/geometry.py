@@ -44,19 +44,28 @@ class BoundingBox(object):
         return BoundingBox(lower=np.minimum(self.lower, other.lower),
                            upper=np.maximum(self.upper, other.upper))
 
+    @classmethod
+    def _own(cls, lower, upper):
+        # fresh arrays the new box owns (no second copy; the train's host path
+        # builds a few dozen boxes per call)
+        b = cls.__new__(cls)
+        b.lower = lower
+        b.upper = upper
+        return b
+
     def split(self, dim, value):
         """R:dbscan/geometry.py:56-71: left keeps [lower, value], right [value, upper]."""
-        left_up = np.copy(self.upper)
+        left_up = self.upper.copy()
         left_up[dim] = value
-        right_lo = np.copy(self.lower)
+        right_lo = self.lower.copy()
         right_lo[dim] = value
-        return (BoundingBox(lower=np.copy(self.lower), upper=left_up),
-                BoundingBox(lower=right_lo, upper=np.copy(self.upper)))
+        return (BoundingBox._own(self.lower.copy(), left_up),
+                BoundingBox._own(right_lo, self.upper.copy()))
 
     def expand(self, eps=0, how='add'):
         """R:dbscan/geometry.py:73-87 ('add' grows by eps, 'multiply' by eps·span)."""
         if how == 'add':
-            return BoundingBox(self.lower - eps, self.upper + eps)
+            return BoundingBox._own(self.lower - eps, self.upper + eps)
         if how == 'multiply':
             span = self.upper - self.lower
             return BoundingBox(self.lower - eps * span, self.upper + eps * span)
@@ -68,7 +77,7 @@ class BoundingBox(object):
 
     def as_array(self):
         """(2, k) fp64 [lower; upper] — the layout the C ABI takes."""
-        return np.stack([np.asarray(self.lower, np.float64), np.asarray(self.upper, np.float64)])
+        return np.array((self.lower, self.upper), np.float64)
 
     def __eq__(self, other):
         return (isinstance(other, BoundingBox) and np.array_equal(self.lower, other.lower)

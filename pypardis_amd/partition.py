@@ -287,13 +287,16 @@ class KDPartitioner(object):
             # astronomically large in high dimension; it would never finish
             raise ValueError(f"max_partitions={self.max_partitions} (> 65536; the default is "
                              "4**k): pass max_partitions explicitly")
-        self._labels = torch.zeros(self.points.n, dtype=torch.int32, device=X.device)
         self._pending = None    # the last level's split, applied on first use
         self._tree = None       # (sizes, cur, axis, boundary, new): pd_train_tree
         levels = _split_schedule(self.max_partitions)
+        device_kd = bool(levels) and self._fused() and DEVICE_DECISIONS
+        # pd_kd_build writes every label from its second level on (no fill)
+        self._labels = (torch.empty if device_kd and len(levels) >= 2 else torch.zeros)(
+            self.points.n, dtype=torch.int32, device=X.device)
         first = None
         trace = None
-        if levels and self._fused() and DEVICE_DECISIONS:
+        if device_kd:
             # the whole BFS in one launch chain (pd_kd_build): the level
             # decisions run on the device, bit-identical to the host's
             try:
@@ -302,6 +305,7 @@ class KDPartitioner(object):
             except _native.PardisError as e:
                 if e.code != _native.PD_EUNSUPPORTED:
                     raise
+                self._labels.zero_()   # the host-level passes start from label 0
         if trace is not None:
             if bad:
                 raise ValueError("Input contains NaN or infinity.")

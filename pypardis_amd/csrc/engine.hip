@@ -581,6 +581,8 @@ __device__ __forceinline__ K key_of(const T (&tv)[D], const KeyGrid<D>& g) {
 // deterministic.  Each point's first record (its lowest neighbourhood) is
 // computed for all lanes at once and stored after the loop, so one step's
 // stores are contiguous; the extra records of the few halo duplicates follow.
+// (92 VGPRs, 5 waves/SIMD: capping it at 6 or 8 waves measured slower — C2
+// halo 1.29 / 1.81 vs 1.22 ms, the cap spills the per-point state)
 template <typename T, int D, typename K, bool MASK>
 __global__ __launch_bounds__(kBlock) void halo_write_kernel(
     const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,

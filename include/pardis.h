@@ -185,6 +185,15 @@ int32_t pd_kd_radix_hist(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, i
                          const int32_t* axis_host, const uint64_t* prefix_host, int32_t shift,
                          int64_t* hist_host, void* stream);
 
+/* The record sort of pd_train on caller arrays (utility; exposed so the
+ * kernel can be tested on its own): stable LSD radix sort of n (key, value)
+ * pairs by key bits [0, key_bits), in place.  keys: device uint32 (key_bytes
+ * 4) or uint64 (8); vals: device uint32.  n < 2^32 - 1.  It is the shuffle
+ * by neighbourhood that R:dbscan/dbscan.py:116-118 (partitionBy) performs,
+ * keyed by (neighbourhood, cell). */
+int32_t pd_sort_pairs(pd_ctx* ctx, void* keys, int32_t key_bytes, uint32_t* vals, int64_t n,
+                      int32_t key_bits, void* stream);
+
 /* ebox_host: P x [lo[d], hi[d]] (inclusive).  counts_host[P] = members per
  * box; if members != NULL it receives the ascending point ids of box 0, then
  * box 1, ... (capacity entries at most). */

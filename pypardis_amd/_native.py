@@ -44,7 +44,7 @@ EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
            "pd_ctx_set_option", "pd_ctx_timings", "pd_bbox", "pd_kd_moments", "pd_kd_counts",
            "pd_kd_split", "pd_halo_members", "pd_cluster", "pd_train", "pd_kd_moments_dd",
            "pd_route", "pd_pack", "pd_train_begin", "pd_train_exports", "pd_merge_exports",
-           "pd_train_end", "pd_select_roots", "pd_sort_u32", "pd_rank_labels",
+           "pd_train_end", "pd_select_roots", "pd_sort_pairs", "pd_sort_u32", "pd_rank_labels",
            "pd_kd_radix_hist", "pd_kd_pass", "pd_owned_results", "pd_scatter_results",
            "pd_comm_unique_id", "pd_comm_init", "pd_comm_init_all", "pd_comm_destroy",
            "pd_comm_all_reduce", "pd_comm_all_gather_v", "pd_comm_all_to_all_v",
@@ -105,6 +105,7 @@ def load():
             "pd_train_end": ([P, I64, P, P, I64, P, P, P], I32),
             "pd_select_roots": ([P, P, P, I64, P, P, P], I32),
             "pd_sort_u32": ([P, P, I64, P], I32),
+            "pd_sort_pairs": ([P, P, I32, P, I64, I32, P], I32),
             "pd_rank_labels": ([P, P, I64, P, I64, P, P], I32),
             "pd_kd_radix_hist": ([P, P, I32, I64, I32, P, I32, P, P, P, I32, P, P], I32),
             "pd_kd_pass": ([P, P, I32, I64, I32, P, I32, I32, P, P, P, P, I32, P, P, P, P, P],
@@ -713,6 +714,20 @@ def sort_u32(data, ctx=None):
     n = data.shape[0]
     _check(load().pd_sort_u32(ctx.ptr, data.data_ptr() if n else None, n, _stream(data.device)))
     return data
+
+
+def sort_pairs(keys, vals, key_bits, ctx=None):
+    """pd_sort_pairs: stable in-place sort of (keys, vals) by key bits [0,
+    key_bits) — the train's record sort.  keys: int32 / int64 device tensor
+    (unsigned order), vals: int32 device tensor of the same length."""
+    ctx = ctx or context(keys.device.index)
+    n = keys.shape[0]
+    if vals.shape[0] != n or vals.dtype != torch.int32 or keys.dtype not in (torch.int32, torch.int64):
+        raise TypeError("keys int32/int64 and vals int32 of one length")
+    _check(load().pd_sort_pairs(ctx.ptr, keys.data_ptr() if n else None, keys.element_size(),
+                                vals.data_ptr() if n else None, n, int(key_bits),
+                                _stream(keys.device)))
+    return keys, vals
 
 
 def rank_labels(keys, roots, ctx=None):

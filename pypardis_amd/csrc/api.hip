@@ -276,6 +276,18 @@ int32_t pd_kd_radix_hist(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, i
     });
 }
 
+int32_t pd_sort_pairs(pd_ctx* ctx, void* keys, int32_t key_bytes, uint32_t* vals, int64_t n,
+                      int32_t key_bits, void* stream) {
+    return guard(ctx, [&] {
+        if (!ctx || n < 0 || (n && (!keys || !vals))) throw Error(PD_EINVAL, "bad arrays");
+        if (key_bytes != 4 && key_bytes != 8) throw Error(PD_EINVAL, "key_bytes must be 4 or 8");
+        if (key_bits < 1 || key_bits > 8 * key_bytes) throw Error(PD_EINVAL, "bad key_bits");
+        if (n >= 0xFFFFFFFFll) throw Error(PD_EINVAL, "n >= 2^32 - 1");
+        sort_pairs_inplace(ctx->c, keys, key_bytes, vals, (uint64_t)n, key_bits,
+                           (hipStream_t)stream);
+    });
+}
+
 int32_t pd_halo_members(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
                         int32_t P, const double* ebox, int64_t* counts, int64_t* members,
                         int64_t capacity, void* stream) {

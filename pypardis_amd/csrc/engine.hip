@@ -34,6 +34,9 @@
 // not merely equal up to permutation.
 #include <cstring>
 #include <rocprim/rocprim.hpp>
+#ifndef PD_SORT_ROCPRIM
+#define PD_SORT_ROCPRIM 0
+#endif
 
 #include <algorithm>
 #include <type_traits>
@@ -43,6 +46,7 @@
 
 #include "compact.hpp"
 #include "internal.hpp"
+#include "rsort.hpp"
 #include "scan.hpp"
 #include "stream.hpp"
 #include "uf.hpp"
@@ -530,11 +534,16 @@ template <typename T, int D>
 __global__ __launch_bounds__(kBlock) void halo_tile_kernel(const T* __restrict__ X, uint64_t n,
                                                            const PartGrid* __restrict__ parts,
                                                            int P, uint32_t* __restrict__ tile_cnt,
-                                                           uint32_t* __restrict__ ctrs) {
+                                                           uint32_t* __restrict__ ctrs,
+                                                           uint32_t* __restrict__ sort_hist) {
     // the train's small counters (dup / root / core / border lists, big and
-    // mid cells, cell pairs): zeroed here, the first kernel of the train,
-    // instead of by fills
-    if (blockIdx.x == 0 && threadIdx.x < kCtrs) ctrs[threadIdx.x] = 0;
+    // mid cells, cell pairs) and the record sort's digit histograms: zeroed
+    // here, the first kernel of the train, instead of by fills
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < kCtrs) ctrs[threadIdx.x] = 0;
+        if (sort_hist)
+            for (int i = threadIdx.x; i < 8 * rsort::kRadix; i += kBlock) sort_hist[i] = 0;
+    }
     uint64_t idx[4];
     T v[4][D];
     unsigned long long m[4];
@@ -2424,6 +2433,56 @@ void launch_border(hipStream_t s, const T* Xs, uint32_t NL, const uint32_t* list
                        list, C, eps, eps2, lo, hi, vals, par, gmin, key_out, rec_out);
 }
 
+// The record sort: the library's onesweep (rsort.hpp), stable, bits [0,
+// key_bits).  Its look-back words and ticket live in the arena and are
+// zeroed only when (re)allocated.  (PD_SORT_ROCPRIM=1 builds rocPRIM's
+// radix_sort_pairs instead, for A/B runs.)
+template <typename K>
+void sort_records(Ctx& ctx, K*& keys, uint32_t*& vals, K* keys2, uint32_t* vals2, uint64_t R,
+                  int key_bits, hipStream_t s, bool hist_zeroed = true) {
+#if PD_SORT_ROCPRIM
+    rocprim::double_buffer<K> kb(keys, keys2);
+    rocprim::double_buffer<uint32_t> vb(vals, vals2);
+    size_t tb = 0;
+    PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
+    void* tmp = ctx.arena.get<char>("sort_tmp", tb);
+    PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
+    keys = kb.current();
+    vals = vb.current();
+#else
+    const uint64_t tiles = rsort::tiles_for(R, (int)sizeof(K));
+    const uint64_t want = std::max<uint64_t>(tiles, ctx.rs_look_tiles);
+    uint64_t* look = ctx.arena.get<uint64_t>("rsort_look", want * rsort::kRadix);
+    if (look != ctx.rs_look || want > ctx.rs_look_tiles) {   // new words: zero them once
+        PD_HIP(hipMemsetAsync(look, 0, sizeof(uint64_t) * rsort::kRadix * want, s));
+        ctx.rs_look = look;
+        ctx.rs_look_tiles = want;
+        ctx.rs_epoch = 0;
+    }
+    unsigned long long* ticket = ctx.arena.get<unsigned long long>("rsort_ticket", 1);
+    if (ticket != ctx.rs_ticket) {
+        PD_HIP(hipMemsetAsync(ticket, 0, sizeof(unsigned long long), s));
+        ctx.rs_ticket = ticket;
+        ctx.rs_tick = 0;
+    }
+    rsort::State st;
+    st.look = look;
+    st.look_tiles = ctx.rs_look_tiles;
+    st.hist = ctx.arena.get<uint32_t>("rsort_hist", 8 * rsort::kRadix);
+    st.ticket = ticket;
+    st.epoch = ctx.rs_epoch;
+    st.tick = ctx.rs_tick;
+    K* ko;
+    uint32_t* vo;
+    // (st.hist zeroed by halo_tile_kernel in the train)
+    rsort::sort_pairs<K>(st, keys, vals, keys2, vals2, R, key_bits, s, &ko, &vo, hist_zeroed);
+    ctx.rs_epoch = st.epoch;
+    ctx.rs_tick = st.tick;
+    keys = ko;
+    vals = vo;
+#endif
+}
+
 // Ordered compaction of record ids satisfying `pred` (keeps the spatial
 // order, so a wave's records stay neighbours).  Returns the count (syncs).
 template <typename Pred>
@@ -2457,8 +2516,9 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     uint32_t* tcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)htiles + 1);
     uint64_t* toff = ctx.arena.get<uint64_t>("tile_off", (size_t)htiles + 1);
     uint32_t* ctrs = ctx.arena.get<uint32_t>("train_ctrs", kCtrs);
+    uint32_t* sort_hist = PD_SORT_ROCPRIM ? nullptr : ctx.arena.get<uint32_t>("rsort_hist", 8 * rsort::kRadix);
     hipLaunchKernelGGL((halo_tile_kernel<T, D>), dim3(htiles), dim3(kBlock), 0, s, X, n, parts, P,
-                       tcnt, ctrs);
+                       tcnt, ctrs, sort_hist);
     const uint64_t R64 = tile_offsets(ctx, tcnt, htiles, toff, s, true);
     if (R64 >= 0xFFFFFFFEull) throw Error(-5, "more than 2^32-2 halo records on one device");
     const uint32_t R = (uint32_t)R64;
@@ -2525,7 +2585,8 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     tm.mark();   // 1
 
     // ---- shuffle by neighbourhood == sort by (neighbourhood, cell) key:
-    // rocPRIM's onesweep over (key, id) pairs, then a gather of the
+    // the library's onesweep (rsort.hpp: stable, one kernel per 8-bit digit,
+    // C2 2.6 vs rocPRIM's 3.0 ms) over (key, id) pairs, then a gather of the
     // coordinates into key order.  (Round 5 measured an MSD bucket sort that
     // carries the coordinate rows instead — slower: C2 8.76 vs 5.91 ms, C4
     // 84 vs 64 ms; DESIGN.md §6, tools/msd_probe.hip.  Also measured: C4's
@@ -2537,16 +2598,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     // the merge's representative per point, initialised for the points of the
     // duplicated records only (by the gather, which lists them), not a fill over n
     uint32_t* rep = P > 1 ? ctx.arena.get<uint32_t>("rep", n) : nullptr;
-    {
-        rocprim::double_buffer<K> kb(keys, keys2);
-        rocprim::double_buffer<uint32_t> vb(vals, vals2);
-        size_t tb = 0;
-        PD_HIP(rocprim::radix_sort_pairs(nullptr, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
-        void* tmp = ctx.arena.get<char>("sort_tmp", tb);
-        PD_HIP(rocprim::radix_sort_pairs(tmp, tb, kb, vb, (size_t)R, 0u, (unsigned)key_bits, s));
-        keys = kb.current();
-        vals = vb.current();
-    }
+    sort_records<K>(ctx, keys, vals, keys2, vals2, (uint64_t)R, key_bits, s);
     tm.mark();   // 2
     hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X, (uint64_t)R,
                        vals, Xs, dup_list, lcount, rep);
@@ -3067,6 +3119,30 @@ void run_d(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& p, uint64_t G, i
 }
 
 }  // namespace
+
+// pd_sort_pairs: the record sort on caller arrays (in place, stable).
+void sort_pairs_inplace(Ctx& ctx, void* keys, int key_bytes, uint32_t* vals, uint64_t n,
+                        int key_bits, hipStream_t s) {
+    if (n == 0) return;
+    auto go = [&](auto* k) {
+        using K = std::remove_pointer_t<decltype(k)>;
+        K* kk = k;
+        uint32_t* vv = vals;
+        K* k2 = ctx.arena.get<K>("usort_keys2", n);
+        uint32_t* v2 = ctx.arena.get<uint32_t>("usort_vals2", n);
+        sort_records<K>(ctx, kk, vv, k2, v2, n, key_bits, s, false);
+        if (kk != k) {
+            PD_HIP(hipMemcpyAsync(k, kk, sizeof(K) * n, hipMemcpyDeviceToDevice, s));
+            PD_HIP(hipMemcpyAsync(vals, vv, sizeof(uint32_t) * n, hipMemcpyDeviceToDevice, s));
+        }
+    };
+    if (key_bytes == 4)
+        go((uint32_t*)keys);
+    else
+        go((uint64_t*)keys);
+    PD_HIP(hipGetLastError());
+}
+
 
 // Labels from cluster keys (key[i] = smallest core point id of i's cluster,
 // 0xFFFFFFFF noise): a key's rank among the cluster roots (points whose key

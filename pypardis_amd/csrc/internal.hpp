@@ -154,6 +154,13 @@ struct Ctx {
                                  // < 0 (default): 4 or 16 by cell occupancy
     int count_rotate = 1024;     // count sweep: lists longer than this start near the query (0: off)
     int count_replay = 0;        // PD_OPT_COUNT_REPLAY: replicas of the count sweep to time (0: off)
+    // the record sort's look-back state (rsort.hpp): words zeroed when
+    // allocated, a 64-bit ticket counter, the host's epoch / ticket copies
+    uint64_t* rs_look = nullptr;
+    uint64_t rs_look_tiles = 0;
+    unsigned long long* rs_ticket = nullptr;
+    uint32_t rs_epoch = 0;
+    unsigned long long rs_tick = 0;
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
     int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow
@@ -339,6 +346,8 @@ void halo_members(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int P,
                   int64_t members_cap, hipStream_t s);
 
 // small helpers (api.hip)
+void sort_pairs_inplace(Ctx& ctx, void* keys, int key_bytes, uint32_t* vals, uint64_t n,
+                        int key_bits, hipStream_t s);
 void* pinned(Ctx& ctx, size_t bytes);
 void sync(hipStream_t s);
 

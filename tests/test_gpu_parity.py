@@ -314,6 +314,39 @@ def test_retired_options_raise(native):
             ctx.set_option(opt, 1)
 
 
+@pytest.mark.parametrize("key_bytes,bits,n", [
+    (4, 32, 0), (4, 32, 1), (4, 8, 5), (4, 1, 8191), (4, 9, 8192), (4, 32, 8193),
+    (4, 7, 1_000_003), (4, 32, 3_000_001), (8, 37, 1), (8, 37, 6145), (8, 64, 200_003),
+    (8, 37, 2_000_000)])
+def test_record_sort_is_stable_and_exact(native, key_bytes, bits, n):
+    """The train's record sort (rsort.hpp, pd_sort_pairs) against numpy's
+    stable argsort: tiles of 8192 / 6144 items, partial last tiles, one-pass
+    and multi-pass key widths, heavy duplicate keys (stability), 64-bit keys."""
+    rng = np.random.default_rng(n + bits)
+    if key_bytes == 4:
+        hi = (1 << bits) - 1
+        if n % 2:   # 1024 distinct keys spread over the key range: long equal runs
+            k = (rng.integers(0, 1024, n, dtype=np.uint64) * np.uint64(max(1, hi // 1023))) & np.uint64(hi)
+        else:
+            k = rng.integers(0, hi + 1, n, dtype=np.uint64)
+        k = k.astype(np.uint32)
+        kt = torch.from_numpy(k.view(np.int32)).cuda()
+    else:
+        k = rng.integers(0, 1 << min(bits, 63), n, dtype=np.uint64)
+        if bits == 64:
+            k |= (rng.integers(0, 2, n, dtype=np.uint64) << np.uint64(63))
+        k[: n // 3] = k[0] if n else k[: n // 3]   # a run of equal keys
+        kt = torch.from_numpy(k.view(np.int64)).cuda()
+    v = np.arange(n, dtype=np.uint32)[::-1].copy()
+    vt = torch.from_numpy(v.view(np.int32)).cuda()
+    native.sort_pairs(kt, vt, bits)
+    order = np.argsort(k, kind="stable")
+    got_k = kt.cpu().numpy().view(np.uint32 if key_bytes == 4 else np.uint64)
+    got_v = vt.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got_k, k[order])
+    assert np.array_equal(got_v, v[order])
+
+
 def test_fp64_input_exact(native):
     from pypardis_amd import synth
     X = synth.blobs_noise(40_000, 2, side=10.0, n_centers=5, sigma=0.3, seed=31).astype(np.float64)

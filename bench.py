@@ -228,7 +228,7 @@ def cpu_baseline(cfg_name, n_sample, n_full, d):
     return out
 
 
-def grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages):
+def grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages, cfg_name="C2"):
     alg_bytes, per = b_nc(rec, cells, d)
     if not t_cnt > 0:   # no kernel time recorded (never expected): no rate, no crash
         t_cnt = 1e30
@@ -270,7 +270,12 @@ def grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages):
             "candidate_tests_per_s": cand / (t_cnt * 1e-3),
             "records_per_s": rec / (t_cnt * 1e-3)}
         ceil, ceil_src = load_ceiling()
-        if ceil and ceil.get("ceiling_candidate_tests_per_s"):
+        if cfg_name != "C2":
+            # the ceiling is the C2 sweep's (its candidate lists and cell
+            # occupancy); other configs' sweeps are not comparable to it
+            roof["latency_frac"] = None
+            roof["latency_note"] = "the latency ceiling is measured on C2 slices only"
+        elif ceil and ceil.get("ceiling_candidate_tests_per_s"):
             # the same kernel with every load of its chain an L2 hit
             roof["latency_frac"] = (cand / (t_cnt * 1e-3)) / ceil["ceiling_candidate_tests_per_s"]
             roof["latency_ceiling"] = {
@@ -589,7 +594,8 @@ def main():
         pmc, pmc_src = load_pmc(args.config)
         stage_roof = None
         if d <= 4:
-            roof, stage_roof = grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages)
+            roof, stage_roof = grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages,
+                                             args.config)
             dtype = f"{'f32' if Xd.dtype == torch.float32 else 'f64'} coords, f64 predicate"
         else:
             roof = dense_roofline(n, d, t_cnt, cells, pmc, pmc_src, refined=gcells,

@@ -75,8 +75,8 @@ enum pd_option {
                                 wraps (dense cells: spreads the row-start hot spot; same
                                 counts, same labels); default 1024, 0 = never */,
     PD_OPT_CENTRE_WINDOW = 13 /* link stage: records after each record tested by the window union
-                                (2, 4, 8, 16, 32 or 64).  Default -1: 4 when cells hold <= 4
-                                records on average, else 16.  A heuristic either way: the cell
+                                (2, 4, 8, 16, 32 or 64).  Default -1: by the records per
+                                occupied cell — 2 up to 2.5, 8 up to 8, else 16.  A heuristic either way: the cell
                                 verify proves or tests every core-core edge, so labels are the
                                 same */,
     PD_OPT_DIR_BUDGET = 14    /* bytes the eps-grid directory may take (flat: 20 B per 64 cells;

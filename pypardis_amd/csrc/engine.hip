@@ -2742,14 +2742,19 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         // (2) window union.  Auto window (PD_OPT_CENTRE_WINDOW < 0): sparse
         // cells (a few records each, C2: 2.3) gain little from the window
         // beyond the fused flatten, so a short one is cheapest (C2 link 6.59
-        // -> 5.96 ms at 16 -> 4); dense cells (C4 city centres) want the long
-        // one (C4 link 71.5 -> 60.6 ms at 4 -> 16)
+        // -> 5.96 ms at 16 -> 4; round 5: 5.45 / 5.33 / 5.42 ms at 4 / 2 / 1,
+        // and 56 ms with the flatten alone); dense cells (C4 city centres)
+        // want the long one (C4 link 71.5 -> 60.6 ms at 4 -> 16)
         int cw = ctx.centre_window;
         if (cw < 0) {
             PD_HIP(hipEventSynchronize(ev_nc));
             (void)hipEventDestroy(ev_nc);
             const uint32_t nc = *h_nc ? *h_nc : 1u;
-            cw = (uint64_t)R <= 4ull * nc ? 4 : 16;
+            // records per occupied cell: <= 2.5 -> 2 (C2: 2.32), <= 8 -> 8
+            // (C4: 2.96, dense cities in sparse noise: link 37.1 / 32.2 /
+            // 56.3 / 142.9 ms at 4 / 8 / 16 / 32; C1: 4.96, 0.58 / 0.60 /
+            // 0.61 ms at 4 / 8 / 16), else 16
+            cw = 2 * (uint64_t)R <= 5ull * nc ? 2 : ((uint64_t)R <= 8ull * nc ? 8 : 16);
         }
         auto go = [&](auto Wc) {
             constexpr int Wv = decltype(Wc)::value;

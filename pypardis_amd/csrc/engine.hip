@@ -2459,25 +2459,17 @@ void sort_records(Ctx& ctx, K*& keys, uint32_t*& vals, K* keys2, uint32_t* vals2
         ctx.rs_look_tiles = want;
         ctx.rs_epoch = 0;
     }
-    unsigned long long* ticket = ctx.arena.get<unsigned long long>("rsort_ticket", 1);
-    if (ticket != ctx.rs_ticket) {
-        PD_HIP(hipMemsetAsync(ticket, 0, sizeof(unsigned long long), s));
-        ctx.rs_ticket = ticket;
-        ctx.rs_tick = 0;
-    }
     rsort::State st;
     st.look = look;
     st.look_tiles = ctx.rs_look_tiles;
     st.hist = ctx.arena.get<uint32_t>("rsort_hist", 8 * rsort::kRadix);
-    st.ticket = ticket;
+    st.ticket = ctx.arena.get<unsigned long long>("rsort_ticket", 1);   // (restarted per sort)
     st.epoch = ctx.rs_epoch;
-    st.tick = ctx.rs_tick;
     K* ko;
     uint32_t* vo;
     // (st.hist zeroed by halo_tile_kernel in the train)
     rsort::sort_pairs<K>(st, keys, vals, keys2, vals2, R, key_bits, s, &ko, &vo, hist_zeroed);
     ctx.rs_epoch = st.epoch;
-    ctx.rs_tick = st.tick;
     keys = ko;
     vals = vo;
 #endif

@@ -154,13 +154,11 @@ struct Ctx {
                                  // < 0 (default): 4 or 16 by cell occupancy
     int count_rotate = 1024;     // count sweep: lists longer than this start near the query (0: off)
     int count_replay = 0;        // PD_OPT_COUNT_REPLAY: replicas of the count sweep to time (0: off)
-    // the record sort's look-back state (rsort.hpp): words zeroed when
-    // allocated, a 64-bit ticket counter, the host's epoch / ticket copies
+    // the record sort's look-back words (rsort.hpp): zeroed when allocated,
+    // then tagged with the pass epoch kept here
     uint64_t* rs_look = nullptr;
     uint64_t rs_look_tiles = 0;
-    unsigned long long* rs_ticket = nullptr;
     uint32_t rs_epoch = 0;
-    unsigned long long rs_tick = 0;
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
     int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow

@@ -23,15 +23,18 @@
 namespace pd {
 namespace rsort {
 
-constexpr int kThreads = 256;   // 4 waves
+constexpr int kThreads = 256;   // histogram kernels
 constexpr int kRadix = 256;
 
 template <typename K>
 struct Tile {
-    // items per thread: 32 (u32 keys: 8192-item tiles, 72 KB of LDS, 2 blocks
-    // per CU; 24: 2.96, 16: 3.18 vs 2.57 ms for 1e8 pairs) or 24 (u64 keys:
-    // 6144-item tiles, 78 KB; 16: 9.9 vs 8.1 ms for 2e8 37-bit pairs)
-    static constexpr int kItems = sizeof(K) == 4 ? 32 : 24;
+    // u32 keys: 512 threads x 16 items (8192-item tiles, 72 KB of LDS, 2
+    // blocks per CU): 2.40 ms for 1e8 pairs (256 x 32: 2.57, 1024 x 12:
+    // 2.58, 256 x 16: 3.18; rocPRIM 3.02).  u64 keys: 256 x 24 (6144-item
+    // tiles, 78 KB): 7.76 ms for 2e8 37-bit pairs (1024 x 8: 8.24, 512 x
+    // 12: 9.96; rocPRIM 8.25).  tools/sort_probe.hip
+    static constexpr int kThreads = sizeof(K) == 4 ? 512 : 256;
+    static constexpr int kItems = sizeof(K) == 4 ? 16 : 24;
     static constexpr int kSize = kThreads * kItems;
 };
 template <typename K>
@@ -63,10 +66,13 @@ __global__ __launch_bounds__(kThreads) void hist_kernel(const K* __restrict__ ke
     }
 }
 
-// hist (places x 256) -> exclusive digit offsets per place, in place.
-__global__ __launch_bounds__(kRadix) void hist_scan_kernel(uint32_t* __restrict__ hist, int places) {
+// hist (places x 256) -> exclusive digit offsets per place, in place; also
+// starts the sort's tile ticket at 0 (pass p's tiles take p * tiles ..).
+__global__ __launch_bounds__(kRadix) void hist_scan_kernel(uint32_t* __restrict__ hist, int places,
+                                                           unsigned long long* __restrict__ ticket) {
     __shared__ uint32_t ws[kRadix / 64];
     const int d = threadIdx.x, lane = d & 63, w = d >> 6;
+    if (d == 0) *ticket = 0ull;
     for (int p = 0; p < places; ++p) {
         const uint32_t v = hist[p * kRadix + d];
         uint32_t x = v;
@@ -100,23 +106,26 @@ __device__ __forceinline__ void st_lb(uint64_t* p, uint64_t v) {
 // offsets; look: ntiles x 256 look-back words (tag << 32 | count; tag =
 // 2 epoch + 1 aggregate of the tile alone, 2 epoch + 2 inclusive of all tiles
 // up to it; older tags read as not yet published); ticket: 64-bit counter,
-// tile = atomicAdd(ticket, 1) - tick0.
-template <typename K, int I = Tile<K>::kItems>
-__global__ __launch_bounds__(kThreads) void pass_kernel(const K* __restrict__ kin,
-                                                        const uint32_t* __restrict__ vin,
-                                                        K* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                        uint64_t n, int shift,
-                                                        const uint32_t* __restrict__ goff,
-                                                        uint64_t* __restrict__ look, uint32_t epoch,
-                                                        unsigned long long* __restrict__ ticket,
-                                                        unsigned long long tick0) {
-    constexpr int T = kThreads * I, NW = kThreads / 64;
+// tile = atomicAdd(ticket, 1) - tick0 (the sort's p-th pass: tick0 = p tiles).
+template <typename K, int I = Tile<K>::kItems, int NT = Tile<K>::kThreads>
+__global__ __launch_bounds__(NT) void pass_kernel(const K* __restrict__ kin,
+                                                  const uint32_t* __restrict__ vin,
+                                                  K* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                  uint64_t n, int shift,
+                                                  const uint32_t* __restrict__ goff,
+                                                  uint64_t* __restrict__ look, uint32_t epoch,
+                                                  unsigned long long* __restrict__ ticket,
+                                                  unsigned long long tick0) {
+    // NT threads (NT / 64 waves) rank the tile; the first 256 also carry one
+    // digit each through the count / scan / look-back phase
+    constexpr int T = NT * I, NW = NT / 64;
+    static_assert(NT >= kRadix && NT % 64 == 0, "one thread per digit");
     __shared__ K sk[T];
     __shared__ uint32_t sv[T];
     __shared__ uint32_t wcnt[NW][kRadix];
     __shared__ uint32_t dbase[kRadix];
     __shared__ uint32_t gbase[kRadix];
-    __shared__ uint32_t ws[NW];
+    __shared__ uint32_t ws[kRadix / 64];
     __shared__ uint32_t s_tile;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tick0);
@@ -154,49 +163,55 @@ __global__ __launch_bounds__(kThreads) void pass_kernel(const K* __restrict__ ki
         if (ok && (m & lt) == 0) wcnt[w][d] = base + (uint32_t)__popcll(m);
     }
     __syncthreads();
+    const bool dig = tid < kRadix;
+    const int d = tid & (kRadix - 1);
     // per digit: the tile's count, the waves' exclusive prefixes (in place)
-    const int d = tid;
     uint32_t h = 0;
-#pragma unroll
-    for (int u = 0; u < NW; ++u) {
-        const uint32_t c = wcnt[u][d];
-        wcnt[u][d] = h;
-        h += c;
-    }
-    // publish the tile's own count first (tile 0: already inclusive)
     uint64_t* lk = look + (uint64_t)tile * kRadix + d;
     const uint64_t agg_tag = (uint64_t)(2u * epoch + 1u) << 32, inc_tag = (uint64_t)(2u * epoch + 2u) << 32;
-    st_lb(lk, (tile == 0 ? inc_tag : agg_tag) | h);
-    // tile-local exclusive digit starts
-    {
-        uint32_t x = h;
+    uint32_t x = 0;
+    if (dig) {
+#pragma unroll
+        for (int u = 0; u < NW; ++u) {
+            const uint32_t c = wcnt[u][d];
+            wcnt[u][d] = h;
+            h += c;
+        }
+        // publish the tile's own count first (tile 0: already inclusive)
+        st_lb(lk, (tile == 0 ? inc_tag : agg_tag) | h);
+        // tile-local exclusive digit starts
+        x = h;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
             if (lane >= o) x += y;
         }
         if (lane == 63) ws[w] = x;
-        __syncthreads();
+    }
+    __syncthreads();
+    if (dig) {
         uint32_t before = 0;
 #pragma unroll
-        for (int u = 0; u < NW; ++u) before += u < w ? ws[u] : 0u;
+        for (int u = 0; u < kRadix / 64; ++u) before += u < w ? ws[u] : 0u;
         dbase[d] = before + x - h;
-    }
-    // look back: items of digit d in the tiles before this one
-    uint32_t excl = 0;
-    if (tile > 0) {
-        int64_t t = (int64_t)tile - 1;
-        while (t >= 0) {
-            const uint64_t s = ld_lb(look + (uint64_t)t * kRadix + d);
-            const uint32_t tag = (uint32_t)(s >> 32);
-            if (tag < 2u * epoch + 1u) continue;   // not published yet: spin
-            excl += (uint32_t)s;
-            if (tag == 2u * epoch + 2u) break;
-            --t;
+        // look back: items of digit d in the tiles before this one (one
+        // dependent load per step; reading 8 words per step measured the
+        // same, 2.57 ms for 1e8 pairs: the walk is short)
+        uint32_t excl = 0;
+        if (tile > 0) {
+            int64_t t = (int64_t)tile - 1;
+            while (t >= 0) {
+                const uint64_t sw = ld_lb(look + (uint64_t)t * kRadix + d);
+                const uint32_t tag = (uint32_t)(sw >> 32);
+                if (tag < 2u * epoch + 1u) continue;   // not published yet: spin
+                excl += (uint32_t)sw;
+                if (tag == 2u * epoch + 2u) break;
+                --t;
+            }
+            st_lb(lk, inc_tag | (excl + h));
         }
-        st_lb(lk, inc_tag | (excl + h));
+        gbase[d] = goff[d] + excl;
     }
-    gbase[d] = goff[d] + excl;
     __syncthreads();
     // stage the tile in digit order
 #pragma unroll
@@ -211,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void pass_kernel(const K* __restrict__ ki
     }
     __syncthreads();
     // contiguous runs per digit
-    for (uint32_t i = tid; i < tn; i += kThreads) {
+    for (uint32_t i = tid; i < tn; i += NT) {
         const K key = sk[i];
         const uint32_t dk = digit_of(key, shift);
         const uint64_t g = (uint64_t)gbase[dk] + (i - dbase[dk]);
@@ -220,20 +235,19 @@ __global__ __launch_bounds__(kThreads) void pass_kernel(const K* __restrict__ ki
     }
 }
 
-// Persistent state of the sorts run on one stream: the look-back words (zero
-// when allocated), the ticket counter and the host's copies of epoch / ticket.
+// State of the sorts run on one stream: the look-back words (zeroed when
+// allocated, then tagged by the host's pass epoch), the digit histograms and
+// the tile ticket (restarted by every sort).
 struct State {
-    uint64_t* look = nullptr;            // look_tiles x 256, zeroed once
+    uint64_t* look = nullptr;            // look_tiles x 256
     uint64_t look_tiles = 0;
     uint32_t* hist = nullptr;            // 8 x 256
     unsigned long long* ticket = nullptr;
     uint32_t epoch = 0;
-    unsigned long long tick = 0;         // tickets handed out so far
 };
 
-inline uint64_t tiles_for(uint64_t n, int key_bytes, int items = 0) {
-    const uint64_t T = (uint64_t)kThreads *
-                       (items ? items : (key_bytes == 4 ? Tile<uint32_t>::kItems : Tile<uint64_t>::kItems));
+inline uint64_t tiles_for(uint64_t n, int key_bytes) {
+    const uint64_t T = key_bytes == 4 ? Tile<uint32_t>::kSize : Tile<uint64_t>::kSize;
     return (n + T - 1) / T;
 }
 
@@ -241,7 +255,7 @@ inline uint64_t tiles_for(uint64_t n, int key_bytes, int items = 0) {
 // sorted pairs end in (*kres, *vres), one of the two.  Stable.  st.look must
 // hold tiles_for(n) tiles; st.hist 8 x 256; st.ticket one counter.
 // hist_zeroed: the caller already zeroed st.hist (8 x 256) on the stream.
-template <typename K, int I = Tile<K>::kItems>
+template <typename K, int I = Tile<K>::kItems, int NT = Tile<K>::kThreads>
 void sort_pairs(State& st, K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, int bits,
                 hipStream_t s, K** kres, uint32_t** vres, bool hist_zeroed = false) {
     *kres = k0;
@@ -252,23 +266,25 @@ void sort_pairs(State& st, K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n,
     if (!hist_zeroed) PD_HIP(hipMemsetAsync(st.hist, 0, sizeof(uint32_t) * kRadix * places, s));
     const unsigned hb = (unsigned)std::min<uint64_t>(2048, (n + kThreads - 1) / kThreads);
     hipLaunchKernelGGL((hist_kernel<K>), dim3(hb), dim3(kThreads), 0, s, k0, n, 0, places, st.hist);
-    hipLaunchKernelGGL(hist_scan_kernel, dim3(1), dim3(kRadix), 0, s, st.hist, places);
-    const uint64_t tiles = tiles_for(n, (int)sizeof(K), I);
+    hipLaunchKernelGGL(hist_scan_kernel, dim3(1), dim3(kRadix), 0, s, st.hist, places, st.ticket);
+    const uint64_t tiles = (n + (uint64_t)NT * I - 1) / ((uint64_t)NT * I);
     if (tiles > st.look_tiles) throw Error(-5, "rsort: look-back buffer too small");
     K* ki = k0;
     uint32_t* vi = v0;
     K* ko = k1;
     uint32_t* vo = v1;
     for (int p = 0; p < places; ++p) {
-        if (st.epoch >= 0x7FFFFFF0u) {   // tags would wrap: start over from zeroed words
+        if (st.epoch >= 0x7FFFFFF0u) {   // tags would overflow: start over from zeroed words
             PD_HIP(hipMemsetAsync(st.look, 0, sizeof(uint64_t) * kRadix * st.look_tiles, s));
             st.epoch = 0;
         }
-        hipLaunchKernelGGL((pass_kernel<K, I>), dim3((unsigned)tiles), dim3(kThreads), 0, s, ki, vi, ko,
-                           vo, n, 8 * p, st.hist + p * kRadix, st.look, st.epoch, st.ticket, st.tick);
+        // (the epoch is consumed before the launch: a pass that fails never
+        // leaves words a later pass could take for its own)
+        const uint32_t ep = st.epoch++;
+        hipLaunchKernelGGL((pass_kernel<K, I, NT>), dim3((unsigned)tiles), dim3(NT), 0, s, ki, vi, ko,
+                           vo, n, 8 * p, st.hist + p * kRadix, st.look, ep, st.ticket,
+                           (unsigned long long)p * tiles);
         PD_HIP(hipGetLastError());
-        ++st.epoch;
-        st.tick += tiles;
         std::swap(ki, ko);
         std::swap(vi, vo);
     }

@@ -86,16 +86,15 @@ float run(const char* name, uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* 
 
 // The library's own onesweep (pypardis_amd/csrc/rsort.hpp) with I items per
 // thread, checked pair for pair against rocPRIM's stable result.
-template <int I>
+template <int I, int NT = 256>
 int run_rs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t* k2, uint32_t* v2,
            const uint32_t* rk, const uint32_t* rv, size_t n, unsigned bits, hipStream_t s) {
     pd::rsort::State st;
-    st.look_tiles = pd::rsort::tiles_for(n, 4, I);
+    st.look_tiles = (n + (uint64_t)NT * I - 1) / ((uint64_t)NT * I);
     CK(hipMalloc(&st.look, sizeof(uint64_t) * 256 * st.look_tiles));
     CK(hipMemset(st.look, 0, sizeof(uint64_t) * 256 * st.look_tiles));
     CK(hipMalloc(&st.hist, sizeof(uint32_t) * 8 * 256));
     CK(hipMalloc(&st.ticket, sizeof(unsigned long long)));
-    CK(hipMemset(st.ticket, 0, sizeof(unsigned long long)));
     std::vector<float> t;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -106,7 +105,7 @@ int run_rs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t* k2,
         CK(hipMemcpyAsync(v1, v0, n * 4, hipMemcpyDeviceToDevice, s));
         CK(hipEventRecord(e0, s));
         try {
-            pd::rsort::sort_pairs<uint32_t, I>(st, k1, v1, k2, v2, n, (int)bits, s, &ok_k, &ok_v);
+            pd::rsort::sort_pairs<uint32_t, I, NT>(st, k1, v1, k2, v2, n, (int)bits, s, &ok_k, &ok_v);
         } catch (const std::exception& e) {
             std::fprintf(stderr, "rsort: %s\n", e.what());
             return 1;
@@ -126,7 +125,7 @@ int run_rs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t* k2,
     for (size_t i = 0; i < n; ++i) diff += (a[i] != c[i] || b[i] != d[i]) ? 1 : 0;
     std::sort(t.begin(), t.end());
     char name[64];
-    std::snprintf(name, sizeof(name), "pd::rsort onesweep, %d items/thread", I);
+    std::snprintf(name, sizeof(name), "pd::rsort onesweep, %d threads x %d items", NT, I);
     std::printf("%-44s %8.3f ms  %6.2f GB/s per pass-byte  %s (%zu pairs differ from rocPRIM)\n", name,
                 t[t.size() / 2], (double)n * 16.0 * ((bits + 7) / 8) / (t[t.size() / 2] * 1e-3) / 1e9,
                 diff ? "MISMATCH" : "identical", diff);
@@ -149,7 +148,7 @@ __global__ void fill64_kernel(uint64_t* k, uint32_t* v, size_t n, uint64_t mask,
 }
 
 // 64-bit keys of `bits` bits (C4: 37): rocPRIM vs the library's sort.
-template <int I>
+template <int I, int NT = 256>
 int run64(size_t n, unsigned bits, hipStream_t s) {
     uint64_t *k0, *k1, *k2;
     uint32_t *v0, *v1, *v2;
@@ -193,19 +192,18 @@ int run64(size_t n, unsigned bits, hipStream_t s) {
         }
     }
     pd::rsort::State st;
-    st.look_tiles = pd::rsort::tiles_for(n, 8, I);
+    st.look_tiles = (n + (uint64_t)NT * I - 1) / ((uint64_t)NT * I);
     CK(hipMalloc(&st.look, sizeof(uint64_t) * 256 * st.look_tiles));
     CK(hipMemset(st.look, 0, sizeof(uint64_t) * 256 * st.look_tiles));
     CK(hipMalloc(&st.hist, sizeof(uint32_t) * 8 * 256));
     CK(hipMalloc(&st.ticket, sizeof(unsigned long long)));
-    CK(hipMemset(st.ticket, 0, sizeof(unsigned long long)));
     for (int it = 0; it < 7; ++it) {
         CK(hipMemcpyAsync(k1, k0, n * 8, hipMemcpyDeviceToDevice, s));
         CK(hipMemcpyAsync(v1, v0, n * 4, hipMemcpyDeviceToDevice, s));
         uint64_t* ok;
         uint32_t* ov;
         CK(hipEventRecord(e0, s));
-        pd::rsort::sort_pairs<uint64_t, I>(st, k1, v1, k2, v2, n, (int)bits, s, &ok, &ov);
+        pd::rsort::sort_pairs<uint64_t, I, NT>(st, k1, v1, k2, v2, n, (int)bits, s, &ok, &ov);
         CK(hipEventRecord(e1, s));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -220,8 +218,8 @@ int run64(size_t n, unsigned bits, hipStream_t s) {
     for (size_t i = 0; i < n; ++i) diff += (ka[i] != kb2[i] || va[i] != vb2[i]) ? 1 : 0;
     std::sort(tr.begin(), tr.end());
     std::sort(tl.begin(), tl.end());
-    std::printf("u64 keys, %u bits, n = %zu: rocPRIM %.3f ms, pd::rsort (%d items/thread) %.3f ms, %s (%zu differ)\n",
-                bits, n, tr[tr.size() / 2], I, tl[tl.size() / 2], diff ? "MISMATCH" : "identical", diff);
+    std::printf("u64 keys, %u bits, n = %zu: rocPRIM %.3f ms, pd::rsort (%d threads x %d items) %.3f ms, %s (%zu differ)\n",
+                bits, n, tr[tr.size() / 2], NT, I, tl[tl.size() / 2], diff ? "MISMATCH" : "identical", diff);
     CK(hipFree(k0)); CK(hipFree(k1)); CK(hipFree(k2));
     CK(hipFree(v0)); CK(hipFree(v1)); CK(hipFree(v2));
     CK(hipFree(tmp)); CK(hipFree(st.look)); CK(hipFree(st.hist)); CK(hipFree(st.ticket));
@@ -273,10 +271,15 @@ int main(int argc, char** argv) {
         CK(hipFree(tmp));
     }
     run_rs<32>(k0, v0, k1, v1, k2, v2, rk, rv, n, bits, s);
+    run_rs<16, 512>(k0, v0, k1, v1, k2, v2, rk, rv, n, bits, s);
+    run_rs<8, 1024>(k0, v0, k1, v1, k2, v2, rk, rv, n, bits, s);
+    run_rs<12, 1024>(k0, v0, k1, v1, k2, v2, rk, rv, n, bits, s);
+    run_rs<12, 512>(k0, v0, k1, v1, k2, v2, rk, rv, n, bits, s);
     CK(hipFree(k0)); CK(hipFree(v0)); CK(hipFree(k1)); CK(hipFree(v1)); CK(hipFree(k2)); CK(hipFree(v2));
     CK(hipFree(rk)); CK(hipFree(rv));
     // C4's shape: 1.0e9 records would need 16 GB here; 2e8 keeps the box light
     run64<24>(200000000, 37, s);
-    run64<32>(200000000, 37, s);
+    run64<12, 512>(200000000, 37, s);
+    run64<8, 1024>(200000000, 37, s);
     return 0;
 }

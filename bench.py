@@ -92,6 +92,8 @@ def parse():
                     help="PD_OPT_LABEL_BUCKETS override (0: one scattered label write per record)")
     ap.add_argument("--centre-window", type=int, default=None,
                     help="PD_OPT_CENTRE_WINDOW override (link window length)")
+    ap.add_argument("--xsub", type=int, default=None,
+                    help="PD_OPT_XSUB override (axis-0 sub-cells per eps)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
@@ -493,7 +495,8 @@ def main():
                      (_native.PD_OPT_DIR_BUDGET, args.dir_budget),
                      (_native.PD_OPT_LABEL_BUCKETS, args.label_buckets),
                      (_native.PD_OPT_DIR_PAGED, args.dir_paged),
-                     (_native.PD_OPT_DENSE_SCREEN, args.dense_screen)):
+                     (_native.PD_OPT_DENSE_SCREEN, args.dense_screen),
+                     (_native.PD_OPT_XSUB, args.xsub)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None

@@ -46,22 +46,39 @@ __device__ __forceinline__ uint32_t digit_of(uint64_t k, int shift) {
 }
 
 // Digit histograms of `places` passes (place p: bits [8p + begin, +8)), one
-// read of the keys.  hist: places x 256 uint32, zeroed by the caller.
+// read of the keys (16-byte loads), each wave counting into its own LDS copy
+// (no atomics between waves).  hist: places x 256 uint32, zeroed by the caller.
 template <typename K>
 __global__ __launch_bounds__(kThreads) void hist_kernel(const K* __restrict__ keys, uint64_t n,
-                                                        int begin, int places,
+                                                        int begin, int places, int vec,
                                                         uint32_t* __restrict__ hist) {
-    __shared__ uint32_t h[8][kRadix];
-    for (int i = threadIdx.x; i < 8 * kRadix; i += kThreads) (&h[0][0])[i] = 0;
+    constexpr int NW = kThreads / 64, V = 16 / sizeof(K);   // keys per 16-byte load
+    __shared__ uint32_t h[NW][8][kRadix];
+    const int w = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < NW * 8 * kRadix; i += kThreads) (&h[0][0][0])[i] = 0;
     __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n;
+    const uint64_t nv = vec ? n / V : 0;   // (vec: keys 16-byte aligned)
+    const uint4* kv = reinterpret_cast<const uint4*>(keys);
+    for (uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < nv;
+         i += (uint64_t)gridDim.x * kThreads) {
+        const uint4 q = kv[i];
+        K k[V];
+        __builtin_memcpy(k, &q, 16);
+#pragma unroll
+        for (int u = 0; u < V; ++u)
+            for (int p = 0; p < places; ++p) atomicAdd(&h[w][p][digit_of(k[u], begin + 8 * p)], 1u);
+    }
+    // the tail (< V keys; every key when unaligned)
+    for (uint64_t i = nv * V + (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * kThreads) {
         const K k = keys[i];
-        for (int p = 0; p < places; ++p) atomicAdd(&h[p][digit_of(k, begin + 8 * p)], 1u);
+        for (int p = 0; p < places; ++p) atomicAdd(&h[w][p][digit_of(k, begin + 8 * p)], 1u);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < places * kRadix; i += kThreads) {
-        const uint32_t c = (&h[0][0])[i];
+        uint32_t c = 0;
+#pragma unroll
+        for (int u = 0; u < NW; ++u) c += (&h[u][0][0])[i];
         if (c) atomicAdd(hist + i, c);
     }
 }
@@ -265,7 +282,9 @@ void sort_pairs(State& st, K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n,
     if (places > 8) throw Error(-5, "rsort: more than 64 key bits");
     if (!hist_zeroed) PD_HIP(hipMemsetAsync(st.hist, 0, sizeof(uint32_t) * kRadix * places, s));
     const unsigned hb = (unsigned)std::min<uint64_t>(2048, (n + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL((hist_kernel<K>), dim3(hb), dim3(kThreads), 0, s, k0, n, 0, places, st.hist);
+    const int vec = ((uintptr_t)k0 & 15) == 0 ? 1 : 0;
+    hipLaunchKernelGGL((hist_kernel<K>), dim3(hb), dim3(kThreads), 0, s, k0, n, 0, places, vec,
+                       st.hist);
     hipLaunchKernelGGL(hist_scan_kernel, dim3(1), dim3(kRadix), 0, s, st.hist, places, st.ticket);
     const uint64_t tiles = (n + (uint64_t)NT * I - 1) / ((uint64_t)NT * I);
     if (tiles > st.look_tiles) throw Error(-5, "rsort: look-back buffer too small");

@@ -347,6 +347,22 @@ def test_record_sort_is_stable_and_exact(native, key_bytes, bits, n):
     assert np.array_equal(got_v, v[order])
 
 
+def test_record_sort_unaligned_keys(native):
+    """pd_sort_pairs on a key view that is not 16-byte aligned (the digit
+    histogram then reads key by key)."""
+    rng = np.random.default_rng(5)
+    n = 100_003
+    k = rng.integers(0, 1 << 20, n + 1, dtype=np.uint64).astype(np.uint32)
+    kt = torch.from_numpy(k.view(np.int32)).cuda()[1:]
+    v = np.arange(n, dtype=np.uint32)
+    vt = torch.from_numpy(v.view(np.int32)).cuda()
+    assert kt.data_ptr() % 16 != 0
+    native.sort_pairs(kt, vt, 20)
+    order = np.argsort(k[1:], kind="stable")
+    assert np.array_equal(kt.cpu().numpy().view(np.uint32), k[1:][order])
+    assert np.array_equal(vt.cpu().numpy().view(np.uint32), v[order])
+
+
 def test_fp64_input_exact(native):
     from pypardis_amd import synth
     X = synth.blobs_noise(40_000, 2, side=10.0, n_centers=5, sigma=0.3, seed=31).astype(np.float64)

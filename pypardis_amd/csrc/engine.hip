@@ -2211,25 +2211,33 @@ constexpr int kLabBlock = 1024;                 // threads per label_bucket tile
 constexpr int kLabPer = 15;                     // pairs per thread
 constexpr int kLabTile = kLabBlock * kLabPer;   // 15360 pairs (120 KiB staged)
 constexpr int kLabMaxBk = 2048;                 // buckets (2 per thread in the scan)
+// Block-local form (n <= kLabMaxBkL << kLabBitsL, C2): buckets of 2^15
+// points, one workgroup per bucket places its keys in an LDS image of the
+// bucket's labels (128 KiB) and writes labels and core flags coalesced.
+constexpr int kLabBitsL = 15;
+constexpr int kLabPerL = 12;                    // 12288 pairs per tile (96 KiB staged)
+constexpr int kLabMaxBkL = 4096;                // 4 per thread in the scan
 
 // (point, key) pairs in record order: pairs[r] = (owner record ? its point :
 // kNone, core: the cluster key | kKeyCoreBit; else kNone — the border sweep
 // fills in its key afterwards).  Written by owner_kernel in bucketed mode.
+template <int PER, int MAXBK>
 __global__ __launch_bounds__(kLabBlock) void label_bucket_kernel(uint32_t R,
                                                                  const uint2* __restrict__ recs,
                                                                  int kLabBits, int nbk,
                                                                  uint32_t* __restrict__ bcnt,
                                                                  uint2* __restrict__ pairs) {
-    __shared__ uint2 stage[kLabTile];
-    __shared__ uint32_t cnt[kLabMaxBk], off[kLabMaxBk], gbase[kLabMaxBk];
+    constexpr int TILE = kLabBlock * PER, BPT = MAXBK / kLabBlock;
+    __shared__ uint2 stage[TILE];
+    __shared__ uint32_t cnt[MAXBK], off[MAXBK], gbase[MAXBK];
     const int tid = threadIdx.x;
-    for (int k = tid; k < kLabMaxBk; k += kLabBlock) cnt[k] = 0;
+    for (int k = tid; k < MAXBK; k += kLabBlock) cnt[k] = 0;
     __syncthreads();
-    const uint64_t t0 = (uint64_t)blockIdx.x * kLabTile;
-    uint2 q[kLabPer];
-    uint32_t lr[kLabPer];
+    const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
+    uint2 q[PER];
+    uint32_t lr[PER];
 #pragma unroll
-    for (int i = 0; i < kLabPer; ++i) {
+    for (int i = 0; i < PER; ++i) {
         const uint64_t r = t0 + (uint64_t)i * kLabBlock + tid;
         q[i] = make_uint2(kNone, kNone);
         if (r < R) {   // streamed once: non-temporal
@@ -2239,27 +2247,32 @@ __global__ __launch_bounds__(kLabBlock) void label_bucket_kernel(uint32_t R,
         }
     }
 #pragma unroll
-    for (int i = 0; i < kLabPer; ++i) {
+    for (int i = 0; i < PER; ++i) {
         const bool ok = q[i].x != kNone && q[i].y != kNone;
         lr[i] = ok ? atomicAdd(&cnt[q[i].x >> kLabBits], 1u) : 0u;
         if (!ok) q[i].x = kNone;
     }
     __syncthreads();
-    uint32_t total;
-    const int k0 = 2 * tid, k1 = 2 * tid + 1;   // two buckets per thread
-    const uint32_t c0 = k0 < nbk ? cnt[k0] : 0u, c1 = k1 < nbk ? cnt[k1] : 0u;
-    const uint32_t ex = block_excl_scan<kLabBlock>(c0 + c1, total);
-    if (k0 < nbk) {
-        off[k0] = ex;
-        gbase[k0] = c0 ? atomicAdd(bcnt + k0, c0) : 0u;
+    uint32_t total, c[BPT], sum = 0;   // BPT consecutive buckets per thread
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+        const int k = BPT * tid + u;
+        c[u] = k < nbk ? cnt[k] : 0u;
+        sum += c[u];
     }
-    if (k1 < nbk) {
-        off[k1] = ex + c0;
-        gbase[k1] = c1 ? atomicAdd(bcnt + k1, c1) : 0u;
+    uint32_t ex = block_excl_scan<kLabBlock>(sum, total);
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) {
+        const int k = BPT * tid + u;
+        if (k < nbk) {
+            off[k] = ex;
+            gbase[k] = c[u] ? atomicAdd(bcnt + k, c[u]) : 0u;
+        }
+        ex += c[u];
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < kLabPer; ++i)
+    for (int i = 0; i < PER; ++i)
         if (q[i].x != kNone) stage[off[q[i].x >> kLabBits] + lr[i]] = q[i];
     __syncthreads();
     for (uint32_t p = tid; p < total; p += kLabBlock) {
@@ -2283,6 +2296,47 @@ __global__ __launch_bounds__(kBlock) void label_scatter_kernel(const uint2* __re
         const unsigned long long w =
             __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p + k));
         key_out[(uint32_t)w] = (uint32_t)(w >> 32);
+    }
+}
+
+// Block-local label pass: one workgroup per bucket of 2^kLabBitsL points.
+// The bucket's (point, key) pairs (in bucket order, from label_bucket_kernel)
+// are placed into an LDS image of its labels (kNone = noise), then the
+// labels (core bit stripped) and the core mask are written coalesced — no
+// key_out fill, no scattered HBM writes, no separate final_label_kernel.
+__global__ __launch_bounds__(kLabBlock) void label_local_kernel(const uint2* __restrict__ pairs,
+                                                                const uint32_t* __restrict__ bcnt,
+                                                                uint64_t n,
+                                                                int32_t* __restrict__ labels,
+                                                                uint8_t* __restrict__ core_out) {
+    constexpr uint32_t NB = 1u << kLabBitsL, MASK = NB - 1;
+    __shared__ uint32_t img[NB];
+    const uint32_t b = blockIdx.x;
+    const int tid = threadIdx.x;
+    for (uint32_t i = tid; i < NB; i += kLabBlock) img[i] = kNone;
+    __syncthreads();
+    const uint32_t c = bcnt[b];
+    const unsigned long long* p =
+        reinterpret_cast<const unsigned long long*>(pairs + ((uint64_t)b << kLabBitsL));
+    constexpr int U = 4;   // loads in flight per thread
+    for (uint32_t k0 = 0; k0 < c; k0 += U * kLabBlock) {
+        unsigned long long w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t k = k0 + u * kLabBlock + tid;
+            w[u] = k < c ? __builtin_nontemporal_load(p + k) : ~0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (k0 + u * kLabBlock + tid < c) img[(uint32_t)w[u] & MASK] = (uint32_t)(w[u] >> 32);
+    }
+    __syncthreads();
+    const uint64_t base = (uint64_t)b << kLabBitsL;
+    const uint32_t m = (uint32_t)std::min<uint64_t>(NB, n - base);
+    for (uint32_t i = tid; i < m; i += kLabBlock) {
+        const uint32_t k = img[i];
+        labels[base + i] = k == kNone ? -1 : (int32_t)(k & ~kKeyCoreBit);
+        if (core_out) core_out[base + i] = (k != kNone && (k & kKeyCoreBit)) ? 1 : 0;
     }
 }
 
@@ -2944,7 +2998,10 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     // C1 1e7 keeps the direct scatter)
     const bool want_buckets = ctx.label_buckets > 0 || (ctx.label_buckets < 0 && n >= (1ull << 26));
     const bool bucketed = a.phase != 2 && core_bit && !a.counts && want_buckets && n > 0;
-    PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
+    // block-local label pass (C2-sized n): every label is written from LDS,
+    // so key_out is neither filled nor used
+    const bool local = bucketed && R && ctx.label_buckets != 2 && ((n + (1ull << kLabBitsL) - 1) >> kLabBitsL) <= (uint64_t)kLabMaxBkL;
+    if (!local) PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
     if (R) {
         uint32_t* blist = ctx.arena.get<uint32_t>("border_list", R);
         const unsigned tiles = (unsigned)(((uint64_t)R + kOwnTile - 1) / kOwnTile);
@@ -2966,7 +3023,18 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         if (NB)
             launch_border<T, D, M>(s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par, gmin,
                                    key_out, recs ? (uint32_t*)recs + 1 : nullptr);
-        if (bucketed) {
+        if (local) {
+            const int nbk = (int)((n + (1ull << kLabBitsL) - 1) >> kLabBitsL);
+            uint32_t* bcnt = ctx.arena.get<uint32_t>("lab_bcnt", (size_t)nbk);
+            uint2* pairs = ctx.arena.get<uint2>("lab_pairs", (size_t)nbk << kLabBitsL);
+            PD_HIP(hipMemsetAsync(bcnt, 0, sizeof(uint32_t) * nbk, s));
+            constexpr int tile = kLabBlock * kLabPerL;
+            const unsigned ltiles = (unsigned)(((uint64_t)R + tile - 1) / tile);
+            hipLaunchKernelGGL((label_bucket_kernel<kLabPerL, kLabMaxBkL>), dim3(ltiles),
+                               dim3(kLabBlock), 0, s, R, recs, kLabBitsL, nbk, bcnt, pairs);
+            hipLaunchKernelGGL(label_local_kernel, dim3((unsigned)nbk), dim3(kLabBlock), 0, s, pairs,
+                               bcnt, (uint64_t)n, a.labels, a.core);
+        } else if (bucketed) {
             // buckets of 2^19 points: a bucket's 2 MB of key_out stays in one
             // XCD's 4 MB L2 (C4 border: 2^20 29.2, 2^19 27.9, 2^18 29.5 ms)
             int kLabBits = 19;
@@ -2977,7 +3045,8 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
             uint2* pairs = ctx.arena.get<uint2>("lab_pairs", (size_t)nbk << kLabBits);
             PD_HIP(hipMemsetAsync(bcnt, 0, sizeof(uint32_t) * nbk, s));
             const unsigned ltiles = (unsigned)(((uint64_t)R + kLabTile - 1) / kLabTile);
-            hipLaunchKernelGGL(label_bucket_kernel, dim3(ltiles), dim3(kLabBlock), 0, s, R, recs,
+            hipLaunchKernelGGL((label_bucket_kernel<kLabPer, kLabMaxBk>), dim3(ltiles),
+                               dim3(kLabBlock), 0, s, R, recs,
                                kLabBits, nbk, bcnt, pairs);
             const unsigned bpb = (1u << kLabBits) / (kBlock * 8);
             hipLaunchKernelGGL(label_scatter_kernel, dim3((unsigned)nbk * bpb), dim3(kBlock), 0, s,
@@ -3003,7 +3072,7 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         return;
     }
     // single device: key_out already holds ranks (root_rank_kernel)
-    if (n)
+    if (n && !local)
         hipLaunchKernelGGL(final_label_kernel, dim3(blocks(n)), dim3(kBlock), 0, s, key_out, n,
                            a.labels, a.core);
     PD_HIP(hipGetLastError());

@@ -89,10 +89,12 @@ enum pd_option {
                                 inside L2-sized buckets) instead of one scattered write per
                                 record: 1 on, 0 off, -1 (default) from 2^26 points on, where
                                 it is faster (C4 1e9: border 42 -> 38 ms; C2 1e8: 4.31 ->
-                                4.10 ms).  Up to 2^27 points the second pass is block-local
-                                (buckets of 2^15 points placed in LDS, labels and core flags
-                                written coalesced); 2 forces the L2-bucket scatter used above
-                                that size.  Same labels either way */,
+                                4.10 ms).  The second pass is block-local (buckets of 2^15
+                                points placed in LDS, labels and core flags written
+                                coalesced); above 2^27 points the first pass's 2^19-point
+                                buckets are split into those first.  2 forces the L2-bucket
+                                scatter instead, 3 the two-level form at any size.  Same
+                                labels either way */,
     PD_OPT_DIR_PAGED = 17     /* eps-grid directory layout: 1 paged (pages of 4096 cells hold a
                                 mask of their occupied 64-cell words; only occupied words are
                                 stored: memory and build time follow the occupied cells, not the

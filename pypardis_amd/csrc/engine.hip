@@ -2299,6 +2299,71 @@ __global__ __launch_bounds__(kBlock) void label_scatter_kernel(const uint2* __re
     }
 }
 
+// Two-level form (n > kLabMaxBkL << kLabBitsL, C4): the coarse buckets of
+// 2^kLabBits points (label_bucket_kernel<kLabPer, kLabMaxBk>) are split into
+// their 2^(kLabBits - kLabBitsL) sub-buckets of 2^kLabBitsL points, a tile of
+// one coarse bucket per workgroup (counting sort by sub-bucket in LDS, runs
+// written whole), for label_local_kernel.
+constexpr int kLabMaxSub = 64;   // kLabBits <= kLabBitsL + 6 (n < 2^32 needs <= 21)
+__global__ __launch_bounds__(kLabBlock) void label_split_kernel(const uint2* __restrict__ pairs,
+                                                                const uint32_t* __restrict__ bcnt,
+                                                                int kLabBits, uint32_t tpb,
+                                                                uint32_t* __restrict__ bcnt2,
+                                                                uint2* __restrict__ pairs2) {
+    constexpr int PER = kLabPerL, TILE = kLabBlock * PER;
+    __shared__ uint2 stage[TILE];
+    __shared__ uint32_t cnt[kLabMaxSub], off[kLabMaxSub], gbase[kLabMaxSub], s_total;
+    const uint32_t b = blockIdx.x / tpb, t = blockIdx.x % tpb;
+    const uint32_t c = bcnt[b];
+    const uint64_t t0 = (uint64_t)t * TILE;
+    if (t0 >= c) return;   // whole workgroup
+    const int tid = threadIdx.x;
+    const int sb = kLabBits - kLabBitsL;
+    const uint32_t nsub = 1u << sb, smask = nsub - 1;
+    if (tid < kLabMaxSub) cnt[tid] = 0;
+    __syncthreads();
+    const uint2* src = pairs + ((uint64_t)b << kLabBits);
+    uint2 q[PER];
+    uint32_t lr[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const uint64_t k = t0 + (uint64_t)i * kLabBlock + tid;
+        q[i] = make_uint2(kNone, kNone);
+        if (k < c) {   // streamed once: non-temporal
+            const unsigned long long w =
+                __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(src + k));
+            q[i] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+        lr[i] = q[i].x != kNone ? atomicAdd(&cnt[(q[i].x >> kLabBitsL) & smask], 1u) : 0u;
+    __syncthreads();
+    if (tid < 64) {   // wave 0: scan of the <= 64 sub-bucket counts
+        const uint32_t v = (uint32_t)tid < nsub ? cnt[tid] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+            if (tid >= o) x += y;
+        }
+        off[tid] = x - v;
+        gbase[tid] = v ? atomicAdd(bcnt2 + ((uint64_t)b << sb) + tid, v) : 0u;
+        if (tid == 63) s_total = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+        if (q[i].x != kNone) stage[off[(q[i].x >> kLabBitsL) & smask] + lr[i]] = q[i];
+    __syncthreads();
+    const uint32_t total = s_total;
+    for (uint32_t p = tid; p < total; p += kLabBlock) {
+        const uint2 v = stage[p];
+        const uint32_t g = v.x >> kLabBitsL, u = g & smask;
+        pairs2[((uint64_t)g << kLabBitsL) + gbase[u] + (p - off[u])] = v;
+    }
+}
+
 // Block-local label pass: one workgroup per bucket of 2^kLabBitsL points.
 // The bucket's (point, key) pairs (in bucket order, from label_bucket_kernel)
 // are placed into an LDS image of its labels (kNone = noise), then the
@@ -3000,7 +3065,13 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     const bool bucketed = a.phase != 2 && core_bit && !a.counts && want_buckets && n > 0;
     // block-local label pass (C2-sized n): every label is written from LDS,
     // so key_out is neither filled nor used
-    const bool local = bucketed && R && ctx.label_buckets != 2 && ((n + (1ull << kLabBitsL) - 1) >> kLabBitsL) <= (uint64_t)kLabMaxBkL;
+    // (n > kLabMaxBkL << kLabBitsL, or PD_OPT_LABEL_BUCKETS 3: two-level, the
+    // coarse buckets split into block-local ones; 2: the L2-bucket scatter)
+    const uint64_t nbkL = (n + (1ull << kLabBitsL) - 1) >> kLabBitsL;
+    const bool local1 = bucketed && R && ctx.label_buckets != 2 && ctx.label_buckets != 3 &&
+                        nbkL <= (uint64_t)kLabMaxBkL;
+    const bool local2 = bucketed && R && ctx.label_buckets != 2 && !local1;
+    const bool local = local1 || local2;
     if (!local) PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
     if (R) {
         uint32_t* blist = ctx.arena.get<uint32_t>("border_list", R);
@@ -3023,8 +3094,30 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         if (NB)
             launch_border<T, D, M>(s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par, gmin,
                                    key_out, recs ? (uint32_t*)recs + 1 : nullptr);
-        if (local) {
-            const int nbk = (int)((n + (1ull << kLabBitsL) - 1) >> kLabBitsL);
+        if (local2) {
+            int kLabBits = 19;
+            while (((n + (1ull << kLabBits) - 1) >> kLabBits) > (uint64_t)kLabMaxBk) ++kLabBits;
+            const int nbk = (int)((n + (1ull << kLabBits) - 1) >> kLabBits);
+            const int sb = kLabBits - kLabBitsL;
+            if (nbk > kLabMaxBk || sb > 6) throw Error(-5, "label buckets: too many points");
+            uint32_t* bcnt = ctx.arena.get<uint32_t>("lab_bcnt", (size_t)nbk);
+            uint2* pairs = ctx.arena.get<uint2>("lab_pairs", (size_t)nbk << kLabBits);
+            const size_t nsub = (size_t)nbk << sb;   // >= nbkL
+            uint32_t* bcnt2 = ctx.arena.get<uint32_t>("lab_bcnt2", nsub);
+            uint2* pairs2 = ctx.arena.get<uint2>("lab_pairs2", (size_t)nbkL << kLabBitsL);
+            PD_HIP(hipMemsetAsync(bcnt, 0, sizeof(uint32_t) * nbk, s));
+            PD_HIP(hipMemsetAsync(bcnt2, 0, sizeof(uint32_t) * nsub, s));
+            const unsigned ltiles = (unsigned)(((uint64_t)R + kLabTile - 1) / kLabTile);
+            hipLaunchKernelGGL((label_bucket_kernel<kLabPer, kLabMaxBk>), dim3(ltiles),
+                               dim3(kLabBlock), 0, s, R, recs, kLabBits, nbk, bcnt, pairs);
+            constexpr uint32_t tile = kLabBlock * kLabPerL;
+            const uint32_t tpb = ((1u << kLabBits) + tile - 1) / tile;
+            hipLaunchKernelGGL(label_split_kernel, dim3((unsigned)nbk * tpb), dim3(kLabBlock), 0, s,
+                               pairs, bcnt, kLabBits, tpb, bcnt2, pairs2);
+            hipLaunchKernelGGL(label_local_kernel, dim3((unsigned)nbkL), dim3(kLabBlock), 0, s,
+                               pairs2, bcnt2, (uint64_t)n, a.labels, a.core);
+        } else if (local) {
+            const int nbk = (int)nbkL;
             uint32_t* bcnt = ctx.arena.get<uint32_t>("lab_bcnt", (size_t)nbk);
             uint2* pairs = ctx.arena.get<uint2>("lab_pairs", (size_t)nbk << kLabBitsL);
             PD_HIP(hipMemsetAsync(bcnt, 0, sizeof(uint32_t) * nbk, s));

@@ -87,9 +87,9 @@ enum pd_option {
     PD_OPT_LABEL_BUCKETS = 15 /* single device: the labels reach input order through two
                                 coalesced passes (pairs bucketed by point id, then scattered
                                 inside L2-sized buckets) instead of one scattered write per
-                                record: 1 on, 0 off, -1 (default) from 2^26 points on, where
+                                record: 1 on, 0 off, -1 (default) from 2^22 points on, where
                                 it is faster (C4 1e9: border 42 -> 38 ms; C2 1e8: 4.31 ->
-                                4.10 ms).  The second pass is block-local (buckets of 2^15
+                                4.10 ms; with the block-local second pass C1 1e7 too).  The second pass is block-local (buckets of 2^15
                                 points placed in LDS, labels and core flags written
                                 coalesced); above 2^27 points the first pass's 2^19-point
                                 buckets are split into those first.  2 forces the L2-bucket

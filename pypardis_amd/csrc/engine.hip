@@ -3059,9 +3059,9 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     // single device, no counts wanted: labels reach input order through the
     // bucketed pair passes instead of owner_kernel's scatter
     // (ctx.label_buckets, PD_OPT_LABEL_BUCKETS)
-    // (automatic from 2^26 points: C2 1e8 border 4.31 -> 4.10 ms, round 5;
-    // C1 1e7 keeps the direct scatter)
-    const bool want_buckets = ctx.label_buckets > 0 || (ctx.label_buckets < 0 && n >= (1ull << 26));
+    // (automatic from 2^22 points since the block-local second pass: C2 1e8
+    // border + label 4.35 -> 3.79 ms, C1 1e7 0.33 -> 0.29 ms, round 5)
+    const bool want_buckets = ctx.label_buckets > 0 || (ctx.label_buckets < 0 && n >= (1ull << 22));
     const bool bucketed = a.phase != 2 && core_bit && !a.counts && want_buckets && n > 0;
     // block-local label pass (C2-sized n): every label is written from LDS,
     // so key_out is neither filled nor used

@@ -84,17 +84,16 @@ enum pd_option {
                                 grows by a common factor until it fits (exact at any width >= eps;
                                 more candidates per record).
                                 Default 32 GiB (PD_T_GRID_GROW reports the factor) */,
-    PD_OPT_LABEL_BUCKETS = 15 /* single device: the labels reach input order through two
-                                coalesced passes (pairs bucketed by point id, then scattered
-                                inside L2-sized buckets) instead of one scattered write per
-                                record: 1 on, 0 off, -1 (default) from 2^22 points on, where
-                                it is faster (C4 1e9: border 42 -> 38 ms; C2 1e8: 4.31 ->
-                                4.10 ms; with the block-local second pass C1 1e7 too).  The second pass is block-local (buckets of 2^15
-                                points placed in LDS, labels and core flags written
-                                coalesced); above 2^27 points the first pass's 2^19-point
-                                buckets are split into those first.  2 forces the L2-bucket
-                                scatter instead, 3 the two-level form at any size.  Same
-                                labels either way */,
+    PD_OPT_LABEL_BUCKETS = 15 /* single device: the labels reach input order through
+                                coalesced passes (pairs bucketed by point id into 2^19-point
+                                buckets, those split into 2^15-point ones, each placed in LDS
+                                and written out with the core flags coalesced) instead of one
+                                scattered write per record: 1 on, 0 off, -1 (default) from
+                                2^22 points on, where it is faster (C2 1e8: border + label
+                                4.35 -> 3.65 ms; C4 1e9: 30.3 -> 25.4 ms; C1 1e7: 0.33 ->
+                                0.29 ms); 2: the round-4 form (2^19-point buckets scattered
+                                inside one XCD's L2, then a key -> label pass).  Same labels
+                                either way */,
     PD_OPT_DIR_PAGED = 17     /* eps-grid directory layout: 1 paged (pages of 4096 cells hold a
                                 mask of their occupied 64-cell words; only occupied words are
                                 stored: memory and build time follow the occupied cells, not the

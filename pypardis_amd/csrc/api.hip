@@ -156,7 +156,7 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             if (value < 1 || value > 16) throw Error(PD_EINVAL, "xsub must be in [1, 16]");
             ctx->c.xsub = (int)value;
         } else if (option == PD_OPT_LABEL_BUCKETS) {
-            ctx->c.label_buckets = value < 0 ? -1 : (value >= 3 ? 3 : value >= 2 ? 2 : (value ? 1 : 0));
+            ctx->c.label_buckets = value < 0 ? -1 : (value == 2 ? 2 : (value ? 1 : 0));
         } else if (option == PD_OPT_DIR_PAGED) {
             ctx->c.dir_paged = value < 0 ? -1 : (value ? 1 : 0);
         } else if (option == PD_OPT_DENSE_SCREEN) {

@@ -2211,12 +2211,11 @@ constexpr int kLabBlock = 1024;                 // threads per label_bucket tile
 constexpr int kLabPer = 15;                     // pairs per thread
 constexpr int kLabTile = kLabBlock * kLabPer;   // 15360 pairs (120 KiB staged)
 constexpr int kLabMaxBk = 2048;                 // buckets (2 per thread in the scan)
-// Block-local form (n <= kLabMaxBkL << kLabBitsL, C2): buckets of 2^15
-// points, one workgroup per bucket places its keys in an LDS image of the
-// bucket's labels (128 KiB) and writes labels and core flags coalesced.
+// Block-local form: buckets of 2^15 points, one workgroup per bucket places
+// its keys in an LDS image of the bucket's labels (128 KiB) and writes labels
+// and core flags coalesced.
 constexpr int kLabBitsL = 15;
-constexpr int kLabPerL = 12;                    // 12288 pairs per tile (96 KiB staged)
-constexpr int kLabMaxBkL = 4096;                // 4 per thread in the scan
+constexpr int kLabPerL = 12;                    // label_split tile: 12288 pairs (96 KiB staged)
 
 // (point, key) pairs in record order: pairs[r] = (owner record ? its point :
 // kNone, core: the cluster key | kKeyCoreBit; else kNone — the border sweep
@@ -2299,11 +2298,13 @@ __global__ __launch_bounds__(kBlock) void label_scatter_kernel(const uint2* __re
     }
 }
 
-// Two-level form (n > kLabMaxBkL << kLabBitsL, C4): the coarse buckets of
-// 2^kLabBits points (label_bucket_kernel<kLabPer, kLabMaxBk>) are split into
-// their 2^(kLabBits - kLabBitsL) sub-buckets of 2^kLabBitsL points, a tile of
-// one coarse bucket per workgroup (counting sort by sub-bucket in LDS, runs
-// written whole), for label_local_kernel.
+// The coarse buckets of 2^kLabBits points (label_bucket_kernel) are split
+// into their 2^(kLabBits - kLabBitsL) sub-buckets of 2^kLabBitsL points, a
+// tile of one coarse bucket per workgroup (counting sort by sub-bucket in LDS,
+// runs of ~700 pairs written whole), for label_local_kernel.  (Bucketing
+// straight into 2^15-point buckets — 3052 for C2, runs of ~3 pairs per tile —
+// measured slower: label_bucket 0.78 vs 0.31 + 0.24 split ms, C2 border
+// 3.80 vs 3.65 ms.)
 constexpr int kLabMaxSub = 64;   // kLabBits <= kLabBitsL + 6 (n < 2^32 needs <= 21)
 __global__ __launch_bounds__(kLabBlock) void label_split_kernel(const uint2* __restrict__ pairs,
                                                                 const uint32_t* __restrict__ bcnt,
@@ -3065,13 +3066,10 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     const bool bucketed = a.phase != 2 && core_bit && !a.counts && want_buckets && n > 0;
     // block-local label pass (C2-sized n): every label is written from LDS,
     // so key_out is neither filled nor used
-    // (n > kLabMaxBkL << kLabBitsL, or PD_OPT_LABEL_BUCKETS 3: two-level, the
-    // coarse buckets split into block-local ones; 2: the L2-bucket scatter)
+    // (the coarse buckets split into block-local ones; PD_OPT_LABEL_BUCKETS
+    // 2: the L2-bucket scatter instead)
     const uint64_t nbkL = (n + (1ull << kLabBitsL) - 1) >> kLabBitsL;
-    const bool local1 = bucketed && R && ctx.label_buckets != 2 && ctx.label_buckets != 3 &&
-                        nbkL <= (uint64_t)kLabMaxBkL;
-    const bool local2 = bucketed && R && ctx.label_buckets != 2 && !local1;
-    const bool local = local1 || local2;
+    const bool local = bucketed && R && ctx.label_buckets != 2;
     if (!local) PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
     if (R) {
         uint32_t* blist = ctx.arena.get<uint32_t>("border_list", R);
@@ -3094,7 +3092,7 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
         if (NB)
             launch_border<T, D, M>(s, Xs, NB, blist, C, eps, eps2, slo, shi, vals, par, gmin,
                                    key_out, recs ? (uint32_t*)recs + 1 : nullptr);
-        if (local2) {
+        if (local) {
             int kLabBits = 19;
             while (((n + (1ull << kLabBits) - 1) >> kLabBits) > (uint64_t)kLabMaxBk) ++kLabBits;
             const int nbk = (int)((n + (1ull << kLabBits) - 1) >> kLabBits);
@@ -3116,17 +3114,6 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
                                pairs, bcnt, kLabBits, tpb, bcnt2, pairs2);
             hipLaunchKernelGGL(label_local_kernel, dim3((unsigned)nbkL), dim3(kLabBlock), 0, s,
                                pairs2, bcnt2, (uint64_t)n, a.labels, a.core);
-        } else if (local) {
-            const int nbk = (int)nbkL;
-            uint32_t* bcnt = ctx.arena.get<uint32_t>("lab_bcnt", (size_t)nbk);
-            uint2* pairs = ctx.arena.get<uint2>("lab_pairs", (size_t)nbk << kLabBitsL);
-            PD_HIP(hipMemsetAsync(bcnt, 0, sizeof(uint32_t) * nbk, s));
-            constexpr int tile = kLabBlock * kLabPerL;
-            const unsigned ltiles = (unsigned)(((uint64_t)R + tile - 1) / tile);
-            hipLaunchKernelGGL((label_bucket_kernel<kLabPerL, kLabMaxBkL>), dim3(ltiles),
-                               dim3(kLabBlock), 0, s, R, recs, kLabBitsL, nbk, bcnt, pairs);
-            hipLaunchKernelGGL(label_local_kernel, dim3((unsigned)nbk), dim3(kLabBlock), 0, s, pairs,
-                               bcnt, (uint64_t)n, a.labels, a.core);
         } else if (bucketed) {
             // buckets of 2^19 points: a bucket's 2 MB of key_out stays in one
             // XCD's 4 MB L2 (C4 border: 2^20 29.2, 2^19 27.9, 2^18 29.5 ms)

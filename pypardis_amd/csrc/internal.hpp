@@ -169,7 +169,7 @@ struct Ctx {
     int dense_screen = 1;        // dense count pass screen: 1 e4m3 (32x32x64), 0 bf16 hi.hi
     int label_buckets = -1;      // labels to input order by bucketed pair passes (PD_OPT_LABEL_BUCKETS;
                                  // -1: from 2^22 points on, where they beat the direct scatter;
-                                 // 2: the L2-bucket scatter; 3: the two-level block-local form)
+                                 // 2: the round-4 L2-bucket scatter)
     Timings t;
     PhaseState st;
     DenseState dn;

@@ -1166,16 +1166,15 @@ def test_label_buckets_equal_direct_scatter(native, cfg, n):
     """PD_OPT_LABEL_BUCKETS (default on): the labels reach input order through
     the bucketed (point, key) pair passes instead of one scattered write per
     owner record — identical labels and core flags from the block-local pass
-    (1: buckets of 2^15 points in LDS), the L2-bucket scatter (2: buckets of
-    2^19), the two-level pass that C4's 1e9 points take (3: 2^19-point buckets
-    split into block-local ones) and the direct scatter (0); several buckets,
+    (1: 2^19-point buckets split into 2^15-point ones placed in LDS), the
+    round-4 L2-bucket scatter (2) and the direct scatter (0); several buckets,
     partial last bucket, noise and border points included."""
     from pypardis_amd import DBSCAN, synth
     X, c = synth.make_config(cfg, n=n, device="cuda" if cfg == "C4" else "cpu")
     Xd = X if torch.is_tensor(X) else _dev(X)
     ctx = native.context()
     outs = []
-    for on in (1, 2, 3, 0):
+    for on in (1, 2, 0):
         ctx.set_option(native.PD_OPT_LABEL_BUCKETS, on)
         try:
             m = DBSCAN(eps=c["eps"], min_samples=c["min_samples"],

@@ -566,24 +566,27 @@ __device__ __forceinline__ void halo_record(const T (&tv)[D], const PartGrid& g,
 // The grid fields a record key needs, per neighbourhood, staged in LDS: the
 // lanes of a wave key their points in different neighbourhoods, and per-lane
 // global loads of the grids cost more than the arithmetic.
+// The linear cell index is accumulated in double: every term is an integer
+// and the grid has fewer than 2^53 cells (checked on the host), so each fma
+// is exact and equals the int64 form, with one conversion per key instead of
+// one per axis (the halo write is VALU-issue bound).
 template <int D>
 struct KeyGrid {
     double lo[D], inv[D];
-    int64_t nc[D];
+    double nc[D], top[D];   // cells per axis, and the last cell index
     uint64_t base;
 };
 
 template <typename T, int D, typename K>
 __device__ __forceinline__ K key_of(const T (&tv)[D], const KeyGrid<D>& g) {
-    uint64_t k = 0;
+    double k = 0.0;
 #pragma unroll
     for (int j = D - 1; j >= 0; --j) {
-        int64_t q = (int64_t)floor(((double)tv[j] - g.lo[j]) * g.inv[j]);
-        q = q < 0 ? 0 : q;
-        q = q >= g.nc[j] ? g.nc[j] - 1 : q;
-        k = k * (uint64_t)g.nc[j] + (uint64_t)q;
+        double q = floor(((double)tv[j] - g.lo[j]) * g.inv[j]);
+        q = fmin(fmax(q, 0.0), g.top[j]);
+        k = fma(k, g.nc[j], q);
     }
-    return (K)(g.base + k);
+    return (K)(g.base + (uint64_t)k);
 }
 
 // Records of a tile in (wave, step, lane, neighbourhood) order:
@@ -632,7 +635,8 @@ __global__ __launch_bounds__(kBlock) void halo_write_kernel(
             for (int j = 0; j < D; ++j) {
                 kg[L].lo[j] = parts[L].lo[j];
                 kg[L].inv[j] = parts[L].inv[j];
-                kg[L].nc[j] = parts[L].nc[j];
+                kg[L].nc[j] = (double)parts[L].nc[j];
+                kg[L].top[j] = (double)(parts[L].nc[j] - 1);
             }
             kg[L].base = parts[L].base;
         }
@@ -2613,6 +2617,8 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     hipStream_t s = a.stream;
     const uint64_t n = (uint64_t)a.n;
     const int P = a.P;
+    // key_of accumulates cell indices in double (exact below 2^53 cells)
+    if (Gtot >= (1ull << 53)) throw Error(-5, "eps grid of 2^53 cells or more");
     tm.mark();   // 0
 
     PartGrid* parts = ctx.arena.get<PartGrid>("parts", P);

@@ -3055,7 +3055,6 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
             hipLaunchKernelGGL(remap_kernel, dim3(blocks(R)), dim3(kBlock), 0, s, R, core, par,
                                a.map_ids, a.map_keys, (uint32_t)a.n_map, cm, gmin, shard_err);
     }
-    uint32_t* key_out = a.phase == 2 ? a.keys_out : ctx.arena.get<uint32_t>("key_out", n);
     // core flags travel in the keys: single device bit 30 (ids < 2^30);
     // sharded (global ids) bit 31 when the caller vouches for ids < 2^31
     // (PD_OPT_SHARD_CORE_BIT), else a byte scattered per owner record
@@ -3066,16 +3065,19 @@ void run_b(Ctx& ctx, TrainArgs& a, EvTimer& tm) {
     // single device, no counts wanted: labels reach input order through the
     // bucketed pair passes instead of owner_kernel's scatter
     // (ctx.label_buckets, PD_OPT_LABEL_BUCKETS)
-    // (automatic from 2^22 points since the block-local second pass: C2 1e8
-    // border + label 4.35 -> 3.79 ms, C1 1e7 0.33 -> 0.29 ms, round 5)
+    // (automatic from 2^22 points since the block-local passes: C2 1e8
+    // border + label 4.35 -> 3.65 ms, C1 1e7 0.33 -> 0.29 ms, round 5)
     const bool want_buckets = ctx.label_buckets > 0 || (ctx.label_buckets < 0 && n >= (1ull << 22));
     const bool bucketed = a.phase != 2 && core_bit && !a.counts && want_buckets && n > 0;
-    // block-local label pass (C2-sized n): every label is written from LDS,
-    // so key_out is neither filled nor used
-    // (the coarse buckets split into block-local ones; PD_OPT_LABEL_BUCKETS
-    // 2: the L2-bucket scatter instead)
+    // block-local passes (coarse buckets split into 2^15-point ones, each
+    // written from an LDS image): every label and core flag is written there,
+    // so there is no key_out buffer, fill or key -> label pass.
+    // PD_OPT_LABEL_BUCKETS 2: the round-4 L2-bucket scatter instead
     const uint64_t nbkL = (n + (1ull << kLabBitsL) - 1) >> kLabBitsL;
     const bool local = bucketed && R && ctx.label_buckets != 2;
+    uint32_t* key_out = a.phase == 2 ? a.keys_out
+                        : local      ? nullptr
+                                     : ctx.arena.get<uint32_t>("key_out", n);
     if (!local) PD_HIP(hipMemsetAsync(key_out, 0xFF, sizeof(uint32_t) * n, s));
     if (R) {
         uint32_t* blist = ctx.arena.get<uint32_t>("border_list", R);

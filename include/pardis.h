@@ -191,7 +191,9 @@ int32_t pd_kd_radix_hist(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, i
 
 /* The record sort of pd_train on caller arrays (utility; exposed so the
  * kernel can be tested on its own): stable LSD radix sort of n (key, value)
- * pairs by key bits [0, key_bits), in place.  keys: device uint32 (key_bytes
+ * pairs by key bits [0, key_bits), in place (bits at and above key_bits are
+ * ignored: pairs whose keys agree below key_bits keep their input order).
+ * keys: device uint32 (key_bytes
  * 4) or uint64 (8); vals: device uint32.  n < 2^32 - 1.  It is the shuffle
  * by neighbourhood that R:dbscan/dbscan.py:116-118 (partitionBy) performs,
  * keyed by (neighbourhood, cell). */

@@ -2559,11 +2559,14 @@ void launch_border(hipStream_t s, const T* Xs, uint32_t NL, const uint32_t* list
 
 // The record sort: the library's onesweep (rsort.hpp), stable, bits [0,
 // key_bits).  Its look-back words and ticket live in the arena and are
-// zeroed only when (re)allocated.  (PD_SORT_ROCPRIM=1 builds rocPRIM's
-// radix_sort_pairs instead, for A/B runs.)
+// zeroed only when (re)allocated.  hist_zeroed (required): true only where
+// the caller knows "rsort_hist" was zeroed on the stream since its last use
+// (the train's halo tile pass does it; the scan then overwrites the
+// histograms with offsets, so a second sort must pass false).
+// (PD_SORT_ROCPRIM=1 builds rocPRIM's radix_sort_pairs instead, for A/B runs.)
 template <typename K>
 void sort_records(Ctx& ctx, K*& keys, uint32_t*& vals, K* keys2, uint32_t* vals2, uint64_t R,
-                  int key_bits, hipStream_t s, bool hist_zeroed = true) {
+                  int key_bits, hipStream_t s, bool hist_zeroed) {
 #if PD_SORT_ROCPRIM
     rocprim::double_buffer<K> kb(keys, keys2);
     rocprim::double_buffer<uint32_t> vb(vals, vals2);
@@ -2716,7 +2719,8 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     // the merge's representative per point, initialised for the points of the
     // duplicated records only (by the gather, which lists them), not a fill over n
     uint32_t* rep = P > 1 ? ctx.arena.get<uint32_t>("rep", n) : nullptr;
-    sort_records<K>(ctx, keys, vals, keys2, vals2, (uint64_t)R, key_bits, s);
+    sort_records<K>(ctx, keys, vals, keys2, vals2, (uint64_t)R, key_bits, s,
+                    /*hist_zeroed=*/!PD_SORT_ROCPRIM);   // by halo_tile_kernel above
     tm.mark();   // 2
     hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X, (uint64_t)R,
                        vals, Xs, dup_list, lcount, rep);

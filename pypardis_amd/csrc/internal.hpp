@@ -151,7 +151,7 @@ struct Ctx {
     bool seq_moments = false;    // reference-order (sequential) KD moment sums
     int xsub = 2;                // axis-0 sub-cells per eps
     int centre_window = -1;      // window union: records after each record tested (2..64);
-                                 // < 0 (default): 4 or 16 by cell occupancy
+                                 // < 0 (default): 2, 8 or 16 by records per occupied cell
     int count_rotate = 1024;     // count sweep: lists longer than this start near the query (0: off)
     int count_replay = 0;        // PD_OPT_COUNT_REPLAY: replicas of the count sweep to time (0: off)
     // the record sort's look-back words (rsort.hpp): zeroed when allocated,

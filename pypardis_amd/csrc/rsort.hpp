@@ -45,12 +45,14 @@ __device__ __forceinline__ uint32_t digit_of(uint64_t k, int shift) {
     return (uint32_t)(k >> shift) & 0xFFu;
 }
 
-// Digit histograms of `places` passes (place p: bits [8p + begin, +8)), one
+// Digit histograms of `places` passes (place p: bits [8p + begin, +8), the
+// last place's digit masked by last_mask so only the sorted bits count), one
 // read of the keys (16-byte loads), each wave counting into its own LDS copy
 // (no atomics between waves).  hist: places x 256 uint32, zeroed by the caller.
 template <typename K>
 __global__ __launch_bounds__(kThreads) void hist_kernel(const K* __restrict__ keys, uint64_t n,
                                                         int begin, int places, int vec,
+                                                        uint32_t last_mask,
                                                         uint32_t* __restrict__ hist) {
     constexpr int NW = kThreads / 64, V = 16 / sizeof(K);   // keys per 16-byte load
     __shared__ uint32_t h[NW][8][kRadix];
@@ -66,13 +68,15 @@ __global__ __launch_bounds__(kThreads) void hist_kernel(const K* __restrict__ ke
         __builtin_memcpy(k, &q, 16);
 #pragma unroll
         for (int u = 0; u < V; ++u)
-            for (int p = 0; p < places; ++p) atomicAdd(&h[w][p][digit_of(k[u], begin + 8 * p)], 1u);
+            for (int p = 0; p < places; ++p)
+                atomicAdd(&h[w][p][digit_of(k[u], begin + 8 * p) & (p == places - 1 ? last_mask : 0xFFu)], 1u);
     }
     // the tail (< V keys; every key when unaligned)
     for (uint64_t i = nv * V + (uint64_t)blockIdx.x * kThreads + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * kThreads) {
         const K k = keys[i];
-        for (int p = 0; p < places; ++p) atomicAdd(&h[w][p][digit_of(k, begin + 8 * p)], 1u);
+        for (int p = 0; p < places; ++p)
+            atomicAdd(&h[w][p][digit_of(k, begin + 8 * p) & (p == places - 1 ? last_mask : 0xFFu)], 1u);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < places * kRadix; i += kThreads) {
@@ -119,7 +123,9 @@ __device__ __forceinline__ void st_lb(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One pass over bits [shift, shift + 8).  goff: this place's exclusive digit
+// One pass over bits [shift, shift + 8) & dmask (dmask < 0xFF on the last
+// pass when the key width is not a multiple of 8: the bits above it are not
+// sorted, as rocPRIM's begin/end bits).  goff: this place's exclusive digit
 // offsets; look: ntiles x 256 look-back words (tag << 32 | count; tag =
 // 2 epoch + 1 aggregate of the tile alone, 2 epoch + 2 inclusive of all tiles
 // up to it; older tags read as not yet published); ticket: 64-bit counter,
@@ -128,7 +134,7 @@ template <typename K, int I = Tile<K>::kItems, int NT = Tile<K>::kThreads>
 __global__ __launch_bounds__(NT) void pass_kernel(const K* __restrict__ kin,
                                                   const uint32_t* __restrict__ vin,
                                                   K* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                  uint64_t n, int shift,
+                                                  uint64_t n, int shift, uint32_t dmask,
                                                   const uint32_t* __restrict__ goff,
                                                   uint64_t* __restrict__ look, uint32_t epoch,
                                                   unsigned long long* __restrict__ ticket,
@@ -168,7 +174,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(const K* __restrict__ kin,
     for (int j = 0; j < I; ++j) {
         const uint32_t i = wbase + 64 * j + lane;
         const bool ok = i < tn;
-        const uint32_t d = digit_of(k[j], shift);
+        const uint32_t d = digit_of(k[j], shift) & dmask;
         unsigned long long m = __ballot(ok);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
@@ -235,7 +241,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(const K* __restrict__ kin,
     for (int j = 0; j < I; ++j) {
         const uint32_t i = wbase + 64 * j + lane;
         if (i < tn) {
-            const uint32_t dj = digit_of(k[j], shift);
+            const uint32_t dj = digit_of(k[j], shift) & dmask;
             const uint32_t p = dbase[dj] + wcnt[w][dj] + rk[j];
             sk[p] = k[j];
             sv[p] = v[j];
@@ -245,7 +251,7 @@ __global__ __launch_bounds__(NT) void pass_kernel(const K* __restrict__ kin,
     // contiguous runs per digit
     for (uint32_t i = tid; i < tn; i += NT) {
         const K key = sk[i];
-        const uint32_t dk = digit_of(key, shift);
+        const uint32_t dk = digit_of(key, shift) & dmask;
         const uint64_t g = (uint64_t)gbase[dk] + (i - dbase[dk]);
         kout[g] = key;
         vout[g] = sv[i];
@@ -269,22 +275,24 @@ inline uint64_t tiles_for(uint64_t n, int key_bytes) {
 }
 
 // Sort (k0, v0) by key bits [0, bits) through the double buffer (k1, v1); the
-// sorted pairs end in (*kres, *vres), one of the two.  Stable.  st.look must
-// hold tiles_for(n) tiles; st.hist 8 x 256; st.ticket one counter.
+// sorted pairs end in (*kres, *vres), one of the two.  Stable; bits at and
+// above `bits` are ignored (pairs equal in [0, bits) keep their input order).
+// st.look must hold tiles_for(n) tiles; st.hist 8 x 256; st.ticket one counter.
 // hist_zeroed: the caller already zeroed st.hist (8 x 256) on the stream.
 template <typename K, int I = Tile<K>::kItems, int NT = Tile<K>::kThreads>
 void sort_pairs(State& st, K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n, int bits,
-                hipStream_t s, K** kres, uint32_t** vres, bool hist_zeroed = false) {
+                hipStream_t s, K** kres, uint32_t** vres, bool hist_zeroed) {
     *kres = k0;
     *vres = v0;
     if (n == 0 || bits <= 0) return;
     const int places = (bits + 7) / 8;
-    if (places > 8) throw Error(-5, "rsort: more than 64 key bits");
+    if (places > 8 || bits > 8 * (int)sizeof(K)) throw Error(-5, "rsort: key bits beyond the key");
+    const uint32_t last_mask = (bits % 8) ? (1u << (bits % 8)) - 1u : 0xFFu;
     if (!hist_zeroed) PD_HIP(hipMemsetAsync(st.hist, 0, sizeof(uint32_t) * kRadix * places, s));
     const unsigned hb = (unsigned)std::min<uint64_t>(2048, (n + kThreads - 1) / kThreads);
     const int vec = ((uintptr_t)k0 & 15) == 0 ? 1 : 0;
     hipLaunchKernelGGL((hist_kernel<K>), dim3(hb), dim3(kThreads), 0, s, k0, n, 0, places, vec,
-                       st.hist);
+                       last_mask, st.hist);
     hipLaunchKernelGGL(hist_scan_kernel, dim3(1), dim3(kRadix), 0, s, st.hist, places, st.ticket);
     const uint64_t tiles = (n + (uint64_t)NT * I - 1) / ((uint64_t)NT * I);
     if (tiles > st.look_tiles) throw Error(-5, "rsort: look-back buffer too small");
@@ -301,7 +309,8 @@ void sort_pairs(State& st, K* k0, uint32_t* v0, K* k1, uint32_t* v1, uint64_t n,
         // leaves words a later pass could take for its own)
         const uint32_t ep = st.epoch++;
         hipLaunchKernelGGL((pass_kernel<K, I, NT>), dim3((unsigned)tiles), dim3(NT), 0, s, ki, vi, ko,
-                           vo, n, 8 * p, st.hist + p * kRadix, st.look, ep, st.ticket,
+                           vo, n, 8 * p, p == places - 1 ? last_mask : 0xFFu,
+                           st.hist + p * kRadix, st.look, ep, st.ticket,
                            (unsigned long long)p * tiles);
         PD_HIP(hipGetLastError());
         std::swap(ki, ko);

@@ -111,14 +111,37 @@ class _Neighborhoods(dict):
         return iter(self.items())
 
 
+def _partition_records(X, keys, n_parts, members, cluster, params):
+    """The reference's per-partition records (R:dbscan/dbscan.py:116-125 with
+    dbscan_partition, :12-34): for each neighbourhood L (partitionBy order)
+    and each of its points in input order, ``(key, 'L:c')`` or ``(key,
+    'L:c*')`` — c the neighbourhood's own sklearn label of the point, '*' a
+    non-core point.  members(L) -> ascending point indices of neighbourhood
+    L; cluster(X_L, eps, min_samples, metric) -> (labels, core) numpy."""
+    recs = []
+    metric = _native.metric_code(params.get('metric', 'euclidean'))
+    for L in range(n_parts):
+        idx = np.asarray(members(L), np.int64)
+        if not len(idx):
+            continue
+        XL = X[torch.from_numpy(idx).to(X.device)].contiguous()
+        lab, core = cluster(XL, params['eps'], params['min_samples'], metric)
+        recs.extend((k, '%i:%i%s' % (L, c, '' if f else '*'))
+                    for k, c, f in zip(keys[idx].tolist(), np.asarray(lab).tolist(),
+                                       np.asarray(core).tolist()))
+    return recs
+
+
+def _device_cluster(X, eps, min_samples, metric):
+    lab, core, _, _ = _native.cluster(X, eps, min_samples, metric)
+    return lab.cpu().numpy(), core.cpu().numpy()
+
+
 class _PartitionRecords(object):
     """``DBSCAN.data`` after ``train`` (R:dbscan/dbscan.py:116-125): the
-    records of the per-partition clustering — for each neighbourhood L (the
-    reference's partitionBy order) and each of its points in input order,
-    ``(key, 'L:c')`` or ``(key, 'L:c*')`` with c the neighbourhood's own
-    sklearn label of the point and '*' for a non-core point (dbscan_partition,
-    R:dbscan/dbscan.py:12-34).  Built lazily on first use, one pd_cluster per
-    neighbourhood; the global labels never depend on it."""
+    records of the per-partition clustering (_partition_records).  Built
+    lazily on first use, one pd_cluster per neighbourhood; the global labels
+    never depend on it."""
 
     def __init__(self, neighbors, params):
         self.neighbors = neighbors
@@ -127,21 +150,10 @@ class _PartitionRecords(object):
 
     def _build(self):
         if self._recs is None:
-            recs = []
-            pts = self.neighbors.points
-            metric = _native.metric_code(self.params.get('metric', 'euclidean'))
-            for L in sorted(self.neighbors):
-                idx = self.neighbors[L].indices()
-                if not len(idx):
-                    continue
-                X = pts.X[torch.from_numpy(np.asarray(idx, np.int64)).to(pts.X.device)]
-                lab, core, _, _ = _native.cluster(X.contiguous(), self.params['eps'],
-                                                  self.params['min_samples'], metric)
-                lab, core = lab.cpu().numpy(), core.cpu().numpy()
-                keys = self.neighbors[L].keys().tolist()
-                recs.extend((k, '%i:%i%s' % (L, c, '' if f else '*'))
-                            for k, c, f in zip(keys, lab.tolist(), core.tolist()))
-            self._recs = recs
+            nb = self.neighbors
+            self._recs = _partition_records(nb.points.X, nb.points.key_array(), len(nb),
+                                            lambda L: nb[L].indices(), _device_cluster,
+                                            self.params)
         return self._recs
 
     def collect(self):
@@ -155,6 +167,55 @@ class _PartitionRecords(object):
 
     def __iter__(self):
         return iter(self._build())
+
+
+class _ShardedPartitionRecords(_PartitionRecords):
+    """``DBSCAN.data`` after a sharded train: the same records as one device
+    would give for the union of every rank's slice (global input order =
+    rank order), like the reference's one RDD over all executors.  The
+    neighbourhoods span ranks, so ``collect()`` / ``take()`` / iteration are
+    collectives (every rank calls them): the slices are all-gathered (keys and
+    coordinates, the reference's ``collect`` to the driver), then each
+    neighbourhood is clustered on this rank's device (``ops``: pd_halo_members
+    + pd_cluster).  ``count()`` all-reduces the neighbourhood sizes of the
+    local slices (a collective too)."""
+
+    def __init__(self, points, gid_base, ebox, params, group, ops):
+        self.points = points
+        self.gid_base = gid_base
+        self.ebox = np.ascontiguousarray(ebox, np.float64)
+        self.params = params
+        self.group = group
+        self.ops = ops
+        self._recs = None
+
+    def _local_keys(self):
+        if self.points.keys is None:
+            return self.gid_base + np.arange(self.points.n, dtype=np.int64)
+        return np.asarray(self.points.key_array())
+
+    def _build(self):
+        if self._recs is None:
+            import torch.distributed as dist
+            parts = [None] * dist.get_world_size(self.group)
+            dist.all_gather_object(parts, (self._local_keys(), self.points.X.cpu().numpy()),
+                                   group=self.group)
+            keys = np.concatenate([p[0] for p in parts])
+            X = torch.from_numpy(np.ascontiguousarray(np.concatenate([p[1] for p in parts])))
+            X = X.to(self.ops.device)
+            counts, members = self.ops.halo_members(X, self.ebox)
+            off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+            self._recs = _partition_records(X, keys, len(self.ebox),
+                                            lambda L: members[off[L]:off[L + 1]],
+                                            self.ops.cluster, self.params)
+        return self._recs
+
+    def count(self):
+        import torch.distributed as dist
+        counts, _ = self.ops.halo_members(self.points.X.to(self.ops.device), self.ebox)
+        t = torch.tensor([int(np.sum(counts))], dtype=torch.int64)
+        dist.all_reduce(t, group=self.group)
+        return int(t.item())
 
 
 class _Assignments(object):
@@ -220,7 +281,10 @@ class DBSCAN(object):
     :min_samples: minimum number of samples within radius eps
     :metric: distance metric (euclidean or cityblock, string or scipy callable)
     :max_partitions: maximum number of partitions used by KDPartitioner
-    :data: the training points (PointSet: keys + device coordinates)
+    :data: before ``train`` None; after it the reference's per-partition
+        records ``(key, 'L:c[*]')`` as an RDD-like object (``collect``,
+        ``count``, ``take``, iteration; R:dbscan/dbscan.py:116-125) — after a
+        sharded train the same records over all ranks, its calls collectives
     :result: (key, cluster label) pairs, sorted by key, via ``collect()``
     :bounding_boxes: label -> BoundingBox of each KD partition
     :expanded_boxes: label -> BoundingBox grown by 2·eps
@@ -351,8 +415,13 @@ class DBSCAN(object):
         P = self.max_partitions if self.max_partitions is not None else 4 ** points.d
         return int(P)
 
-    def _set_sharded(self, points, labels, core, res, result):
-        self.data = points
+    def _set_sharded(self, points, labels, core, res, result, group=None, ops=None):
+        ebox = np.ascontiguousarray(res.boxes, np.float64)
+        params = {'eps': self.eps, 'min_samples': self.min_samples, 'metric': self.metric}
+        if group is not None:
+            self.data = _ShardedPartitionRecords(points, res.gid_base, ebox, params, group, ops)
+        else:   # one process holds every slice: the single-device records
+            self.data = None
         self.labels_ = labels
         self.core_sample_mask_ = core
         self.n_clusters_ = res.n_clusters
@@ -360,6 +429,8 @@ class DBSCAN(object):
         self.expanded_boxes = {L: box.expand(2 * self.eps)
                                for L, box in sorted(res.bounding_boxes.items())}
         self.neighbors = _Neighborhoods(points, self.expanded_boxes)
+        if group is None:
+            self.data = _PartitionRecords(self.neighbors, params)
         self.result = result
         self.shard = res
         return self
@@ -372,7 +443,9 @@ class DBSCAN(object):
                                         max_partitions=P, group=group,
                                         keep_owned=self.keep_shard_records)
         result = _ShardedAssignments(points, res.local_labels, res.gid_base, res.n_total, group)
-        return self._set_sharded(points, res.local_labels, res.local_core, res, result)
+        ops = distributed.NativeOps(points.X.device)
+        return self._set_sharded(points, res.local_labels, res.local_core, res, result,
+                                 group, ops)
 
     def _train_devices(self, data, metric):
         from . import distributed

@@ -44,6 +44,7 @@ this rank's GPU).  Collectives run on ``comm_device``: the GPU under RCCL
 """
 from __future__ import annotations
 
+import heapq
 import time
 
 import numpy as np
@@ -90,6 +91,15 @@ class NativeOps(object):
 
     def split(self, X, labels, sel, axes, boundary, new):
         _native.kd_split(X, labels, sel, axes, boundary, new, ctx=self.ctx)
+
+    # -- per-neighbourhood records (DBSCAN.data after a sharded train)
+    def halo_members(self, X, ebox):
+        counts, members = _native.halo_members(X, ebox, ctx=self.ctx)
+        return counts, members.cpu().numpy()
+
+    def cluster(self, X, eps, min_samples, metric):
+        lab, core, _, _ = _native.cluster(X, eps, min_samples, metric, ctx=self.ctx)
+        return lab.cpu().numpy(), core.cpu().numpy()
 
     # -- routing
     def route(self, X, ebox, part_rank, world):
@@ -218,7 +228,7 @@ def dd_combine(parts):
     return mom
 
 
-def partition_ranks(P, world, weights=None, order=None, method=None):
+def partition_ranks(P, world, weights=None, order=None, method=None, chosen=None):
     """Neighbourhood -> rank, and each neighbourhood's index among its rank's
     neighbourhoods (ascending label, so a rank's records keep the KD order).
 
@@ -234,7 +244,10 @@ def partition_ranks(P, world, weights=None, order=None, method=None):
           (ties: smaller label), each to the least-loaded rank (ties: smaller
           rank); the better balance on skewed leaves, at no locality;
       None — 'ordered' unless its largest load exceeds LPT's by more than 5 %.
-    Labels do not depend on the placement (any assignment is exact)."""
+    ``chosen``: an optional dict that receives {'placement': the method used}.
+    Labels do not depend on the placement (any assignment is exact).
+    Cost: O(P log P) for both methods (P up to 65536 leaves)."""
+    used = "blocks"
     if weights is None or P <= world:
         part_rank = np.array([L * world // P for L in range(P)], np.int32)
     else:
@@ -242,18 +255,22 @@ def partition_ranks(P, world, weights=None, order=None, method=None):
         if w.shape != (P,):
             raise ValueError("one weight per partition expected")
         lpt = np.zeros(P, np.int32)
-        load = np.zeros(world, np.float64)
-        for L in sorted(range(P), key=lambda L: (-w[L], L)):
-            r = int(np.argmin(load))   # first minimum: the smallest rank on ties
+        # heaviest first onto the least-loaded rank (a heap of (load, rank):
+        # ties go to the smaller rank, as argmin's first minimum did)
+        heap = [(0.0, r) for r in range(world)]
+        for L in np.lexsort((np.arange(P), -w)):
+            load, r = heapq.heappop(heap)
             lpt[L] = r
-            load[r] += w[L]
-        part_rank = lpt
+            heapq.heappush(heap, (load + w[L], r))
+        part_rank, used = lpt, "lpt"
         if method in (None, "ordered") and order is not None:
-            ordd = _ordered_cut(w, list(order), world)
+            ordd = _ordered_cut(w, order, world)
             lo = np.bincount(ordd, weights=w, minlength=world).max()
             ll = np.bincount(lpt, weights=w, minlength=world).max()
             if method == "ordered" or lo <= 1.05 * ll:
-                part_rank = ordd
+                part_rank, used = ordd, "ordered"
+    if chosen is not None:
+        chosen["placement"] = used
     local_index = np.zeros(P, np.int32)
     for r in range(world):
         idx = np.nonzero(part_rank == r)[0]
@@ -261,47 +278,72 @@ def partition_ranks(P, world, weights=None, order=None, method=None):
     return part_rank, local_index
 
 
+def _greedy_runs(S, V):
+    """Run starts of the greedy cut of prefix sums S into runs of weight <= V
+    (each run as long as it may be)."""
+    P = len(S) - 1
+    starts, i = [], 0
+    while i < P:
+        starts.append(i)
+        j = int(np.searchsorted(S, S[i] + V, side="right")) - 1
+        i = max(j, i + 1)   # a run holds at least one leaf
+    return starts
+
+
 def _ordered_cut(w, order, world):
     """Leaves in `order` cut into min(world, P) non-empty contiguous runs with
-    the smallest possible largest run weight (dynamic programme over the
-    prefix sums, O(world P^2)); run k -> rank k."""
-    ws = np.array([float(w[L]) for L in order], np.float64)
+    the smallest possible largest run weight; run k -> rank k.
+
+    The smallest feasible bound V is found by bisection over the real line
+    with the greedy cut as the feasibility test (a cut into <= K runs of
+    weight <= V exists iff the greedy one uses <= K runs; monotone in V), so
+    the cost is O(K log P) per step and O(P) memory — no (P+1)^2 tables.
+    Runs are then split (never raising the largest) until there are K."""
+    order = np.asarray(order, np.int64)
+    ws = np.asarray(w, np.float64)[order]
     P = len(ws)
     K = min(world, P)
     S = np.concatenate([[0.0], np.cumsum(ws)])
-    INF = np.inf
-    dp = np.full(P + 1, INF)
-    dp[1:] = S[1:]                       # one run over the first i leaves
-    arg = np.zeros((K + 1, P + 1), np.int64)
-    jj = np.arange(P + 1)[:, None]
-    ii = np.arange(P + 1)[None, :]
-    for k in range(2, K + 1):
-        cost = np.maximum(dp[:, None], S[None, :] - S[:, None])   # [j, i]
-        cost = np.where((jj < ii) & (jj >= k - 1), cost, INF)
-        arg[k] = np.argmin(cost, axis=0)
-        dp = cost[arg[k], np.arange(P + 1)]
-    # walk the cuts back from (K, P)
-    cuts, i = [P], P
-    for k in range(K, 1, -1):
-        i = int(arg[k][i])
-        cuts.append(i)
-    cuts.append(0)
-    cuts = cuts[::-1]                    # run k = leaves [cuts[k], cuts[k + 1])
-    part_rank = np.zeros(len(w), np.int32)
+    lo, hi = float(ws.max()), float(S[-1])
+    if len(_greedy_runs(S, lo)) > K:
+        for _ in range(200):
+            mid = 0.5 * (lo + hi)
+            if not lo < mid < hi:
+                break
+            if len(_greedy_runs(S, mid)) <= K:
+                hi = mid
+            else:
+                lo = mid
+        V = hi
+    else:
+        V = lo
+    starts = _greedy_runs(S, V)
+    # fewer than K runs: split the last multi-leaf runs until there are K
+    bounds = starts + [P]
+    while len(bounds) - 1 < K:
+        for k in range(len(bounds) - 2, -1, -1):
+            if bounds[k + 1] - bounds[k] > 1:
+                bounds.insert(k + 1, bounds[k + 1] - 1)
+                break
+    part_rank = np.zeros(len(ws), np.int32)
     for k in range(K):
-        for pos in range(cuts[k], cuts[k + 1]):
-            part_rank[order[pos]] = k
+        part_rank[order[bounds[k]:bounds[k + 1]]] = k
     return part_rank
 
 
 def kd_leaf_order(splits):
     """KD leaves in depth-first (spatial) order: a split (cur -> cur, new)
-    replaces cur by [cur (v < boundary), new] (R:dbscan/partition.py:66-68)."""
-    seq = [0]
+    replaces cur by [cur (v < boundary), new] (R:dbscan/partition.py:66-68).
+    Built from the tree in O(P): a label's later splits nest inside it, so
+    label L expands to L, then the subtrees of its new labels, latest first."""
+    kids = {}
     for sp in splits:
-        cur, nl = int(sp[0]), int(sp[1])
-        i = seq.index(cur)
-        seq[i:i + 1] = [cur, nl]
+        kids.setdefault(int(sp[0]), []).append(int(sp[1]))
+    seq, stack = [], [0]
+    while stack:
+        L = stack.pop()
+        seq.append(L)
+        stack.extend(kids.get(L, ()))   # popped latest-first
     return seq
 
 
@@ -793,14 +835,9 @@ def train_sharded(X, eps, min_samples, metric=_native.PD_EUCLIDEAN, max_partitio
     if placement != "blocks" and P > W:
         weights = leaf_sizes(splits, n_total, P)
         order = kd_leaf_order(splits)
-    part_rank, local_index = partition_ranks(P, W, weights, order, placement)
-    if weights is None:
-        stats["placement"] = "blocks"
-    elif placement in ("lpt", "ordered"):
-        stats["placement"] = placement
-    else:
-        chk, _ = partition_ranks(P, W, weights, order, "ordered")
-        stats["placement"] = "ordered" if np.array_equal(chk, part_rank) else "lpt"
+    chosen = {}
+    part_rank, local_index = partition_ranks(P, W, weights, order, placement, chosen)
+    stats["placement"] = chosen["placement"]
     if W == 1:
         # every neighbourhood is here: the slice is the record set as it is
         Xr, gid, owner, xr = X, None, kdlab, None

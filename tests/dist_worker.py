@@ -58,7 +58,11 @@ def run_rank(rank, world, port, X, eps, min_samples, metric, P, out_dir, native,
             model.train(data)
             res = model.shard
             pairs = model.assignments()
+            recs = model.data.collect()   # a collective: every rank calls it
             extra = dict(n_clusters_=np.int64(model.n_clusters_),
+                         data_keys=np.array([str(k) for k, _ in recs]),
+                         data_recs=np.array([v for _, v in recs]),
+                         data_count=np.int64(model.data.count()),
                          boxes_api=np.array([model.bounding_boxes[L].as_array()
                                              for L in sorted(model.bounding_boxes)]),
                          assign_keys=np.array([str(k) for k, _ in pairs]),

@@ -93,6 +93,21 @@ class OracleOps(object):
             m = (lab == L) & (x[:, axes[s]] >= boundary[s])
             lab[m] = new[s]
 
+    def halo_members(self, X, ebox):
+        """pd_halo_members restated (R:dbscan/dbscan.py:136-151, inclusive
+        contains): per neighbourhood its point indices, ascending."""
+        x = X.numpy().astype(np.float64)
+        ebox = np.asarray(ebox, np.float64)
+        mem = [np.nonzero(np.all(x >= ebox[L, 0], 1) & np.all(x <= ebox[L, 1], 1))[0]
+               for L in range(len(ebox))]
+        return np.array([len(m) for m in mem], np.int64), \
+            (np.concatenate(mem) if mem else np.zeros(0, np.int64)).astype(np.int64)
+
+    def cluster(self, X, eps, min_samples, metric):
+        lab, core, _, _ = oracle.dbscan(X.numpy(), eps, min_samples,
+                                        ["euclidean", "cityblock"][metric])
+        return lab, core
+
     def route(self, X, ebox, part_rank, world):
         x = X.numpy().astype(np.float64)
         mask = np.zeros(len(x), np.int64)

@@ -98,6 +98,68 @@ def test_partition_ranks_ordered():
     assert set(pr.tolist()) == set(range(8))
 
 
+def _dp_cut_max(w, order, world):
+    """The smallest largest run load of a cut of `order` into min(world, P)
+    contiguous runs, by the O(world P^2) dynamic programme (the round-5 form)."""
+    ws = np.asarray(w, np.float64)[list(order)]
+    P = len(ws)
+    S = np.concatenate([[0.0], np.cumsum(ws)])
+    dp = S.copy()
+    dp[0] = np.inf
+    for _ in range(2, min(world, P) + 1):
+        nd = np.full(P + 1, np.inf)
+        for i in range(1, P + 1):
+            nd[i] = min((max(dp[j], S[i] - S[j]) for j in range(1, i)), default=np.inf)
+        dp = nd
+    return dp[P]
+
+
+def test_ordered_cut_is_optimal_and_scales():
+    """the ordered cut by bisection + greedy feasibility is as good
+    as the exact dynamic programme (random small cases), every rank gets a
+    non-empty contiguous run, and P = 65536 leaves over 8 ranks costs
+    O(P log P) — no (P+1)^2 tables; kd_leaf_order is built from the tree."""
+    import collections
+    import time
+    from pypardis_amd.distributed import _ordered_cut, kd_leaf_order
+    rng = np.random.default_rng(5)
+    for t in range(120):
+        P, W = int(rng.integers(1, 24)), int(rng.integers(1, 9))
+        w = rng.zipf(1.5, P).astype(np.float64) if t % 2 else rng.random(P) + 0.1
+        order = list(rng.permutation(P))
+        pr = _ordered_cut(w, order, W)
+        assert len(set(pr.tolist())) == min(W, P)
+        runs = [int(pr[L]) for L in order]
+        assert runs == sorted(runs)
+        best = _dp_cut_max(w, order, W)
+        assert np.bincount(pr, weights=w).max() <= best * (1 + 1e-12)
+    # a BFS schedule of 65536 leaves (labels as _create_partitions assigns them)
+    P, splits, nxt, q = 65536, [], 1, collections.deque([0])
+    while nxt < P:
+        level, q = list(q), collections.deque()
+        for c in level:
+            if nxt < P:
+                splits.append((c, nxt, 0, 0, 0, 0))
+                q.extend([c, nxt])
+                nxt += 1
+            else:
+                q.append(c)
+    t0 = time.perf_counter()
+    order = kd_leaf_order(splits)
+    assert sorted(order) == list(range(P))
+    w = rng.zipf(1.3, P).astype(np.float64)
+    pr, li = partition_ranks(P, 8, w, order, "ordered")
+    assert time.perf_counter() - t0 < 10.0
+    assert set(pr.tolist()) == set(range(8))
+    assert [int(pr[L]) for L in order] == sorted(int(pr[L]) for L in order)
+    # the depth-first order equals the splice-based definition on a small tree
+    seq = [0]
+    for cur, nl, *_ in splits[:300]:
+        i = seq.index(cur)
+        seq[i:i + 1] = [cur, nl]
+    assert kd_leaf_order(splits[:300]) == seq
+
+
 @pytest.mark.parametrize("name,world,P", [("b3d_20k", 3, 8), ("lattice_900", 2, 8)])
 def test_sharded_lpt_equals_blocks(tmp_path, name, world, P):
     """The sharded train with LPT leaf placement (non-contiguous label sets
@@ -207,6 +269,38 @@ def test_reference_api_in_process_group(tmp_path, name, world, P, keyed):
         np.testing.assert_array_equal(z["assign_keys"], want_keys[order])
         np.testing.assert_array_equal(z["assign_labels"], g["sk_labels"][order])
         assert int(z["count"]) == len(X)
+
+
+@pytest.mark.parametrize("name,world,P,keyed", [("c0_p3", 2, 3, False), ("b2d_20k", 3, 8, True)])
+def test_sharded_model_data_is_partition_records(tmp_path, name, world, P, keyed):
+    """DBSCAN.data after a sharded train (a gloo group) is the
+    reference's per-partition records (R:dbscan/dbscan.py:116-125): for each
+    neighbourhood, in partition order, its members in input order as (key,
+    'L:c[*]') with the neighbourhood's own sklearn labels — the records one
+    device gives for the union of the slices (same KD boxes: exact sums), on
+    every rank; count() equals the number of records."""
+    g = load_golden(name)
+    X = g["X"]
+    eps, ms = float(g["eps"]), int(g["min_samples"])
+    out = run_world(world, X, eps, ms, 0, P, str(tmp_path), api=True, keyed=keyed)
+    kd = oracle.kd_partition(X, P, sums="exact")
+    _, _, members = oracle.halo(X, kd["box_lo"], kd["box_hi"], eps)
+    want_k, want_s = [], []
+    for L, idx in enumerate(members):
+        if not len(idx):
+            continue
+        lab, core, _, _ = oracle.dbscan(X[idx], eps, ms)
+        want_k += [("k%06d" % i) if keyed else str(i) for i in idx.tolist()]
+        want_s += ["%i:%i%s" % (L, c, "" if f else "*") for c, f in zip(lab.tolist(), core.tolist())]
+    for z in out["ranks"]:
+        assert z["data_keys"].tolist() == want_k
+        assert z["data_recs"].tolist() == want_s
+        assert int(z["data_count"]) == len(want_k)
+    if name == "c0_p3" and np.array_equal(kd["box_lo"], g["box_lo"]):
+        # the exact-sum boxes are the reference's here: its own records
+        po = g["part_out"]
+        ref = ["%i:%i%s" % (L, c, "" if f else "*") for L, _, c, f in po.tolist()]
+        assert want_k == [str(int(k)) for k in po[:, 1]] and want_s == ref
 
 
 def test_train_threads_local_comm():

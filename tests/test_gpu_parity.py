@@ -347,6 +347,25 @@ def test_record_sort_is_stable_and_exact(native, key_bytes, bits, n):
     assert np.array_equal(got_v, v[order])
 
 
+@pytest.mark.parametrize("key_bytes,bits", [(4, 20), (4, 13), (8, 37), (8, 3)])
+def test_record_sort_ignores_bits_above_key_bits(native, key_bytes, bits):
+    """pd_sort_pairs sorts by key bits [0, key_bits) only — keys
+    with bits set above key_bits order as numpy's stable sort of the masked
+    keys (equal masked keys keep their input order), not by the 8-bit digit's
+    upper bits."""
+    rng = np.random.default_rng(bits)
+    n = 300_007
+    dt = np.uint32 if key_bytes == 4 else np.uint64
+    k = rng.integers(0, np.iinfo(np.int64).max, n, dtype=np.uint64).astype(dt)
+    v = np.arange(n, dtype=np.uint32)
+    kt = torch.from_numpy(k.view(np.int32 if key_bytes == 4 else np.int64)).cuda()
+    vt = torch.from_numpy(v.view(np.int32)).cuda()
+    native.sort_pairs(kt, vt, bits)
+    order = np.argsort(k & dt((1 << bits) - 1), kind="stable")
+    assert np.array_equal(kt.cpu().numpy().view(dt), k[order])
+    assert np.array_equal(vt.cpu().numpy().view(np.uint32), v[order])
+
+
 def test_record_sort_unaligned_keys(native):
     """pd_sort_pairs on a key view that is not 16-byte aligned (the digit
     histogram then reads key by key)."""

@@ -94,6 +94,8 @@ def parse():
                     help="PD_OPT_CENTRE_WINDOW override (link window length)")
     ap.add_argument("--xsub", type=int, default=None,
                     help="PD_OPT_XSUB override (axis-0 sub-cells per eps)")
+    ap.add_argument("--halo-passes", type=int, default=None,
+                    help="PD_OPT_HALO_PASSES override (1 single pass, 2 tile counts + scan)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
@@ -134,15 +136,19 @@ def load_pmc(config="C2"):
     return None, None
 
 
-def load_ceiling():
-    """Newest count-sweep latency ceiling (profiles/rNN_vMM_count_ceiling.json,
-    tools/count_ceiling.py): the shipped count kernel on L2-resident C2 slices."""
+def load_ceiling(config="C2"):
+    """Newest count-sweep latency ceiling of `config`
+    (profiles/rNN_vMM_count_ceiling[_cK].json, tools/count_ceiling.py): the
+    shipped count kernel on L2-resident slices of that config (its "config"
+    field names it)."""
     fs = sorted(glob.glob(os.path.join(HERE, "profiles", "*count_ceiling*.json")), key=_order)
     for f in reversed(fs):
         try:
-            return json.load(open(f)), os.path.basename(f)
+            c = json.load(open(f))
         except Exception:
             continue
+        if str(c.get("config", "C2")).split()[0] == config:
+            return c, os.path.basename(f)
     return None, None
 
 
@@ -271,20 +277,21 @@ def grid_roofline(rec, cells, d, t_cnt, sweep, pmc, pmc_src, stages, cfg_name="C
             "candidate_tests": cand, "candidate_tests_per_record": cand / rec,
             "candidate_tests_per_s": cand / (t_cnt * 1e-3),
             "records_per_s": rec / (t_cnt * 1e-3)}
-        ceil, ceil_src = load_ceiling()
-        if cfg_name != "C2":
-            # the ceiling is the C2 sweep's (its candidate lists and cell
-            # occupancy); other configs' sweeps are not comparable to it
+        ceil, ceil_src = load_ceiling(cfg_name)
+        if not (ceil and ceil.get("ceiling_candidate_tests_per_s")):
+            # each config's sweep (its candidate lists and cell occupancy)
+            # needs its own ceiling
             roof["latency_frac"] = None
-            roof["latency_note"] = "the latency ceiling is measured on C2 slices only"
-        elif ceil and ceil.get("ceiling_candidate_tests_per_s"):
+            roof["latency_note"] = f"no latency ceiling measured for {cfg_name}"
+        else:
             # the same kernel with every load of its chain an L2 hit
             roof["latency_frac"] = (cand / (t_cnt * 1e-3)) / ceil["ceiling_candidate_tests_per_s"]
             roof["latency_ceiling"] = {
                 "candidate_tests_per_s": ceil["ceiling_candidate_tests_per_s"],
                 "points": ceil.get("ceiling_points"), "source": ceil_src,
-                "note": "count4_kernel on a density-preserving C2 slice whose records, "
-                        "directory and cell starts fit each XCD's L2 (tools/count_ceiling.py)"}
+                "note": f"count4_kernel on a {cfg_name} slice ({ceil.get('config', '')}) "
+                        "whose records, directory and cell starts fit each XCD's L2, "
+                        "replicated to the full run's lanes (tools/count_ceiling.py)"}
     stage = None
     if pmc and stages.get("link"):
         kb = {}
@@ -496,7 +503,8 @@ def main():
                      (_native.PD_OPT_LABEL_BUCKETS, args.label_buckets),
                      (_native.PD_OPT_DIR_PAGED, args.dir_paged),
                      (_native.PD_OPT_DENSE_SCREEN, args.dense_screen),
-                     (_native.PD_OPT_XSUB, args.xsub)):
+                     (_native.PD_OPT_XSUB, args.xsub),
+                     (_native.PD_OPT_HALO_PASSES, args.halo_passes)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None

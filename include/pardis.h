@@ -115,7 +115,15 @@ enum pd_option {
                                 the records (lane i sweeps record i mod R; replicas write the
                                 same values) and put its time in PD_T_COUNT_KERNEL — on a record
                                 set small enough to stay in L2, the sweep's latency ceiling.
-                                Default 0 (off) */
+                                Default 0 (off) */,
+    PD_OPT_HALO_PASSES = 25   /* grid train halo records: 2 (default) tile counts, scan, write
+                                (two reads of the points); 1: one pass — each tile counts its
+                                records, takes its offset by decoupled look-back and writes them
+                                into buffers of a guessed capacity (a larger total reruns 2);
+                                measured slower on C2 (halo 1.62 vs 1.31 ms), kept for A/B.
+                                Same records either way */,
+    PD_OPT_HALO_CAP = 26      /* single-pass halo record capacity (tests: force the overflow
+                                path); 0 (default): n + n/8 + 4096 */
     /* Retired in round 5 (measured A/Bs whose losing kernels were removed;
        pd_ctx_set_option returns PD_EINVAL for them, and the numbers are not
        reused): 4 LINK_MODE, 5 JUMP_ROUNDS, 9 SWEEP_VARIANT, 10 BORDER_ROOTS,
@@ -139,6 +147,8 @@ enum pd_timing_slot {
     PD_T_DIR_WORDS,            /* directory words it allocated (paged: occupied + 1) */
     PD_T_S_COUNT_BATCHES,      /* count sweep (PD_OPT_SWEEP_STATS): wave batches swept */
     PD_T_S_COUNT_STAGED,       /*   (retired LDS-staged count sweep: always 0) */
+    PD_T_HALO_FALLBACK,        /* 1 if the last single-pass halo overflowed its capacity and
+                                  the two-pass form ran */
     PD_T_NSLOTS
 };
 

@@ -31,13 +31,16 @@ PD_OPT_DIR_PAGED = 17
 PD_OPT_DENSE_SCREEN = 18
 PD_OPT_SHARD_CORE_BIT = 19
 PD_OPT_COUNT_REPLAY = 24
+PD_OPT_HALO_PASSES = 25
+PD_OPT_HALO_CAP = 26
 # retired in round 5 (pardis.h): set_option raises for them
 PD_OPT_RETIRED = (4, 5, 9, 10, 16, 20, 21, 22, 23)
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
                 "label", "total", "records", "cells_n", "grid_cells", "key_bits", "core_records",
                 "s_count_cand", "s_link_cand", "s_link_hit", "s_link_core", "s_link_same",
                 "s_link_find_same", "s_link_unions", "s_verify_pairs", "grid_grow",
-                "count_kernel", "dir_paged", "dir_words", "s_count_batches", "s_count_staged"]
+                "count_kernel", "dir_paged", "dir_words", "s_count_batches", "s_count_staged",
+                "halo_fallback"]
 
 # every symbol include/pardis.h declares (tests/test_abi.py checks the .so)
 EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",

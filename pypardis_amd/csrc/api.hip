@@ -164,6 +164,12 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
             ctx->c.dense_screen = (int)value;
         } else if (option == PD_OPT_SHARD_CORE_BIT) {
             ctx->c.shard_core_bit = value != 0;
+        } else if (option == PD_OPT_HALO_PASSES) {
+            if (value != 1 && value != 2) throw Error(PD_EINVAL, "halo passes is 1 or 2");
+            ctx->c.halo_passes = (int)value;
+        } else if (option == PD_OPT_HALO_CAP) {
+            if (value < 0) throw Error(PD_EINVAL, "halo capacity must be >= 0");
+            ctx->c.halo_cap = value;
         } else if (option == PD_OPT_COUNT_REPLAY) {
             if (value < 0 || value > 65536) throw Error(PD_EINVAL, "count replay must be in [0, 65536]");
             ctx->c.count_replay = (int)value;
@@ -193,7 +199,7 @@ int32_t pd_ctx_timings(pd_ctx* ctx, double* out, int32_t n) {
                                        (double)t.sweep[6], (double)t.sweep[7], t.grid_grow,
                                        (double)t.count_kernel, (double)t.dir_paged,
                                        (double)t.dir_words, (double)t.sweep[8],
-                                       (double)t.sweep[9]};
+                                       (double)t.sweep[9], (double)t.halo_fallback};
         for (int i = 0; i < n && i < PD_T_NSLOTS; ++i) out[i] = v[i];
     });
 }

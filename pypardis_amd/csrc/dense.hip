@@ -335,8 +335,14 @@ struct TileShared {
 // QT: 32-query groups per wave (B operand tiles held in registers).  QT = 4
 // doubles the MFMA work per streamed byte (each staged tile feeds 2 x 4 x 3 x
 // KS MFMAs per wave) at one wave per SIMD.
-constexpr int kF8Waves = 3;   // e4m3 count pass: waves per SIMD (no bf16 query fragments held)
-constexpr int kF8QT = 2;      // e4m3 count pass: query tiles (of 32) per wave
+#ifndef PD_F8_WAVES
+#define PD_F8_WAVES 3
+#endif
+#ifndef PD_F8_QT
+#define PD_F8_QT 2
+#endif
+constexpr int kF8Waves = PD_F8_WAVES;   // e4m3 count pass: waves per SIMD (no bf16 query fragments held)
+constexpr int kF8QT = PD_F8_QT;         // e4m3 count pass: query tiles (of 32) per wave
 
 // The e4m3 count pass streams each tile through two register stages ahead of
 // a double-buffered LDS tile.  (Measured and retired in round 4: an LDS-DMA

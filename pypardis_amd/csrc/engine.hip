@@ -54,6 +54,26 @@
 namespace pd {
 namespace {
 
+// Device-side bounds checks (debug builds: -DPD_CHECK_BOUNDS=1, e.g.
+// tools/build_variant.sh): every checked access that would leave its buffer
+// is skipped and the first one recorded (site << 48 | index); the host reads
+// the record after the kernel (check_bounds) and throws.  Off (the default),
+// PD_OK is `true` and costs nothing.
+#ifndef PD_CHECK_BOUNDS
+#define PD_CHECK_BOUNDS 0
+#endif
+#if PD_CHECK_BOUNDS
+__device__ unsigned long long g_oob[2];   // [0] violations, [1] the first
+__device__ __forceinline__ bool pd_ok(bool c, unsigned site, uint64_t idx) {
+    if (!c && atomicAdd(&g_oob[0], 1ull) == 0ull)
+        g_oob[1] = ((unsigned long long)site << 48) | (idx & 0xFFFFFFFFFFFFull);
+    return c;
+}
+#define PD_OK(cond, site, idx) pd_ok((cond), (site), (uint64_t)(idx))
+#else
+#define PD_OK(cond, site, idx) true
+#endif
+
 // ------------------------------------------------------------------ helpers
 // (union-find primitives: uf.hpp)
 
@@ -459,10 +479,13 @@ __device__ __forceinline__ int tree_owner(const KdTree& t, const int32_t* slot,
     int lab = 0;
     for (int l = 0; l < t.nl; ++l) {
         if (lab >= t.ntab[l]) continue;
+        if (!PD_OK(t.toff[l] + lab < t.nslot, 1, t.toff[l] + lab)) continue;
         const int sl = slot[t.toff[l] + lab];
         if (sl < 0) continue;
         const int e = t.eoff[l] + sl;
+        if (!PD_OK(e < t.ne, 2, e)) continue;
         const int ax = ax_new[2 * e];
+        if (!PD_OK(ax >= 0 && ax < D, 3, ax)) continue;
         T x = v[0];
 #pragma unroll
         for (int j = 1; j < D; ++j) x = ax == j ? v[j] : x;
@@ -486,10 +509,10 @@ __device__ __forceinline__ int tree_owner(const KdTree& t, const int32_t* slot,
 template <typename T, int D, bool MASK>
 __device__ __forceinline__ void halo_points(const T* __restrict__ X, uint64_t n,
                                             const PartGrid* __restrict__ parts, int P,
+                                            uint64_t tile,
                                             uint64_t (&idx)[4], T (&v)[4][D],
                                             unsigned long long (&m)[4], uint32_t (&cnt)[4]) {
-    const uint64_t base = (uint64_t)blockIdx.x * (4 * kBlock) + (threadIdx.x >> 6) * 256 +
-                          (threadIdx.x & 63);
+    const uint64_t base = tile * (4 * kBlock) + (threadIdx.x >> 6) * 256 + (threadIdx.x & 63);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         idx[q] = base + 64 * q;
@@ -548,7 +571,7 @@ __global__ __launch_bounds__(kBlock) void halo_tile_kernel(const T* __restrict__
     T v[4][D];
     unsigned long long m[4];
     uint32_t cnt[4];
-    halo_points<T, D, false>(X, n, parts, P, idx, v, m, cnt);
+    halo_points<T, D, false>(X, n, parts, P, blockIdx.x, idx, v, m, cnt);
     const uint32_t t = block_sum_u32(cnt[0] + cnt[1] + cnt[2] + cnt[3]);
     if (threadIdx.x == 0) tile_count_out(tile_cnt, t);
 }
@@ -595,20 +618,24 @@ __device__ __forceinline__ K key_of(const T (&tv)[D], const KeyGrid<D>& g) {
 // stores are contiguous; the extra records of the few halo duplicates follow.
 // (92 VGPRs, 5 waves/SIMD: capping it at 6 or 8 waves measured slower — C2
 // halo 1.29 / 1.81 vs 1.22 ms, the cap spills the per-point state)
-template <typename T, int D, typename K, bool MASK>
-__global__ __launch_bounds__(kBlock) void halo_write_kernel(
-    const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
-    const int32_t* __restrict__ owner, KdTree tree, const uint64_t* __restrict__ tile_off,
-    K* __restrict__ keys, uint32_t* __restrict__ vals) {
-    uint64_t idx[4];
-    T v[4][D];
-    unsigned long long m[4];
-    uint32_t cnt[4];
-    halo_points<T, D, MASK>(X, n, parts, P, idx, v, m, cnt);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t ex[4], wtot = 0;
+// Every record store is bounded by `cap` (the buffers' length): the
+// single-pass form writes before it knows the total, and a tile past the
+// capacity must not store (the host then reruns the two-pass form).
+template <int D>
+struct HaloLds {
+    uint32_t ws[kBlock / 64];
+    KeyGrid<D> kg[64];
+    int32_t t_slot[kTreeSlots], t_axn[2 * kTreeSplits];
+    double t_bd[kTreeSplits];
+};
+
+// the per-wave exclusive record offsets of the four steps; the wave's total
+template <int Q>
+__device__ __forceinline__ uint32_t wave_offsets(const uint32_t (&cnt)[Q], uint32_t (&ex)[Q]) {
+    const int lane = threadIdx.x & 63;
+    uint32_t wtot = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < Q; ++q) {
         uint32_t x = cnt[q];
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -618,65 +645,192 @@ __global__ __launch_bounds__(kBlock) void halo_write_kernel(
         ex[q] = wtot + x - cnt[q];
         wtot += (uint32_t)__shfl((int)x, 63, 64);
     }
-    __shared__ uint32_t ws[kBlock / 64];
-    __shared__ KeyGrid<D> kg[MASK ? 64 : 1];
-    __shared__ int32_t t_slot[MASK ? kTreeSlots : 1], t_axn[MASK ? 2 * kTreeSplits : 1];
-    __shared__ double t_bd[MASK ? kTreeSplits : 1];
+    return wtot;
+}
+
+// stage the split tree and the key grids in LDS (MASK: P <= 64); returns
+// whether the tree is read from LDS.  The caller synchronises after.
+template <typename T, int D, bool MASK>
+__device__ __forceinline__ bool halo_stage(HaloLds<D>& L, const PartGrid* __restrict__ parts,
+                                           int P, const KdTree& tree) {
     const bool tree_lds = MASK && tree.nl && tree.nslot <= kTreeSlots && tree.ne <= kTreeSplits;
     if (tree_lds) {
-        for (int k = threadIdx.x; k < tree.nslot; k += kBlock) t_slot[k] = tree.slot[k];
-        for (int k = threadIdx.x; k < 2 * tree.ne; k += kBlock) t_axn[k] = tree.ax_new[k];
-        for (int k = threadIdx.x; k < tree.ne; k += kBlock) t_bd[k] = tree.bound[k];
+        for (int k = threadIdx.x; k < tree.nslot; k += kBlock) L.t_slot[k] = tree.slot[k];
+        for (int k = threadIdx.x; k < 2 * tree.ne; k += kBlock) L.t_axn[k] = tree.ax_new[k];
+        for (int k = threadIdx.x; k < tree.ne; k += kBlock) L.t_bd[k] = tree.bound[k];
     }
-    if (lane == 0) ws[w] = wtot;
     if constexpr (MASK) {
-        for (int L = threadIdx.x; L < P; L += kBlock) {
+        for (int q = threadIdx.x; q < P; q += kBlock) {
 #pragma unroll
             for (int j = 0; j < D; ++j) {
-                kg[L].lo[j] = parts[L].lo[j];
-                kg[L].inv[j] = parts[L].inv[j];
-                kg[L].nc[j] = (double)parts[L].nc[j];
-                kg[L].top[j] = (double)(parts[L].nc[j] - 1);
+                L.kg[q].lo[j] = parts[q].lo[j];
+                L.kg[q].inv[j] = parts[q].inv[j];
+                L.kg[q].nc[j] = (double)parts[q].nc[j];
+                L.kg[q].top[j] = (double)(parts[q].nc[j] - 1);
             }
-            kg[L].base = parts[L].base;
+            L.kg[q].base = parts[q].base;
         }
     }
-    __syncthreads();
-    uint64_t wbase = tile_off[blockIdx.x];
-#pragma unroll
-    for (int u = 0; u < kBlock / 64; ++u) wbase += u < w ? ws[u] : 0u;
+    return tree_lds;
+}
+
+// write the records of one tile's points from record offset wbase (this
+// wave's first record); stores at or past cap are dropped
+template <typename T, int D, typename K, bool MASK>
+__device__ __forceinline__ void halo_emit(const HaloLds<D>& L, const PartGrid* __restrict__ parts,
+                                          int P, const int32_t* __restrict__ owner,
+                                          const KdTree& tree, bool tree_lds, uint64_t n,
+                                          const uint64_t (&idx)[4], const T (&v)[4][D],
+                                          const unsigned long long (&m)[4],
+                                          const uint32_t (&cnt)[4], const uint32_t (&ex)[4],
+                                          uint64_t wbase, uint64_t cap, K* __restrict__ keys,
+                                          uint32_t* __restrict__ vals) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         if (!cnt[q]) continue;
+        if (!PD_OK(idx[q] < n, 4, idx[q])) continue;
         // P == 1: neighbourhood 0
         const int own = owner  ? owner[idx[q]]
                         : !tree.nl ? 0
-                        : tree_lds ? tree_owner<T, D>(tree, t_slot, t_axn, t_bd, v[q])
+                        : tree_lds ? tree_owner<T, D>(tree, L.t_slot, L.t_axn, L.t_bd, v[q])
                                    : tree_owner<T, D>(tree, tree.slot, tree.ax_new, tree.bound, v[q]);
+        (void)PD_OK(own >= 0 && own < P, 5, (uint32_t)own);
         const uint32_t tag = (uint32_t)idx[q] | (cnt[q] >= 2 ? kDupBit : 0u);
         uint64_t o = wbase + ex[q];
         if constexpr (MASK) {
             unsigned long long mm = m[q];
             do {
-                const int L = __ffsll(mm) - 1;
+                const int Lb = __ffsll(mm) - 1;
                 mm &= mm - 1;
-                const K key = key_of<T, D, K>(v[q], kg[L]);
-                keys[o] = key;
-                vals[o] = tag | (own == L ? kOwnerBit : 0u);
+                const K key = key_of<T, D, K>(v[q], L.kg[Lb]);
+                if (o < cap) {
+                    keys[o] = key;
+                    vals[o] = tag | (own == Lb ? kOwnerBit : 0u);
+                }
                 ++o;
             } while (mm);
         } else {
-            for (int L = 0; L < P; ++L) {
-                const PartGrid& g = parts[L];
+            for (int Lb = 0; Lb < P; ++Lb) {
+                const PartGrid& g = parts[Lb];
                 if (!in_box_t<T, D>(v[q], g)) continue;
                 K key;
                 halo_record<T, D, K>(v[q], g, key);
-                keys[o] = key;
-                vals[o] = tag | (own == L ? kOwnerBit : 0u);
+                if (o < cap) {
+                    keys[o] = key;
+                    vals[o] = tag | (own == Lb ? kOwnerBit : 0u);
+                }
                 ++o;
             }
         }
+        (void)PD_OK(o - (wbase + ex[q]) == cnt[q], 6, o);
     }
+}
+
+template <typename T, int D, typename K, bool MASK>
+__global__ __launch_bounds__(kBlock) void halo_write_kernel(
+    const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
+    const int32_t* __restrict__ owner, KdTree tree, const uint64_t* __restrict__ tile_off,
+    uint64_t cap, K* __restrict__ keys, uint32_t* __restrict__ vals) {
+    uint64_t idx[4];
+    T v[4][D];
+    unsigned long long m[4];
+    uint32_t cnt[4], ex[4];
+    halo_points<T, D, MASK>(X, n, parts, P, blockIdx.x, idx, v, m, cnt);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t wtot = wave_offsets<4>(cnt, ex);
+    __shared__ HaloLds<D> L;
+    const bool tree_lds = halo_stage<T, D, MASK>(L, parts, P, tree);
+    if (lane == 0) L.ws[w] = wtot;
+    __syncthreads();
+    uint64_t wbase = tile_off[blockIdx.x];
+#pragma unroll
+    for (int u = 0; u < kBlock / 64; ++u) wbase += u < w ? L.ws[u] : 0u;
+    halo_emit<T, D, K, MASK>(L, parts, P, owner, tree, tree_lds, n, idx, v, m, cnt, ex, wbase, cap,
+                             keys, vals);
+}
+
+// Single-pass halo (PD_OPT_HALO_PASSES = 1): each tile counts its records,
+// learns the records of the tiles before it by decoupled look-back, and
+// writes them — one read of the points instead of two, no scan, at the price
+// of buffers sized before the total is known (cap; the host reruns the
+// two-pass form when the total passes it).  Tiles take their index from a
+// ticket (atomicAdd - tick0), so the tiles a tile waits for were dispatched
+// before it: forward progress without assuming a dispatch order.  Look-back
+// words: tag << 32 | records (tag 2 epoch + 1: the tile's own count, 2 epoch
+// + 2: inclusive of every tile before; older epochs' tags read as
+// unpublished); counts saturate at 2^32 - 1, far past any capacity.  The
+// last tile writes the total (64-bit) for the host.  Tile 0 zeroes the
+// train's counters and the sort histograms (the tile kernel's job in the
+// two-pass form).
+template <typename T, int D, typename K, bool MASK>
+__global__ __launch_bounds__(kBlock) void halo1_kernel(
+    const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
+    const int32_t* __restrict__ owner, KdTree tree, uint64_t cap, K* __restrict__ keys,
+    uint32_t* __restrict__ vals, uint64_t* __restrict__ look, uint32_t epoch,
+    unsigned long long* __restrict__ ticket, unsigned long long tick0, uint32_t ntiles,
+    unsigned long long* __restrict__ total, uint32_t* __restrict__ ctrs,
+    uint32_t* __restrict__ sort_hist) {
+    __shared__ HaloLds<D> L;
+    __shared__ uint32_t s_tile;
+    __shared__ unsigned long long s_base;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_tile = (uint32_t)(atomicAdd(ticket, 1ull) - tick0);
+    const bool tree_lds = halo_stage<T, D, MASK>(L, parts, P, tree);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    if (!PD_OK(tile < ntiles, 7, tile)) return;   // (a ticket past the grid: never)
+    if (tile == 0) {
+        if (threadIdx.x < kCtrs) ctrs[threadIdx.x] = 0;
+        if (sort_hist)
+            for (int i = threadIdx.x; i < 8 * rsort::kRadix; i += kBlock) sort_hist[i] = 0;
+    }
+    uint64_t idx[4];
+    T v[4][D];
+    unsigned long long m[4];
+    uint32_t cnt[4], ex[4];
+    halo_points<T, D, MASK>(X, n, parts, P, tile, idx, v, m, cnt);
+    const uint32_t wtot = wave_offsets<4>(cnt, ex);
+    if (lane == 0) L.ws[w] = wtot;
+    __syncthreads();
+    if (w == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int u = 0; u < kBlock / 64; ++u) t += L.ws[u];
+        const uint32_t agg = 2u * epoch + 1u, inc = 2u * epoch + 2u;
+        if (lane == 0) rsort::st_lb(look + tile, ((uint64_t)(tile == 0 ? inc : agg) << 32) | t);
+        uint64_t excl = 0;
+        // look back 64 tiles at a time: lane l reads tile (front - l); the
+        // nearest inclusive word ends the walk, every word up to it must be
+        // published (else spin)
+        for (int64_t front = (int64_t)tile - 1; front >= 0;) {
+            const int64_t tt = front - lane;
+            const uint64_t wv = tt >= 0 ? rsort::ld_lb(look + tt) : ((uint64_t)inc << 32);
+            const uint32_t tag = (uint32_t)(wv >> 32);
+            const unsigned long long pub = __ballot(tag == agg || tag == inc);
+            const unsigned long long incl = __ballot(tag == inc);
+            const int stop = incl ? __ffsll((long long)incl) - 1 : 63;
+            const unsigned long long need = stop == 63 ? ~0ull : ((2ull << stop) - 1ull);
+            if ((pub & need) != need) continue;   // a tile up to `stop` not published yet
+            uint64_t x = lane <= stop ? (uint32_t)wv : 0u;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) x += (uint64_t)__shfl_xor((long long)x, o, 64);
+            excl += x;
+            if (incl) break;
+            front -= 64;
+        }
+        if (lane == 0) {
+            const uint64_t it = excl + t;
+            if (tile > 0) rsort::st_lb(look + tile, ((uint64_t)inc << 32) | (it < 0xFFFFFFFFull ? it : 0xFFFFFFFFull));
+            if (tile == ntiles - 1) *total = it;
+            s_base = excl;
+        }
+    }
+    __syncthreads();
+    uint64_t wbase = s_base;
+#pragma unroll
+    for (int u = 0; u < kBlock / 64; ++u) wbase += u < w ? L.ws[u] : 0u;
+    halo_emit<T, D, K, MASK>(L, parts, P, owner, tree, tree_lds, n, idx, v, m, cnt, ex, wbase, cap,
+                             keys, vals);
 }
 
 // Coordinates into key order (padded rows); also lists the records of halo
@@ -2594,7 +2748,7 @@ void sort_records(Ctx& ctx, K*& keys, uint32_t*& vals, K* keys2, uint32_t* vals2
     st.epoch = ctx.rs_epoch;
     K* ko;
     uint32_t* vo;
-    // (st.hist zeroed by halo_tile_kernel in the train)
+    // (st.hist zeroed by the halo pass in the train)
     rsort::sort_pairs<K>(st, keys, vals, keys2, vals2, R, key_bits, s, &ko, &vo, hist_zeroed);
     ctx.rs_epoch = st.epoch;
     keys = ko;
@@ -2612,6 +2766,27 @@ uint32_t select_records(Ctx& ctx, const char* name, uint32_t R, Pred pred, uint3
     return (uint32_t)compact_ordered(ctx, "sel_cmp", (uint64_t)R, pred, list, nullptr, s);
 }
 
+// PD_CHECK_BOUNDS builds: after a checked kernel, read the violation record
+// and throw with the site and the first index (nothing in normal builds).
+void check_bounds(hipStream_t s, const char* kernel) {
+#if PD_CHECK_BOUNDS
+    unsigned long long h[2] = {0, 0};
+    PD_HIP(hipStreamSynchronize(s));
+    PD_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_oob), sizeof(h), 0, hipMemcpyDeviceToHost));
+    if (h[0]) {
+        const unsigned long long z[2] = {0, 0};
+        PD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_oob), z, sizeof(z), 0, hipMemcpyHostToDevice));
+        throw Error(-1, std::string("bounds check failed in ") + kernel + ": " +
+                            std::to_string(h[0]) + " violation(s), first at site " +
+                            std::to_string(h[1] >> 48) + " index " +
+                            std::to_string(h[1] & 0xFFFFFFFFFFFFull));
+    }
+#else
+    (void)s;
+    (void)kernel;
+#endif
+}
+
 // Phase A: halo records, sort, cell directory, core counts, union-find,
 // component keys (marks 0..8).  Leaves its device state in ctx.st.
 template <typename T, int D, typename K, int M>
@@ -2625,33 +2800,15 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     tm.mark();   // 0
 
     PartGrid* parts = ctx.arena.get<PartGrid>("parts", P);
-    {
-        PartGrid* h = (PartGrid*)pinned(ctx, sizeof(PartGrid) * P);
-        std::memcpy(h, hparts.data(), sizeof(PartGrid) * P);
-        PD_HIP(hipMemcpyAsync(parts, h, sizeof(PartGrid) * P, hipMemcpyHostToDevice, s));
-    }
     const T* X = (const T*)a.X;
 
-    // ---- halo records (R:dbscan/dbscan.py:136-151): tile counts, scan, write
-    const unsigned htiles = (unsigned)std::max<uint64_t>(1, (n + 4 * kBlock - 1) / (4 * kBlock));
-    uint32_t* tcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)htiles + 1);
-    uint64_t* toff = ctx.arena.get<uint64_t>("tile_off", (size_t)htiles + 1);
-    uint32_t* ctrs = ctx.arena.get<uint32_t>("train_ctrs", kCtrs);
-    uint32_t* sort_hist = PD_SORT_ROCPRIM ? nullptr : ctx.arena.get<uint32_t>("rsort_hist", 8 * rsort::kRadix);
-    hipLaunchKernelGGL((halo_tile_kernel<T, D>), dim3(htiles), dim3(kBlock), 0, s, X, n, parts, P,
-                       tcnt, ctrs, sort_hist);
-    const uint64_t R64 = tile_offsets(ctx, tcnt, htiles, toff, s, true);
-    if (R64 >= 0xFFFFFFFEull) throw Error(-5, "more than 2^32-2 halo records on one device");
-    const uint32_t R = (uint32_t)R64;
-    ctx.t.records = R;
-    K* keys = ctx.arena.get<K>("keys", R);
-    uint32_t* vals = ctx.arena.get<uint32_t>("vals", R);
-    K* keys2 = ctx.arena.get<K>("keys2", R);
-    uint32_t* vals2 = ctx.arena.get<uint32_t>("vals2", R);
+    // the split tree (pd_train_tree): per level a label -> slot table, per
+    // split (axis, new label) and the boundary — host tables first, then ONE
+    // pinned block carries the grids and the tree (no sync between uploads)
     KdTree tree;
+    std::vector<int32_t> t_int;
+    std::vector<double> t_bd;
     if (!a.owner && a.tree_levels > 0) {
-        // upload the split tree: per level a label -> slot table, per split
-        // (axis, new label) and the boundary
         const int nl = a.tree_levels;
         if (nl > 16) throw Error(-5, "KD split tree deeper than 16 levels");
         std::vector<int> ntab(nl, 1), toff(nl, 0), eoff(nl, 0);
@@ -2664,26 +2821,19 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
             nslot += ntab[l];
             ne += a.tree_sizes[l];
         }
-        const size_t ib = sizeof(int32_t) * ((size_t)nslot + 2 * ne);
-        const size_t db = (ib + 7) & ~size_t(7);
-        char* h = (char*)pinned(ctx, db + sizeof(double) * ne);
-        int32_t* hs = (int32_t*)h;
-        int32_t* hx = hs + nslot;
-        double* hb = (double*)(h + db);
-        for (int k = 0; k < nslot; ++k) hs[k] = -1;
+        t_int.assign((size_t)nslot + 2 * ne, -1);
+        t_bd.assign(ne, 0.0);
         for (int l = 0; l < nl; ++l)
             for (int k = 0; k < a.tree_sizes[l]; ++k) {
                 const int e = eoff[l] + k, L = a.tree_cur[e];
-                if (L < 0 || a.tree_axis[e] < 0 || a.tree_axis[e] >= D)
+                if (L < 0 || L >= P || a.tree_new[e] < 0 || a.tree_new[e] >= P ||
+                    a.tree_axis[e] < 0 || a.tree_axis[e] >= D || t_int[toff[l] + L] != -1)
                     throw Error(-1, "bad KD split tree");
-                hs[toff[l] + L] = k;
-                hx[2 * e] = a.tree_axis[e];
-                hx[2 * e + 1] = a.tree_new[e];
-                hb[e] = a.tree_bound[e];
+                t_int[toff[l] + L] = k;
+                t_int[nslot + 2 * e] = a.tree_axis[e];
+                t_int[nslot + 2 * e + 1] = a.tree_new[e];
+                t_bd[e] = a.tree_bound[e];
             }
-        char* dt = ctx.arena.get<char>("kd_tree", db + sizeof(double) * ne);
-        PD_HIP(hipMemcpyAsync(dt, h, db + sizeof(double) * ne, hipMemcpyHostToDevice, s));
-        sync(s);   // the pinned block is reused by later uploads (the halo scan already synced)
         tree.nl = nl;
         for (int l = 0; l < nl; ++l) {
             tree.ntab[l] = ntab[l];
@@ -2692,17 +2842,102 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         }
         tree.nslot = nslot;
         tree.ne = ne;
-        tree.slot = (const int32_t*)dt;
-        tree.ax_new = (const int32_t*)dt + nslot;
-        tree.bound = (const double*)(dt + db);
     }
-    if (P <= 64)
-        hipLaunchKernelGGL((halo_write_kernel<T, D, K, true>), dim3(htiles), dim3(kBlock), 0, s, X,
-                           n, parts, P, a.owner, tree, toff, keys, vals);
-    else
-        hipLaunchKernelGGL((halo_write_kernel<T, D, K, false>), dim3(htiles), dim3(kBlock), 0, s,
-                           X, n, parts, P, a.owner, tree, toff, keys, vals);
-    PD_HIP(hipGetLastError());
+    {
+        const size_t pb = (sizeof(PartGrid) * P + 15) & ~size_t(15);
+        const size_t ib = (sizeof(int32_t) * t_int.size() + 7) & ~size_t(7);
+        const size_t tb = ib + sizeof(double) * t_bd.size();
+        char* h = (char*)pinned(ctx, pb + tb);
+        std::memcpy(h, hparts.data(), sizeof(PartGrid) * P);
+        PD_HIP(hipMemcpyAsync(parts, h, sizeof(PartGrid) * P, hipMemcpyHostToDevice, s));
+        if (tree.nl) {
+            std::memcpy(h + pb, t_int.data(), sizeof(int32_t) * t_int.size());
+            std::memcpy(h + pb + ib, t_bd.data(), sizeof(double) * t_bd.size());
+            char* dt = ctx.arena.get<char>("kd_tree", tb);
+            PD_HIP(hipMemcpyAsync(dt, h + pb, tb, hipMemcpyHostToDevice, s));
+            tree.slot = (const int32_t*)dt;
+            tree.ax_new = (const int32_t*)dt + tree.nslot;
+            tree.bound = (const double*)(dt + ib);
+        }
+        // (the block is next written by a D2H copy ordered after these on s,
+        // and read by the host only after a sync)
+    }
+
+    // ---- halo records (R:dbscan/dbscan.py:136-151)
+    const unsigned htiles = (unsigned)std::max<uint64_t>(1, (n + 4 * kBlock - 1) / (4 * kBlock));
+    uint32_t* ctrs = ctx.arena.get<uint32_t>("train_ctrs", kCtrs);
+    uint32_t* sort_hist = PD_SORT_ROCPRIM ? nullptr : ctx.arena.get<uint32_t>("rsort_hist", 8 * rsort::kRadix);
+    uint64_t R64 = ~0ull;
+    K *keys = nullptr, *keys2 = nullptr;
+    uint32_t *vals = nullptr, *vals2 = nullptr;
+    ctx.t.halo_fallback = 0;
+    if (ctx.halo_passes == 1) {
+        // single pass into buffers of a guessed capacity: n/8 + 4096 records
+        // of halo copies (the BASELINE configs duplicate 0.004-1 % at full
+        // size), or 5 % over the last train's records per point when that was
+        // more (small sets / many partitions duplicate more); a total past it
+        // reruns the two-pass form below
+        const double grow = std::max(1.125, 1.05 * ctx.h1_ratio);
+        const uint64_t cap = std::min<uint64_t>(
+            ctx.halo_cap > 0 ? (uint64_t)ctx.halo_cap : (uint64_t)(grow * (double)n) + 4096,
+            0xFFFFFFFDull);
+        keys = ctx.arena.get<K>("keys", cap);
+        vals = ctx.arena.get<uint32_t>("vals", cap);
+        uint64_t* look = ctx.arena.get<uint64_t>("halo_look", htiles);
+        auto* tick = ctx.arena.get<unsigned long long>("halo_ticket", 2);   // [0] ticket, [1] total
+        if (look != ctx.h1_look || htiles > ctx.h1_look_tiles || tick != ctx.h1_tick ||
+            ctx.h1_epoch >= 0x7FFFFFF0u) {   // new words: zero them once
+            PD_HIP(hipMemsetAsync(look, 0, sizeof(uint64_t) * htiles, s));
+            PD_HIP(hipMemsetAsync(tick, 0, sizeof(unsigned long long) * 2, s));
+            ctx.h1_look = look;
+            ctx.h1_look_tiles = htiles;
+            ctx.h1_tick = tick;
+            ctx.h1_epoch = 0;
+            ctx.h1_tick0 = 0;
+        }
+        const uint32_t ep = ctx.h1_epoch++;
+        const unsigned long long t0 = ctx.h1_tick0;
+        ctx.h1_tick0 += htiles;
+        if (P <= 64)
+            hipLaunchKernelGGL((halo1_kernel<T, D, K, true>), dim3(htiles), dim3(kBlock), 0, s, X, n,
+                               parts, P, a.owner, tree, cap, keys, vals, look, ep, tick, t0,
+                               htiles, tick + 1, ctrs, sort_hist);
+        else
+            hipLaunchKernelGGL((halo1_kernel<T, D, K, false>), dim3(htiles), dim3(kBlock), 0, s, X,
+                               n, parts, P, a.owner, tree, cap, keys, vals, look, ep, tick, t0,
+                               htiles, tick + 1, ctrs, sort_hist);
+        PD_HIP(hipGetLastError());
+        check_bounds(s, "halo1_kernel");
+        uint64_t* h = (uint64_t*)pinned(ctx, sizeof(uint64_t));
+        PD_HIP(hipMemcpyAsync(h, tick + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        sync(s);
+        if (*h <= cap) R64 = *h;
+        ctx.t.halo_fallback = R64 == ~0ull ? 1 : 0;
+    }
+    if (R64 == ~0ull) {
+        // two passes: tile counts, scan, write
+        uint32_t* tcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)htiles + 1);
+        uint64_t* toff = ctx.arena.get<uint64_t>("tile_off", (size_t)htiles + 1);
+        hipLaunchKernelGGL((halo_tile_kernel<T, D>), dim3(htiles), dim3(kBlock), 0, s, X, n, parts,
+                           P, tcnt, ctrs, sort_hist);
+        R64 = tile_offsets(ctx, tcnt, htiles, toff, s, true);
+        if (R64 >= 0xFFFFFFFEull) throw Error(-5, "more than 2^32-2 halo records on one device");
+        keys = ctx.arena.get<K>("keys", R64);
+        vals = ctx.arena.get<uint32_t>("vals", R64);
+        if (P <= 64)
+            hipLaunchKernelGGL((halo_write_kernel<T, D, K, true>), dim3(htiles), dim3(kBlock), 0, s,
+                               X, n, parts, P, a.owner, tree, toff, R64, keys, vals);
+        else
+            hipLaunchKernelGGL((halo_write_kernel<T, D, K, false>), dim3(htiles), dim3(kBlock), 0,
+                               s, X, n, parts, P, a.owner, tree, toff, R64, keys, vals);
+        PD_HIP(hipGetLastError());
+        check_bounds(s, "halo_write_kernel");
+    }
+    const uint32_t R = (uint32_t)R64;
+    ctx.t.records = R;
+    ctx.h1_ratio = n ? (double)R / (double)n : 1.0;
+    keys2 = ctx.arena.get<K>("keys2", R);
+    vals2 = ctx.arena.get<uint32_t>("vals2", R);
     tm.mark();   // 1
 
     // ---- shuffle by neighbourhood == sort by (neighbourhood, cell) key:
@@ -2715,12 +2950,12 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     // sort 46.1 vs 40.6 ms, profiles/r05_v3_ab_sort_10bit.txt.)
     T* Xs = ctx.arena.get<T>("Xs", (size_t)R * Stride<D>::v);
     uint32_t* dup_list = ctx.arena.get<uint32_t>("dup_list", R);
-    uint32_t* lcount = ctrs;   // dup, roots, core, border (zeroed by halo_tile_kernel)
+    uint32_t* lcount = ctrs;   // dup, roots, core, border (zeroed by the halo pass)
     // the merge's representative per point, initialised for the points of the
     // duplicated records only (by the gather, which lists them), not a fill over n
     uint32_t* rep = P > 1 ? ctx.arena.get<uint32_t>("rep", n) : nullptr;
     sort_records<K>(ctx, keys, vals, keys2, vals2, (uint64_t)R, key_bits, s,
-                    /*hist_zeroed=*/!PD_SORT_ROCPRIM);   // by halo_tile_kernel above
+                    /*hist_zeroed=*/!PD_SORT_ROCPRIM);   // by the halo pass above
     tm.mark();   // 2
     hipLaunchKernelGGL((gather_kernel<T, D>), dim3(blocks(R)), dim3(kBlock), 0, s, X, (uint64_t)R,
                        vals, Xs, dup_list, lcount, rep);
@@ -2903,7 +3138,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         {   // (3) cell and word roots in one pass
             uint32_t* big = ctx.arena.get<uint32_t>("big_cells", R / (kWordBig + 1) + 1);
             uint32_t* mid = ctx.arena.get<uint32_t>("mid_cells", R / (kMidCell + 1) + 1);
-            uint32_t* nbig = ctrs + 8;   // [0] big, [1] mid (zeroed by halo_tile_kernel)
+            uint32_t* nbig = ctrs + 8;   // [0] big, [1] mid (zeroed by the halo pass)
             // (wroot starts at kNone: init_kernel)
             if ((uint64_t)W < 0xFFFFFFFFull)   // directory slots < 2^32 - 1
                 hipLaunchKernelGGL((cell_word_root_kernel<K, true>), dim3(blocks(R)), dim3(kBlock), 0,
@@ -2920,7 +3155,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         }
         const uint32_t pcap = (uint32_t)std::min<uint64_t>(R, 64ull << 20);
         uint2* plist = ctx.arena.get<uint2>("pair_list", pcap);
-        uint32_t* pcount = ctrs + 10;   // (zeroed by halo_tile_kernel)
+        uint32_t* pcount = ctrs + 10;   // (zeroed by the halo pass)
         // (4) verify: screen every cell, then work on the flagged ones only
         const unsigned vtiles = blocks(R);
         uint8_t* vflag = ctx.arena.get<uint8_t>("verify_flags", R);

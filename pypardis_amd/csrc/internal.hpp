@@ -46,6 +46,7 @@ struct Timings {
     float halo = 0, sort = 0, gather = 0, cells = 0, count = 0, link = 0, merge = 0,
           roots = 0, border = 0, label = 0, total = 0;
     int64_t records = 0, cells_n = 0, grid_cells = 0, core_records = 0, key_bits = 0;
+    int64_t halo_fallback = 0;   // single-pass halo overflowed its capacity: two passes ran
     // PD_OPT_SWEEP_STATS: count candidates; link candidates, predicate hits,
     // core hits, hits already under the root, finds that met the root, unions;
     // cell pairs tested record by record (link mode 3)
@@ -159,6 +160,17 @@ struct Ctx {
     uint64_t* rs_look = nullptr;
     uint64_t rs_look_tiles = 0;
     uint32_t rs_epoch = 0;
+    // the single-pass halo's look-back words, ticket and total (zeroed when
+    // allocated, then tagged / offset by the epoch and ticket base kept here)
+    int halo_passes = 2;         // PD_OPT_HALO_PASSES: 2 tile counts + scan (default), 1 single
+                                 // pass (look-back; measured slower on C2: halo 1.62 vs 1.31 ms)
+    int64_t halo_cap = 0;        // PD_OPT_HALO_CAP: single-pass record capacity (0: n + n/8 + 4096)
+    uint64_t* h1_look = nullptr;
+    uint64_t h1_look_tiles = 0;
+    unsigned long long* h1_tick = nullptr;
+    unsigned long long h1_tick0 = 0;
+    uint32_t h1_epoch = 0;
+    double h1_ratio = 1.0;       // records per point of the last grid train (sizes the next cap)
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
     int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow

@@ -1180,6 +1180,49 @@ def test_train_many_partitions_fallbacks(native, P):
     assert m.n_clusters_ == nc_o and len(m.bounding_boxes) == P
 
 
+@pytest.mark.parametrize("P,cap", [(8, 0), (8, 1000), (8, -1), (300, 0), (300, 1000),
+                                   (300, -1), (1000, 0), (1000, 1000)])
+def test_halo_single_pass_equals_two_pass(native, P, cap):
+    """PD_OPT_HALO_PASSES: the single-pass halo (look-back offsets into
+    buffers of a guessed capacity) writes the same records as the two-pass
+    form — identical labels, core flags and record counts — with the key grids
+    and the split tree in LDS (P <= 64), the unmasked kernel reading the tree
+    from global memory (P = 300) and owner labels (P = 1000); cap 1000 forces
+    the overflow fallback (every tile past the capacity drops its stores, the
+    host reruns two passes), cap -1 sets the capacity to exactly the total
+    (no fallback, every slot written).  The round-5 fault (an illegal access
+    on the P = 300 overflow path) is this case.  A second train at the
+    default capacity follows one that overflowed: the capacity grows to the
+    previous records per point, so it takes a single pass."""
+    from pypardis_amd import DBSCAN, synth
+    X, cfg = synth.make_config("C2", n=200_000)
+    lab_o, core_o, _, nc_o = oracle.dbscan(X, cfg["eps"], cfg["min_samples"])
+    ctx = native.context()
+    Xd = _dev(X)
+    try:
+        ctx.set_option(native.PD_OPT_HALO_PASSES, 2)
+        m2 = DBSCAN(eps=cfg["eps"], min_samples=cfg["min_samples"], max_partitions=P).train(Xd)
+        R = int(ctx.timings()["records"])
+        ctx.set_option(native.PD_OPT_HALO_PASSES, 1)
+        ctx.set_option(native.PD_OPT_HALO_CAP, R if cap < 0 else cap)
+        m1 = DBSCAN(eps=cfg["eps"], min_samples=cfg["min_samples"], max_partitions=P).train(Xd)
+        t = ctx.timings()
+        ctx.set_option(native.PD_OPT_HALO_CAP, 0)   # (still the single pass)
+        m0 = DBSCAN(eps=cfg["eps"], min_samples=cfg["min_samples"], max_partitions=P).train(Xd)
+        t0 = ctx.timings()
+    finally:
+        ctx.set_option(native.PD_OPT_HALO_PASSES, 2)
+        ctx.set_option(native.PD_OPT_HALO_CAP, 0)
+    assert int(t["records"]) == R
+    if cap != 0:   # (the default capacity adapts to the previous train's records)
+        assert int(t["halo_fallback"]) == (1 if cap == 1000 else 0)
+    assert int(t0["records"]) == R and int(t0["halo_fallback"]) == 0
+    for m in (m0, m1, m2):
+        assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)
+        assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_o)
+        assert m.n_clusters_ == nc_o
+
+
 @pytest.mark.parametrize("cfg,n", [("C2", 2_000_000), ("C4", 3_000_000), ("C1", 500_000)])
 def test_label_buckets_equal_direct_scatter(native, cfg, n):
     """PD_OPT_LABEL_BUCKETS (default on): the labels reach input order through

@@ -16,8 +16,16 @@ headline kernel reaches (bench.py's roofline.latency_frac).
 Candidates per record come from one instrumented step (PD_OPT_SWEEP_STATS;
 same sweep order and early exit), replicas test the same candidates.
 
-  python tools/count_ceiling.py [--sizes 250000,500000,1000000,2000000]
+  python tools/count_ceiling.py [--config C2|C1|C4] [--sizes 250000,500000,1000000,2000000]
                                 [--full 100000000] [--out gpurun_out/count_ceiling.json]
+
+C1 slices are density-preserving like C2's (synth.make_config).  C4 has no
+density-preserving generator (its cities are fixed on the globe), so its
+slices are stratified window samples of the full 1B-point set: the globe is
+cut into 1-degree cells (1000 eps, so cell-border effects touch ~0.4 % of the
+points) and every k-th cell in raster order is kept whole — local densities
+are the full set's, and the mix of dense and sparse cells is its in
+expectation; the full measurement is the 1B-point set itself.
 """
 import argparse
 import json
@@ -31,8 +39,9 @@ import torch
 from pypardis_amd import _native, synth
 
 ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="C2", choices=["C2", "C1", "C4"])
 ap.add_argument("--sizes", default="250000,500000,1000000,2000000")
-ap.add_argument("--full", type=int, default=100_000_000)
+ap.add_argument("--full", type=int, default=None)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--out", default=None)
 args = ap.parse_args()
@@ -41,11 +50,32 @@ ctx = _native.context(0)
 dev = torch.device("cuda:0")
 
 
+_c4_full = None
+
+
+def points(n):
+    """(device points, eps, min_samples) of an n-point slice of the config."""
+    global _c4_full
+    if args.config != "C4":
+        X, cfg = synth.make_config(args.config, n=n)
+        return torch.from_numpy(X).to(dev), cfg["eps"], cfg["min_samples"]
+    cfg = dict(synth.CONFIGS["C4"])
+    if _c4_full is None:
+        _c4_full, _ = synth.make_config("C4", device=dev)
+    if n >= _c4_full.shape[0]:
+        return _c4_full, cfg["eps"], cfg["min_samples"]
+    # stratified 1-degree cells: keep every k-th cell in raster order
+    X = _c4_full
+    cx = torch.floor(X[:, 0].double() + 180.0).long()
+    cy = torch.floor(X[:, 1].double() + 60.0).long()
+    cell = cy * 360 + cx
+    k = max(1, int(round(X.shape[0] / n)))
+    keep = (cell % k) == 0
+    return X[keep].contiguous(), cfg["eps"], cfg["min_samples"]
+
+
 def measure(n, replay_lanes=None):
-    X, cfg = synth.make_config("C2", n=n)
-    Xd = torch.from_numpy(X).to(dev)
-    del X
-    eps, ms = cfg["eps"], cfg["min_samples"]
+    Xd, eps, ms = points(n)
     ctx.set_option(_native.PD_OPT_SWEEP_STATS, 1)
     _native.cluster(Xd, eps, ms)
     st = ctx.timings()
@@ -75,6 +105,8 @@ def measure(n, replay_lanes=None):
             "candidate_tests_per_s": tests / (tc * 1e-3), "lanes_per_s": lanes / (tc * 1e-3)}
 
 
+if args.full is None:
+    args.full = synth.CONFIGS[args.config]["n"]
 full = measure(args.full)
 print(json.dumps(full), flush=True)
 small = [measure(int(s), replay_lanes=full["records"]) for s in args.sizes.split(",")]
@@ -83,8 +115,9 @@ for r in small:
 best = max(small, key=lambda r: r["candidate_tests_per_s"])
 out = {"tool": "tools/count_ceiling.py",
        "kernel": "count4_kernel (the shipped 8-waves/SIMD build, replay mode)",
-       "config": "C2 density-preserving slices, max_partitions=1 (pd_cluster), replicated to "
-                 "the full run's lane count",
+       "config": f"{args.config} " + ("stratified 1-degree-cell samples of the full set"
+                                       if args.config == "C4" else "density-preserving slices") +
+                 ", max_partitions=1 (pd_cluster), replicated to the full run's lane count",
        "l2_resident_replay": small, "full": full,
        "ceiling_candidate_tests_per_s": best["candidate_tests_per_s"],
        "ceiling_points": best["points"],

@@ -96,6 +96,10 @@ def parse():
                     help="PD_OPT_XSUB override (axis-0 sub-cells per eps)")
     ap.add_argument("--halo-passes", type=int, default=None,
                     help="PD_OPT_HALO_PASSES override (1 single pass, 2 tile counts + scan)")
+    ap.add_argument("--kd-fuse", type=int, default=None,
+                    help="PD_OPT_KD_FUSE override (1: counts + children's moments in one pass)")
+    ap.add_argument("--verify-fused", type=int, default=None,
+                    help="PD_OPT_VERIFY_FUSED override (1: cell verify over every cell, screen inline)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
@@ -504,7 +508,9 @@ def main():
                      (_native.PD_OPT_DIR_PAGED, args.dir_paged),
                      (_native.PD_OPT_DENSE_SCREEN, args.dense_screen),
                      (_native.PD_OPT_XSUB, args.xsub),
-                     (_native.PD_OPT_HALO_PASSES, args.halo_passes)):
+                     (_native.PD_OPT_HALO_PASSES, args.halo_passes),
+                     (_native.PD_OPT_KD_FUSE, args.kd_fuse),
+                     (_native.PD_OPT_VERIFY_FUSED, args.verify_fused)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None

@@ -123,7 +123,21 @@ enum pd_option {
                                 measured slower on C2 (halo 1.62 vs 1.31 ms), kept for A/B.
                                 Same records either way */,
     PD_OPT_HALO_CAP = 26      /* single-pass halo record capacity (tests: force the overflow
-                                path); 0 (default): n + n/8 + 4096 */
+                                path); 0 (default): n + n/8 + 4096 */,
+    PD_OPT_KD_FUSE = 27       /* device-decided KD (pd_kd_build): 0 (default) a moments pass and
+                                a counts pass per level; 1: a level of <= 2 splits counts its
+                                candidates and sums the moments of each (split, candidate
+                                interval) in one pass, so the next level's moments need no pass
+                                of their own (4 passes over the points instead of 6 at
+                                max_partitions = 8) — measured slower on C2 (the interval-slot
+                                counting sort costs more than the pass it saves), kept for A/B.
+                                Same splits either way */,
+    PD_OPT_VERIFY_FUSED = 28  /* link stage cell verify: 0 (default) a screen pass flags the cells
+                                whose forward rows hold another root, then the flagged cells are
+                                listed and verified; 1: one pass over every cell with the screen
+                                inline (no flags, list, scan or host read) — measured slower on
+                                C2 (link 5.52 vs 5.32 ms: the flagged lanes' work diverges inside
+                                every wave), kept for A/B.  Same labels */
     /* Retired in round 5 (measured A/Bs whose losing kernels were removed;
        pd_ctx_set_option returns PD_EINVAL for them, and the numbers are not
        reused): 4 LINK_MODE, 5 JUMP_ROUNDS, 9 SWEEP_VARIANT, 10 BORDER_ROOTS,

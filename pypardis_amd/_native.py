@@ -33,6 +33,8 @@ PD_OPT_SHARD_CORE_BIT = 19
 PD_OPT_COUNT_REPLAY = 24
 PD_OPT_HALO_PASSES = 25
 PD_OPT_HALO_CAP = 26
+PD_OPT_KD_FUSE = 27
+PD_OPT_VERIFY_FUSED = 28
 # retired in round 5 (pardis.h): set_option raises for them
 PD_OPT_RETIRED = (4, 5, 9, 10, 16, 20, 21, 22, 23)
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",

@@ -167,6 +167,10 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         } else if (option == PD_OPT_HALO_PASSES) {
             if (value != 1 && value != 2) throw Error(PD_EINVAL, "halo passes is 1 or 2");
             ctx->c.halo_passes = (int)value;
+        } else if (option == PD_OPT_VERIFY_FUSED) {
+            ctx->c.verify_fused = value != 0;
+        } else if (option == PD_OPT_KD_FUSE) {
+            ctx->c.kd_fuse = value != 0;
         } else if (option == PD_OPT_HALO_CAP) {
             if (value < 0) throw Error(PD_EINVAL, "halo capacity must be >= 0");
             ctx->c.halo_cap = value;

@@ -2183,9 +2183,15 @@ __global__ __launch_bounds__(kBlock) void cell_verify_kernel(
     uint32_t nlist, const uint32_t* __restrict__ croot, const uint32_t* __restrict__ wroot,
     Cells C, int xsub, double eps, double eps2, float lo, float hi, uint32_t* __restrict__ par,
     uint2* __restrict__ plist, uint32_t pcap, uint32_t* __restrict__ pcount,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, const uint32_t* __restrict__ ncells) {
     constexpr int NF = ForwardRows<D, K>::NF;
     constexpr uint32_t kBuf = 1024;
+    // clist == nullptr (PD_OPT_VERIFY_FUSED): every cell, i.e. the screen
+    // fused in (the grid covers the records; blocks past the last cell leave)
+    if (!clist) {
+        nlist = *ncells;
+        if (blockIdx.x * kBlock >= nlist) return;
+    }
     // cell pairs whose roots differ go to a list, resolved by pair_kernel, so
     // the rare record-level work does not stall this kernel's waves: staged
     // per block in LDS, one global reservation per block (overflow of the
@@ -2195,7 +2201,7 @@ __global__ __launch_bounds__(kBlock) void cell_verify_kernel(
     if (threadIdx.x == 0) lcnt = 0;
     __syncthreads();
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t c = i < nlist ? clist[i] : 0u;
+    const uint32_t c = i < nlist ? (clist ? clist[i] : i) : 0u;
     const uint32_t rc = i < nlist ? croot[c] : kNone;
     uint32_t pairs = 0;
     if (rc != kNone) {
@@ -3162,15 +3168,23 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         uint32_t* vlist = ctx.arena.get<uint32_t>("verify_list", R);
         uint32_t* vcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)vtiles + 1);
         uint64_t* voff = ctx.arena.get<uint64_t>("tile_off", (size_t)vtiles + 1);
-        hipLaunchKernelGGL((verify_screen_kernel<D, K>), dim3(vtiles), dim3(kBlock), 0, s, keys,
-                           dncells, croot, wroot, C, xsub_of(ctx), vflag, vcnt);
-        const uint32_t NV = (uint32_t)tile_offsets(ctx, vcnt, vtiles, voff, s, true);
-        if (NV) {
-            hipLaunchKernelGGL(flag_list_kernel, dim3(vtiles), dim3(kBlock), 0, s, vflag, dncells,
-                               voff, vlist);
-            hipLaunchKernelGGL((cell_verify_kernel<T, D, M, K>), dim3(blocks(NV)), dim3(kBlock), 0,
-                               s, Xs, keys, vlist, NV, croot, wroot, C, xsub_of(ctx), eps, eps2,
-                               slo, shi, par, plist, pcap, pcount, sst);
+        if (ctx.verify_fused) {
+            // one pass over every cell: the screen's test inline (no flags,
+            // no list, no scan, no host read of the flagged count)
+            hipLaunchKernelGGL((cell_verify_kernel<T, D, M, K>), dim3(vtiles), dim3(kBlock), 0, s,
+                               Xs, keys, nullptr, 0u, croot, wroot, C, xsub_of(ctx), eps, eps2,
+                               slo, shi, par, plist, pcap, pcount, sst, dncells);
+        } else {
+            hipLaunchKernelGGL((verify_screen_kernel<D, K>), dim3(vtiles), dim3(kBlock), 0, s, keys,
+                               dncells, croot, wroot, C, xsub_of(ctx), vflag, vcnt);
+            const uint32_t NV = (uint32_t)tile_offsets(ctx, vcnt, vtiles, voff, s, true);
+            if (NV) {
+                hipLaunchKernelGGL(flag_list_kernel, dim3(vtiles), dim3(kBlock), 0, s, vflag, dncells,
+                                   voff, vlist);
+                hipLaunchKernelGGL((cell_verify_kernel<T, D, M, K>), dim3(blocks(NV)), dim3(kBlock), 0,
+                                   s, Xs, keys, vlist, NV, croot, wroot, C, xsub_of(ctx), eps, eps2,
+                                   slo, shi, par, plist, pcap, pcount, sst, nullptr);
+            }
         }
         hipLaunchKernelGGL((pair_kernel<T, D, M>), dim3(std::min(blocks(pcap), 4096u)), dim3(kBlock), 0, s, Xs, plist,
                            pcount, pcap, cstart, croot, eps, eps2, slo, shi, par);

@@ -631,11 +631,14 @@ __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X
 // Deterministic finish of kd_pass_kernel's block partials: per quantity,
 // lane t folds blocks t, t + 256, ... in order, then a fixed-shape tree over
 // the lanes (dd sums / counts / min / max).  out[W] as one block's layout.
+// One block per quantity (grid W; a lo word's block leaves at once — its hi
+// word's block writes both): the quantities reduce in parallel, each in the
+// same fixed order as before (round 6: 111 -> ~10 us for 16 x 13 moments).
 __global__ __launch_bounds__(kBlock) void kd_finish_kernel(const double* __restrict__ part, int nb,
                                                            int WM, int G, int D, int W,
                                                            double* __restrict__ out) {
     __shared__ double sh[kBlock], sl[kBlock];
-    for (int k = 0; k < W; ++k) {
+    for (int k = blockIdx.x; k < W; k += gridDim.x) {
         const bool mom = k < WM;
         const int r = mom ? k % G : 0;
         if (mom && r != 0 && (r - 1) % 2 == 1) continue;   // lo word: handled with its hi
@@ -836,6 +839,275 @@ __global__ __launch_bounds__(kBlock) void counts_reg_kernel(
     __syncthreads();
     for (int k = threadIdx.x; k < n_sel * 8 && k < NS * 8; k += kBlock)
         if (s_cnt[k]) atomicAdd(&out[k], (unsigned long long)s_cnt[k]);
+}
+
+// ---------------------------------------------------------------- fused level pass 2
+// Counts and the NEXT level's moments in one read of X (kd_build; VERDICT
+// r05 #6): apply the previous level's split (SP, R:dbscan/partition.py:66-68;
+// labels written back where they change, or all of them when none were
+// written yet, !LAB), count this level's seven candidate compares per split
+// (:60-63, counts_reg_kernel's register counters: c[s][i] = #(v[axis] <
+// bound i), c[s][7] = #points) and, MOM, the double-double moments (:86-89)
+// of every (split, interval) pair — interval q = #{i : v[axis] >= bound i}
+// in 0..7.  The bounds mean + (i - 3) 0.3 std are non-decreasing, so the
+// child a boundary i* makes is a run of intervals: left (v < bound i*) is q
+// <= i*, right (v >= bound i*, the split's predicate) is q > i*.  The next
+// level's moments are then dd sums of whole intervals (kdb_children_kernel),
+// with no moments pass of their own; exact double-double sums do not depend
+// on grouping, so they equal that pass's totals.
+// MOM tiles: a counting sort of the tile by interval slot in LDS, then wave
+// w sums slots w, w + NW, ... (NS * 8 / NW slots per wave, in registers).
+template <typename T, int D, bool LAB, bool SP, int NS, bool MOM, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(
+    (MOM && NS == 1 && sizeof(T) * D <= 12) ? 4 : 1))) void kdf_kernel(
+    const T* __restrict__ X, uint64_t n, int32_t* __restrict__ labels, SplitTab sp,
+    const int32_t* __restrict__ slot_of, int ntab, const int32_t* __restrict__ axis,
+    const double* __restrict__ bounds, int n_sel, unsigned long long* __restrict__ cnt_out,
+    double* __restrict__ part) {
+    constexpr int NT = 64 * NW;
+    constexpr int K = (sizeof(T) * D <= 16) ? 2 : 1;
+    constexpr int TP = 4 * K * NT;   // points per tile
+    constexpr int NI = NS * 8;       // interval slots
+    constexpr int SPW = MOM ? NI / NW : 1;
+    constexpr int G = 1 + 4 * D;
+    static_assert(!MOM || (NI % NW == 0 && SPW >= 1), "slots per wave");
+    __shared__ T s_val[MOM ? TP * D : 1];
+    // per (wave, slot): running ranks, then the wave's first position; per
+    // slot: the tile's total and first position
+    __shared__ int s_lcnt[MOM ? NW : 1][MOM ? NI : 1], s_woff[MOM ? NW : 1][MOM ? NI : 1];
+    __shared__ int s_tot[MOM ? NI : 1], s_seg[MOM ? NI : 1];
+    // MOM: this level's axes and bounds by slot (one lookup per point, no
+    // per-slot branches) and the block's points per (slot, interval) — the
+    // counts follow from them: v < bound i  <=>  interval <= i
+    __shared__ int s_axc[MOM ? NS : 1];
+    __shared__ double s_bnd[MOM ? NS * 7 : 1];
+    __shared__ unsigned int s_icnt[MOM ? NI : 1];
+    __shared__ int s_slot[SP ? kTabLds : 1], s_ax[SP ? kTabLds : 1], s_nl[SP ? kTabLds : 1];
+    __shared__ double s_bd[SP ? kTabLds : 1];
+    __shared__ int s_cur[kTabLds];
+    __shared__ unsigned int s_cnt[NS * 8];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    if constexpr (SP) {
+        for (int k = tid; k < sp.ntab; k += NT) s_slot[k] = sp.slot_of[k];
+        for (int k = tid; k < sp.nsplit; k += NT) {
+            s_ax[k] = sp.axis[k];
+            s_bd[k] = sp.boundary[k];
+            s_nl[k] = sp.newlab[k];
+        }
+    }
+    for (int k = tid; k < ntab; k += NT) s_cur[k] = slot_of[k];
+    for (int k = tid; k < NS * 8; k += NT) s_cnt[k] = 0;
+    if constexpr (MOM) {
+        for (int k = tid; k < NW * NI; k += NT) (&s_lcnt[0][0])[k] = 0;
+        for (int k = tid; k < NI; k += NT) s_icnt[k] = 0;
+        for (int k = tid; k < NS; k += NT) s_axc[k] = k < n_sel ? axis[k] : 0;
+        for (int k = tid; k < NS * 7; k += NT) s_bnd[k] = k < n_sel * 7 ? bounds[k] : 0.0;
+    }
+    int ax[NS];
+    double b[NS][7];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+        ax[q] = q < n_sel ? axis[q] : 0;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) b[q][i] = q < n_sel ? bounds[q * 7 + i] : 0.0;
+    }
+    __syncthreads();
+    uint32_t c[NS][8];
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c[q][i] = 0;
+    double ac[SPW];
+    DD as[SPW][D], aq[SPW][D];
+#pragma unroll
+    for (int o = 0; o < SPW; ++o) {
+        ac[o] = 0.0;
+#pragma unroll
+        for (int j = 0; j < D; ++j) as[o][j] = aq[o][j] = DD{0.0, 0.0};
+    }
+    const uint64_t nch = (n + 3) / 4;
+    const uint64_t ntile = (n + TP - 1) / TP;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+        T v[K][4][D];
+        int slot[K][4];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t ch = t * (TP / 4) + (uint64_t)k * NT + tid;
+            int m = 0;
+            if (ch < nch) {
+                m = load_chunk<T, D, true>(X, n, ch, v[k]);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int j = 0; j < D; ++j) v[k][q][j] = T(0);
+            }
+            int lab[4] = {0, 0, 0, 0};
+            if constexpr (LAB) {
+                if (m) load_labels4<true>(labels, ch, m, lab);
+            }
+            if constexpr (SP) {
+                bool changed = false;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int L = lab[q];
+                    if (q >= m || L < 0 || L >= sp.ntab) continue;
+                    const int a = s_slot[L];
+                    if (a < 0) continue;
+                    const double x = (double)pick_axis<T, D>(v[k][q], s_ax[a]);
+                    if (x >= s_bd[a]) {
+                        lab[q] = s_nl[a];
+                        changed = true;
+                    }
+                }
+                if (m && (changed || !LAB)) store_labels4<true>(labels, ch, m, lab);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int L = lab[q];
+                const int sl = (q < m && L >= 0 && L < ntab) ? s_cur[L] : -1;
+                slot[k][q] = -1;
+                if constexpr (MOM) {
+                    if (sl >= 0) {
+                        const double x = (double)pick_axis<T, D>(v[k][q], s_axc[sl]);
+                        int qi = 0;
+#pragma unroll
+                        for (int i = 0; i < 7; ++i) qi += x >= s_bnd[sl * 7 + i] ? 1 : 0;
+                        slot[k][q] = sl * 8 + qi;
+                    }
+                } else {
+#pragma unroll
+                    for (int sI = 0; sI < NS; ++sI) {
+                        if (sl != sI) continue;
+                        const double x = (double)pick_axis<T, D>(v[k][q], ax[sI]);
+                        ++c[sI][7];
+#pragma unroll
+                        for (int i = 0; i < 7; ++i) c[sI][i] += x < b[sI][i] ? 1u : 0u;
+                    }
+                }
+            }
+        }
+        if constexpr (MOM) {
+            // counting sort of the tile by interval slot: each item's rank
+            // among its wave's items of the slot (5-ballot peer mask, running
+            // per-(wave, slot) counters in LDS, as rsort's pass_kernel ranks
+            // digits), then the slots' and waves' starts, then the staging
+            int rk[K][4];
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int sl = slot[k][q];
+                    const unsigned u5 = sl < 0 ? 31u : (unsigned)sl;
+                    unsigned long long mk = ~0ull;
+#pragma unroll
+                    for (int bt = 0; bt < 5; ++bt) {
+                        const unsigned long long bb = __ballot((u5 >> bt) & 1u);
+                        mk &= ((u5 >> bt) & 1u) ? bb : ~bb;
+                    }
+                    const int base = sl >= 0 ? s_lcnt[w][sl] : 0;
+                    rk[k][q] = base + __popcll(mk & lt);
+                    if (sl >= 0 && (mk & lt) == 0) s_lcnt[w][sl] = base + __popcll(mk);
+                }
+            __syncthreads();
+            if (tid < NI) {
+                int a = 0;
+#pragma unroll
+                for (int u = 0; u < NW; ++u) a += s_lcnt[u][tid];
+                s_tot[tid] = a;
+                s_icnt[tid] += (unsigned int)a;
+            }
+            __syncthreads();
+            if (tid < NI) {
+                int a = 0;
+                for (int h = 0; h < tid; ++h) a += s_tot[h];
+                s_seg[tid] = a;
+#pragma unroll
+                for (int u = 0; u < NW; ++u) {
+                    s_woff[u][tid] = a;
+                    a += s_lcnt[u][tid];
+                    s_lcnt[u][tid] = 0;   // (restarted for the next tile)
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int sl = slot[k][q];
+                    if (sl < 0) continue;
+                    const int pos = s_woff[w][sl] + rk[k][q];
+#pragma unroll
+                    for (int j = 0; j < D; ++j) s_val[pos * D + j] = v[k][q][j];
+                }
+            __syncthreads();
+#pragma unroll
+            for (int o = 0; o < SPW; ++o) {
+                const int g = w + o * NW;
+                const int start = s_seg[g], len = s_tot[g];
+                for (int i = lane; i < len; i += 64) {
+                    const T* p = s_val + (size_t)(start + i) * D;
+                    ac[o] += 1.0;
+#pragma unroll
+                    for (int j = 0; j < D; ++j) {
+                        const T x = p[j];
+                        const T xx = x * x;   // squared in the input precision (numpy)
+                        dd_acc(as[o][j], (double)x);
+                        dd_acc(aq[o][j], (double)xx);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if constexpr (!MOM) {
+        // counts: one wave reduction and one LDS atomic per counter and wave
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                uint32_t x = c[q][i];
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, 64);
+                if (lane == 0 && x) atomicAdd(&s_cnt[q * 8 + i], x);
+            }
+    } else {
+        // counts from the intervals: #(v < bound i) = points in intervals
+        // <= i (bounds non-decreasing; NaN bounds: v < NaN never holds)
+        __syncthreads();
+        if (tid < NS * 8) {
+            const int sI = tid >> 3, i = tid & 7;
+            unsigned int x = 0;
+            for (int q = 0; q < 8; ++q) x += (i == 7 || q <= i) ? s_icnt[sI * 8 + q] : 0u;
+            if (i < 7 && isnan(s_bnd[sI * 7 + i])) x = 0;
+            s_cnt[tid] = x;
+        }
+    }
+    if constexpr (MOM) {
+        // each slot has one owner wave: its lane 0 writes the block partial
+        double* out = part + (uint64_t)blockIdx.x * NI * G;
+#pragma unroll
+        for (int o = 0; o < SPW; ++o) {
+            const int g = w + o * NW;
+            const double x = wave_sum(ac[o]);
+            if (lane == 0) out[g * G] = x;
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                const DD a = wave_dd(as[o][j]);
+                const DD q2 = wave_dd(aq[o][j]);
+                if (lane == 0) {
+                    out[g * G + 1 + 2 * j] = a.hi;
+                    out[g * G + 2 + 2 * j] = a.lo;
+                    out[g * G + 1 + 2 * D + 2 * j] = q2.hi;
+                    out[g * G + 2 + 2 * D + 2 * j] = q2.lo;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < n_sel * 8 && k < NS * 8; k += NT)
+        if (s_cnt[k]) atomicAdd(&cnt_out[k], (unsigned long long)s_cnt[k]);
 }
 
 // ---------------------------------------------------------------- split
@@ -1153,7 +1425,7 @@ void run_pass(Ctx& ctx, const T* X, int64_t n, int32_t* labels, const SplitTab& 
     res.assign(W, 0.0);
     if constexpr (W > 0) {
         double* fin = ctx.arena.get<double>("pass_fin", W);
-        hipLaunchKernelGGL(kd_finish_kernel, dim3(1), dim3(kBlock), 0, s, part, nb, WM, G, D, W,
+        hipLaunchKernelGGL(kd_finish_kernel, dim3(W), dim3(kBlock), 0, s, part, nb, WM, G, D, W,
                            fin);
         PD_HIP(hipGetLastError());
         double* h = (double*)pinned(ctx, sizeof(double) * W);
@@ -1442,6 +1714,37 @@ __global__ void kdb_boundary_kernel(const unsigned long long* __restrict__ cnt, 
     t[12] = boundary[k];
 }
 
+// The next level's moments from this level's interval moments (kdf_kernel):
+// split k's left child is its intervals q <= i* (i* = the chosen candidate,
+// trace[11]), the right child q > i*; dst[2k + side] = the child's slot in the
+// next level (-1: not split there).  Counts are exact integers; the sums are
+// double-double additions of whole intervals (exact, so equal to a moments
+// pass over the child).
+__global__ void kdb_children_kernel(const double* __restrict__ fin, int S, int G,
+                                    const double* __restrict__ trace,
+                                    const int32_t* __restrict__ dst, double* __restrict__ mom) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = idx >> 1, side = idx & 1;
+    if (k >= S) return;
+    const int j = dst[2 * k + side];
+    if (j < 0) return;
+    const int bi = (int)trace[(size_t)k * kTrace + 11];
+    const int q0 = side ? bi + 1 : 0, q1 = side ? 7 : bi;
+    double* o = mom + (size_t)j * G;
+    double c = 0.0;
+    for (int q = q0; q <= q1; ++q) c += fin[((size_t)k * 8 + q) * G];
+    o[0] = c;
+    for (int r = 1; r < G; r += 2) {
+        DD a{0.0, 0.0};
+        for (int q = q0; q <= q1; ++q) {
+            const double* p = fin + ((size_t)k * 8 + q) * G;
+            a = dd_add(a, DD{p[r], p[r + 1]});
+        }
+        o[r] = a.hi;
+        o[r + 1] = a.lo;
+    }
+}
+
 namespace {
 // run_pass without the host sync: the finished quantities stay on the device
 // (fin: NG x G moments, then the bbox; may be null when the pass has none).
@@ -1465,7 +1768,7 @@ void run_pass_dev(Ctx& ctx, const T* X, int64_t n, int32_t* labels, const SplitT
                        X, (uint64_t)n, labels, sp, sel, part);
     PD_HIP(hipGetLastError());
     if constexpr (W > 0) {
-        hipLaunchKernelGGL(kd_finish_kernel, dim3(1), dim3(kBlock), 0, s, part, nb, WM, G, D, W,
+        hipLaunchKernelGGL(kd_finish_kernel, dim3(W), dim3(kBlock), 0, s, part, nb, WM, G, D, W,
                            fin);
         PD_HIP(hipGetLastError());
     }
@@ -1524,6 +1827,39 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
     }
     double* trace = ctx.arena.get<double>("kdb_trace", (size_t)total * kTrace);
     unsigned long long* dcnt = ctx.arena.get<unsigned long long>("kdb_cnt", (size_t)kTabLds * 8);
+    // Fused levels (kdf_kernel): a level of <= 2 splits whose
+    // children are exactly the next level's splits counts its candidates and
+    // sums its (split, interval) moments in one pass; the next level's
+    // moments come from those (kdb_children_kernel) and its own counting pass
+    // applies this level's split.  dst[l]: per split of level l, the slot of
+    // its left / right child in level l + 1 (-1: not split there).
+    std::vector<char> fuse(n_levels, 0);
+    std::vector<std::vector<int32_t>> dst(n_levels);
+    for (int l = 0; ctx.kd_fuse && l + 1 < n_levels; ++l) {
+        const int S = sizes[l], S1 = sizes[l + 1];
+        if (S > 2 || S1 > 4) continue;
+        std::vector<int32_t> dd(2 * S, -1);
+        int found = 0;
+        for (int j = 0; j < S1; ++j) {
+            const int X = cur[first[l + 1] + j];
+            for (int k = 0; k < S; ++k) {
+                if (cur[first[l] + k] == X && dd[2 * k] < 0) { dd[2 * k] = j; ++found; break; }
+                if (newl[first[l] + k] == X && dd[2 * k + 1] < 0) { dd[2 * k + 1] = j; ++found; break; }
+            }
+        }
+        if (found != S1) continue;   // a split of level l + 1 is not a child of level l
+        fuse[l] = 1;
+        dst[l] = dd;
+    }
+    int32_t* ddst = ctx.arena.get<int32_t>("kdb_dst", (size_t)n_levels * 8);
+    {
+        std::vector<int32_t> hd((size_t)n_levels * 8, -1);
+        for (int l = 0; l < n_levels; ++l)
+            for (size_t i = 0; i < dst[l].size(); ++i) hd[(size_t)l * 8 + i] = dst[l][i];
+        int32_t* hp = (int32_t*)(h + off[n_levels]);   // (the trace's block: read back only later)
+        std::memcpy(hp, hd.data(), sizeof(int32_t) * hd.size());
+        PD_HIP(hipMemcpyAsync(ddst, hp, sizeof(int32_t) * hd.size(), hipMemcpyHostToDevice, s));
+    }
     dispatch_t(dtype, [&](auto tp) {
         using T = std::remove_pointer_t<decltype(tp)>;
         dispatch_d(d, [&](auto Dc) {
@@ -1532,14 +1868,21 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
             const T* Xt = (const T*)X;
             double* fin0 = ctx.arena.get<double>("kdb_fin0", G + 2 * D + 1);
             double* mom = ctx.arena.get<double>("kdb_mom", (size_t)kTabLds * G);
+            double* momc = ctx.arena.get<double>("kdb_momc", (size_t)2 * 8 * G);   // children's
+            double* ifin = ctx.arena.get<double>("kdb_ifin", (size_t)2 * 8 * G);   // interval moments
             const SplitTab none{nullptr, 0, nullptr, nullptr, nullptr, 0};
             run_pass_dev<T, D, false, false, 1, true>(ctx, Xt, n, labels, none,
                                                       make_int4(cur[0], -2, -2, -2), fin0, s);
+            bool labels_written = false;   // some pass wrote the labels
             for (int l = 0; l < n_levels; ++l) {
                 const int S = sizes[l];
                 const int32_t* sel = cur + first[l];
                 const double* m = fin0;
-                if (l > 0) {
+                // this level's counting pass still has the previous split to apply
+                const bool pending = l > 0 && fuse[l - 1];
+                if (l > 0 && pending) {
+                    m = momc;
+                } else if (l > 0) {
                     const Lv& p = lv[l - 1];
                     const SplitTab sp{p.slot, ntab[l - 1], p.axis, p.boundary, p.newlab, sizes[l - 1]};
                     for (int g0 = 0; g0 < S; g0 += kGroup) {
@@ -1548,7 +1891,7 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                         for (int g = 0; g < ng; ++g) (&sl.x)[g] = sel[g0 + g];
                         dispatch_ng(ng, [&](auto NGc) {
                             constexpr int NG = decltype(NGc)::value;
-                            if (g0 == 0 && l == 1)   // labels all 0 so far: not read
+                            if (g0 == 0 && !labels_written)   // labels all 0 so far: not read
                                 run_pass_dev<T, D, false, true, NG, false>(ctx, Xt, n, labels, sp, sl,
                                                                            mom, s);
                             else if (g0 == 0)
@@ -1559,18 +1902,74 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                                     ctx, Xt, n, labels, none, sl, mom + (size_t)g0 * G, s);
                         });
                     }
+                    labels_written = true;
                     m = mom;
                 }
                 double* tr = trace + (size_t)first[l] * kTrace;
                 hipLaunchKernelGGL(kdb_axes_kernel, dim3(1), dim3(kTabLds), 0, s, m, S, D, G,
                                    lv[l].axis, lv[l].bounds, tr, dcnt);
                 const unsigned nb4 = grid_for((n + 3) / 4, 2048);
-                if (S <= 4) {
+                if (fuse[l] || pending) {
+                    // kdf_kernel: the previous split (pending), the counts, and
+                    // (fuse) the children's interval moments
+                    const Lv* pv = pending ? &lv[l - 1] : nullptr;
+                    const SplitTab sp = pending ? SplitTab{pv->slot, ntab[l - 1], pv->axis, pv->boundary,
+                                                           pv->newlab, sizes[l - 1]}
+                                                : none;
+                    auto go = [&](auto LABc, auto SPc, auto NSc, auto MOMc) {
+                        constexpr bool LAB_ = decltype(LABc)::value, SP_ = decltype(SPc)::value,
+                                       MOM_ = decltype(MOMc)::value;
+                        constexpr int NS_ = decltype(NSc)::value;
+                        constexpr int NW_ = (MOM_ && NS_ == 2) ? 8 : 4;
+                        constexpr int TP_ = 4 * ((sizeof(T) * D <= 16) ? 2 : 1) * 64 * NW_;
+                        static int resident = 0;
+                        if (!resident) {
+                            int per_cu = 0, dev = 0, cus = 0;
+                            PD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                                &per_cu,
+                                reinterpret_cast<const void*>(&kdf_kernel<T, D, LAB_, SP_, NS_, MOM_, NW_>),
+                                64 * NW_, 0));
+                            PD_HIP(hipGetDevice(&dev));
+                            PD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+                            resident = std::max(1, per_cu) * std::max(1, cus);
+                        }
+                        const int nb = (int)std::min<int64_t>(resident, std::max<int64_t>(1, (n + TP_ - 1) / TP_));
+                        double* part = MOM_ ? ctx.arena.get<double>("pass_part", (size_t)nb * NS_ * 8 * G)
+                                            : nullptr;
+                        hipLaunchKernelGGL((kdf_kernel<T, D, LAB_, SP_, NS_, MOM_, NW_>), dim3(nb),
+                                           dim3(64 * NW_), 0, s, Xt, (uint64_t)n, labels, sp, lv[l].slot,
+                                           ntab[l], lv[l].axis, lv[l].bounds, S, dcnt, part);
+                        PD_HIP(hipGetLastError());
+                        if constexpr (MOM_) {
+                            hipLaunchKernelGGL(kd_finish_kernel, dim3(NS_ * 8 * G), dim3(kBlock), 0, s, part, nb,
+                                               NS_ * 8 * G, G, D, NS_ * 8 * G, ifin);
+                            PD_HIP(hipGetLastError());
+                        }
+                    };
+                    using TT = std::true_type;
+                    using FF = std::false_type;
+                    auto ns = [&](auto LABc, auto SPc, auto MOMc) {
+                        if (S == 1) go(LABc, SPc, std::integral_constant<int, 1>{}, MOMc);
+                        else if (S == 2) go(LABc, SPc, std::integral_constant<int, 2>{}, MOMc);
+                        else if constexpr (!decltype(MOMc)::value)
+                            go(LABc, SPc, std::integral_constant<int, 4>{}, MOMc);
+                    };
+                    if (S > 4 || (fuse[l] && S > 2)) throw Error(-1, "kd_build: fused level too wide");
+                    if (fuse[l]) {
+                        if (!pending) ns(FF{}, FF{}, TT{});   // level 0: labels all 0, nothing to apply
+                        else if (!labels_written) ns(FF{}, TT{}, TT{});
+                        else ns(TT{}, TT{}, TT{});
+                    } else {
+                        if (!labels_written) ns(FF{}, TT{}, FF{});
+                        else ns(TT{}, TT{}, FF{});
+                    }
+                    if (pending) labels_written = true;
+                } else if (S <= 4) {
                     auto go = [&](auto NSc) {
                         constexpr int NS = decltype(NSc)::value;
                         hipLaunchKernelGGL((counts_reg_kernel<T, D, NS>), dim3(nb4), dim3(kBlock), 0,
-                                           s, Xt, (uint64_t)n, l == 0 ? nullptr : labels, lv[l].slot, ntab[l],
-                                           lv[l].axis, lv[l].bounds, S, dcnt);
+                                           s, Xt, (uint64_t)n, labels_written ? labels : nullptr,
+                                           lv[l].slot, ntab[l], lv[l].axis, lv[l].bounds, S, dcnt);
                     };
                     if (S == 1)
                         go(std::integral_constant<int, 1>{});
@@ -1590,6 +1989,11 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                 hipLaunchKernelGGL(kdb_boundary_kernel, dim3(1), dim3(kTabLds), 0, s, dcnt, S,
                                    lv[l].bounds, lv[l].boundary, tr);
                 PD_HIP(hipGetLastError());
+                if (fuse[l]) {
+                    hipLaunchKernelGGL(kdb_children_kernel, dim3(1), dim3(64), 0, s, ifin, S, G, tr,
+                                       ddst + (size_t)l * 8, momc);
+                    PD_HIP(hipGetLastError());
+                }
             }
             // the last level's split alone (or left to the caller: pd_train_tree
             // replays the split tree, the labels are then applied lazily)
@@ -1597,7 +2001,7 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                 const Lv& p = lv[n_levels - 1];
                 const SplitTab sp{p.slot, ntab[n_levels - 1], p.axis, p.boundary, p.newlab,
                                   sizes[n_levels - 1]};
-                if (n_levels == 1)   // no level pass wrote the labels yet
+                if (!labels_written)   // no level pass wrote the labels yet
                     run_pass_dev<T, D, false, true, 0, false>(ctx, Xt, n, labels, sp,
                                                               make_int4(-2, -2, -2, -2), nullptr, s);
                 else

@@ -3,6 +3,8 @@
 // as torch allocations and the arena are).
 #pragma once
 
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace pd {
@@ -73,12 +75,23 @@ __device__ __forceinline__ void store_labels4(int32_t* __restrict__ L, uint64_t 
     }
 }
 
+// v[ax] for a per-lane ax, as a bitwise select over the D values: written as
+// a select chain, the compiler turns it into an indexed load from a stack copy
+// of v (a scratch round trip per point with a full vmcnt wait, 112 bytes of
+// scratch per lane in the KD split passes).
 template <typename T, int D>
 __device__ __forceinline__ T pick_axis(const T (&v)[D], int ax) {
-    T r = v[0];
+    using U = std::conditional_t<sizeof(T) == 4, uint32_t, uint64_t>;
+    U r = 0;
 #pragma unroll
-    for (int j = 1; j < D; ++j) r = ax == j ? v[j] : r;
-    return r;
+    for (int j = 0; j < D; ++j) {
+        U b;
+        __builtin_memcpy(&b, &v[j], sizeof(T));
+        r |= b & (U)0 - (U)(ax == j);
+    }
+    T out;
+    __builtin_memcpy(&out, &r, sizeof(T));
+    return out;
 }
 
 }  // namespace pd

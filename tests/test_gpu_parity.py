@@ -1140,23 +1140,33 @@ def _kd_case(name):
 def test_kd_device_decisions_equal_host(native, name, P):
     """pd_kd_build (level decisions on the device, one sync) gives the per-pass
     host-decided path's split trace, boxes and labels bit for bit — levels of
-    1..128 splits, fp32 / fp64, zero variance, fewer points than partitions."""
+    1..128 splits, fp32 / fp64, zero variance, fewer points than partitions —
+    without the fused levels (the default) and with them (PD_OPT_KD_FUSE:
+    counts + the children's interval moments in one pass)."""
     from pypardis_amd import KDPartitioner, partition
     X = _kd_case(name)
     Xd = _dev(X)
     a = KDPartitioner(Xd, P)
+    ctx = native.context()
+    ctx.set_option(native.PD_OPT_KD_FUSE, 1)
+    try:
+        c = KDPartitioner(Xd, P)
+    finally:
+        ctx.set_option(native.PD_OPT_KD_FUSE, 0)
     partition.DEVICE_DECISIONS = False
     try:
         b = KDPartitioner(Xd, P)
     finally:
         partition.DEVICE_DECISIONS = True
-    sa, fa = _kd_arrays(a.splits)
     sb, fb = _kd_arrays(b.splits)
-    assert np.array_equal(sa, sb)
-    assert np.array_equal(fa, fb, equal_nan=True)
-    assert np.array_equal(a.box_array(), b.box_array(), equal_nan=True)
-    assert torch.equal(a.labels, b.labels)
-    assert a.data_box[0].tolist() == b.data_box[0].tolist()
+    for m in (a, c):
+        sa, fa = _kd_arrays(m.splits)
+        assert np.array_equal(sa, sb)
+        assert np.array_equal(fa, fb, equal_nan=True)
+        assert np.array_equal(m.box_array(), b.box_array(), equal_nan=True)
+        assert torch.equal(m.labels, b.labels)
+        assert m.data_box[0].tolist() == b.data_box[0].tolist()
+    sa, fa = _kd_arrays(a.splits)
     if name == "c2_1m" and P == 8:   # and the oracle's exact restatement
         ref = oracle.kd_partition(X, P, sums="exact")
         assert np.array_equal(sa, _kd_arrays(ref["splits"])[0])
@@ -1221,6 +1231,27 @@ def test_halo_single_pass_equals_two_pass(native, P, cap):
         assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)
         assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_o)
         assert m.n_clusters_ == nc_o
+
+
+@pytest.mark.parametrize("cfg,n", [("C2", 2_000_000), ("C4", 3_000_000), ("C1", 500_000)])
+def test_verify_fused_equals_listed(native, cfg, n):
+    """PD_OPT_VERIFY_FUSED: the cell verify over every cell with the screen
+    inline gives the labels of the screen -> flag list -> verify form."""
+    from pypardis_amd import DBSCAN, synth
+    X, c = synth.make_config(cfg, n=n, device="cuda" if cfg == "C4" else "cpu")
+    Xd = X if torch.is_tensor(X) else _dev(X)
+    ctx = native.context()
+    outs = []
+    for on in (1, 0):
+        ctx.set_option(native.PD_OPT_VERIFY_FUSED, on)
+        try:
+            m = DBSCAN(eps=c["eps"], min_samples=c["min_samples"],
+                       max_partitions=c.get("max_partitions") or 1).train(Xd)
+        finally:
+            ctx.set_option(native.PD_OPT_VERIFY_FUSED, 0)
+        outs.append((m.labels_.clone(), m.core_sample_mask_.clone(), m.n_clusters_))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
 
 
 @pytest.mark.parametrize("cfg,n", [("C2", 2_000_000), ("C4", 3_000_000), ("C1", 500_000)])

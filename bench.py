@@ -100,6 +100,8 @@ def parse():
                     help="PD_OPT_KD_FUSE override (1: counts + children's moments in one pass)")
     ap.add_argument("--verify-fused", type=int, default=None,
                     help="PD_OPT_VERIFY_FUSED override (1: cell verify over every cell, screen inline)")
+    ap.add_argument("--halo-tree", type=int, default=None,
+                    help="PD_OPT_HALO_TREE override (1: box tests only near split planes)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
@@ -510,7 +512,8 @@ def main():
                      (_native.PD_OPT_XSUB, args.xsub),
                      (_native.PD_OPT_HALO_PASSES, args.halo_passes),
                      (_native.PD_OPT_KD_FUSE, args.kd_fuse),
-                     (_native.PD_OPT_VERIFY_FUSED, args.verify_fused)):
+                     (_native.PD_OPT_VERIFY_FUSED, args.verify_fused),
+                     (_native.PD_OPT_HALO_TREE, args.halo_tree)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None

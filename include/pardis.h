@@ -137,7 +137,13 @@ enum pd_option {
                                 listed and verified; 1: one pass over every cell with the screen
                                 inline (no flags, list, scan or host read) — measured slower on
                                 C2 (link 5.52 vs 5.32 ms: the flagged lanes' work diverges inside
-                                every wave), kept for A/B.  Same labels */
+                                every wave), kept for A/B.  Same labels */,
+    PD_OPT_HALO_TREE = 29     /* grid train halo (two-pass form, split tree replayed, P <= 64):
+                                1 (default) a point farther than 2 eps from every split plane on
+                                its KD path is in its owner's expanded box only — one record, no
+                                box tests; the points near a plane are listed per tile and take
+                                the full test.  0: every point tests every expanded box.  Same
+                                records either way */
     /* Retired in round 5 (measured A/Bs whose losing kernels were removed;
        pd_ctx_set_option returns PD_EINVAL for them, and the numbers are not
        reused): 4 LINK_MODE, 5 JUMP_ROUNDS, 9 SWEEP_VARIANT, 10 BORDER_ROOTS,

@@ -35,6 +35,7 @@ PD_OPT_HALO_PASSES = 25
 PD_OPT_HALO_CAP = 26
 PD_OPT_KD_FUSE = 27
 PD_OPT_VERIFY_FUSED = 28
+PD_OPT_HALO_TREE = 29
 # retired in round 5 (pardis.h): set_option raises for them
 PD_OPT_RETIRED = (4, 5, 9, 10, 16, 20, 21, 22, 23)
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",

@@ -167,6 +167,8 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         } else if (option == PD_OPT_HALO_PASSES) {
             if (value != 1 && value != 2) throw Error(PD_EINVAL, "halo passes is 1 or 2");
             ctx->c.halo_passes = (int)value;
+        } else if (option == PD_OPT_HALO_TREE) {
+            ctx->c.halo_tree = value != 0;
         } else if (option == PD_OPT_VERIFY_FUSED) {
             ctx->c.verify_fused = value != 0;
         } else if (option == PD_OPT_KD_FUSE) {

@@ -494,6 +494,37 @@ __device__ __forceinline__ int tree_owner(const KdTree& t, const int32_t* slot,
     return lab;
 }
 
+// tree_owner, and whether the point lies within `marg` (2 eps, grown) of a
+// split plane on its path, or of a non-finite one.  A point farther than
+// 2 eps from every plane on its path lies in its owner's expanded box only:
+// any other KD box is separated from it by one of those planes (the first
+// split where the two paths part), so its 2 eps expansion cannot reach it.
+template <typename T, int D>
+__device__ __forceinline__ int tree_owner_near(const KdTree& t, const int32_t* slot,
+                                               const int32_t* ax_new, const double* bound,
+                                               double marg, const T (&v)[D], bool& near) {
+    int lab = 0;
+    near = false;
+    for (int l = 0; l < t.nl; ++l) {
+        if (lab >= t.ntab[l]) continue;
+        if (!PD_OK(t.toff[l] + lab < t.nslot, 1, t.toff[l] + lab)) continue;
+        const int sl = slot[t.toff[l] + lab];
+        if (sl < 0) continue;
+        const int e = t.eoff[l] + sl;
+        if (!PD_OK(e < t.ne, 2, e)) continue;
+        const int ax = ax_new[2 * e];
+        if (!PD_OK(ax >= 0 && ax < D, 3, ax)) continue;
+        T x = v[0];
+#pragma unroll
+        for (int j = 1; j < D; ++j) x = ax == j ? v[j] : x;
+        const double xd = (double)x, b = bound[e];
+        // (2^-20 |b|: far beyond the fp64 expand's and the fp32 bounds' rounding)
+        near |= !(fabs(xd - b) > marg + 9.5367431640625e-07 * fabs(b));
+        if (xd >= b) lab = ax_new[2 * e + 1];
+    }
+    return lab;
+}
+
 // Halo records (R:dbscan/dbscan.py:136-151) in two ordered passes over the
 // points: halo_tile_kernel counts each tile's records (a tile = one block's
 // 4·256 points), the host scans the tile counts (rocPRIM), and
@@ -506,6 +537,15 @@ __device__ __forceinline__ int tree_owner(const KdTree& t, const int32_t* slot,
 // The membership of each point is a bit mask over the neighbourhoods (P <=
 // 64; MASK = false recomputes instead), built branch-free in the input
 // precision with one wave-uniform grid load per neighbourhood.
+// The near-plane points of a tile, listed in LDS: (thread << 2 | step), and
+// each one's full-test record count and neighbourhood mask.
+struct NearLds {
+    uint32_t n;
+    uint32_t list[4 * kBlock];
+    uint32_t cnt[4 * kBlock];
+    unsigned long long mask[4 * kBlock];
+};
+
 template <typename T, int D, bool MASK>
 __device__ __forceinline__ void halo_points(const T* __restrict__ X, uint64_t n,
                                             const PartGrid* __restrict__ parts, int P,
@@ -532,6 +572,69 @@ __device__ __forceinline__ void halo_points(const T* __restrict__ X, uint64_t n,
     }
 }
 
+// halo_points with the split tree in LDS (P <= 64, pd_train_tree): each
+// point's owner by the tree replay; a point far from every split plane on its
+// path is in its owner's expanded box alone (tree_owner_near) — one record, no
+// box tests; the few near a plane (the halo duplicates and their
+// neighbours, ~1-2 % at the BASELINE configs) are listed block-wide and take
+// the full test, one list entry per lane.  Same counts and masks as
+// halo_points.  own[q]: the owner (-1 past n).  The caller zeroes nl.n and
+// synchronises before the call.
+template <typename T, int D>
+__device__ __forceinline__ void halo_points_tree(const T* __restrict__ X, uint64_t n,
+                                                 const PartGrid* __restrict__ parts, int P,
+                                                 uint64_t tile, const KdTree& tree,
+                                                 const int32_t* t_slot, const int32_t* t_axn,
+                                                 const double* t_bd, double marg, NearLds& nl,
+                                                 uint64_t (&idx)[4], T (&v)[4][D],
+                                                 unsigned long long (&m)[4], uint32_t (&cnt)[4],
+                                                 int (&own)[4]) {
+    const uint64_t base = tile * (4 * kBlock) + (threadIdx.x >> 6) * 256 + (threadIdx.x & 63);
+    int slotq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        idx[q] = base + 64 * q;
+        const bool ok = idx[q] < n;
+#pragma unroll
+        for (int j = 0; j < D; ++j) v[q][j] = ok ? X[idx[q] * D + j] : T(NAN);
+        bool near = false;
+        own[q] = ok ? tree_owner_near<T, D>(tree, t_slot, t_axn, t_bd, marg, v[q], near) : -1;
+        cnt[q] = ok ? 1u : 0u;
+        m[q] = ok ? 1ull << (own[q] & 63) : 0ull;
+        slotq[q] = -1;
+        if (ok && near) {
+            slotq[q] = (int)atomicAdd(&nl.n, 1u);
+            nl.list[slotq[q]] = (threadIdx.x << 2) | (uint32_t)q;
+        }
+    }
+    __syncthreads();
+    const uint32_t nn = nl.n;
+    const uint64_t tb = tile * (4 * kBlock);
+    for (uint32_t k = threadIdx.x; k < nn; k += kBlock) {
+        const uint32_t e = nl.list[k], th = e >> 2, q = e & 3;
+        const uint64_t i = tb + (th >> 6) * 256 + (th & 63) + 64 * q;
+        T u[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) u[j] = X[i * D + j];
+        uint32_t c = 0;
+        unsigned long long mm = 0;
+        for (int Lb = 0; Lb < P; ++Lb) {
+            const bool in = in_box_t<T, D>(u, parts[Lb]);
+            c += in ? 1u : 0u;
+            mm |= (unsigned long long)in << Lb;
+        }
+        nl.cnt[k] = c;
+        nl.mask[k] = mm;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (slotq[q] >= 0) {
+            cnt[q] = nl.cnt[slotq[q]];
+            m[q] = nl.mask[slotq[q]];
+        }
+}
+
 __device__ __forceinline__ uint32_t block_sum_u32(uint32_t v) {
     __shared__ uint32_t ws[kBlock / 64];
 #pragma unroll
@@ -553,10 +656,13 @@ __device__ __forceinline__ void tile_count_out(uint32_t* tile_cnt, uint32_t c) {
 
 constexpr int kCtrs = 16;   // train counters: [0..7] lists, [8..9] big / mid cells, [10] pairs
 
-template <typename T, int D>
+// TREE (the split tree in LDS, P <= 64): the near-plane fast path
+// (halo_points_tree); marg = 2 eps, slightly grown.
+template <typename T, int D, bool TREE>
 __global__ __launch_bounds__(kBlock) void halo_tile_kernel(const T* __restrict__ X, uint64_t n,
                                                            const PartGrid* __restrict__ parts,
-                                                           int P, uint32_t* __restrict__ tile_cnt,
+                                                           int P, KdTree tree, double marg,
+                                                           uint32_t* __restrict__ tile_cnt,
                                                            uint32_t* __restrict__ ctrs,
                                                            uint32_t* __restrict__ sort_hist) {
     // the train's small counters (dup / root / core / border lists, big and
@@ -571,7 +677,21 @@ __global__ __launch_bounds__(kBlock) void halo_tile_kernel(const T* __restrict__
     T v[4][D];
     unsigned long long m[4];
     uint32_t cnt[4];
-    halo_points<T, D, false>(X, n, parts, P, blockIdx.x, idx, v, m, cnt);
+    if constexpr (TREE) {
+        __shared__ int32_t t_slot[kTreeSlots], t_axn[2 * kTreeSplits];
+        __shared__ double t_bd[kTreeSplits];
+        __shared__ NearLds nl;
+        for (int k = threadIdx.x; k < tree.nslot; k += kBlock) t_slot[k] = tree.slot[k];
+        for (int k = threadIdx.x; k < 2 * tree.ne; k += kBlock) t_axn[k] = tree.ax_new[k];
+        for (int k = threadIdx.x; k < tree.ne; k += kBlock) t_bd[k] = tree.bound[k];
+        if (threadIdx.x == 0) nl.n = 0;
+        __syncthreads();
+        int own[4];
+        halo_points_tree<T, D>(X, n, parts, P, blockIdx.x, tree, t_slot, t_axn, t_bd, marg, nl, idx,
+                               v, m, cnt, own);
+    } else {
+        halo_points<T, D, false>(X, n, parts, P, blockIdx.x, idx, v, m, cnt);
+    }
     const uint32_t t = block_sum_u32(cnt[0] + cnt[1] + cnt[2] + cnt[3]);
     if (threadIdx.x == 0) tile_count_out(tile_cnt, t);
 }
@@ -676,7 +796,8 @@ __device__ __forceinline__ bool halo_stage(HaloLds<D>& L, const PartGrid* __rest
 
 // write the records of one tile's points from record offset wbase (this
 // wave's first record); stores at or past cap are dropped
-template <typename T, int D, typename K, bool MASK>
+// PRE: the owners are already known (own_in, halo_points_tree)
+template <typename T, int D, typename K, bool MASK, bool PRE = false>
 __device__ __forceinline__ void halo_emit(const HaloLds<D>& L, const PartGrid* __restrict__ parts,
                                           int P, const int32_t* __restrict__ owner,
                                           const KdTree& tree, bool tree_lds, uint64_t n,
@@ -684,13 +805,14 @@ __device__ __forceinline__ void halo_emit(const HaloLds<D>& L, const PartGrid* _
                                           const unsigned long long (&m)[4],
                                           const uint32_t (&cnt)[4], const uint32_t (&ex)[4],
                                           uint64_t wbase, uint64_t cap, K* __restrict__ keys,
-                                          uint32_t* __restrict__ vals) {
+                                          uint32_t* __restrict__ vals, const int (&own_in)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         if (!cnt[q]) continue;
         if (!PD_OK(idx[q] < n, 4, idx[q])) continue;
         // P == 1: neighbourhood 0
-        const int own = owner  ? owner[idx[q]]
+        const int own = PRE      ? own_in[q]
+                        : owner  ? owner[idx[q]]
                         : !tree.nl ? 0
                         : tree_lds ? tree_owner<T, D>(tree, L.t_slot, L.t_axn, L.t_bd, v[q])
                                    : tree_owner<T, D>(tree, tree.slot, tree.ax_new, tree.bound, v[q]);
@@ -726,27 +848,40 @@ __device__ __forceinline__ void halo_emit(const HaloLds<D>& L, const PartGrid* _
     }
 }
 
-template <typename T, int D, typename K, bool MASK>
+template <typename T, int D, typename K, bool MASK, bool TREE = false>
 __global__ __launch_bounds__(kBlock) void halo_write_kernel(
     const T* __restrict__ X, uint64_t n, const PartGrid* __restrict__ parts, int P,
-    const int32_t* __restrict__ owner, KdTree tree, const uint64_t* __restrict__ tile_off,
-    uint64_t cap, K* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const int32_t* __restrict__ owner, KdTree tree, double marg,
+    const uint64_t* __restrict__ tile_off, uint64_t cap, K* __restrict__ keys,
+    uint32_t* __restrict__ vals) {
+    static_assert(!TREE || MASK, "the near-plane path builds masks");
     uint64_t idx[4];
     T v[4][D];
     unsigned long long m[4];
     uint32_t cnt[4], ex[4];
-    halo_points<T, D, MASK>(X, n, parts, P, blockIdx.x, idx, v, m, cnt);
+    int own[4] = {0, 0, 0, 0};
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t wtot = wave_offsets<4>(cnt, ex);
     __shared__ HaloLds<D> L;
-    const bool tree_lds = halo_stage<T, D, MASK>(L, parts, P, tree);
+    __shared__ std::conditional_t<TREE, NearLds, char> nl;
+    bool tree_lds;
+    if constexpr (TREE) {
+        tree_lds = halo_stage<T, D, MASK>(L, parts, P, tree);   // (true by the host's choice)
+        if (threadIdx.x == 0) nl.n = 0;
+        __syncthreads();
+        halo_points_tree<T, D>(X, n, parts, P, blockIdx.x, tree, L.t_slot, L.t_axn, L.t_bd, marg,
+                               nl, idx, v, m, cnt, own);
+    } else {
+        halo_points<T, D, MASK>(X, n, parts, P, blockIdx.x, idx, v, m, cnt);
+        tree_lds = halo_stage<T, D, MASK>(L, parts, P, tree);
+    }
+    const uint32_t wtot = wave_offsets<4>(cnt, ex);
     if (lane == 0) L.ws[w] = wtot;
     __syncthreads();
     uint64_t wbase = tile_off[blockIdx.x];
 #pragma unroll
     for (int u = 0; u < kBlock / 64; ++u) wbase += u < w ? L.ws[u] : 0u;
-    halo_emit<T, D, K, MASK>(L, parts, P, owner, tree, tree_lds, n, idx, v, m, cnt, ex, wbase, cap,
-                             keys, vals);
+    halo_emit<T, D, K, MASK, TREE>(L, parts, P, owner, tree, tree_lds, n, idx, v, m, cnt, ex, wbase,
+                                   cap, keys, vals, own);
 }
 
 // Single-pass halo (PD_OPT_HALO_PASSES = 1): each tile counts its records,
@@ -829,8 +964,9 @@ __global__ __launch_bounds__(kBlock) void halo1_kernel(
     uint64_t wbase = s_base;
 #pragma unroll
     for (int u = 0; u < kBlock / 64; ++u) wbase += u < w ? L.ws[u] : 0u;
+    const int own0[4] = {0, 0, 0, 0};
     halo_emit<T, D, K, MASK>(L, parts, P, owner, tree, tree_lds, n, idx, v, m, cnt, ex, wbase, cap,
-                             keys, vals);
+                             keys, vals, own0);
 }
 
 // Coordinates into key order (padded rows); also lists the records of halo
@@ -1626,6 +1762,13 @@ __device__ __forceinline__ void row_range3(const Cells& C, const Count3Grid<T, D
     e = e > s ? e : s;
 }
 
+#ifndef PD_COUNT_WPE
+#define PD_COUNT_WPE 8
+#endif
+#ifndef PD_BORDER_WPE
+#define PD_BORDER_WPE 8
+#endif
+constexpr int kCountWpe = PD_COUNT_WPE, kBorderWpe = PD_BORDER_WPE;   // (A/B builds override)
 // WPE: the minimum waves per SIMD the register allocation must allow (1: no
 // constraint, the instrumented sweep; 8: at most 64 VGPRs, the default — the
 // candidate gathers want the occupancy: C2 count 4.87 -> 4.58 ms).
@@ -2679,7 +2822,7 @@ void launch_count(hipStream_t s, const T* Xs, uint32_t R, const Cells& C, double
         hipLaunchKernelGGL((count4_kernel<T, D, M, true, 1>), dim3(blocks(R)), dim3(kBlock), 0, s,
                            Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st, 0u);
     else
-        hipLaunchKernelGGL((count4_kernel<T, D, M, false, 8>), dim3(blocks(R)), dim3(kBlock), 0, s,
+        hipLaunchKernelGGL((count4_kernel<T, D, M, false, kCountWpe>), dim3(blocks(R)), dim3(kBlock), 0, s,
                            Xs, R, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt, st, 0u);
 }
 
@@ -2696,7 +2839,7 @@ float replay_count(hipStream_t s, const T* Xs, uint32_t R, uint32_t reps, const 
     PD_HIP(hipEventCreate(&e0));
     PD_HIP(hipEventCreate(&e1));
     PD_HIP(hipEventRecord(e0, s));
-    hipLaunchKernelGGL((count4_kernel<T, D, M, false, 8, true>), dim3(blocks(RL)), dim3(kBlock), 0,
+    hipLaunchKernelGGL((count4_kernel<T, D, M, false, kCountWpe, true>), dim3(blocks(RL)), dim3(kBlock), 0,
                        s, Xs, (uint32_t)RL, C, eps, eps2, lo, hi, ms, full, rot_min, core, mn, cnt,
                        (unsigned long long*)nullptr, R);
     PD_HIP(hipEventRecord(e1, s));
@@ -2713,7 +2856,7 @@ void launch_border(hipStream_t s, const T* Xs, uint32_t NL, const uint32_t* list
                    double eps, double eps2, float lo, float hi, const uint32_t* vals,
                    const uint32_t* par, const uint32_t* gmin, uint32_t* key_out,
                    uint32_t* rec_out = nullptr) {
-    hipLaunchKernelGGL((border4_kernel<T, D, M, 8>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
+    hipLaunchKernelGGL((border4_kernel<T, D, M, kBorderWpe>), dim3(blocks(NL)), dim3(kBlock), 0, s, Xs, NL,
                        list, C, eps, eps2, lo, hi, vals, par, gmin, key_out, rec_out);
 }
 
@@ -2924,18 +3067,29 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         // two passes: tile counts, scan, write
         uint32_t* tcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)htiles + 1);
         uint64_t* toff = ctx.arena.get<uint64_t>("tile_off", (size_t)htiles + 1);
-        hipLaunchKernelGGL((halo_tile_kernel<T, D>), dim3(htiles), dim3(kBlock), 0, s, X, n, parts,
-                           P, tcnt, ctrs, sort_hist);
+        // the near-plane fast path needs the split tree in LDS (P <= 64)
+        const bool tree_fast = ctx.halo_tree && P <= 64 && !a.owner && tree.nl &&
+                               tree.nslot <= kTreeSlots && tree.ne <= kTreeSplits;
+        const double marg = 2.0 * a.eps * (1.0 + 9.5367431640625e-07);
+        if (tree_fast)
+            hipLaunchKernelGGL((halo_tile_kernel<T, D, true>), dim3(htiles), dim3(kBlock), 0, s, X, n,
+                               parts, P, tree, marg, tcnt, ctrs, sort_hist);
+        else
+            hipLaunchKernelGGL((halo_tile_kernel<T, D, false>), dim3(htiles), dim3(kBlock), 0, s, X,
+                               n, parts, P, tree, marg, tcnt, ctrs, sort_hist);
         R64 = tile_offsets(ctx, tcnt, htiles, toff, s, true);
         if (R64 >= 0xFFFFFFFEull) throw Error(-5, "more than 2^32-2 halo records on one device");
         keys = ctx.arena.get<K>("keys", R64);
         vals = ctx.arena.get<uint32_t>("vals", R64);
-        if (P <= 64)
+        if (tree_fast)
+            hipLaunchKernelGGL((halo_write_kernel<T, D, K, true, true>), dim3(htiles), dim3(kBlock), 0,
+                               s, X, n, parts, P, a.owner, tree, marg, toff, R64, keys, vals);
+        else if (P <= 64)
             hipLaunchKernelGGL((halo_write_kernel<T, D, K, true>), dim3(htiles), dim3(kBlock), 0, s,
-                               X, n, parts, P, a.owner, tree, toff, R64, keys, vals);
+                               X, n, parts, P, a.owner, tree, marg, toff, R64, keys, vals);
         else
             hipLaunchKernelGGL((halo_write_kernel<T, D, K, false>), dim3(htiles), dim3(kBlock), 0,
-                               s, X, n, parts, P, a.owner, tree, toff, R64, keys, vals);
+                               s, X, n, parts, P, a.owner, tree, marg, toff, R64, keys, vals);
         PD_HIP(hipGetLastError());
         check_bounds(s, "halo_write_kernel");
     }

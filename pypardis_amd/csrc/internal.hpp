@@ -174,6 +174,7 @@ struct Ctx {
     bool kd_fuse = false;        // PD_OPT_KD_FUSE: kd_build fuses counts + the children's moments
                                  // (measured slower on C2: outside the train 2.79-3.32 vs 2.61-2.96 ms)
     bool verify_fused = false;   // PD_OPT_VERIFY_FUSED: cell verify over every cell, screen inline
+    bool halo_tree = true;       // PD_OPT_HALO_TREE: halo membership tests only near split planes
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
     int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow

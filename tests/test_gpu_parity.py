@@ -1233,6 +1233,59 @@ def test_halo_single_pass_equals_two_pass(native, P, cap):
         assert m.n_clusters_ == nc_o
 
 
+HALO_TREE = [("c2", 8), ("c2", 64), ("c4", 8), ("c4", 37), ("lattice", 16), ("f64_4d", 13),
+             ("dup", 8), ("city", 5)]
+
+
+@pytest.mark.parametrize("case,P", HALO_TREE, ids=[f"{c}-P{p}" for c, p in HALO_TREE])
+def test_halo_tree_equals_full_test(native, case, P):
+    """PD_OPT_HALO_TREE (default on): the halo's near-plane fast path — a
+    point farther than 2 eps from every split plane on its KD path gets its
+    owner's record only, the rest the full box test — writes the records of
+    the full test (same count) and gives the oracle's labels: 2-D / 3-D / 4-D,
+    fp32 / fp64, lattice points exactly on split planes, duplicates, cityblock,
+    up to 64 partitions."""
+    from pypardis_amd import DBSCAN, synth
+    rng = np.random.default_rng(P)
+    metric, eps, ms = "euclidean", 0.1, 10
+    if case == "c2":
+        X, cfg = synth.make_config("C2", n=300_000)
+        eps, ms = cfg["eps"], cfg["min_samples"]
+    elif case == "c4":
+        X = synth.gps_skew(400_000, seed=8, n_cities=300).numpy()
+        eps, ms = 0.01, 20
+    elif case == "lattice":
+        g = np.arange(200, dtype=np.float32) * np.float32(0.05)
+        X = np.stack(np.meshgrid(g, g, indexing="ij"), -1).reshape(-1, 2)
+        eps, ms = float(np.float32(0.05)), 5
+    elif case == "f64_4d":
+        X = rng.normal(size=(150_000, 4)) * 3.0
+        eps, ms = 0.35, 8
+    elif case == "dup":
+        X = np.repeat(rng.uniform(0, 5, size=(20_000, 3)).astype(np.float32), 5, axis=0)
+        eps, ms = 0.05, 6
+    else:
+        X = synth.blobs_noise(120_000, 2, side=30.0, n_centers=10, sigma=0.7, noise_frac=0.2,
+                              seed=24)
+        metric, eps, ms = "cityblock", 0.06, 8
+    lab_o, core_o, _, nc_o = oracle.dbscan(X, eps, ms, metric)
+    ctx = native.context()
+    Xd = _dev(X)
+    out = []
+    for on in (1, 0):
+        ctx.set_option(native.PD_OPT_HALO_TREE, on)
+        try:
+            m = DBSCAN(eps=eps, min_samples=ms, metric=metric, max_partitions=P).train(Xd)
+        finally:
+            ctx.set_option(native.PD_OPT_HALO_TREE, 1)
+        out.append((m, int(ctx.timings()["records"])))
+    assert out[0][1] == out[1][1]
+    for m, _ in out:
+        assert np.array_equal(m.labels_.cpu().numpy().astype(np.int64), lab_o)
+        assert np.array_equal(m.core_sample_mask_.cpu().numpy(), core_o)
+        assert m.n_clusters_ == nc_o
+
+
 @pytest.mark.parametrize("cfg,n", [("C2", 2_000_000), ("C4", 3_000_000), ("C1", 500_000)])
 def test_verify_fused_equals_listed(native, cfg, n):
     """PD_OPT_VERIFY_FUSED: the cell verify over every cell with the screen

@@ -102,6 +102,8 @@ def parse():
                     help="PD_OPT_VERIFY_FUSED override (1: cell verify over every cell, screen inline)")
     ap.add_argument("--halo-tree", type=int, default=None,
                     help="PD_OPT_HALO_TREE override (1: box tests only near split planes)")
+    ap.add_argument("--kd-replay", type=int, default=None,
+                    help="PD_OPT_KD_REPLAY override (1: KD passes replay the splits, no labels)")
     ap.add_argument("--rehearse", action="store_true",
                     help="N>1 on one GPU: gloo backend, every rank on cuda:0 (correctness "
                          "rehearsal of the sharded path; not a measurement)")
@@ -513,7 +515,8 @@ def main():
                      (_native.PD_OPT_HALO_PASSES, args.halo_passes),
                      (_native.PD_OPT_KD_FUSE, args.kd_fuse),
                      (_native.PD_OPT_VERIFY_FUSED, args.verify_fused),
-                     (_native.PD_OPT_HALO_TREE, args.halo_tree)):
+                     (_native.PD_OPT_HALO_TREE, args.halo_tree),
+                     (_native.PD_OPT_KD_REPLAY, args.kd_replay)):
         if val is not None:
             ctx.set_option(opt, val)
     Xh = None

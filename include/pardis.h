@@ -139,11 +139,19 @@ enum pd_option {
                                 C2 (link 5.52 vs 5.32 ms: the flagged lanes' work diverges inside
                                 every wave), kept for A/B.  Same labels */,
     PD_OPT_HALO_TREE = 29     /* grid train halo (two-pass form, split tree replayed, P <= 64):
-                                1 (default) a point farther than 2 eps from every split plane on
-                                its KD path is in its owner's expanded box only — one record, no
-                                box tests; the points near a plane are listed per tile and take
-                                the full test.  0: every point tests every expanded box.  Same
-                                records either way */
+                                0 (default) every point tests every expanded box; 1: a point
+                                farther than 2 eps from every split plane on its KD path is in
+                                its owner's expanded box only — one record, no box tests — and
+                                the points near a plane are listed per tile for the full test;
+                                measured slower (C2 halo 1.36 vs 1.19 ms, C4 11.3 vs 9.4 ms: the
+                                dependent tree walk and the list cost more than the box tests),
+                                kept for A/B.  Same records either way */,
+    PD_OPT_KD_REPLAY = 30     /* pd_kd_build with final_split = 2 (DBSCAN.train's KD): 0 (default)
+                                labels in HBM, read and rewritten by each level's passes; 1 each
+                                pass recomputes the points' labels by replaying the splits
+                                decided so far (tables in LDS) — no int32 label traffic, but the
+                                walk costs more than it saves (KD C2 2.76 vs 2.55 ms, C4 18.7 vs
+                                17.1 ms), kept for A/B.  Same splits either way */
     /* Retired in round 5 (measured A/Bs whose losing kernels were removed;
        pd_ctx_set_option returns PD_EINVAL for them, and the numbers are not
        reused): 4 LINK_MODE, 5 JUMP_ROUNDS, 9 SWEEP_VARIANT, 10 BORDER_ROOTS,
@@ -422,11 +430,27 @@ int32_t pd_dense_finish(pd_ctx* ctx, const int32_t* best, int32_t* labels, uint8
  * < 256, 16-byte aligned X / labels; PD_EUNSUPPORTED otherwise (use the
  * per-pass entry points).  final_split = 0 leaves the last level's split
  * unapplied (labels then hold the previous level's; pd_train_tree replays
- * the tree itself, pd_kd_split applies it when the labels are wanted). */
+ * the tree itself, pd_kd_split applies it when the labels are wanted);
+ * final_split = 2: the caller needs no labels (it replays the tree itself:
+ * pd_train_tree, pd_kd_labels) — the passes then replay the splits decided
+ * so far from tables in LDS instead of reading and writing an int32 label
+ * per point (PD_OPT_KD_REPLAY; trees of <= 256 splits), and the labels array
+ * is left unspecified. */
 int32_t pd_kd_build(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
                     int32_t* labels, int32_t n_levels, const int32_t* level_sizes_host,
                     const int32_t* cur_host, const int32_t* newlab_host, int32_t final_split,
                     double* trace_host, double* lohi_host, int64_t* bad_host, void* stream);
+
+/* The KD labels of every point from a finished split tree (the
+ * R:dbscan/partition.py:66-68 filters replayed per point: level l, a point
+ * whose label has a split moves to newlab when v[axis] >= boundary) — the
+ * labels of a pd_kd_build run with final_split = 2, on request.  The tree in
+ * BFS order as pd_train_tree's: level_sizes_host[l] splits, then per split
+ * cur / axis / boundary / newlab (host arrays).  labels: device int32[n]. */
+int32_t pd_kd_labels(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                     int32_t* labels, int32_t n_levels, const int32_t* level_sizes_host,
+                     const int32_t* cur_host, const int32_t* axis_host,
+                     const double* boundary_host, const int32_t* newlab_host, void* stream);
 
 /* ---- Sharded train, device-resident variant (no host round trip per KD
  * level, one ordered pass per exchange side).  The KD partition of

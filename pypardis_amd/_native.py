@@ -36,6 +36,7 @@ PD_OPT_HALO_CAP = 26
 PD_OPT_KD_FUSE = 27
 PD_OPT_VERIFY_FUSED = 28
 PD_OPT_HALO_TREE = 29
+PD_OPT_KD_REPLAY = 30
 # retired in round 5 (pardis.h): set_option raises for them
 PD_OPT_RETIRED = (4, 5, 9, 10, 16, 20, 21, 22, 23)
 TIMING_SLOTS = ["halo", "sort", "gather", "cells", "count", "link", "merge", "roots", "border",
@@ -55,7 +56,7 @@ EXPORTS = ["pd_abi_version", "pd_last_error", "pd_ctx_create", "pd_ctx_destroy",
            "pd_comm_unique_id", "pd_comm_init", "pd_comm_init_all", "pd_comm_destroy",
            "pd_comm_all_reduce", "pd_comm_all_gather_v", "pd_comm_all_to_all_v",
            "pd_comm_broadcast", "pd_dense_count", "pd_dense_link", "pd_dense_border",
-           "pd_dense_finish", "pd_kd_build", "pd_train_tree", "pd_kdx_begin", "pd_kdx_moments",
+           "pd_dense_finish", "pd_kd_build", "pd_kd_labels", "pd_train_tree", "pd_kdx_begin", "pd_kdx_moments",
            "pd_kdx_axes", "pd_kdx_counts", "pd_kdx_boundary", "pd_kdx_end", "pd_route2",
            "pd_pack2", "pd_results", "pd_results_scatter", "pd_comm_exchange", "pd_comm_abort",
            "pd_comm_self_check", "pd_comm_size"]
@@ -131,6 +132,7 @@ def load():
             "pd_dense_border": ([P, P, I32, P, P, P], I32),
             "pd_dense_finish": ([P, P, P, P, P, P, P], I32),
             "pd_kd_build": ([P, P, I32, I64, I32, P, I32, P, P, P, I32, P, P, P, P], I32),
+            "pd_kd_labels": ([P, P, I32, I64, I32, P, I32, P, P, P, P, P, P], I32),
             "pd_train_tree": ([P, P, I32, I64, I32, D, I32, I32, I32, P, P, I32, P, P, P, P, P, P, P,
                                P, P, P], I32),
             "pd_kdx_begin": ([P, I32, I32, P, P, P, P], I32),
@@ -331,9 +333,11 @@ KD_TRACE = 13
 
 def kd_build(X, labels, levels, final_split=True, ctx=None):
     """pd_kd_build: the whole min_var BFS in one launch chain.  levels: the
-    BFS schedule (lists of (cur, new) label pairs).  Returns (lo, hi, bad,
-    trace (n_splits, 13)); raises PardisError(PD_EUNSUPPORTED) when the
-    fused path does not apply."""
+    BFS schedule (lists of (cur, new) label pairs).  final_split: True / 1
+    apply the last split to `labels`, False / 0 leave it, 2 the labels are
+    not needed (the passes replay the splits; kd_labels recovers them).
+    Returns (lo, hi, bad, trace (n_splits, 13)); raises
+    PardisError(PD_EUNSUPPORTED) when the fused path does not apply."""
     dt = _check_points(X)
     ctx = ctx or context(X.device.index)
     n, d = X.shape
@@ -345,9 +349,25 @@ def kd_build(X, labels, levels, final_split=True, ctx=None):
     bad = np.zeros(1, np.int64)
     _check(load().pd_kd_build(ctx.ptr, X.data_ptr(), dt, n, d, labels.data_ptr(), len(sizes),
                               sizes.ctypes.data, cur.ctypes.data, new.ctypes.data,
-                              int(bool(final_split)), trace.ctypes.data, lohi.ctypes.data,
-                              bad.ctypes.data, _stream(X.device)))
+                              2 if final_split == 2 else int(bool(final_split)),
+                              trace.ctypes.data, lohi.ctypes.data, bad.ctypes.data,
+                              _stream(X.device)))
     return lohi[:d], lohi[d:], int(bad[0]), trace
+
+
+def kd_labels(X, labels, tree, ctx=None):
+    """pd_kd_labels: every point's KD label by replaying a finished split
+    tree (sizes, cur, axis, boundary, new) — KDPartitioner.split_tree()."""
+    dt = _check_points(X)
+    ctx = ctx or context(X.device.index)
+    n, d = X.shape
+    sizes, cur, axis, bound, new = (np.ascontiguousarray(a) for a in tree)
+    sizes, cur, axis, new = (a.astype(np.int32) for a in (sizes, cur, axis, new))
+    bound = bound.astype(np.float64)
+    _check(load().pd_kd_labels(ctx.ptr, X.data_ptr(), dt, n, d, labels.data_ptr() if n else None,
+                               len(sizes), sizes.ctypes.data, cur.ctypes.data, axis.ctypes.data,
+                               bound.ctypes.data, new.ctypes.data, _stream(X.device)))
+    return labels
 
 
 def round_dd(dd):

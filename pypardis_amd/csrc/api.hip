@@ -167,6 +167,8 @@ int32_t pd_ctx_set_option(pd_ctx* ctx, int32_t option, int64_t value) {
         } else if (option == PD_OPT_HALO_PASSES) {
             if (value != 1 && value != 2) throw Error(PD_EINVAL, "halo passes is 1 or 2");
             ctx->c.halo_passes = (int)value;
+        } else if (option == PD_OPT_KD_REPLAY) {
+            ctx->c.kd_replay = value != 0;
         } else if (option == PD_OPT_HALO_TREE) {
             ctx->c.halo_tree = value != 0;
         } else if (option == PD_OPT_VERIFY_FUSED) {
@@ -607,8 +609,24 @@ int32_t pd_kd_build(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_
         if (!labels || n_levels < 1 || !sizes || !cur || !newlab || !trace || !lohi)
             throw Error(PD_EINVAL, "null argument");
         if (d > kMaxDim) throw Error(PD_EUNSUPPORTED, "kd_build: d > 4");
-        kd_build(ctx->c, X, dtype, n, d, labels, n_levels, sizes, cur, newlab, final_split != 0,
+        if (final_split < 0 || final_split > 2) throw Error(PD_EINVAL, "final_split is 0, 1 or 2");
+        kd_build(ctx->c, X, dtype, n, d, labels, n_levels, sizes, cur, newlab, final_split,
                  trace, lohi, bad, (hipStream_t)stream);
+    });
+}
+
+int32_t pd_kd_labels(pd_ctx* ctx, const void* X, int32_t dtype, int64_t n, int32_t d,
+                     int32_t* labels, int32_t n_levels, const int32_t* sizes, const int32_t* cur,
+                     const int32_t* axis, const double* boundary, const int32_t* newlab,
+                     void* stream) {
+    return guard(ctx, [&] {
+        check_common(ctx, X, n, d);
+        if (n && !labels) throw Error(PD_EINVAL, "null labels");
+        if (n_levels < 0 || n_levels > 16 || (n_levels && (!sizes || !cur || !axis || !boundary || !newlab)))
+            throw Error(PD_EINVAL, "bad split tree");
+        if (n == 0) return;
+        kd_labels(ctx->c, X, dtype, n, d, labels, n_levels, sizes, cur, axis, boundary, newlab,
+                  (hipStream_t)stream);
     });
 }
 

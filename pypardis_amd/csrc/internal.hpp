@@ -174,7 +174,9 @@ struct Ctx {
     bool kd_fuse = false;        // PD_OPT_KD_FUSE: kd_build fuses counts + the children's moments
                                  // (measured slower on C2: outside the train 2.79-3.32 vs 2.61-2.96 ms)
     bool verify_fused = false;   // PD_OPT_VERIFY_FUSED: cell verify over every cell, screen inline
-    bool halo_tree = true;       // PD_OPT_HALO_TREE: halo membership tests only near split planes
+    bool halo_tree = false;      // PD_OPT_HALO_TREE: halo membership tests only near split planes
+                                 // (measured slower: C2 halo 1.36 vs 1.19 ms, C4 11.3 vs 9.4 ms)
+    bool kd_replay = false;      // PD_OPT_KD_REPLAY: KD passes replay the splits instead of labels
     bool screen = true;          // fp32 screening of fp32 inputs (exact either way)
     bool sweep_stats = false;    // tally sweep candidates / union-find outcomes
     int64_t dir_budget = 32ll << 30;   // eps-grid directory bytes before cells grow
@@ -277,8 +279,14 @@ void kd_pass(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labe
 // The whole min_var BFS (exact sums) in one launch chain, the level
 // decisions on the device; trace: 13 doubles per split (kd.hip kd_build).
 void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels, int n_levels,
-              const int32_t* sizes, const int32_t* cur, const int32_t* newl, bool final_split,
+              const int32_t* sizes, const int32_t* cur, const int32_t* newl, int final_mode,
               double* trace_out, double* lohi, int64_t* bad, hipStream_t s);
+// The KD labels of every point by replaying a finished BFS split tree
+// (host arrays: tree_sizes[l] splits at level l, cur -> new when v[axis] >=
+// bound) — pd_kd_labels, for a pd_kd_build run in final mode 2.
+void kd_labels(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels,
+               int n_levels, const int32_t* sizes, const int32_t* cur, const int32_t* axis,
+               const double* bound, const int32_t* newl, hipStream_t s);
 void kd_moments_dd(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32_t* labels,
                    int n_sel, const int32_t* sel_host, double* out_host, hipStream_t s);
 // Sharded device-decided KD (kd.hip): begin -> per level (moments -> [caller:

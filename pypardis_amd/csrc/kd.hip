@@ -273,6 +273,54 @@ constexpr int kDirectMax = 1;
 // (false: one block-wide counting sort per tile, each wave summing one label)
 constexpr bool kWaveRegroup = false;   // measured slower on C2: 0.69 / 1.00 vs 0.61 / 0.82 ms
 
+// Label replay (kd_build, round 6): instead of reading and
+// writing an int32 label per point per pass, a pass recomputes each point's
+// label by replaying the BFS splits decided so far on its coordinates (level
+// l, the label's slot: v[axis] >= boundary moves it to the new label,
+// R:dbscan/partition.py:66-68) — the halo pass's tree_owner, from tables in
+// LDS.  Levels 0 .. nl-1; per level the label -> slot table and per split
+// (axis, new label, boundary), the axes and boundaries as the device decided
+// them (kdb_axes_kernel / kdb_boundary_kernel).
+constexpr int kMaxLevels = 16, kRSlots = 512, kRSplits = 256;
+struct ReplayTab {
+    int nl = 0;
+    int ntab[kMaxLevels], nsplit[kMaxLevels], toff[kMaxLevels], eoff[kMaxLevels];
+    const int32_t* slot[kMaxLevels];
+    const int32_t* axis[kMaxLevels];
+    const int32_t* newlab[kMaxLevels];
+    const double* boundary[kMaxLevels];
+};
+struct ReplayLds {
+    int32_t slot[kRSlots];
+    int32_t axis[kRSplits], newlab[kRSplits];
+    double bd[kRSplits];
+};
+
+__device__ __forceinline__ void replay_stage(ReplayLds& R, const ReplayTab& rp, int tid, int nt) {
+    for (int l = 0; l < rp.nl; ++l) {
+        for (int k = tid; k < rp.ntab[l]; k += nt) R.slot[rp.toff[l] + k] = rp.slot[l][k];
+        for (int k = tid; k < rp.nsplit[l]; k += nt) {
+            R.axis[rp.eoff[l] + k] = rp.axis[l][k];
+            R.newlab[rp.eoff[l] + k] = rp.newlab[l][k];
+            R.bd[rp.eoff[l] + k] = rp.boundary[l][k];
+        }
+    }
+}
+
+template <typename T, int D>
+__device__ __forceinline__ int replay_label(const ReplayLds& R, const ReplayTab& rp,
+                                            const T (&v)[D]) {
+    int lab = 0;
+    for (int l = 0; l < rp.nl; ++l) {
+        if (lab >= rp.ntab[l]) continue;
+        const int sl = R.slot[rp.toff[l] + lab];
+        if (sl < 0) continue;
+        const int e = rp.eoff[l] + sl;
+        if ((double)pick_axis<T, D>(v, R.axis[e]) >= R.bd[e]) lab = R.newlab[e];
+    }
+    return lab;
+}
+
 // NG = labels whose moments this pass accumulates (0: none); LAB: labels are
 // read (false: every point has label 0, the first level); SP: the previous
 // level's splits are applied first; BB: bbox + non-finite count.
@@ -285,10 +333,13 @@ constexpr bool kWaveRegroup = false;   // measured slower on C2: 0.69 / 1.00 vs 
 // work per point is then that of one label, whatever NG is.
 // Block partials: NG x [count, (sum hi, lo) x D, (sumsq hi, lo) x D], then
 // the bbox [lo x D, hi x D, bad].
-template <typename T, int D, bool LAB, bool SP, int NG, bool BB>
+// RP: labels replayed from the split tree (rp), none read or written (LAB
+// and SP unused).
+template <typename T, int D, bool LAB, bool SP, int NG, bool BB, bool RP = false>
 __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X, uint64_t n,
                                                          int32_t* __restrict__ labels, SplitTab sp,
-                                                         int4 sel, double* __restrict__ part) {
+                                                         int4 sel, double* __restrict__ part,
+                                                         ReplayTab rp) {
     constexpr int K = (sizeof(T) * D <= 16) ? 2 : 1;
     constexpr int TP = 4 * K * kBlock;   // points per tile
     constexpr int NW = kBlock / 64;
@@ -299,7 +350,11 @@ __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X
     __shared__ int s_slot[SP ? kTabLds : 1], s_ax[SP ? kTabLds : 1], s_nl[SP ? kTabLds : 1];
     __shared__ double s_bd[SP ? kTabLds : 1];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    if constexpr (SP) {
+    __shared__ std::conditional_t<RP, ReplayLds, char> s_rp;
+    if constexpr (RP) {
+        replay_stage(s_rp, rp, tid, kBlock);
+        __syncthreads();
+    } else if constexpr (SP) {
         for (int k = tid; k < sp.ntab; k += kBlock) s_slot[k] = sp.slot_of[k];
         for (int k = tid; k < sp.nsplit; k += kBlock) {
             s_ax[k] = sp.axis[k];
@@ -350,10 +405,13 @@ __global__ __launch_bounds__(kBlock) void kd_pass_kernel(const T* __restrict__ X
                     for (int j = 0; j < D; ++j) v[k][q][j] = T(0);
             }
             int lab[4] = {0, 0, 0, 0};
-            if constexpr (LAB) {
+            if constexpr (RP) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) lab[q] = replay_label<T, D>(s_rp, rp, v[k][q]);
+            } else if constexpr (LAB) {
                 if (m) load_labels4<true>(labels, ch, m, lab);
             }
-            if constexpr (SP) {
+            if constexpr (SP && !RP) {
                 bool changed = false;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
@@ -733,8 +791,10 @@ __global__ __launch_bounds__(kBlock) void counts4_kernel(
     const T* __restrict__ X, uint64_t n, const int32_t* __restrict__ labels,
     const int32_t* __restrict__ slot_of, int n_label_tab, const int32_t* __restrict__ axis,
     const double* __restrict__ bounds, int n_sel, int mono, int rep,
-    unsigned long long* __restrict__ out) {
+    unsigned long long* __restrict__ out, ReplayTab rp) {
     extern __shared__ unsigned int lcnt[];   // rep * n_sel * 8
+    __shared__ ReplayLds s_rp;   // (rp.nl > 0: labels replayed instead of read)
+    replay_stage(s_rp, rp, threadIdx.x, kBlock);
     __shared__ int s_slot[kTabLds], s_ax[kTabLds];
     __shared__ double s_bd[kTabLds * 7];
     for (int k = threadIdx.x; k < rep * n_sel * 8; k += kBlock) lcnt[k] = 0;
@@ -749,7 +809,12 @@ __global__ __launch_bounds__(kBlock) void counts4_kernel(
         T v[4][D];
         const int m = load_chunk<T, D, true>(X, n, ch, v);
         int lab[4];
-        load_labels4<true>(labels, ch, m, lab);
+        if (rp.nl) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) lab[q] = replay_label<T, D>(s_rp, rp, v[q]);
+        } else {
+            load_labels4<true>(labels, ch, m, lab);
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             if (q >= m || lab[q] < 0 || lab[q] >= n_label_tab) continue;
@@ -782,11 +847,14 @@ __global__ __launch_bounds__(kBlock) void counts4_kernel(
 // serialise): c[s][i] = #points of slot s with v[axis] < bound i, c[s][7] =
 // #points of slot s; one wave reduction and one LDS atomic per counter and
 // wave at the end.  Labels < kTabLds.
-template <typename T, int D, int NS>
+template <typename T, int D, int NS, bool RP = false>
 __global__ __launch_bounds__(kBlock) void counts_reg_kernel(
     const T* __restrict__ X, uint64_t n, const int32_t* __restrict__ labels,
     const int32_t* __restrict__ slot_of, int n_label_tab, const int32_t* __restrict__ axis,
-    const double* __restrict__ bounds, int n_sel, unsigned long long* __restrict__ out) {
+    const double* __restrict__ bounds, int n_sel, unsigned long long* __restrict__ out,
+    ReplayTab rp) {
+    __shared__ std::conditional_t<RP, ReplayLds, char> s_rp;
+    if constexpr (RP) replay_stage(s_rp, rp, threadIdx.x, kBlock);
     __shared__ int s_slot[kTabLds];
     __shared__ unsigned int s_cnt[NS * 8];
     for (int k = threadIdx.x; k < n_label_tab; k += kBlock) s_slot[k] = slot_of[k];
@@ -811,7 +879,12 @@ __global__ __launch_bounds__(kBlock) void counts_reg_kernel(
         T v[4][D];
         const int m = load_chunk<T, D, true>(X, n, ch, v);
         int lab[4] = {0, 0, 0, 0};   // labels == nullptr: every point in label 0
-        if (labels) load_labels4<true>(labels, ch, m, lab);
+        if constexpr (RP) {
+#pragma unroll
+            for (int p = 0; p < 4; ++p) lab[p] = replay_label<T, D>(s_rp, rp, v[p]);
+        } else if (labels) {
+            load_labels4<true>(labels, ch, m, lab);
+        }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const int L = lab[p];
@@ -1420,7 +1493,7 @@ void run_pass(Ctx& ctx, const T* X, int64_t n, int32_t* labels, const SplitTab& 
     const int nb = (int)std::min<int64_t>(resident, std::max<int64_t>(1, (n + TP - 1) / TP));
     double* part = ctx.arena.get<double>("pass_part", (size_t)nb * (W > 0 ? W : 1));
     hipLaunchKernelGGL((kd_pass_kernel<T, D, LAB, SP, NG, BB>), dim3(nb), dim3(kBlock), 0, s,
-                       X, (uint64_t)n, labels, sp, sel, part);
+                       X, (uint64_t)n, labels, sp, sel, part, ReplayTab{});
     PD_HIP(hipGetLastError());
     res.assign(W, 0.0);
     if constexpr (W > 0) {
@@ -1554,7 +1627,7 @@ void kd_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32
                     constexpr int NS = decltype(NSc)::value;
                     hipLaunchKernelGGL((counts_reg_kernel<T, D, NS>), dim3(nb4), dim3(kBlock), 0, s,
                                        (const T*)X, (uint64_t)n, labels, t.slot_of, t.ntab, t.axis,
-                                       t.dbl, n_sel, dcnt);
+                                       t.dbl, n_sel, dcnt, ReplayTab{});
                 };
                 if (n_sel == 1)
                     go(std::integral_constant<int, 1>{});
@@ -1574,7 +1647,7 @@ void kd_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int32
                 hipLaunchKernelGGL((counts4_kernel<T, D>), dim3(nb4), dim3(kBlock),
                                    sizeof(unsigned int) * rep * n_sel * 8, s, (const T*)X,
                                    (uint64_t)n, labels, t.slot_of, t.ntab, t.axis, t.dbl, n_sel,
-                                   mono ? 1 : 0, rep, dcnt);
+                                   mono ? 1 : 0, rep, dcnt, ReplayTab{});
             });
         });
     } else
@@ -1720,6 +1793,41 @@ __global__ void kdb_boundary_kernel(const unsigned long long* __restrict__ cnt, 
 // next level (-1: not split there).  Counts are exact integers; the sums are
 // double-double additions of whole intervals (exact, so equal to a moments
 // pass over the child).
+// Labels from a finished split tree (pd_kd_labels): replay every level per
+// point, tables read through the caches (a one-off pass on request).
+struct TreeG {
+    int nl;
+    int ntab[kMaxLevels], toff[kMaxLevels], eoff[kMaxLevels];
+    const int32_t* slot;     // concatenated per level: label -> split index in the level (-1)
+    const int32_t* ax_new;   // per split: axis, new label
+    const double* bound;     // per split
+};
+
+template <typename T, int D>
+__global__ __launch_bounds__(kBlock) void kd_label_kernel(const T* __restrict__ X, uint64_t n,
+                                                          int32_t* __restrict__ labels, TreeG t) {
+    const uint64_t nch = (n + 3) / 4;
+    for (uint64_t ch = (uint64_t)blockIdx.x * kBlock + threadIdx.x; ch < nch;
+         ch += (uint64_t)gridDim.x * kBlock) {
+        T v[4][D];
+        const int m = load_chunk<T, D, true>(X, n, ch, v);
+        int lab[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int L = 0;
+            for (int l = 0; l < t.nl; ++l) {
+                if (L >= t.ntab[l]) continue;
+                const int sl = t.slot[t.toff[l] + L];
+                if (sl < 0) continue;
+                const int e = t.eoff[l] + sl;
+                if ((double)pick_axis<T, D>(v[q], t.ax_new[2 * e]) >= t.bound[e]) L = t.ax_new[2 * e + 1];
+            }
+            lab[q] = L;
+        }
+        store_labels4<true>(labels, ch, m, lab);
+    }
+}
+
 __global__ void kdb_children_kernel(const double* __restrict__ fin, int S, int G,
                                     const double* __restrict__ trace,
                                     const int32_t* __restrict__ dst, double* __restrict__ mom) {
@@ -1748,24 +1856,25 @@ __global__ void kdb_children_kernel(const double* __restrict__ fin, int S, int G
 namespace {
 // run_pass without the host sync: the finished quantities stay on the device
 // (fin: NG x G moments, then the bbox; may be null when the pass has none).
-template <typename T, int D, bool LAB, bool SP, int NG, bool BB>
+// RP: labels replayed from rp (kd_pass_kernel), none read or written.
+template <typename T, int D, bool LAB, bool SP, int NG, bool BB, bool RP = false>
 void run_pass_dev(Ctx& ctx, const T* X, int64_t n, int32_t* labels, const SplitTab& sp, int4 sel,
-                  double* fin, hipStream_t s) {
+                  double* fin, hipStream_t s, const ReplayTab& rp = ReplayTab{}) {
     constexpr int G = 1 + 4 * D, WM = NG * G, W = WM + (BB ? 2 * D + 1 : 0);
     constexpr int TP = 4 * kBlock * ((sizeof(T) * D <= 16) ? 2 : 1);
     static int resident = 0;
     if (!resident) {
         int per_cu = 0, dev = 0, cus = 0;
         PD_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, reinterpret_cast<const void*>(&kd_pass_kernel<T, D, LAB, SP, NG, BB>), kBlock, 0));
+            &per_cu, reinterpret_cast<const void*>(&kd_pass_kernel<T, D, LAB, SP, NG, BB, RP>), kBlock, 0));
         PD_HIP(hipGetDevice(&dev));
         PD_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         resident = std::max(1, per_cu) * std::max(1, cus);
     }
     const int nb = (int)std::min<int64_t>(resident, std::max<int64_t>(1, (n + TP - 1) / TP));
     double* part = ctx.arena.get<double>("pass_part", (size_t)nb * (W > 0 ? W : 1));
-    hipLaunchKernelGGL((kd_pass_kernel<T, D, LAB, SP, NG, BB>), dim3(nb), dim3(kBlock), 0, s,
-                       X, (uint64_t)n, labels, sp, sel, part);
+    hipLaunchKernelGGL((kd_pass_kernel<T, D, LAB, SP, NG, BB, RP>), dim3(nb), dim3(kBlock), 0, s,
+                       X, (uint64_t)n, labels, sp, sel, part, rp);
     PD_HIP(hipGetLastError());
     if constexpr (W > 0) {
         hipLaunchKernelGGL(kd_finish_kernel, dim3(W), dim3(kBlock), 0, s, part, nb, WM, G, D, W,
@@ -1775,9 +1884,69 @@ void run_pass_dev(Ctx& ctx, const T* X, int64_t n, int32_t* labels, const SplitT
 }
 }  // namespace
 
+// final_mode: 0 leave the labels at the last level's labels (its split not
+// applied), 1 apply the last split too, 2 the caller needs no labels at all
+// (it replays the split tree itself: pd_train_tree, pd_kd_labels) — the
+// levels then replay the splits instead of reading and writing labels
+// (ctx.kd_replay, the tables fitting ReplayLds).
+void kd_labels(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels,
+               int n_levels, const int32_t* sizes, const int32_t* cur, const int32_t* axis,
+               const double* bound, const int32_t* newl, hipStream_t s) {
+    if (n <= 0) return;
+    if (!vec_ok(d, X, labels)) throw Error(-5, "kd_labels: d <= 4, 16-byte aligned inputs only");
+    if (n_levels > kMaxLevels) throw Error(-5, "kd_labels: more than 16 levels");
+    TreeG t{};
+    t.nl = n_levels;
+    std::vector<int32_t> ints;
+    std::vector<double> bd;
+    int ne = 0, nslot = 0;
+    for (int l = 0; l < n_levels; ++l) {
+        int nt = 1;
+        for (int k = 0; k < sizes[l]; ++k) nt = std::max(nt, cur[ne + k] + 1);
+        t.ntab[l] = nt;
+        t.toff[l] = nslot;
+        t.eoff[l] = ne;
+        nslot += nt;
+        ne += sizes[l];
+    }
+    ints.assign((size_t)nslot + 2 * ne, -1);
+    bd.assign(std::max(ne, 1), 0.0);
+    for (int l = 0; l < n_levels; ++l)
+        for (int k = 0; k < sizes[l]; ++k) {
+            const int e = t.eoff[l] + k, L = cur[e];
+            if (L < 0 || L >= t.ntab[l] || axis[e] < 0 || axis[e] >= d || newl[e] < 0)
+                throw Error(-1, "kd_labels: bad split tree");
+            ints[t.toff[l] + L] = k;
+            ints[nslot + 2 * e] = axis[e];
+            ints[nslot + 2 * e + 1] = newl[e];
+            bd[e] = bound[e];
+        }
+    const size_t ib = (sizeof(int32_t) * ints.size() + 7) & ~size_t(7);
+    char* h = (char*)pinned(ctx, ib + sizeof(double) * bd.size());
+    std::memcpy(h, ints.data(), sizeof(int32_t) * ints.size());
+    std::memcpy(h + ib, bd.data(), sizeof(double) * bd.size());
+    char* dt = ctx.arena.get<char>("kdl_tables", ib + sizeof(double) * bd.size());
+    PD_HIP(hipMemcpyAsync(dt, h, ib + sizeof(double) * bd.size(), hipMemcpyHostToDevice, s));
+    t.slot = (const int32_t*)dt;
+    t.ax_new = (const int32_t*)dt + nslot;
+    t.bound = (const double*)(dt + ib);
+    const unsigned nb = grid_for((n + 3) / 4, 4096);
+    dispatch_t(dtype, [&](auto tp) {
+        using T = std::remove_pointer_t<decltype(tp)>;
+        dispatch_d(d, [&](auto Dc) {
+            constexpr int D = decltype(Dc)::value;
+            hipLaunchKernelGGL((kd_label_kernel<T, D>), dim3(nb), dim3(kBlock), 0, s, (const T*)X,
+                               (uint64_t)n, labels, t);
+        });
+    });
+    PD_HIP(hipGetLastError());
+    sync(s);   // (the pinned block is reused by the next upload)
+}
+
 void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* labels, int n_levels,
-              const int32_t* sizes, const int32_t* cur, const int32_t* newl, bool final_split,
+              const int32_t* sizes, const int32_t* cur, const int32_t* newl, int final_mode,
               double* trace_out, double* lohi, int64_t* bad, hipStream_t s) {
+    const bool final_split = final_mode == 1;
     if (n <= 0 || n_levels <= 0) throw Error(-1, "kd_build: no points or no levels");
     if (ctx.seq_moments || !vec_ok(d, X, labels))
         throw Error(-5, "kd_build: d <= 4, 16-byte aligned inputs and exact sums only");
@@ -1833,9 +2002,24 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
     // moments come from those (kdb_children_kernel) and its own counting pass
     // applies this level's split.  dst[l]: per split of level l, the slot of
     // its left / right child in level l + 1 (-1: not split there).
+    // label replay: every level's tables in ReplayLds
+    bool replay = final_mode == 2 && ctx.kd_replay && n_levels <= kMaxLevels;
+    ReplayTab rpt;
+    {
+        int so = 0, eo = 0;
+        for (int l = 0; l < n_levels && l < kMaxLevels; ++l) {
+            rpt.ntab[l] = ntab[l];
+            rpt.nsplit[l] = sizes[l];
+            rpt.toff[l] = so;
+            rpt.eoff[l] = eo;
+            so += ntab[l];
+            eo += sizes[l];
+        }
+        replay = replay && so <= kRSlots && eo <= kRSplits;
+    }
     std::vector<char> fuse(n_levels, 0);
     std::vector<std::vector<int32_t>> dst(n_levels);
-    for (int l = 0; ctx.kd_fuse && l + 1 < n_levels; ++l) {
+    for (int l = 0; ctx.kd_fuse && !replay && l + 1 < n_levels; ++l) {
         const int S = sizes[l], S1 = sizes[l + 1];
         if (S > 2 || S1 > 4) continue;
         std::vector<int32_t> dd(2 * S, -1);
@@ -1860,6 +2044,12 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
         std::memcpy(hp, hd.data(), sizeof(int32_t) * hd.size());
         PD_HIP(hipMemcpyAsync(ddst, hp, sizeof(int32_t) * hd.size(), hipMemcpyHostToDevice, s));
     }
+    for (int l = 0; replay && l < n_levels; ++l) {
+        rpt.slot[l] = lv[l].slot;
+        rpt.axis[l] = lv[l].axis;
+        rpt.newlab[l] = lv[l].newlab;
+        rpt.boundary[l] = lv[l].boundary;
+    }
     dispatch_t(dtype, [&](auto tp) {
         using T = std::remove_pointer_t<decltype(tp)>;
         dispatch_d(d, [&](auto Dc) {
@@ -1880,8 +2070,22 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                 const double* m = fin0;
                 // this level's counting pass still has the previous split to apply
                 const bool pending = l > 0 && fuse[l - 1];
+                ReplayTab rpl = rpt;   // the levels decided so far
+                rpl.nl = l;
                 if (l > 0 && pending) {
                     m = momc;
+                } else if (l > 0 && replay) {
+                    for (int g0 = 0; g0 < S; g0 += kGroup) {
+                        const int ng = std::min(S - g0, kGroup);
+                        int4 sl = make_int4(-2, -2, -2, -2);
+                        for (int g = 0; g < ng; ++g) (&sl.x)[g] = sel[g0 + g];
+                        dispatch_ng(ng, [&](auto NGc) {
+                            constexpr int NG = decltype(NGc)::value;
+                            run_pass_dev<T, D, false, false, NG, false, true>(
+                                ctx, Xt, n, labels, none, sl, mom + (size_t)g0 * G, s, rpl);
+                        });
+                    }
+                    m = mom;
                 } else if (l > 0) {
                     const Lv& p = lv[l - 1];
                     const SplitTab sp{p.slot, ntab[l - 1], p.axis, p.boundary, p.newlab, sizes[l - 1]};
@@ -1967,9 +2171,16 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                 } else if (S <= 4) {
                     auto go = [&](auto NSc) {
                         constexpr int NS = decltype(NSc)::value;
-                        hipLaunchKernelGGL((counts_reg_kernel<T, D, NS>), dim3(nb4), dim3(kBlock), 0,
-                                           s, Xt, (uint64_t)n, labels_written ? labels : nullptr,
-                                           lv[l].slot, ntab[l], lv[l].axis, lv[l].bounds, S, dcnt);
+                        if (replay && l > 0)
+                            hipLaunchKernelGGL((counts_reg_kernel<T, D, NS, true>), dim3(nb4),
+                                               dim3(kBlock), 0, s, Xt, (uint64_t)n, nullptr,
+                                               lv[l].slot, ntab[l], lv[l].axis, lv[l].bounds, S,
+                                               dcnt, rpl);
+                        else
+                            hipLaunchKernelGGL((counts_reg_kernel<T, D, NS>), dim3(nb4), dim3(kBlock), 0,
+                                               s, Xt, (uint64_t)n, labels_written ? labels : nullptr,
+                                               lv[l].slot, ntab[l], lv[l].axis, lv[l].bounds, S, dcnt,
+                                               ReplayTab{});
                     };
                     if (S == 1)
                         go(std::integral_constant<int, 1>{});
@@ -1983,7 +2194,7 @@ void kd_build(Ctx& ctx, const void* X, int dtype, int64_t n, int d, int32_t* lab
                     hipLaunchKernelGGL((counts4_kernel<T, D>), dim3(nb4), dim3(kBlock),
                                        sizeof(unsigned int) * rep * S * 8, s, Xt, (uint64_t)n, labels,
                                        lv[l].slot, ntab[l], lv[l].axis, lv[l].bounds, S, 0, rep,
-                                       dcnt);
+                                       dcnt, replay ? rpl : ReplayTab{});
                 }
                 PD_HIP(hipGetLastError());
                 hipLaunchKernelGGL(kdb_boundary_kernel, dim3(1), dim3(kTabLds), 0, s, dcnt, S,
@@ -2225,7 +2436,7 @@ void kdx_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int3
                     constexpr int NS = decltype(NSc)::value;
                     hipLaunchKernelGGL((counts_reg_kernel<T, D, NS>), dim3(nb4), dim3(kBlock), 0, s,
                                        Xt, (uint64_t)n, labels, v.slot, k.ntab[level], v.axis,
-                                       v.bounds, S, out);
+                                       v.bounds, S, out, ReplayTab{});
                 };
                 if (S == 1)
                     go(std::integral_constant<int, 1>{});
@@ -2238,7 +2449,7 @@ void kdx_counts(Ctx& ctx, const void* X, int dtype, int64_t n, int d, const int3
                 while (rep > 1 && (size_t)rep * S * 8 * sizeof(unsigned int) > 48 * 1024) rep >>= 1;
                 hipLaunchKernelGGL((counts4_kernel<T, D>), dim3(nb4), dim3(kBlock),
                                    sizeof(unsigned int) * rep * S * 8, s, Xt, (uint64_t)n, labels,
-                                   v.slot, k.ntab[level], v.axis, v.bounds, S, 0, rep, out);
+                                   v.slot, k.ntab[level], v.axis, v.bounds, S, 0, rep, out, ReplayTab{});
             }
         });
     });

@@ -300,8 +300,10 @@ class KDPartitioner(object):
             # the whole BFS in one launch chain (pd_kd_build): the level
             # decisions run on the device, bit-identical to the host's
             try:
+                # final mode 2: the labels are not written (the passes replay
+                # the splits; the labels property replays the finished tree)
                 lo, hi, bad, trace = _native.kd_build(X, self._labels, levels,
-                                                      final_split=False)
+                                                      final_split=2)
             except _native.PardisError as e:
                 if e.code != _native.PD_EUNSUPPORTED:
                     raise
@@ -341,11 +343,11 @@ class KDPartitioner(object):
 
     @property
     def labels(self):
-        """KD label of every point (device int32, input order)."""
+        """KD label of every point (device int32, input order), computed on
+        first use by replaying the split tree (pd_kd_labels)."""
         if self._pending is not None:
-            sel, axes, boundary, new = self._pending
             self._pending = None
-            _native.kd_split(self.points.X, self._labels, sel, axes, boundary, new)
+            _native.kd_labels(self.points.X, self._labels, self._tree)
         return self._labels
 
     def split_tree(self):

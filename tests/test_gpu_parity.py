@@ -1141,8 +1141,10 @@ def test_kd_device_decisions_equal_host(native, name, P):
     """pd_kd_build (level decisions on the device, one sync) gives the per-pass
     host-decided path's split trace, boxes and labels bit for bit — levels of
     1..128 splits, fp32 / fp64, zero variance, fewer points than partitions —
-    without the fused levels (the default) and with them (PD_OPT_KD_FUSE:
-    counts + the children's interval moments in one pass)."""
+    without the fused levels (the default), with them (PD_OPT_KD_FUSE:
+    counts + the children's interval moments in one pass) and with the
+    labels replayed from the split tree instead of kept in HBM
+    (PD_OPT_KD_REPLAY)."""
     from pypardis_amd import KDPartitioner, partition
     X = _kd_case(name)
     Xd = _dev(X)
@@ -1153,13 +1155,19 @@ def test_kd_device_decisions_equal_host(native, name, P):
         c = KDPartitioner(Xd, P)
     finally:
         ctx.set_option(native.PD_OPT_KD_FUSE, 0)
+    ctx.set_option(native.PD_OPT_KD_REPLAY, 1)
+    try:
+        r = KDPartitioner(Xd, P)
+        r.labels   # (replayed now, under the option)
+    finally:
+        ctx.set_option(native.PD_OPT_KD_REPLAY, 0)
     partition.DEVICE_DECISIONS = False
     try:
         b = KDPartitioner(Xd, P)
     finally:
         partition.DEVICE_DECISIONS = True
     sb, fb = _kd_arrays(b.splits)
-    for m in (a, c):
+    for m in (a, c, r):
         sa, fa = _kd_arrays(m.splits)
         assert np.array_equal(sa, sb)
         assert np.array_equal(fa, fb, equal_nan=True)
@@ -1239,7 +1247,7 @@ HALO_TREE = [("c2", 8), ("c2", 64), ("c4", 8), ("c4", 37), ("lattice", 16), ("f6
 
 @pytest.mark.parametrize("case,P", HALO_TREE, ids=[f"{c}-P{p}" for c, p in HALO_TREE])
 def test_halo_tree_equals_full_test(native, case, P):
-    """PD_OPT_HALO_TREE (default on): the halo's near-plane fast path — a
+    """PD_OPT_HALO_TREE (opt-in, measured slower): the halo's near-plane path — a
     point farther than 2 eps from every split plane on its KD path gets its
     owner's record only, the rest the full box test — writes the records of
     the full test (same count) and gives the oracle's labels: 2-D / 3-D / 4-D,
@@ -1277,7 +1285,7 @@ def test_halo_tree_equals_full_test(native, case, P):
         try:
             m = DBSCAN(eps=eps, min_samples=ms, metric=metric, max_partitions=P).train(Xd)
         finally:
-            ctx.set_option(native.PD_OPT_HALO_TREE, 1)
+            ctx.set_option(native.PD_OPT_HALO_TREE, 0)
         out.append((m, int(ctx.timings()["records"])))
     assert out[0][1] == out[1][1]
     for m, _ in out:

@@ -128,6 +128,17 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 // distinct key per wave: consecutive records mostly share a component, and a
 // big cluster's root otherwise takes ~1e5 serialised atomics.  Every lane of
 // the wave must call this (no early return before it).
+#ifndef PD_GMIN_CACHED
+#define PD_GMIN_CACHED 0
+#endif
+// The skip test's read of the current minimum: any stale value is >= the
+// current one, so an L1-cached read is as exact as an L2 one (it may only
+// cost an atomic the fresher read would have skipped).
+__device__ __forceinline__ uint32_t gmin_peek(const uint32_t* p) {
+    if constexpr (PD_GMIN_CACHED) return *p;
+    else return ld_rlx(p);
+}
+
 __device__ __forceinline__ void wave_atomic_min(uint32_t* base, bool valid, uint32_t key,
                                                 uint32_t val) {
     const int lane = threadIdx.x & 63;
@@ -140,7 +151,7 @@ __device__ __forceinline__ void wave_atomic_min(uint32_t* base, bool valid, uint
         // keys only decrease: a stale read is >= the current minimum, so
         // skipping when it is already <= m is exact; a hot root (a city of
         // 1e8 records) then takes reads, not a queue of atomics
-        if (lane == leader && m < ld_rlx(base + lk)) atomicMin(base + lk, m);
+        if (lane == leader && m < gmin_peek(base + lk)) atomicMin(base + lk, m);
         active &= ~__ballot(mine);
     }
 }
@@ -969,6 +980,9 @@ __global__ __launch_bounds__(kBlock) void halo1_kernel(
                              keys, vals, own0);
 }
 
+#ifndef PD_DUP_BLOCK
+#define PD_DUP_BLOCK 1   // (A/B builds: 0 = one append per wave)
+#endif
 // Coordinates into key order (padded rows); also lists the records of halo
 // points that live in several neighbourhoods (the merge only touches those)
 // and starts those points' merge representative (rep) at kNone.
@@ -988,7 +1002,19 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const T* __restrict__ X,
         for (int j = 0; j < S; ++j) Xs[r * S + j] = j < D ? X[i * D + j] : T(0);
         if (rep && (v & kDupBit)) rep[i] = kNone;
     }
+#if PD_DUP_BLOCK
+    // one reservation per block, not per wave: the list's single counter is
+    // a hot L2 line (the root list's appends had cost 0.8 ms of 1.06)
+    __shared__ uint32_t s_dbase;
+    const bool dp = r < R && (v & kDupBit);
+    uint32_t tot;
+    const uint32_t off = block_excl_scan(dp ? 1u : 0u, tot);
+    if (threadIdx.x == 0 && tot) s_dbase = atomicAdd(dup_count, tot);
+    __syncthreads();
+    if (dp) dup_list[s_dbase + off] = (uint32_t)r;
+#else
     wave_append(dup_list, dup_count, r < R && (v & kDupBit), (uint32_t)r);
+#endif
 }
 
 template <typename K>
@@ -1225,6 +1251,11 @@ __global__ __launch_bounds__(kBlock) void dir_write_kernel(uint4* __restrict__ d
 // parent is the smaller of them that is core and below r — two candidates
 // leave about half the trees of one (tools/init_forest_study.py).
 constexpr int kSubTiles = 4;   // init_kernel / roots_kernel: record tiles per block
+#ifndef PD_ROOTS_SUB
+#define PD_ROOTS_SUB 4
+#endif
+constexpr int kRootSub = PD_ROOTS_SUB;   // roots_kernel: record tiles per block
+constexpr int kRootLists = 64, kRootCntStride = 32;   // root lists, one 128-B counter line each
 // Also starts the per-record component keys (gmin) and the directory-word
 // roots (wroot, W words) at kNone — the fills they needed before.
 __global__ __launch_bounds__(kBlock) void init_kernel(uint32_t R, const uint8_t* __restrict__ core,
@@ -1315,67 +1346,79 @@ __global__ __launch_bounds__(kBlock) void merge_kernel(const uint32_t* __restric
     }
 }
 
-// Roots: every core record's parent becomes its root (flatten), each root
+// Roots: every core record's parent becomes its root (flatten) and each root
 // gets the smallest (global) point id of its component (wave-aggregated
-// atomicMin), and the roots are listed (one entry per component of this
-// device) with the count of core records.
+// atomicMin); with stats, the count of core records.
 __global__ __launch_bounds__(kBlock) void roots_kernel(uint32_t R, const uint32_t* __restrict__ vals,
                                                        const uint32_t* __restrict__ gid,
                                                        uint32_t* __restrict__ par,
                                                        uint32_t* __restrict__ gmin,
-                                                       uint32_t* __restrict__ root_list,
+                                                       uint32_t* __restrict__ rlist,
+                                                       uint32_t* __restrict__ rcnt, uint32_t seg,
                                                        uint32_t* __restrict__ counts, int stats) {
-    // kSubTiles record tiles of kBlock per block; a lane's kSubTiles records
+    // kRootSub record tiles of kBlock per block; a lane's kRootSub records
     // are read together (parents, first parent step, point ids) and their
     // minima folded per root in the lane before the wave-aggregated atomics:
     // one aggregation per distinct root of the lane (usually one), not one
     // per record
     uint32_t ncore = 0;
-    uint32_t rr[kSubTiles], x0[kSubTiles], root[kSubTiles], pt[kSubTiles];
-    bool core[kSubTiles];
+    uint32_t rr[kRootSub], x0[kRootSub], root[kRootSub], pt[kRootSub];
+    bool core[kRootSub];
 #pragma unroll
-    for (int q = 0; q < kSubTiles; ++q) {
-        rr[q] = (blockIdx.x * kSubTiles + q) * kBlock + threadIdx.x;
+    for (int q = 0; q < kRootSub; ++q) {
+        rr[q] = (blockIdx.x * kRootSub + q) * kBlock + threadIdx.x;
         x0[q] = rr[q] < R ? par[rr[q]] : kNone;
         core[q] = x0[q] != kNone;
     }
 #pragma unroll
-    for (int q = 0; q < kSubTiles; ++q) {
+    for (int q = 0; q < kRootSub; ++q) {
         root[q] = core[q] ? par[x0[q]] : 0u;   // the first step, all four in flight
         pt[q] = core[q] ? (vals[rr[q]] & kIdMask) : kNone;
     }
+    // longer chains (a tree the verify / pair / merge unions hung under
+    // another after the cell roots flattened it): the lane's kRootSub walks
+    // advance together, one round of loads in flight per step, instead of
+    // one walk after another
+    bool more[kRootSub];
 #pragma unroll
-    for (int q = 0; q < kSubTiles; ++q) {
-        if (!core[q]) continue;
-        uint32_t x = root[q] == x0[q] ? x0[q] : root[q];
-        if (x != x0[q]) {   // longer chain (rare after the link's flattening)
-            while (true) {
-                const uint32_t p = par[x];
-                if (p == x) break;
-                x = p;
-            }
-            par[rr[q]] = x;
+    for (int q = 0; q < kRootSub; ++q) more[q] = core[q] && root[q] != x0[q];
+    while (true) {
+        bool any = false;
+#pragma unroll
+        for (int q = 0; q < kRootSub; ++q) any |= more[q];
+        if (!__any(any)) break;
+        uint32_t p[kRootSub];
+#pragma unroll
+        for (int q = 0; q < kRootSub; ++q) p[q] = more[q] ? par[root[q]] : root[q];
+#pragma unroll
+        for (int q = 0; q < kRootSub; ++q) {
+            if (p[q] == root[q]) more[q] = false;
+            root[q] = p[q];
         }
-        root[q] = x;
+    }
+#pragma unroll
+    for (int q = 0; q < kRootSub; ++q) {
+        if (!core[q]) continue;
+        if (root[q] != x0[q]) par[rr[q]] = root[q];
         if (gid) pt[q] = gid[pt[q]];
         ncore += 1u;
     }
-    bool left[kSubTiles];
+    bool left[kRootSub];
 #pragma unroll
-    for (int q = 0; q < kSubTiles; ++q) left[q] = core[q];
+    for (int q = 0; q < kRootSub; ++q) left[q] = core[q];
     while (true) {
         // the lane's first remaining root and the smallest point id under it
         bool have = false;
         uint32_t key = 0, m = kNone;
 #pragma unroll
-        for (int q = 0; q < kSubTiles; ++q) {
+        for (int q = 0; q < kRootSub; ++q) {
             if (left[q] && !have) {
                 have = true;
                 key = root[q];
             }
         }
 #pragma unroll
-        for (int q = 0; q < kSubTiles; ++q) {
+        for (int q = 0; q < kRootSub; ++q) {
             if (left[q] && root[q] == key) {
                 m = pt[q] < m ? pt[q] : m;
                 left[q] = false;
@@ -1384,11 +1427,27 @@ __global__ __launch_bounds__(kBlock) void roots_kernel(uint32_t R, const uint32_
         if (!__any(have)) break;
         wave_atomic_min(gmin, have, key, m);
     }
-    // roots are rare (one per component): a wave-aggregated append is cheap
-    if (root_list) {
+    // the roots, listed (single device) into kRootLists lists, one
+    // reservation per block: one list counter taking an append per wave
+    // with a root (96K on C2) serialised at its L2 channel — 0.8 of the
+    // kernel's 1.06 ms; block b appends to list b % kRootLists, whose blocks
+    // hold at most seg records
+    if (rlist) {
+        __shared__ uint32_t s_rbase;
+        uint32_t nr = 0;
 #pragma unroll
-        for (int q = 0; q < kSubTiles; ++q)
-            wave_append(root_list, counts, core[q] && root[q] == rr[q], rr[q]);
+        for (int q = 0; q < kRootSub; ++q) nr += core[q] && root[q] == rr[q] ? 1u : 0u;
+        uint32_t tot;
+        uint32_t off = block_excl_scan(nr, tot);
+        const uint32_t k = blockIdx.x % kRootLists;
+        if (threadIdx.x == 0 && tot) s_rbase = atomicAdd(rcnt + k * kRootCntStride, tot);
+        __syncthreads();
+        if (tot) {
+            uint32_t* out = rlist + (size_t)k * seg + s_rbase;
+#pragma unroll
+            for (int q = 0; q < kRootSub; ++q)
+                if (core[q] && root[q] == rr[q]) out[off++] = rr[q];
+        }
     }
     if (stats) {   // core records (sweep statistics): one atomic per block
         const uint32_t c = block_sum_u32(ncore);
@@ -1402,25 +1461,38 @@ __global__ __launch_bounds__(kBlock) void roots_kernel(uint32_t R, const uint32_
 // mark each component's key in an n-bit map, scan the words' popcounts, and
 // a root's label is its word's prefix plus the bits below it in the word —
 // no sort, and the component count stays on the device (no host sync).
-__global__ __launch_bounds__(kBlock) void root_mark_kernel(const uint32_t* __restrict__ root_list,
-                                                           const uint32_t* __restrict__ count,
+// The lists' slots: list k holds rcnt[k * kRootCntStride] roots from slot
+// k * seg; block b of a grid of kRootLists * m blocks walks list b % kRootLists.
+__global__ __launch_bounds__(kBlock) void root_mark_kernel(const uint32_t* __restrict__ rlist,
+                                                           const uint32_t* __restrict__ rcnt,
+                                                           uint32_t seg,
                                                            const uint32_t* __restrict__ gmin,
                                                            uint32_t* __restrict__ kbits) {
-    const uint32_t C = *count;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < C; i += gridDim.x * kBlock) {
-        const uint32_t g = gmin[root_list[i]];
+    const uint32_t k = blockIdx.x % kRootLists, m = gridDim.x / kRootLists;
+    const uint32_t c = rcnt[k * kRootCntStride];
+    const uint32_t* l = rlist + (size_t)k * seg;
+    for (uint32_t i = (blockIdx.x / kRootLists) * kBlock + threadIdx.x; i < c; i += m * kBlock) {
+        const uint32_t g = gmin[l[i]];
         atomicOr(kbits + (g >> 5), 1u << (g & 31));
     }
 }
 
-__global__ __launch_bounds__(kBlock) void root_rank_kernel(const uint32_t* __restrict__ root_list,
-                                                           const uint32_t* __restrict__ count,
+// ... and the component count (the map's population: one bit per component
+// key) into *count, read with the train's last copy back.
+__global__ __launch_bounds__(kBlock) void root_rank_kernel(const uint32_t* __restrict__ rlist,
+                                                           const uint32_t* __restrict__ rcnt,
+                                                           uint32_t seg,
                                                            const uint32_t* __restrict__ kbits,
                                                            const uint32_t* __restrict__ kpre,
-                                                           uint32_t* __restrict__ gmin) {
-    const uint32_t C = *count;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < C; i += gridDim.x * kBlock) {
-        const uint32_t r = root_list[i], g = gmin[r];
+                                                           uint64_t NW, uint32_t* __restrict__ gmin,
+                                                           uint32_t* __restrict__ count) {
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        *count = kpre[NW - 1] + (uint32_t)__popc(kbits[NW - 1]);
+    const uint32_t k = blockIdx.x % kRootLists, m = gridDim.x / kRootLists;
+    const uint32_t c = rcnt[k * kRootCntStride];
+    const uint32_t* l = rlist + (size_t)k * seg;
+    for (uint32_t i = (blockIdx.x / kRootLists) * kBlock + threadIdx.x; i < c; i += m * kBlock) {
+        const uint32_t r = l[i], g = gmin[r];
         gmin[r] = kpre[g >> 5] + (uint32_t)__popc(kbits[g >> 5] & ((1u << (g & 31)) - 1u));
     }
 }
@@ -2787,9 +2859,9 @@ struct EvTimer {
 };
 
 inline unsigned blocks(uint64_t n) { return n ? (unsigned)((n + kBlock - 1) / kBlock) : 1u; }
-// blocks of kSubTiles record tiles (init_kernel, roots_kernel)
-inline unsigned sub_blocks(uint64_t n) {
-    return n ? (unsigned)((n + (uint64_t)kBlock * kSubTiles - 1) / ((uint64_t)kBlock * kSubTiles)) : 1u;
+// blocks of `sub` record tiles (init_kernel: kSubTiles, roots_kernel: kRootSub)
+inline unsigned sub_blocks(uint64_t n, int sub = kSubTiles) {
+    return n ? (unsigned)((n + (uint64_t)kBlock * sub - 1) / ((uint64_t)kBlock * sub)) : 1u;
 }
 
 // Exclusive scan of `tiles` per-tile counts into u64 offsets (off[tiles] =
@@ -3252,10 +3324,12 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         // (1) forest from the count pass's two smallest neighbours
         uint32_t* wroot = ctx.arena.get<uint32_t>("word_root", W);
         // (single device: the n-bit component-key map of rank_roots, zeroed here)
+        // (+ the root lists' counters after it, from a 128-B boundary)
         const uint64_t NW = a.phase == 0 ? (n + 31) / 32 : 0;
-        uint32_t* kbits = NW ? ctx.arena.get<uint32_t>("key_bits", NW) : nullptr;
-        hipLaunchKernelGGL(init_kernel, dim3(sub_blocks(std::max<uint64_t>(std::max<uint64_t>(R, W), NW))),
-                           dim3(kBlock), 0, s, R, core, mn, 1, par, gmin, wroot, (uint64_t)W, kbits, NW);
+        const uint64_t NWz = NW ? ((NW + 31) & ~uint64_t(31)) + kRootLists * kRootCntStride : 0;
+        uint32_t* kbits = NW ? ctx.arena.get<uint32_t>("key_bits", NWz) : nullptr;
+        hipLaunchKernelGGL(init_kernel, dim3(sub_blocks(std::max<uint64_t>(std::max<uint64_t>(R, W), NWz))),
+                           dim3(kBlock), 0, s, R, core, mn, 1, par, gmin, wroot, (uint64_t)W, kbits, NWz);
         // (2) window union.  Auto window (PD_OPT_CENTRE_WINDOW < 0): sparse
         // cells (a few records each, C2: 2.3) gain little from the window
         // beyond the fused flatten, so a short one is cheapest (C2 link 6.59
@@ -3355,21 +3429,25 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
     }
     tm.mark();   // 7
     if (R) {
-        // single device: the components are listed so that their keys can be
-        // ranked here (labels); sharded: keys stay global ids (merge first)
-        uint32_t* root_list = a.phase == 0 ? ctx.arena.get<uint32_t>("root_list", R) : nullptr;
+        // single device: the component keys are ranked here (labels);
+        // sharded: keys stay global ids (merge first)
         // (gmin starts at kNone: init_kernel)
-        hipLaunchKernelGGL(roots_kernel, dim3(sub_blocks(R)), dim3(kBlock), 0, s, R, vals, a.gid, par,
-                           gmin, root_list, lcount + 1, ctx.sweep_stats ? 1 : 0);
+        const unsigned rb = sub_blocks(R, kRootSub);
+        const uint32_t seg = ((rb + kRootLists - 1) / kRootLists) * (uint32_t)(kRootSub * kBlock);
+        const uint64_t NW = a.phase == 0 ? (n + 31) / 32 : 0;
+        uint32_t* rlist = NW ? ctx.arena.get<uint32_t>("root_list", (size_t)seg * kRootLists) : nullptr;
+        uint32_t* rcnt = NW ? ctx.arena.get<uint32_t>("key_bits", 1) + ((NW + 31) & ~uint64_t(31))
+                            : nullptr;   // (zeroed by init_kernel)
+        hipLaunchKernelGGL(roots_kernel, dim3(rb), dim3(kBlock), 0, s, R, vals, a.gid, par, gmin, rlist,
+                           rcnt, seg, lcount + 1, ctx.sweep_stats ? 1 : 0);
         if (a.phase == 0) {
             // rank the component keys on the device; the component count is
             // read with the train's last copy back (finish)
-            const uint64_t NW = (n + 31) / 32;
-            uint32_t* kbits = ctx.arena.get<uint32_t>("key_bits", NW);
+            uint32_t* kbits = ctx.arena.get<uint32_t>("key_bits", 1);
             uint32_t* kpre = ctx.arena.get<uint32_t>("key_pre", NW);
-            const unsigned gb = std::min(blocks(R), 1024u);
-            hipLaunchKernelGGL(root_mark_kernel, dim3(gb), dim3(kBlock), 0, s, root_list, lcount + 1,
-                               gmin, kbits);
+            const unsigned gb = kRootLists * 16;
+            hipLaunchKernelGGL(root_mark_kernel, dim3(gb), dim3(kBlock), 0, s, rlist, rcnt, seg, gmin,
+                               kbits);
             rocprim::transform_iterator<const uint32_t*, PopcOp, uint32_t> pc(kbits, PopcOp{});
             size_t tb = 0;
             PD_HIP(rocprim::exclusive_scan(nullptr, tb, pc, kpre, 0u, (size_t)NW,
@@ -3377,8 +3455,8 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
             void* tmp = ctx.arena.get<char>("key_scan_tmp", tb);
             PD_HIP(rocprim::exclusive_scan(tmp, tb, pc, kpre, 0u, (size_t)NW,
                                            rocprim::plus<uint32_t>(), s));
-            hipLaunchKernelGGL(root_rank_kernel, dim3(gb), dim3(kBlock), 0, s, root_list, lcount + 1,
-                               kbits, kpre, gmin);
+            hipLaunchKernelGGL(root_rank_kernel, dim3(gb), dim3(kBlock), 0, s, rlist, rcnt, seg, kbits,
+                               kpre, NW, gmin, lcount + 1);
         } else if (ctx.sweep_stats) {
             uint32_t* h = (uint32_t*)pinned(ctx, sizeof(uint32_t) * 4);
             PD_HIP(hipMemcpyAsync(h, lcount + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, s));

@@ -980,9 +980,6 @@ __global__ __launch_bounds__(kBlock) void halo1_kernel(
                              keys, vals, own0);
 }
 
-#ifndef PD_DUP_BLOCK
-#define PD_DUP_BLOCK 1   // (A/B builds: 0 = one append per wave)
-#endif
 // Coordinates into key order (padded rows); also lists the records of halo
 // points that live in several neighbourhoods (the merge only touches those)
 // and starts those points' merge representative (rep) at kNone.
@@ -1002,19 +999,7 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(const T* __restrict__ X,
         for (int j = 0; j < S; ++j) Xs[r * S + j] = j < D ? X[i * D + j] : T(0);
         if (rep && (v & kDupBit)) rep[i] = kNone;
     }
-#if PD_DUP_BLOCK
-    // one reservation per block, not per wave: the list's single counter is
-    // a hot L2 line (the root list's appends had cost 0.8 ms of 1.06)
-    __shared__ uint32_t s_dbase;
-    const bool dp = r < R && (v & kDupBit);
-    uint32_t tot;
-    const uint32_t off = block_excl_scan(dp ? 1u : 0u, tot);
-    if (threadIdx.x == 0 && tot) s_dbase = atomicAdd(dup_count, tot);
-    __syncthreads();
-    if (dp) dup_list[s_dbase + off] = (uint32_t)r;
-#else
     wave_append(dup_list, dup_count, r < R && (v & kDupBit), (uint32_t)r);
-#endif
 }
 
 template <typename K>

@@ -1977,9 +1977,6 @@ __device__ __forceinline__ void lds_union(uint32_t* lp, uint32_t a, uint32_t b) 
 // component's representative unites the two trees in the global forest —
 // one global union per pair of trees the window joins (the wave's edges
 // between the same two trees cost one), instead of a find per edge.
-#ifndef PD_WINDOW_GLOBAL
-#define PD_WINDOW_GLOBAL 1   // (A/B builds: 0 = the window's edges stay in LDS, verify joins)
-#endif
 template <typename T, int D, int M, int W, bool ST>
 __global__ __launch_bounds__(kBlock) void window_uf_kernel(const T* __restrict__ Xs, uint32_t R,
                                                            double eps, double eps2, float lo,
@@ -2052,9 +2049,7 @@ __global__ __launch_bounds__(kBlock) void window_uf_kernel(const T* __restrict__
         // the slot before carries the same pair of trees: its lane unites them
         if (e > 0 && sp[w][e - 1] == pe && lds_find(lp[w], (uint32_t)(e - 1)) == lr) continue;
         if constexpr (ST) ++st.unions;
-#if PD_WINDOW_GLOBAL
         uf_link_roots(par, uf_find_l1(par, pl), uf_find_l1(par, pe));
-#endif
     }
     if constexpr (ST) {   // one atomic per block and counter
         const uint32_t c = block_sum_u32(st.cand), h = block_sum_u32(st.hit),

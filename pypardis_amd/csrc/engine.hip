@@ -3238,16 +3238,23 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
                 hipLaunchKernelGGL((dir_bits_kernel<K, 6, false>), dim3(blocks(R)), dim3(kBlock), 0,
                                    s, ckeys, dncells, pages);
         }
+        // (the cell count rides on the same sync, beside the total in the
+        // pinned block: the word pass then launches over the cells, not the
+        // records — C4: a third of the waves)
+        if (R) PD_HIP(hipMemcpyAsync((char*)pinned(ctx, 16) + 8, dncells, sizeof(uint32_t),
+                                     hipMemcpyDeviceToHost, s));
         const uint64_t nw = prefix_words(pages, NP, true);
         W = nw + 1;
         dir = ctx.arena.get<uint4>("dir", W);
         if (R)
         {
+            const uint32_t nch = *(const uint32_t*)((const char*)pinned(ctx, 16) + 8);
+            const uint64_t wg = std::max<uint64_t>(1, std::min<uint64_t>(nch, R));
             if (sizeof(K) == 4 || key_bits <= 37)   // word ids < 2^31
-                hipLaunchKernelGGL((word_write_kernel<K, true>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                hipLaunchKernelGGL((word_write_kernel<K, true>), dim3(blocks(wg)), dim3(kBlock), 0, s,
                                    ckeys, dncells, pages, dir);
             else
-                hipLaunchKernelGGL((word_write_kernel<K, false>), dim3(blocks(R)), dim3(kBlock), 0, s,
+                hipLaunchKernelGGL((word_write_kernel<K, false>), dim3(blocks(wg)), dim3(kBlock), 0, s,
                                    ckeys, dncells, pages, dir);
         }
         else
@@ -3322,10 +3329,15 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         // and 56 ms with the flatten alone); dense cells (C4 city centres)
         // want the long one (C4 link 71.5 -> 60.6 ms at 4 -> 16)
         int cw = ctx.centre_window;
+        // the per-cell kernels' grid: the cells when the host knows their
+        // count (the auto window), else the records (a bound: the kernels
+        // read the count on the device and leave past it)
+        uint64_t cgrid = R;
         if (cw < 0) {
             PD_HIP(hipEventSynchronize(ev_nc));
             (void)hipEventDestroy(ev_nc);
             const uint32_t nc = *h_nc ? *h_nc : 1u;
+            cgrid = std::min<uint64_t>(nc, R);
             // records per occupied cell: <= 2.5 -> 2 (C2: 2.32), <= 8 -> 8
             // (C4: 2.96, dense cities in sparse noise: link 37.1 / 32.2 /
             // 56.3 / 142.9 ms at 4 / 8 / 16 / 32; C1: 4.96, 0.58 / 0.60 /
@@ -3360,11 +3372,11 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
             uint32_t* nbig = ctrs + 8;   // [0] big, [1] mid (zeroed by the halo pass)
             // (wroot starts at kNone: init_kernel)
             if ((uint64_t)W < 0xFFFFFFFFull)   // directory slots < 2^32 - 1
-                hipLaunchKernelGGL((cell_word_root_kernel<K, true>), dim3(blocks(R)), dim3(kBlock), 0,
+                hipLaunchKernelGGL((cell_word_root_kernel<K, true>), dim3(blocks(cgrid)), dim3(kBlock), 0,
                                    s, cstart, dncells, ckeys, par, croot, wroot, mid, nbig + 1, big,
                                    nbig, pages);
             else
-                hipLaunchKernelGGL((cell_word_root_kernel<K, false>), dim3(blocks(R)), dim3(kBlock),
+                hipLaunchKernelGGL((cell_word_root_kernel<K, false>), dim3(blocks(cgrid)), dim3(kBlock),
                                    0, s, cstart, dncells, ckeys, par, croot, wroot, mid, nbig + 1,
                                    big, nbig, pages);
             hipLaunchKernelGGL((mid_cell_word_root_kernel<K>), dim3(2048), dim3(kBlock), 0, s,
@@ -3376,7 +3388,7 @@ void run_a(Ctx& ctx, TrainArgs& a, const std::vector<PartGrid>& hparts, uint64_t
         uint2* plist = ctx.arena.get<uint2>("pair_list", pcap);
         uint32_t* pcount = ctrs + 10;   // (zeroed by the halo pass)
         // (4) verify: screen every cell, then work on the flagged ones only
-        const unsigned vtiles = blocks(R);
+        const unsigned vtiles = blocks(cgrid);
         uint8_t* vflag = ctx.arena.get<uint8_t>("verify_flags", R);
         uint32_t* vlist = ctx.arena.get<uint32_t>("verify_list", R);
         uint32_t* vcnt = ctx.arena.get<uint32_t>("tile_cnt", (size_t)vtiles + 1);

@@ -1567,13 +1567,34 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
     // kOwnPer consecutive records per thread (a tile of kOwnTile records per
     // block: a quarter of the workgroups of one record per thread, which
     // dominated these light passes over C4's 1e9 records)
+    // (the thread's four values / flags in one 16-B / 4-B load each, and the
+    // pairs staged in LDS and written out as whole 16-B runs: stored one
+    // record per lane at a 32-B stride, the pairs' partial sectors reached
+    // HBM separately — 3.1 GB written per C2 launch for 0.8 GB of pairs)
+    __shared__ uint2 s_rec[kOwnTile];
+    const uint32_t r0 = (blockIdx.x * kBlock + threadIdx.x) * kOwnPer;
+    uint32_t vq[kOwnPer];
+    uint8_t cq[kOwnPer];
+    if (r0 + kOwnPer <= R && !((uintptr_t)vals & 15)) {
+        const uint4 v4 = *reinterpret_cast<const uint4*>(vals + r0);
+        const uint32_t c4 = *reinterpret_cast<const uint32_t*>(core + r0);
+        vq[0] = v4.x, vq[1] = v4.y, vq[2] = v4.z, vq[3] = v4.w;
+#pragma unroll
+        for (int q = 0; q < kOwnPer; ++q) cq[q] = (uint8_t)(c4 >> (8 * q));
+    } else {
+#pragma unroll
+        for (int q = 0; q < kOwnPer; ++q) {
+            vq[q] = r0 + q < R ? vals[r0 + q] : 0u;
+            cq[q] = r0 + q < R ? core[r0 + q] : 0;
+        }
+    }
     uint32_t nb = 0;
 #pragma unroll
     for (int q = 0; q < kOwnPer; ++q) {
-        const uint32_t r = (blockIdx.x * kBlock + threadIdx.x) * kOwnPer + q;
-        const uint32_t v = r < R ? vals[r] : 0u;
+        const uint32_t r = r0 + q;
+        const uint32_t v = vq[q];
         const bool own = r < R && (v & kOwnerBit);
-        const uint8_t fl = own ? core[r] : 0;
+        const uint8_t fl = own ? cq[q] : 0;
         // the record's key: core -> its component's; a border record with a
         // single neighbour (bit 2) -> that neighbour's if it is core (the
         // border sweep's smallest core key, over one candidate); else none
@@ -1586,8 +1607,8 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
             const uint32_t pj = par[j];
             key = pj != kNone ? gmin[pj] : kNone;
         }
-        if (recs && r < R)   // bucketed labels: the pair in record order, coalesced
-            recs[r] = make_uint2(own ? v & kIdMask : kNone, key);
+        if (recs)   // bucketed labels: the pair in record order
+            s_rec[threadIdx.x * kOwnPer + q] = make_uint2(own ? v & kIdMask : kNone, key);
         if (own) {
             const uint32_t pt = v & kIdMask;
             if (core_out && !core_mask) core_out[pt] = fl & 1;
@@ -1599,6 +1620,18 @@ __global__ __launch_bounds__(kBlock) void owner_kernel(uint32_t R, const uint32_
         }
         // the rest of the border candidates go to the sweep
         nb += own && (fl & 3) == 2 && !((fl & 4) && mn) ? 1u : 0u;
+    }
+    if (recs) {
+        __syncthreads();
+        const uint32_t base = blockIdx.x * kOwnTile;
+        for (uint32_t i = threadIdx.x; i < kOwnTile / 2; i += kBlock) {
+            const uint32_t r = base + 2 * i;
+            if (r + 1 < R)
+                *reinterpret_cast<uint4*>(recs + r) =
+                    make_uint4(s_rec[2 * i].x, s_rec[2 * i].y, s_rec[2 * i + 1].x, s_rec[2 * i + 1].y);
+            else if (r < R)
+                recs[r] = s_rec[2 * i];
+        }
     }
     // border candidates (owner record, not core, has a neighbour) per tile;
     // border_list_kernel lists them in order after a scan of the counts
@@ -1616,12 +1649,17 @@ __global__ __launch_bounds__(kBlock) void border_list_kernel(uint32_t R,
     bool cand[kOwnPer];
     uint32_t nc = 0;
     const uint32_t r0 = (blockIdx.x * kBlock + threadIdx.x) * kOwnPer;
+    uint32_t c4 = 0;   // the four flags in one load; vals read only for candidates
+    if (r0 + kOwnPer <= R)
+        c4 = *reinterpret_cast<const uint32_t*>(core + r0);
+    else
+        for (int q = 0; q < kOwnPer; ++q) c4 |= r0 + q < R ? (uint32_t)core[r0 + q] << (8 * q) : 0u;
 #pragma unroll
     for (int q = 0; q < kOwnPer; ++q) {
         const uint32_t r = r0 + q;
-        const uint8_t fl = r < R ? core[r] : 0;
+        const uint32_t fl = (c4 >> (8 * q)) & 0xFFu;
         // (owner_kernel's rule: single-neighbour records are attached there)
-        cand[q] = r < R && (vals[r] & kOwnerBit) && (fl & 3) == 2 && !(fl & 4);
+        cand[q] = r < R && (fl & 3) == 2 && !(fl & 4) && (vals[r] & kOwnerBit);
         nc += cand[q] ? 1u : 0u;
     }
     uint32_t btot;
